@@ -1,0 +1,173 @@
+// ATen bindings: registers the framework kernels as torch.ops.tgpipe.* (CUDA == HIP
+// dispatch key on ROCm builds) and validates shapes / dtypes / devices before launching.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+namespace tgpipe {
+namespace {
+
+hipStream_t stream_of(const at::Tensor& t) {
+  return at::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_f32_gpu(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void dbn_track(const at::Tensor& x, at::Tensor& sum, at::Tensor& sumsq) {
+  check_f32_gpu(x, "x");
+  check_f32_gpu(sum, "sum");
+  check_f32_gpu(sumsq, "sumsq");
+  TORCH_CHECK(x.dim() >= 2, "x must be at least 2-D");
+  const int64_t n = x.size(0), c = x.size(1);
+  const int64_t s = c == 0 || n == 0 ? 0 : x.numel() / (n * c);
+  TORCH_CHECK(sum.numel() == c && sumsq.numel() == c, "stat buffers must have C elements");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  launch_dbn_track(x.data_ptr<float>(), sum.data_ptr<float>(), sumsq.data_ptr<float>(), n, c, s,
+                   stream_of(x));
+}
+
+void dbn_commit(at::Tensor& sum, at::Tensor& sumsq, at::Tensor& running_mean,
+                at::Tensor& running_var, double count, double momentum) {
+  check_f32_gpu(sum, "sum");
+  check_f32_gpu(sumsq, "sumsq");
+  check_f32_gpu(running_mean, "running_mean");
+  check_f32_gpu(running_var, "running_var");
+  const int64_t c = sum.numel();
+  TORCH_CHECK(sumsq.numel() == c && running_mean.numel() == c && running_var.numel() == c,
+              "all buffers must have C elements");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(sum.device());
+  launch_dbn_commit(sum.data_ptr<float>(), sumsq.data_ptr<float>(),
+                    running_mean.data_ptr<float>(), running_var.data_ptr<float>(), c, count,
+                    momentum, stream_of(sum));
+}
+
+std::vector<at::Tensor> dna_forward(const at::Tensor& x, double p, double eps, double slope,
+                                    int64_t seed, int64_t offset, bool dropout) {
+  check_f32_gpu(x, "x");
+  TORCH_CHECK(x.dim() >= 3, "expected (N, C, *spatial) input");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout probability must be in [0, 1)");
+  const int64_t planes = x.size(0) * x.size(1);
+  const int64_t s = planes == 0 ? 0 : x.numel() / planes;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty_like(x);
+  auto opts = x.options();
+  auto mean = at::empty({planes}, opts);
+  auto rstd = at::empty({planes}, opts);
+  auto scale = at::empty({planes}, opts);
+  launch_dna_forward(x.data_ptr<float>(), y.data_ptr<float>(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), scale.data_ptr<float>(), planes, s,
+                     static_cast<float>(p), static_cast<float>(eps), static_cast<float>(slope),
+                     static_cast<uint64_t>(seed), static_cast<uint64_t>(offset), dropout,
+                     stream_of(x));
+  return {y, mean, rstd, scale};
+}
+
+at::Tensor dna_backward(const at::Tensor& dy_in, const at::Tensor& x, const at::Tensor& mean,
+                        const at::Tensor& rstd, const at::Tensor& scale, double slope) {
+  check_f32_gpu(x, "x");
+  auto dy = dy_in.contiguous();
+  check_f32_gpu(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy and x must have the same shape");
+  const int64_t planes = x.size(0) * x.size(1);
+  const int64_t s = planes == 0 ? 0 : x.numel() / planes;
+  TORCH_CHECK(mean.numel() == planes && rstd.numel() == planes && scale.numel() == planes,
+              "saved statistics must have N*C elements");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto dx = at::empty_like(x);
+  launch_dna_backward(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), scale.data_ptr<float>(), dx.data_ptr<float>(),
+                      planes, s, static_cast<float>(slope), stream_of(x));
+  return dx;
+}
+
+at::Tensor dropout(const at::Tensor& x_in, double p, int64_t seed, int64_t offset) {
+  auto x = x_in.contiguous();
+  check_f32_gpu(x, "x");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout probability must be in [0, 1)");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty_like(x);
+  launch_dropout(x.data_ptr<float>(), y.data_ptr<float>(), x.numel(), static_cast<float>(p),
+                 static_cast<uint64_t>(seed), static_cast<uint64_t>(offset), stream_of(x));
+  return y;
+}
+
+at::Tensor philox_uniform(int64_t n, int64_t seed, int64_t offset, at::Device device) {
+  TORCH_CHECK(device.is_cuda(), "philox_uniform runs on the GPU");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(device);
+  auto out = at::empty({n}, at::TensorOptions().dtype(at::kFloat).device(device));
+  launch_philox_uniform(out.data_ptr<float>(), n, static_cast<uint64_t>(seed),
+                        static_cast<uint64_t>(offset), stream_of(out));
+  return out;
+}
+
+void spin(int64_t ns, at::Device device) {
+  TORCH_CHECK(device.is_cuda(), "spin runs on the GPU");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(device);
+  launch_spin(static_cast<uint64_t>(ns),
+              at::hip::getCurrentHIPStream(device.index()).stream());
+}
+
+void copy_segments(at::TensorList srcs, at::TensorList dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size(), "srcs and dsts must pair up");
+  if (srcs.empty()) return;
+  const auto device = srcs[0].device();
+  TORCH_CHECK(device.is_cuda(), "copy_segments runs on the GPU");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(device);
+  std::vector<Segment> segs;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    TORCH_CHECK(srcs[i].is_contiguous() && dsts[i].is_contiguous(), "segments must be contiguous");
+    TORCH_CHECK(srcs[i].device() == device && dsts[i].device() == device,
+                "segments must live on one device");
+    const int64_t bytes = srcs[i].numel() * srcs[i].element_size();
+    TORCH_CHECK(bytes == dsts[i].numel() * dsts[i].element_size(), "segment size mismatch");
+    segs.push_back({srcs[i].data_ptr(), dsts[i].data_ptr(), bytes});
+  }
+  const hipStream_t stream = at::hip::getCurrentHIPStream(device.index()).stream();
+  for (size_t i = 0; i < segs.size(); i += kMaxSegments) {
+    const int count = static_cast<int>(std::min<size_t>(kMaxSegments, segs.size() - i));
+    launch_segments_copy(segs.data() + i, count, stream);
+  }
+}
+
+}  // namespace
+}  // namespace tgpipe
+
+TORCH_LIBRARY(tgpipe, m) {
+  m.def("dbn_track(Tensor x, Tensor(a!) sum, Tensor(b!) sumsq) -> ()");
+  m.def("dbn_commit(Tensor(a!) sum, Tensor(b!) sumsq, Tensor(c!) running_mean, "
+        "Tensor(d!) running_var, float count, float momentum) -> ()");
+  m.def("dna_forward(Tensor x, float p, float eps, float slope, int seed, int offset, "
+        "bool dropout) -> Tensor[]");
+  m.def("dna_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor scale, "
+        "float slope) -> Tensor");
+  m.def("dropout(Tensor x, float p, int seed, int offset) -> Tensor");
+  m.def("philox_uniform(int n, int seed, int offset, Device device) -> Tensor");
+  m.def("spin(int ns, Device device) -> ()");
+  m.def("copy_segments(Tensor[] srcs, Tensor(a!)[] dsts) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
+  m.impl("dbn_track", &tgpipe::dbn_track);
+  m.impl("dbn_commit", &tgpipe::dbn_commit);
+  m.impl("dna_forward", &tgpipe::dna_forward);
+  m.impl("dna_backward", &tgpipe::dna_backward);
+  m.impl("dropout", &tgpipe::dropout);
+  m.impl("copy_segments", &tgpipe::copy_segments);
+}
+
+TORCH_LIBRARY_IMPL(tgpipe, CompositeExplicitAutograd, m) {
+  m.impl("philox_uniform", &tgpipe::philox_uniform);
+  m.impl("spin", &tgpipe::spin);
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "torchgpipe_amd native HIP kernels (gfx950)";
+}

@@ -1,0 +1,51 @@
+// Host-side launchers of the framework's HIP kernels (gfx950 / CDNA4).
+// Pure HIP (no ATen) so that kernels.hip compiles in seconds; the ATen
+// bindings in bindings.cpp validate shapes/dtypes before calling these.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tgpipe {
+
+// K1: per-channel sum / sum of squares of x[N, C, S] accumulated into sum[C], sumsq[C].
+void launch_dbn_track(const float* x, float* sum, float* sumsq, int64_t n, int64_t c, int64_t s,
+                      hipStream_t stream);
+
+// K2: running stats EMA from accumulated sums; zeroes the sums.
+void launch_dbn_commit(float* sum, float* sumsq, float* running_mean, float* running_var,
+                       int64_t c, double count, double momentum, hipStream_t stream);
+
+// Fused Dropout2d(p) -> InstanceNorm2d(eps, affine=False) -> LeakyReLU(slope) over
+// planes x[P, S] (P = N*C, S = H*W).  Saves per-plane mean (of x), rstd (of the
+// dropped-out input) and the dropout scale (0 or 1/(1-p)).
+void launch_dna_forward(const float* x, float* y, float* mean, float* rstd, float* scale,
+                        int64_t planes, int64_t s, float p, float eps, float slope,
+                        uint64_t seed, uint64_t offset, bool dropout, hipStream_t stream);
+
+void launch_dna_backward(const float* dy, const float* x, const float* mean, const float* rstd,
+                         const float* scale, float* dx, int64_t planes, int64_t s, float slope,
+                         hipStream_t stream);
+
+// Elementwise inverted dropout with explicit Philox (seed, offset); the mask is
+// regenerated in backward instead of stored.
+void launch_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, uint64_t offset,
+                    hipStream_t stream);
+
+// Uniform [0,1) Philox draws (tests / reference checks).
+void launch_philox_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
+                           hipStream_t stream);
+
+// Spin for `ns` nanoseconds of wall time (s_memrealtime, 100 MHz) — race tests.
+void launch_spin(uint64_t ns, hipStream_t stream);
+
+// Multi-tensor pack/unpack: copy `count` byte segments between separate buffers
+// and one contiguous buffer in a single launch (inter-stage message packing).
+struct Segment {
+  const void* src;
+  void* dst;
+  int64_t bytes;
+};
+constexpr int kMaxSegments = 16;
+void launch_segments_copy(const Segment* segs, int count, hipStream_t stream);
+
+}  // namespace tgpipe

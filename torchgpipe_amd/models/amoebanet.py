@@ -1,0 +1,221 @@
+"""AmoebaNet-D as a flat ``nn.Sequential`` (benchmark model).
+
+Same architecture as the reference benchmark model
+(``benchmarks/models/amoebanet/__init__.py:138-194``, ``operations.py``,
+``genotype.py``): a ReLU-Conv-BN stem, two reduction cells, then three
+stacks of ``L/3`` normal cells separated by reduction cells, and a classifier.
+Cells exchange ``(x, skip)`` tuples, so pipeline boundaries carry two tensors.
+AmoebaNet-D(18, 256) = 24 layers, 122.47 M parameters; the reference balance
+tables (``benchmarks/amoebanetd-speed/main.py:35-96``) apply unchanged.
+
+Kept quirks of the reference for benchmark fidelity: the normal-cell concat is
+TensorFlow's ``[0, 3, 4, 6]``, and ``max_pool_3x3`` is an average pool
+(``operations.py:57-59`` in the reference).
+"""
+from collections import OrderedDict
+from typing import Callable, Iterator, List, Tuple, Union
+
+import torch
+from torch import Tensor, nn
+
+__all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS']
+
+
+class Operation(nn.Module):
+    def __init__(self, name: str, module: nn.Module) -> None:
+        super().__init__()
+        self.name = name
+        self.module = module
+
+    def __repr__(self) -> str:
+        return f'Operation[{self.name}]'
+
+    def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
+        return self.module(x)
+
+
+def relu_conv_bn(cin: int, cout: int, kernel=1, stride=1, padding=0) -> nn.Sequential:  # type: ignore[no-untyped-def]
+    return nn.Sequential(nn.ReLU(inplace=False),
+                         nn.Conv2d(cin, cout, kernel, stride, padding, bias=False),
+                         nn.BatchNorm2d(cout))
+
+
+class FactorizedReduce(nn.Module):
+    """Stride-2 reduction via two offset 1×1 convs concatenated on channels."""
+
+    def __init__(self, cin: int, cout: int) -> None:
+        super().__init__()
+        self.relu = nn.ReLU(inplace=False)
+        self.pad = nn.ZeroPad2d((0, 1, 0, 1))
+        self.conv1 = nn.Conv2d(cin, cout // 2, kernel_size=1, stride=2, bias=False)
+        self.conv2 = nn.Conv2d(cin, cout // 2, kernel_size=1, stride=2, bias=False)
+        self.bn = nn.BatchNorm2d(cout)
+
+    def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
+        x = self.relu(x)
+        shifted = self.pad(x[:, :, 1:, 1:])
+        return self.bn(torch.cat([self.conv1(x), self.conv2(shifted)], dim=1))
+
+
+def op_none(c: int, stride: int) -> Operation:
+    return Operation('none', nn.Identity() if stride == 1 else FactorizedReduce(c, c))
+
+
+def op_avg_pool_3x3(c: int, stride: int) -> Operation:
+    return Operation('avg_pool_3x3',
+                     nn.AvgPool2d(3, stride=stride, padding=1, count_include_pad=False))
+
+
+def op_max_pool_3x3(c: int, stride: int) -> Operation:
+    # Reference quirk: implemented as an average pool.
+    return Operation('max_pool_3x3',
+                     nn.AvgPool2d(3, stride=stride, padding=1, count_include_pad=False))
+
+
+def op_max_pool_2x2(c: int, stride: int) -> Operation:
+    return Operation('max_pool_2x2', nn.MaxPool2d(2, stride=stride, padding=0))
+
+
+def _bottleneck(c: int, middle: List[nn.Module]) -> nn.Sequential:
+    q = c // 4
+    return nn.Sequential(nn.ReLU(inplace=False), nn.Conv2d(c, q, 1, bias=False), nn.BatchNorm2d(q),
+                         *middle,
+                         nn.ReLU(inplace=False), nn.Conv2d(q, c, 1, bias=False), nn.BatchNorm2d(c))
+
+
+def op_conv_1x7_7x1(c: int, stride: int) -> Operation:
+    q = c // 4
+    middle: List[nn.Module] = [
+        nn.ReLU(inplace=False),
+        nn.Conv2d(q, q, (1, 7), stride=(1, stride), padding=(0, 3), bias=False),
+        nn.BatchNorm2d(q),
+        nn.ReLU(inplace=False),
+        nn.Conv2d(q, q, (7, 1), stride=(stride, 1), padding=(3, 0), bias=False),
+        nn.BatchNorm2d(q),
+    ]
+    return Operation('conv_1x7_7x1', _bottleneck(c, middle))
+
+
+def op_conv_1x1(c: int, stride: int) -> Operation:
+    return Operation('conv_1x1', nn.Sequential(nn.ReLU(inplace=False),
+                                               nn.Conv2d(c, c, 1, stride=stride, bias=False),
+                                               nn.BatchNorm2d(c)))
+
+
+def op_conv_3x3(c: int, stride: int) -> Operation:
+    q = c // 4
+    middle: List[nn.Module] = [nn.ReLU(inplace=False),
+                               nn.Conv2d(q, q, 3, stride=stride, padding=1, bias=False),
+                               nn.BatchNorm2d(q)]
+    return Operation('conv_3x3', _bottleneck(c, middle))
+
+
+OpFactory = Callable[[int, int], Operation]
+
+# AmoebaNet-D genotype: (input state index, operation) pairs, two per node.
+NORMAL_OPERATIONS: List[Tuple[int, OpFactory]] = [
+    (1, op_conv_1x1), (1, op_max_pool_3x3),
+    (1, op_none), (0, op_conv_1x7_7x1),
+    (0, op_conv_1x1), (0, op_conv_1x7_7x1),
+    (2, op_max_pool_3x3), (2, op_none),
+    (1, op_avg_pool_3x3), (5, op_conv_1x1),
+]
+NORMAL_CONCAT = [0, 3, 4, 6]
+
+REDUCTION_OPERATIONS: List[Tuple[int, OpFactory]] = [
+    (0, op_max_pool_2x2), (0, op_max_pool_3x3),
+    (2, op_none), (1, op_conv_3x3),
+    (2, op_conv_1x7_7x1), (2, op_max_pool_3x3),
+    (3, op_none), (1, op_max_pool_2x2),
+    (2, op_avg_pool_3x3), (3, op_conv_1x1),
+]
+REDUCTION_CONCAT = [4, 5, 6]
+
+
+class Classify(nn.Module):
+    def __init__(self, channels_prev: int, num_classes: int) -> None:
+        super().__init__()
+        self.pool = nn.AvgPool2d(7)
+        self.flat = nn.Flatten()
+        self.fc = nn.Linear(channels_prev, num_classes)
+
+    def forward(self, states: Tuple[Tensor, Tensor]) -> Tensor:  # type: ignore[override]
+        x, _ = states
+        return self.fc(self.flat(self.pool(x)))
+
+
+class Stem(nn.Module):
+    def __init__(self, channels: int) -> None:
+        super().__init__()
+        self.relu = nn.ReLU(inplace=False)
+        self.conv = nn.Conv2d(3, channels, 3, stride=2, padding=1, bias=False)
+        self.bn = nn.BatchNorm2d(channels)
+
+    def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
+        return self.bn(self.conv(self.relu(x)))
+
+
+class Cell(nn.Module):
+    def __init__(self, c_prev_prev: int, c_prev: int, c: int, reduction: bool,
+                 reduction_prev: bool) -> None:
+        super().__init__()
+        self.reduce1 = relu_conv_bn(c_prev, c)
+        self.reduce2: nn.Module = nn.Identity()
+        if reduction_prev:
+            self.reduce2 = FactorizedReduce(c_prev_prev, c)
+        elif c_prev_prev != c:
+            self.reduce2 = relu_conv_bn(c_prev_prev, c)
+
+        genotype = REDUCTION_OPERATIONS if reduction else NORMAL_OPERATIONS
+        self.concat = REDUCTION_CONCAT if reduction else NORMAL_CONCAT
+        self.indices = [i for i, _ in genotype]
+        self.operations = nn.ModuleList(
+            factory(c, 2 if reduction and i < 2 else 1) for i, factory in genotype)
+
+    def extra_repr(self) -> str:
+        return f'indices: {self.indices}'
+
+    def forward(self, states: Union[Tensor, Tuple[Tensor, Tensor]]  # type: ignore[override]
+                ) -> Tuple[Tensor, Tensor]:
+        s1, s2 = states if isinstance(states, tuple) else (states, states)
+        skip = s1
+        nodes = [self.reduce1(s1), self.reduce2(s2)]
+        ops = list(self.operations)
+        for k in range(0, len(ops), 2):
+            left = ops[k](nodes[self.indices[k]])
+            right = ops[k + 1](nodes[self.indices[k + 1]])
+            nodes.append(left + right)
+        return torch.cat([nodes[i] for i in self.concat], dim=1), skip
+
+
+def amoebanetd(num_classes: int = 10, num_layers: int = 4, num_filters: int = 512
+               ) -> nn.Sequential:
+    """Build AmoebaNet-D(num_layers, num_filters) as a flat ``nn.Sequential``."""
+    assert num_layers % 3 == 0
+    repeat = num_layers // 3
+    channels = num_filters // 4
+    state = {'pp': channels, 'p': channels, 'c': channels, 'red_prev': False}
+
+    def cells(reduction: bool, scale: int, count: int) -> Iterator[Cell]:
+        state['c'] *= scale
+        for _ in range(count):
+            cell = Cell(state['pp'], state['p'], state['c'], reduction, state['red_prev'])
+            state['pp'] = state['p']
+            state['p'] = state['c'] * len(cell.concat)
+            state['red_prev'] = reduction
+            yield cell
+
+    layers: 'OrderedDict[str, nn.Module]' = OrderedDict()
+    layers['stem1'] = Stem(channels)
+    layers['stem2'] = next(cells(True, 2, 1))
+    layers['stem3'] = next(cells(True, 2, 1))
+    for i, cell in enumerate(cells(False, 1, repeat)):
+        layers[f'cell1_normal{i + 1}'] = cell
+    layers['cell2_reduction'] = next(cells(True, 2, 1))
+    for i, cell in enumerate(cells(False, 1, repeat)):
+        layers[f'cell3_normal{i + 1}'] = cell
+    layers['cell4_reduction'] = next(cells(True, 2, 1))
+    for i, cell in enumerate(cells(False, 1, repeat)):
+        layers[f'cell5_normal{i + 1}'] = cell
+    layers['classify'] = Classify(state['p'], num_classes)
+    return nn.Sequential(layers)

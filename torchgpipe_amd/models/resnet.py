@@ -1,0 +1,99 @@
+"""ResNet-101 as a flat, skippable ``nn.Sequential`` (benchmark model).
+
+Same structure as the reference benchmark model
+(``benchmarks/models/resnet/__init__.py:18-92``, ``bottleneck.py:31-79``):
+each bottleneck becomes a run of flat layers, with the residual carried by a
+``@skippable`` ``Identity`` (stash) / ``Residual`` (pop) pair isolated in a
+per-block namespace.  ResNet-101 = 370 layers, 44.55 M parameters.
+"""
+from collections import OrderedDict
+from typing import Any, Generator, List, Optional
+
+from torch import Tensor, nn
+
+from torchgpipe_amd.models.flatten import flatten_sequential
+from torchgpipe_amd.skip import Namespace, pop, skippable, stash
+
+__all__ = ['resnet101', 'build_resnet']
+
+
+@skippable(stash=['identity'])
+class Identity(nn.Module):
+    def forward(self, x: Tensor) -> Generator:  # type: ignore[override]
+        yield stash('identity', x)
+        return x
+
+
+@skippable(pop=['identity'])
+class Residual(nn.Module):
+    def __init__(self, downsample: Optional[nn.Module] = None) -> None:
+        super().__init__()
+        self.downsample = downsample
+
+    def forward(self, x: Tensor) -> Generator:  # type: ignore[override]
+        identity = yield pop('identity')
+        if self.downsample is not None:
+            identity = self.downsample(identity)
+        return x + identity
+
+
+def bottleneck(inplanes: int, planes: int, stride: int = 1,
+               downsample: Optional[nn.Module] = None, inplace: bool = False) -> nn.Sequential:
+    ns = Namespace()
+    layers: 'OrderedDict[str, nn.Module]' = OrderedDict()
+    layers['identity'] = Identity().isolate(ns)
+    layers['conv1'] = nn.Conv2d(inplanes, planes, 1, bias=False)
+    layers['bn1'] = nn.BatchNorm2d(planes)
+    layers['relu1'] = nn.ReLU(inplace=inplace)
+    layers['conv2'] = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+    layers['bn2'] = nn.BatchNorm2d(planes)
+    layers['relu2'] = nn.ReLU(inplace=inplace)
+    layers['conv3'] = nn.Conv2d(planes, planes * 4, 1, bias=False)
+    layers['bn3'] = nn.BatchNorm2d(planes * 4)
+    layers['residual'] = Residual(downsample).isolate(ns)
+    layers['relu3'] = nn.ReLU(inplace=inplace)
+    return nn.Sequential(layers)
+
+
+def build_resnet(layers: List[int], num_classes: int = 1000, inplace: bool = False
+                 ) -> nn.Sequential:
+    inplanes = 64
+
+    def make_layer(planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
+        nonlocal inplanes
+        downsample = None
+        if stride != 1 or inplanes != planes * 4:
+            downsample = nn.Sequential(nn.Conv2d(inplanes, planes * 4, 1, stride=stride,
+                                                 bias=False),
+                                       nn.BatchNorm2d(planes * 4))
+        seq = [bottleneck(inplanes, planes, stride, downsample, inplace)]
+        inplanes = planes * 4
+        seq += [bottleneck(inplanes, planes, inplace=inplace) for _ in range(1, blocks)]
+        return nn.Sequential(*seq)
+
+    model = nn.Sequential(OrderedDict([
+        ('conv1', nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)),
+        ('bn1', nn.BatchNorm2d(64)),
+        ('relu', nn.ReLU()),
+        ('maxpool', nn.MaxPool2d(kernel_size=3, stride=2, padding=1)),
+        ('layer1', make_layer(64, layers[0])),
+        ('layer2', make_layer(128, layers[1], stride=2)),
+        ('layer3', make_layer(256, layers[2], stride=2)),
+        ('layer4', make_layer(512, layers[3], stride=2)),
+        ('avgpool', nn.AdaptiveAvgPool2d((1, 1))),
+        ('flat', nn.Flatten()),
+        ('fc', nn.Linear(512 * 4, num_classes)),
+    ]))
+    model = flatten_sequential(model)
+
+    for m in model.modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode='fan_out', nonlinearity='relu')
+        elif isinstance(m, nn.BatchNorm2d):
+            nn.init.constant_(m.weight, 1)
+            nn.init.constant_(m.bias, 0)
+    return model
+
+
+def resnet101(**kwargs: Any) -> nn.Sequential:
+    return build_resnet([3, 4, 23, 3], **kwargs)
