@@ -1,0 +1,214 @@
+#!/usr/bin/env python
+"""Headline benchmark: U-Net(5,64) (or AmoebaNet-D(18,256)) GPipe training throughput.
+
+Metric (BASELINE.json): samples/sec of a full SGD training step (forward,
+backward with checkpoint recomputation, optimizer step) of U-Net(5,64) on
+3×192×192 synthetic images at 1/2/4/8 pipeline partitions, using the
+reference's experiment tables (``benchmarks/unet-speed/main.py:23-68``):
+
+    N=1  pipeline-1  B=80,  chunks=2,  balance [241]
+    N=2  pipeline-2  B=512, chunks=32, balance [104, 137]
+    N=4  pipeline-4  B=512, chunks=16, balance [30, 66, 84, 61]
+    N=8  pipeline-8  B=640, chunks=40, balance [16, 27, 31, 44, 22, 57, 27, 17]
+
+One process per GPU (``torch.distributed.run``), RCCL point-to-point between
+stages; fp32 like the reference.  Rank 0 prints one JSON line.
+
+    python bench.py --gpus 1 --steps 5 --warmup 2
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+        bench.py --gpus 8
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+# Reference (Tesla P40) throughputs of the same experiments, BASELINE.md §1/§2.
+UNET_EXPERIMENTS = {
+    1: dict(name='pipeline-1', batch=80, chunks=2, balance=[241], ref=24.456),
+    2: dict(name='pipeline-2', batch=512, chunks=32, balance=[104, 137], ref=35.502),
+    4: dict(name='pipeline-4', batch=512, chunks=16, balance=[30, 66, 84, 61], ref=67.042),
+    8: dict(name='pipeline-8', batch=640, chunks=40,
+            balance=[16, 27, 31, 44, 22, 57, 27, 17], ref=88.497),
+}
+AMOEBA_EXPERIMENTS = {
+    2: dict(name='n2m32', batch=1280, chunks=32, balance=[9, 15], ref=47.386),
+    4: dict(name='n4m32', batch=1152, chunks=32, balance=[3, 6, 7, 8], ref=72.412),
+    8: dict(name='n8m32', batch=1280, chunks=32, balance=[2, 2, 2, 3, 3, 4, 4, 4], ref=132.413),
+    1: dict(name='n1m32', batch=640, chunks=32, balance=[24], ref=None),
+}
+
+
+def parse() -> argparse.Namespace:
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
+    p.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
+    p.add_argument('--steps', type=int, default=5)
+    p.add_argument('--warmup', type=int, default=2)
+    p.add_argument('--model', choices=['unet', 'amoebanet'], default='unet')
+    p.add_argument('--checkpoint', choices=['always', 'except_last', 'never'], default=None,
+                   help='override the experiment checkpoint mode (default: reference mode)')
+    p.add_argument('--batch', type=int, default=None, help='override the global batch')
+    p.add_argument('--chunks', type=int, default=None, help='override the micro-batch count')
+    p.add_argument('--unfused', action='store_true', help='use the unfused PyTorch U-Net cells')
+    p.add_argument('--cudnn-benchmark', action='store_true',
+                   help='MIOpen exhaustive find (slow first step, cached afterwards)')
+    p.add_argument('--profile-steps', type=int, default=0,
+                   help='after timing, run N more steps under torch.profiler (rank 0)')
+    return p.parse_args()
+
+
+def even_balance(layers: int, parts: int) -> list:
+    base, extra = divmod(layers, parts)
+    return [base + (1 if i < extra else 0) for i in range(parts)]
+
+
+def main() -> None:
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU')
+
+    gpu = torch.cuda.is_available()
+    device = torch.device('cuda', local_rank) if gpu else torch.device('cpu')
+    if gpu:
+        torch.cuda.set_device(device)
+        torch.backends.cudnn.benchmark = args.cudnn_benchmark
+    if world > 1:
+        dist.init_process_group('nccl' if gpu else 'gloo', rank=rank, world_size=world,
+                                device_id=device if gpu else None)
+
+    from torchgpipe_amd.models import amoebanetd, unet
+    from torchgpipe_amd.parallel import PipelineStage
+
+    table = UNET_EXPERIMENTS if args.model == 'unet' else AMOEBA_EXPERIMENTS
+    if args.model == 'unet':
+        exp = dict(table.get(world) or dict(name=f'pipeline-{world}', batch=80 * world,
+                                            chunks=4 * world, balance=even_balance(241, world),
+                                            ref=None))
+        model = unet(depth=5, num_convs=5, base_channels=64, input_channels=3,
+                     output_channels=1, fused=not args.unfused)
+        in_shape = (3, 192, 192)
+        checkpoint = 'except_last'
+        model_name = 'U-Net(5,64)'
+    else:
+        exp = dict(table.get(world) or dict(name=f'n{world}m32', batch=160 * world, chunks=32,
+                                            balance=even_balance(24, world), ref=None))
+        model = amoebanetd(num_classes=1000, num_layers=18, num_filters=256)
+        in_shape = (3, 224, 224)
+        checkpoint = 'except_last' if exp['chunks'] > 1 else 'always'
+        model_name = 'AmoebaNet-D(18,256)'
+    if args.checkpoint:
+        checkpoint = args.checkpoint
+    if args.batch:
+        exp['batch'] = args.batch
+    if args.chunks:
+        exp['chunks'] = args.chunks
+    batch, chunks, balance = exp['batch'], exp['chunks'], exp['balance']
+
+    stage = PipelineStage(model, balance, device=device, chunks=chunks, checkpoint=checkpoint)
+    del model
+    optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
+
+    gen = torch.Generator(device=device).manual_seed(0)
+    x = torch.rand(batch, *in_shape, device=device, generator=gen) if stage.is_first else None
+    if args.model == 'unet':
+        target = torch.ones(batch, 1, 192, 192, device=device) if stage.is_last else None
+        loss_fn = F.binary_cross_entropy_with_logits
+    else:
+        target = (torch.randint(1000, (batch,), device=device, generator=gen)
+                  if stage.is_last else None)
+        loss_fn = F.cross_entropy
+    from torchgpipe_amd.parallel.stage import signature_of
+    signature = signature_of(torch.empty(batch, *in_shape, device='meta'))
+
+    def step() -> None:
+        stage.train_step(x, target, loss_fn, signature=signature)
+        optimizer.step()
+        optimizer.zero_grad(set_to_none=True)
+
+    def sync() -> None:
+        if world > 1:
+            dist.barrier()
+        if gpu:
+            torch.cuda.synchronize(device)
+
+    t0 = time.time()
+    for k in range(args.warmup):
+        step()
+        sync()
+        if rank == 0:
+            print(f'[bench] warmup step {k + 1}/{args.warmup} done at {time.time() - t0:.1f}s',
+                  file=sys.stderr, flush=True)
+    warm_s = time.time() - t0
+
+    sync()
+    start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - start
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if args.profile_steps and rank == 0:
+        from torch.profiler import ProfilerActivity, profile
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if gpu else [])
+        with profile(activities=acts) as prof:
+            for _ in range(args.profile_steps):
+                step()
+            sync()
+        print(prof.key_averages().table(sort_by='cuda_time_total' if gpu else 'cpu_time_total',
+                                        row_limit=30), file=sys.stderr)
+
+    samples_per_s = batch * args.steps / elapsed
+    if rank == 0:
+        ref = exp.get('ref')
+        mem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if gpu else 0.0
+        print(json.dumps({
+            'metric': f'{model_name} GPipe training throughput (samples/sec)',
+            'value': round(samples_per_s, 3),
+            'unit': 'samples/sec',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(1000 * elapsed / args.steps, 3),
+            'higher_is_better': True,
+            'scaling': 'strong',
+            'vs_baseline': round(samples_per_s / ref, 3) if ref else None,
+            'dtype': 'fp32',
+            'data': 'synthetic (torch.rand inputs, constant targets), random-init weights',
+            'config': {
+                'model': model_name,
+                'experiment': exp['name'],
+                'global_batch': batch,
+                'seq_len': None,
+                'input': 'x'.join(map(str, in_shape)),
+                'chunks': chunks,
+                'balance': balance,
+                'checkpoint': checkpoint,
+                'parallelism': f'pp{world}',
+                'fused_cells': args.model == 'unet' and not args.unfused,
+                'baseline_samples_per_sec_p40': ref,
+                'rank0_peak_mem_gib': round(mem, 2),
+                'warmup_s': round(warm_s, 1),
+            },
+        }), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

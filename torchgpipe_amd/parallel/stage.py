@@ -1,0 +1,479 @@
+"""Multi-process GPipe: one process per GPU, RCCL point-to-point between stages.
+
+This is the MI355X-native counterpart of the reference's ``DistributedGPipe``
+(``torchgpipe/distributed/gpipe.py:75-194``), re-designed around
+``torch.distributed`` (RCCL over xGMI) instead of RPC with CPU staging, and
+without its feature gaps: activation checkpointing with *pre-gradient*
+recomputation, deferred BatchNorm and ``@skippable`` long skips all work
+across processes.
+
+Per rank ``j`` (owning partition ``j``), one training step is the GPipe
+fill-drain schedule over ``m`` micro-batches::
+
+    forward  i = 0 .. m-1:   recv act(i) from j-1, recv skips(i) from their stash ranks
+                             run partition (checkpointed if i < checkpoint_stop)
+                             isend act(i) to j+1, isend skips(i) to their pop ranks
+    backward i = m-1 .. 0:   post recv grad(i) from j+1 and from the skip pop ranks
+                             recompute(i) if checkpointed      ← overlaps the transfer
+                             wait; autograd.backward(outputs(i), grads(i))
+                             isend input grads to j-1 and to the skip stash ranks
+
+Skip tensors travel directly from the stash rank to the pop rank (one xGMI
+hop on the fully connected MI355X mesh), exactly like ``PortalCopy`` in the
+single-process engine.
+
+Every cell is a function ``flat_inputs → flat_outputs`` where ``flat_inputs``
+= activation tensors + skips popped from other ranks and ``flat_outputs`` =
+output tensors + skips stashed for other ranks, so checkpointing
+(``Checkpointing``) treats cross-rank skips like any other input/output.
+"""
+from collections import OrderedDict
+from typing import Any, Callable, Dict, Hashable, List, Optional, Sequence, Tuple, Union
+
+import torch
+import torch.distributed as dist
+from torch import Tensor, nn
+
+from torchgpipe_amd import microbatch
+from torchgpipe_amd.batchnorm import DeferredBatchNorm, set_micro_batches
+from torchgpipe_amd.checkpoint import Checkpointing
+from torchgpipe_amd.gpipe import check_balance, partition_layers, verify_module
+from torchgpipe_amd.microbatch import Batch
+from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P
+from torchgpipe_amd.skip.layout import SkipLayout, inspect_skip_layout
+from torchgpipe_amd.skip.namespace import Namespace
+from torchgpipe_amd.skip.skippable import Skippable, verify_skippables
+from torchgpipe_amd.skip.tracker import SkipTracker, use_skip_tracker
+from torchgpipe_amd.utils import trace
+
+__all__ = ['PipelineStage', 'signature_of']
+
+Tensors = Tuple[Tensor, ...]
+TensorOrTensors = Union[Tensor, Tensors]
+Key = Tuple[Namespace, str]
+Signature = Tuple[Any, ...]
+
+
+def signature_of(input: TensorOrTensors) -> Signature:
+    """Hashable description of a mini-batch: shape and dtype code of each tensor."""
+    tensors = (input,) if isinstance(input, Tensor) else tuple(input)
+    return tuple((tuple(t.shape), _DTYPE_CODE[t.dtype]) for t in tensors)
+
+
+def _encode_signature(sig: Signature) -> Tensor:
+    words: List[int] = [len(sig)]
+    for shape, code in sig:
+        words += [len(shape), *shape, code]
+    out = torch.zeros(128, dtype=torch.int64)
+    out[:len(words)] = torch.tensor(words, dtype=torch.int64)
+    return out
+
+
+def _decode_signature(payload: Tensor) -> Signature:
+    words = payload.tolist()
+    count, pos = words[0], 1
+    sig = []
+    for _ in range(count):
+        ndim = words[pos]
+        shape = tuple(words[pos + 1:pos + 1 + ndim])
+        sig.append((shape, words[pos + 1 + ndim]))
+        pos += 2 + ndim
+    return tuple(sig)
+
+
+def _micro_batch_count(sig: Signature, chunks: int) -> int:
+    batch = sig[0][0][0] if sig and sig[0][0] else 1
+    return len(torch.empty(batch, 0).chunk(chunks)) if batch > 0 else 0
+
+
+class _RemoteSkipTracker(SkipTracker):
+    """Skip tracker of one cell: local skips in a dict, cross-rank ones captured."""
+
+    def __init__(self, layout: SkipLayout, rank: int, popped: Dict[Key, Tensor]) -> None:
+        super().__init__()
+        self.layout = layout
+        self.rank = rank
+        self.popped = popped
+        self.stashed: Dict[Key, Optional[Tensor]] = {}
+
+    def save(self, batch: Batch, ns: Namespace, name: str, tensor: Optional[Tensor]) -> None:
+        src, dst = self.layout.route(ns, name)
+        if dst != self.rank:
+            self.stashed[(ns, name)] = tensor
+        else:
+            super().save(batch, ns, name, tensor)
+
+    def load(self, batch: Batch, ns: Namespace, name: str) -> Optional[Tensor]:
+        src, dst = self.layout.route(ns, name)
+        if src != self.rank:
+            return self.popped.pop((ns, name))
+        return super().load(batch, ns, name)
+
+
+class _Cell:
+    """Bookkeeping of one micro-batch on this rank."""
+
+    __slots__ = ('index', 'inputs', 'outputs', 'out_atomic', 'chk', 'n_act_out')
+
+    def __init__(self, index: int) -> None:
+        self.index = index
+        self.inputs: List[Tensor] = []      # leaves: activations + popped remote skips
+        self.outputs: List[Tensor] = []     # outputs + stashed remote skips
+        self.out_atomic = True
+        self.chk: Optional[Checkpointing] = None
+        self.n_act_out = 0
+
+
+class PipelineStage:
+    """One pipeline stage of a multi-process GPipe (this rank's partition).
+
+    Args:
+        module: the *whole* ``nn.Sequential`` (it may live on the ``meta``
+            device; only this rank's layers are materialised).
+        balance: layers per partition; ``len(balance)`` = pipeline depth.
+        rank: this rank's stage index (default: rank in ``group``).
+        device: device of this stage (default: ``cuda:LOCAL_RANK`` or CPU).
+        chunks: number of micro-batches.
+        checkpoint: ``'always'``, ``'except_last'`` or ``'never'``.
+        group: process group of the pipeline (default: WORLD); its size must
+            equal ``len(balance)``.
+        ctrl_group: ``gloo`` group for shape metadata (default: WORLD if it is
+            gloo, otherwise a new gloo group over the same ranks).
+        deferred_batch_norm: convert BatchNorm layers to DeferredBatchNorm.
+        pack: pack multi-tensor messages into one transfer (HIP kernel).
+    """
+
+    def __init__(self, module: nn.Sequential, balance: Sequence[int], *,
+                 rank: Optional[int] = None, device: Optional[torch.device] = None,
+                 chunks: int = 1, checkpoint: str = 'except_last',
+                 group: Optional[dist.ProcessGroup] = None,
+                 ctrl_group: Optional[dist.ProcessGroup] = None,
+                 deferred_batch_norm: bool = False, pack: bool = True,
+                 materialize: Optional[Callable[[nn.Module], None]] = None) -> None:
+        if chunks <= 0:
+            raise ValueError('number of chunks must be positive integer')
+        if checkpoint not in ('always', 'except_last', 'never'):
+            raise ValueError("checkpoint is not one of 'always', 'except_last', or 'never'")
+        verify_module(module)
+        verify_skippables(module)
+        balance = list(balance)
+        check_balance(module, balance)
+
+        self.group = group
+        distributed = dist.is_available() and dist.is_initialized()
+        if not distributed and len(balance) != 1:
+            raise RuntimeError('a multi-stage pipeline needs torch.distributed to be initialized')
+        self.world = dist.get_world_size(group) if distributed else 1
+        self.rank = (dist.get_rank(group) if distributed else 0) if rank is None else rank
+        if self.world != len(balance):
+            raise ValueError(f'pipeline group has {self.world} ranks but balance has '
+                             f'{len(balance)} partitions')
+        self.ranks = [dist.get_global_rank(group, r) if group is not None else r
+                      for r in range(self.world)]
+        self.n = len(balance)
+        self.balance = balance
+        self.chunks = chunks
+        self.checkpoint = checkpoint
+        self.training = True
+
+        if device is None:
+            device = torch.device('cpu')
+        self.device = device
+
+        groups = partition_layers(module, balance)
+        parts = [nn.Sequential(g) for g in groups]
+        self.layout = inspect_skip_layout(parts)
+        partition = parts[self.rank]
+        if deferred_batch_norm:
+            partition = DeferredBatchNorm.convert_deferred_batch_norm(partition, chunks)
+        if materialize is not None:
+            materialize(partition)
+        self.partition = partition.to(device)
+        self._has_dbn = any(isinstance(m, DeferredBatchNorm) for m in partition.modules())
+
+        # Cross-rank skip routes touching this rank, in a canonical order that every
+        # rank derives identically: (peer, global index of the stash layer, name).
+        # Namespaces are random UUIDs that differ between processes, so they
+        # must never decide the order.
+        stash_index: Dict[Key, int] = {}
+        for idx, layer in enumerate(module.children()):
+            if isinstance(layer, Skippable):
+                for key in layer.stashable():
+                    stash_index[key] = idx
+        self.in_skips: List[Tuple[int, Key]] = sorted(
+            ((src, (ns, name)) for src, ns, name in self.layout.copy_policy(self.rank)),
+            key=lambda r: (r[0], stash_index[r[1]], r[1][1]))
+        self.out_skips: List[Tuple[int, Key]] = sorted(
+            ((dst, (ns, name)) for dst, ns, name in self.layout.send_policy(self.rank)),
+            key=lambda r: (r[0], stash_index[r[1]], r[1][1]))
+
+        if ctrl_group is None and distributed:
+            if dist.get_backend(group) == 'gloo':
+                ctrl_group = group
+            else:
+                ctrl_group = dist.new_group(ranks=self.ranks, backend='gloo')
+        self.ctrl_group = ctrl_group
+        self.p2p = P2P(device, group=group, ctrl_group=ctrl_group, pack=pack)
+
+        self._cells: List[_Cell] = []
+        self._sig: Optional[Signature] = None
+        self._m = 0
+
+    # -- module-like helpers ----------------------------------------------------------------
+
+    def parameters(self):  # type: ignore[no-untyped-def]
+        return self.partition.parameters()
+
+    def train(self, mode: bool = True) -> 'PipelineStage':
+        self.training = mode
+        self.partition.train(mode)
+        return self
+
+    def eval(self) -> 'PipelineStage':
+        return self.train(False)
+
+    @property
+    def is_first(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def is_last(self) -> bool:
+        return self.rank == self.n - 1
+
+    def checkpoint_stop(self, m: int) -> int:
+        if not (self.training and torch.is_grad_enabled()):
+            return 0
+        return {'always': m, 'except_last': m - 1, 'never': 0}[self.checkpoint]
+
+    # -- signature --------------------------------------------------------------------------
+
+    def _agree_signature(self, input: Optional[TensorOrTensors],
+                         signature: Optional[Signature]) -> Signature:
+        """Every rank needs the step's input signature (micro-batch count, meta keys).
+
+        Rank 0 ships it to the others over the gloo control group (non-blocking
+        sends, so rank 0 never waits for a rank still busy with the previous
+        step).  Callers that know the signature on every rank pass it in and
+        skip this exchange.
+        """
+        if signature is not None:
+            return signature
+        if self.is_first:
+            if input is None:
+                raise ValueError('the first stage needs the input mini-batch')
+            sig = signature_of(input)
+            payload = _encode_signature(sig)
+            for r in range(1, self.n):
+                self.p2p.send_control(payload, self.ranks[r])
+            return sig
+        payload = torch.zeros(128, dtype=torch.int64)
+        self.p2p.recv_control(payload, self.ranks[0])
+        return _decode_signature(payload)
+
+    def _key(self, kind: str, i: int, peer: int) -> Hashable:
+        return (self._sig, self.training, torch.is_grad_enabled(), kind, i, peer)
+
+    # -- forward ----------------------------------------------------------------------------
+
+    def _make_fn(self, cell: _Cell, n_act: int, in_atomic: bool
+                 ) -> Callable[[Tensors], Tensors]:
+        in_keys = [key for _, key in self.in_skips]
+        out_keys = [key for _, key in self.out_skips]
+        partition = self.partition
+        label = f'fwd mb{cell.index} stage{self.rank}'
+
+        def fn(flat: Tensors) -> Tensors:
+            acts = flat[:n_act]
+            popped = dict(zip(in_keys, flat[n_act:]))
+            tracker = _RemoteSkipTracker(self.layout, self.rank, popped)
+            with use_skip_tracker(tracker), trace.range(label):
+                out = partition(acts[0] if in_atomic else tuple(acts))
+            batch = Batch(out)
+            cell.out_atomic = batch.atomic
+            cell.n_act_out = len(batch)
+            stashed = []
+            for key in out_keys:
+                t = tracker.stashed.get(key)
+                if t is None:
+                    raise RuntimeError(f"skip '{key[1]}' was not stashed")
+                stashed.append(t)
+            return tuple(batch) + tuple(stashed)
+
+        return fn
+
+    def forward(self, input: Optional[TensorOrTensors] = None, *,
+                signature: Optional[Signature] = None) -> List[TensorOrTensors]:
+        """Run the forward pass of every micro-batch on this stage.
+
+        The first stage passes the mini-batch; the others pass ``None``.
+        Returns the per-micro-batch outputs (meaningful on the last stage).
+        """
+        if input is not None:
+            microbatch.check(input)
+        sig = self._agree_signature(input, signature)
+        if sig != self._sig:
+            self._sig = sig
+        m = _micro_batch_count(sig, self.chunks)
+        self._m = m
+        if self._has_dbn:
+            set_micro_batches(self.partition, m)
+        stop = self.checkpoint_stop(m)
+
+        batches: Optional[List[Batch]] = None
+        if self.is_first:
+            assert input is not None
+            batches = microbatch.scatter(input, self.chunks)
+
+        prev = self.ranks[self.rank - 1] if self.rank > 0 else None
+        nxt = self.ranks[self.rank + 1] if not self.is_last else None
+        self._cells = []
+        outputs: List[TensorOrTensors] = []
+
+        for i in range(m):
+            cell = _Cell(i)
+            # 1. inputs: activations + cross-rank skips (posted before waiting on any)
+            if self.is_first:
+                assert batches is not None
+                b = batches[i]
+                acts = [t.to(self.device, non_blocking=True) for t in b]
+                in_atomic = b.atomic
+                act_msg = None
+            else:
+                act_msg = self.p2p.recv(prev, self._key('act', i, prev))  # type: ignore[arg-type]
+                in_atomic = True
+            skip_msgs = [(self.p2p.recv(self.ranks[src], self._key('skip', i, self.ranks[src])))
+                         for src in sorted({s for s, _ in self.in_skips})]
+            if act_msg is not None:
+                acts = act_msg.wait()
+                in_atomic = act_msg.atomic
+            popped: List[Tensor] = []
+            for msg in skip_msgs:
+                popped += msg.wait()
+            flat = list(acts) + popped
+            cell.inputs = flat
+
+            # 2. compute
+            fn = self._make_fn(cell, len(acts), in_atomic)
+            if i < stop:
+                cell.chk = Checkpointing(fn, Batch(tuple(flat)))
+                out = list(cell.chk.checkpoint())
+            else:
+                out = list(fn(tuple(flat)))
+            cell.outputs = out
+            self._cells.append(cell)
+
+            # 3. outputs: activation to the next stage, skips to their pop ranks
+            act_out = out[:cell.n_act_out]
+            if nxt is not None:
+                self.p2p.send(act_out, nxt, self._key('act', i, self.ranks[self.rank]),
+                              atomic=cell.out_atomic)
+            by_dst: Dict[int, List[Tensor]] = OrderedDict()
+            for (dst, _), t in zip(self.out_skips, out[cell.n_act_out:]):
+                by_dst.setdefault(dst, []).append(t)
+            for dst in sorted(by_dst):
+                self.p2p.send(by_dst[dst], self.ranks[dst],
+                              self._key('skip', i, self.ranks[self.rank]))
+            outputs.append(act_out[0] if cell.out_atomic else tuple(act_out))
+        return outputs
+
+    # -- backward ---------------------------------------------------------------------------
+
+    def backward(self, losses: Optional[Sequence[Tensor]] = None) -> None:
+        """Back-propagate every micro-batch (reverse order) and ship input gradients.
+
+        The last stage passes one scalar loss per micro-batch; the others pass
+        ``None``.
+        """
+        if self.is_last and losses is None:
+            raise ValueError('the last stage must pass the per-micro-batch losses')
+        nxt = self.ranks[self.rank + 1] if not self.is_last else None
+        prev = self.ranks[self.rank - 1] if self.rank > 0 else None
+        me = self.ranks[self.rank]
+
+        for cell in reversed(self._cells):
+            i = cell.index
+            # 1. post the gradient receives first ...
+            grad_msg = None
+            if nxt is not None and any(t.requires_grad for t in cell.outputs[:cell.n_act_out]):
+                grad_msg = self.p2p.recv(nxt, self._key('gact', i, nxt))
+            skip_grad_msgs = []
+            for dst in sorted({d for d, _ in self.out_skips}):
+                skip_grad_msgs.append(
+                    (dst, self.p2p.recv(self.ranks[dst], self._key('gskip', i, self.ranks[dst]))))
+            # 2. ... then recompute while they are in flight
+            if cell.chk is not None:
+                with trace.range(f'recompute mb{i} stage{self.rank}'):
+                    cell.chk.recompute_now()
+
+            # 3. backward through this cell
+            tensors: List[Tensor] = []
+            grads: List[Tensor] = []
+            act_out = cell.outputs[:cell.n_act_out]
+            if self.is_last:
+                assert losses is not None
+                tensors.append(losses[i])
+                grads.append(torch.ones_like(losses[i]))
+            elif grad_msg is not None:
+                received = iter(grad_msg.wait())
+                for t in act_out:
+                    if t.requires_grad:
+                        tensors.append(t)
+                        grads.append(next(received))
+            skip_out = cell.outputs[cell.n_act_out:]
+            dst_of = [d for d, _ in self.out_skips]
+            for dst, msg in skip_grad_msgs:
+                received = iter(msg.wait())
+                for d, t in zip(dst_of, skip_out):
+                    if d == dst:
+                        g = next(received)
+                        if t.requires_grad:
+                            tensors.append(t)
+                            grads.append(g)
+            with trace.range(f'bwd mb{i} stage{self.rank}'):
+                if tensors:
+                    torch.autograd.backward(tensors, grads)
+
+            # 4. ship input gradients upstream
+            n_in_act = len(cell.inputs) - len(self.in_skips)
+            if prev is not None:
+                gin = [self._grad_of(t) for t in cell.inputs[:n_in_act] if t.requires_grad]
+                self.p2p.send(gin, prev, self._key('gact', i, me))
+            skip_in = cell.inputs[n_in_act:]
+            by_src: Dict[int, List[Tensor]] = {}
+            for (src, _), t in zip(self.in_skips, skip_in):
+                by_src.setdefault(src, []).append(self._grad_of(t))
+            for src in sorted(by_src):
+                self.p2p.send(by_src[src], self.ranks[src], self._key('gskip', i, me))
+            cell.inputs = []
+            cell.outputs = []
+            cell.chk = None
+        self._cells = []
+        self.p2p.flush()
+
+    @staticmethod
+    def _grad_of(t: Tensor) -> Tensor:
+        return t.grad if t.grad is not None else torch.zeros_like(t)
+
+    # -- convenience ------------------------------------------------------------------------
+
+    def train_step(self, input: Optional[TensorOrTensors], target: Optional[Tensor],
+                   loss_fn: Callable[[Tensor, Tensor], Tensor], *,
+                   signature: Optional[Signature] = None) -> Optional[Tensor]:
+        """Forward + backward of one mini-batch; returns the mean loss on the last stage.
+
+        ``loss_fn(output, target)`` must be a mean-reduced loss; per-micro-batch
+        losses are weighted by micro-batch size so the gradient equals the
+        full-batch gradient of the reference (loss on the gathered output).
+        """
+        outputs = self.forward(input, signature=signature)
+        if not self.is_last:
+            self.backward(None)
+            return None
+        assert target is not None
+        targets = target.chunk(self.chunks)
+        total = float(target.size(0))
+        losses = [loss_fn(out, tgt) * (tgt.size(0) / total)  # type: ignore[arg-type]
+                  for out, tgt in zip(outputs, targets)]
+        self.backward(losses)
+        with torch.no_grad():
+            return torch.stack([l.detach() for l in losses]).sum()
