@@ -1,0 +1,162 @@
+"""Multi-process pipeline (PipelineStage / DistributedGPipe) on gloo CPU ranks.
+
+The same code path runs over RCCL on MI355X; here every rank is a CPU process.
+"""
+import copy
+
+import pytest
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from tests.distributed.mp_util import run
+from torchgpipe_amd.skip import Namespace, pop, skippable, stash
+
+
+@skippable(stash=['skip'])
+class Stash(nn.Module):
+    def forward(self, x):
+        yield stash('skip', x)
+        return x
+
+
+@skippable(pop=['skip'])
+class PopAdd(nn.Module):
+    def forward(self, x):
+        s = yield pop('skip')
+        return x + s
+
+
+class Split(nn.Module):
+    def forward(self, x):
+        return x, x * 0.5
+
+
+class Merge(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc = nn.Linear(8, 8)
+
+    def forward(self, xy):
+        x, y = xy
+        return self.fc(x) + y
+
+
+def build(dropout=0.0):
+    torch.manual_seed(1234)
+    ns = Namespace()
+    return nn.Sequential(
+        nn.Linear(4, 8), Stash().isolate(ns), nn.Tanh(),       # 0-2
+        nn.Linear(8, 8), Split(),                               # 3-4  (tuple boundary)
+        Merge(), nn.Dropout(dropout),                           # 5-6
+        PopAdd().isolate(ns), nn.Linear(8, 2))                  # 7-8
+
+
+BALANCE = [3, 2, 4]
+X = torch.randn(12, 4, generator=torch.Generator().manual_seed(5))
+T = torch.randn(12, 2, generator=torch.Generator().manual_seed(6))
+
+
+def reference_grads():
+    model = build()
+    loss = F.mse_loss(model(X), T)
+    loss.backward()
+    grads = [p.grad.clone() for p in model.parameters()]
+    return grads, loss.item()
+
+
+def _stage_worker(rank, world, checkpoint, chunks, links, dropout):
+    from torchgpipe_amd.parallel import PipelineStage
+    stage = PipelineStage(build(dropout), BALANCE, chunks=chunks, checkpoint=checkpoint,
+                          links=links)
+    torch.manual_seed(100 + rank)
+    loss = stage.train_step(X if rank == 0 else None, T if rank == world - 1 else None,
+                            F.mse_loss)
+    return {'grads': [p.grad.clone() for p in stage.parameters()],
+            'loss': None if loss is None else loss.item(),
+            'in_skips': len(stage.in_skips), 'out_skips': len(stage.out_skips)}
+
+
+@pytest.mark.parametrize('checkpoint', ['always', 'except_last', 'never'])
+def test_stage_gradients_match_single_process(tmp_path, checkpoint):
+    results = run(_stage_worker, 3, tmp_path, checkpoint, 4, None, 0.0)
+    grads, loss = reference_grads()
+    got = [g for r in results for g in r['grads']]
+    assert len(got) == len(grads)
+    for a, b in zip(got, grads):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    assert abs(results[-1]['loss'] - loss) < 1e-6
+    # rank 0 stashes for rank 2; rank 2 pops it
+    assert results[0]['out_skips'] == 1 and results[2]['in_skips'] == 1
+
+
+def test_stage_with_dedicated_link_groups(tmp_path):
+    results = run(_stage_worker, 3, tmp_path, 'except_last', 3, True, 0.0)
+    grads, _ = reference_grads()
+    for a, b in zip([g for r in results for g in r['grads']], grads):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_stage_dropout_recompute_replays_rng(tmp_path):
+    never = run(_stage_worker, 3, tmp_path / 'never', 'never', 4, None, 0.5)
+    always = run(_stage_worker, 3, tmp_path / 'always', 'always', 4, None, 0.5)
+    for rn, ra in zip(never, always):
+        for a, b in zip(rn['grads'], ra['grads']):
+            torch.testing.assert_close(a, b)
+
+
+def _api_worker(rank, world):
+    from torchgpipe_amd.distributed import DistributedGPipe
+    workers = {r: f'worker{r}' for r in range(world)}
+    model = DistributedGPipe(build(), rank, workers, BALANCE, 4)
+    outputs = model.forward(X if rank == 0 else None)
+    if rank == world - 1:
+        losses = [F.mse_loss(o, t) * (len(t) / len(T)) for o, t in zip(outputs, T.chunk(4))]
+        model.backward(losses)
+    else:
+        model.backward(None)
+    return [p.grad.clone() for p in model.parameters()]
+
+
+def test_distributed_gpipe_api(tmp_path):
+    results = run(_api_worker, 3, tmp_path)
+    grads, _ = reference_grads()
+    for a, b in zip([g for r in results for g in r], grads):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def _loader_worker(rank, world):
+    from torchgpipe_amd.distributed import DistributedGPipeDataLoader
+    data = [(torch.full((2, 3), float(i)), torch.full((2,), float(i) + 0.5)) for i in range(3)]
+    loader = DistributedGPipeDataLoader(data if rank == 0 else None, rank, chunks=2,
+                                        num_iterations=3, last_stage=rank == world - 1,
+                                        last_stage_name=f'worker{world - 1}')
+    out = []
+    for x, t in loader:
+        out.append((None if x is None else x.clone(), None if t is None else t.clone()))
+    return out
+
+
+def test_data_loader_ships_targets_to_last_stage(tmp_path):
+    results = run(_loader_worker, 3, tmp_path)
+    assert [x[0, 0].item() for x, t in results[0]] == [0.0, 1.0, 2.0]
+    assert all(t is None for _, t in results[0])
+    assert all(x is None and t is None for x, t in results[1])
+    assert [t[0].item() for x, t in results[2]] == [0.5, 1.5, 2.5]
+
+
+def _eval_worker(rank, world):
+    from torchgpipe_amd.parallel import PipelineStage
+    stage = PipelineStage(build(), BALANCE, chunks=3)
+    stage.eval()
+    with torch.no_grad():
+        outs = stage.forward(X if rank == 0 else None)
+    return outs
+
+
+def test_eval_forward_matches_plain_model(tmp_path):
+    results = run(_eval_worker, 3, tmp_path)
+    model = build().eval()
+    with torch.no_grad():
+        want = model(X)
+    torch.testing.assert_close(torch.cat(results[-1]), want)

@@ -1,0 +1,125 @@
+import copy
+
+import pytest
+import torch
+from torch import nn
+
+from torchgpipe_amd import GPipe
+from torchgpipe_amd.skip import Namespace, pop, skippable, stash
+
+
+@skippable(stash=['1to3'])
+class Layer1(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc = nn.Linear(4, 4)
+
+    def forward(self, x):
+        yield stash('1to3', x)
+        return self.fc(x)
+
+
+class Layer2(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc = nn.Linear(4, 4)
+
+    def forward(self, x):
+        return torch.tanh(self.fc(x))
+
+
+@skippable(pop=['1to3'])
+class Layer3(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc = nn.Linear(4, 4)
+
+    def forward(self, x):
+        skip = yield pop('1to3')
+        return self.fc(x) + skip
+
+
+@pytest.mark.parametrize('balance', [[3], [1, 2], [2, 1], [1, 1, 1]])
+@pytest.mark.parametrize('checkpoint', ['always', 'except_last', 'never'])
+def test_1to3_matches_plain_sequential(balance, checkpoint):
+    torch.manual_seed(0)
+    plain = nn.Sequential(Layer1(), Layer2(), Layer3())
+    piped = GPipe(copy.deepcopy(plain), balance, devices=['cpu'] * len(balance), chunks=3,
+                  checkpoint=checkpoint)
+    x = torch.rand(6, 4, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_()
+    y = plain(x)
+    y2 = piped(x2)
+    torch.testing.assert_close(y, y2)
+    y.norm().backward()
+    y2.norm().backward()
+    torch.testing.assert_close(x.grad, x2.grad)
+    for p, q in zip(plain.parameters(), piped.parameters()):
+        torch.testing.assert_close(p.grad, q.grad)
+
+
+def test_none_skip():
+    @skippable(stash=['none'])
+    class Stash(nn.Module):
+        def forward(self, x):
+            yield stash('none', None)
+            return x
+
+    @skippable(pop=['none'])
+    class Pop(nn.Module):
+        def forward(self, x):
+            none = yield pop('none')
+            assert none is None
+            return x
+
+    model = GPipe(nn.Sequential(Stash(), Pop()), [1, 1], devices=['cpu', 'cpu'], chunks=5)
+    x = torch.rand(10, requires_grad=True)
+    y = model(x)
+
+    def assert_grad_fn_is_not_portal(grad_fn, visited=None):
+        visited = set() if visited is None else visited
+        if grad_fn in visited or grad_fn is None:
+            return
+        assert 'Portal' not in type(grad_fn).__name__
+        visited.add(grad_fn)
+        for next_fn, _ in grad_fn.next_functions:
+            assert_grad_fn_is_not_portal(next_fn, visited)
+
+    assert_grad_fn_is_not_portal(y.grad_fn)
+    y.sum().backward()
+    assert torch.allclose(x.grad, torch.ones_like(x))
+
+
+def test_namespaced_unet_like_skips_across_partitions():
+    @skippable(stash=['skip'])
+    class Stash(nn.Module):
+        def forward(self, x):
+            yield stash('skip', x)
+            return x * 2
+
+    @skippable(pop=['skip'])
+    class PopAdd(nn.Module):
+        def forward(self, x):
+            s = yield pop('skip')
+            return x + s
+
+    ns = [Namespace(), Namespace()]
+    layers = [Stash().isolate(ns[0]), nn.Linear(2, 2), Stash().isolate(ns[1]), nn.Linear(2, 2),
+              PopAdd().isolate(ns[1]), nn.Linear(2, 2), PopAdd().isolate(ns[0])]
+    torch.manual_seed(0)
+    plain = nn.Sequential(*layers)
+    piped = GPipe(copy.deepcopy(plain), [2, 2, 2, 1], devices=['cpu'] * 4, chunks=4)
+    x = torch.rand(8, 2)
+    torch.testing.assert_close(plain(x), piped(x))
+
+
+@pytest.mark.gpu
+@pytest.mark.multigpu
+def test_1to3_across_gpus():
+    if torch.cuda.device_count() < 3:
+        pytest.skip('needs 3 GPUs')
+    torch.manual_seed(0)
+    plain = nn.Sequential(Layer1(), Layer2(), Layer3())
+    piped = GPipe(copy.deepcopy(plain), [1, 1, 1], devices=[0, 1, 2], chunks=3)
+    x = torch.rand(6, 4)
+    torch.testing.assert_close(plain(x), piped(x.cuda(0)).cpu())

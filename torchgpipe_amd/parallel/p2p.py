@@ -135,9 +135,15 @@ class P2P:
 
     def __init__(self, device: torch.device, group: Optional[dist.ProcessGroup] = None,
                  ctrl_group: Optional[dist.ProcessGroup] = None,
-                 pack: bool = True) -> None:
+                 pack: bool = True,
+                 link_groups: Optional[Dict[int, dist.ProcessGroup]] = None) -> None:
         self.device = device
         self.group = group
+        # One 2-rank communicator per peer ("link"): RCCL then runs every link on
+        # its own stream, so a send waiting for a slow peer never holds back
+        # traffic to another peer (an eagerly initialised default group would
+        # serialise all unbatched point-to-point ops on one stream).
+        self.link_groups = link_groups or {}
         self.ctrl_group = ctrl_group
         self.pack = pack
         self._meta: Dict[Hashable, Tuple[List[TensorMeta], bool]] = {}
@@ -191,11 +197,11 @@ class P2P:
         if len(tensors) == 1 or not self.pack:
             for t in tensors:
                 self._pending_sends.append(dist.isend(t.detach().contiguous(), dst,
-                                                      group=self.group))
+                                                      group=self._link(dst)))
             return
         buf = torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=tensors[0].device)
         misc.pack([t.detach() for t in tensors], buf)
-        self._pending_sends.append(dist.isend(buf, dst, group=self.group))
+        self._pending_sends.append(dist.isend(buf, dst, group=self._link(dst)))
 
     def recv(self, src: int, key: Hashable) -> Message:
         """Post a receive from ``src``; the returned handle's ``wait()`` yields tensors."""
@@ -208,10 +214,13 @@ class P2P:
             return Message([], [], None, metas, atomic)
         if len(metas) == 1 or not self.pack:
             out = [torch.empty(m.shape, dtype=m.dtype, device=self.device) for m in metas]
-            works = [dist.irecv(t, src, group=self.group) for t in out]
+            works = [dist.irecv(t, src, group=self._link(src)) for t in out]
             return Message(works, out, None, metas, atomic)
         buf = torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=self.device)
-        return Message([dist.irecv(buf, src, group=self.group)], None, buf, metas, atomic)
+        return Message([dist.irecv(buf, src, group=self._link(src))], None, buf, metas, atomic)
+
+    def _link(self, peer: int) -> Optional[dist.ProcessGroup]:
+        return self.link_groups.get(peer, self.group)
 
     @staticmethod
     def _packed_nbytes(metas: Sequence[TensorMeta]) -> int:

@@ -141,6 +141,10 @@ class PipelineStage:
             gloo, otherwise a new gloo group over the same ranks).
         deferred_batch_norm: convert BatchNorm layers to DeferredBatchNorm.
         pack: pack multi-tensor messages into one transfer (HIP kernel).
+        links: one 2-rank communicator per used link (default: on for RCCL,
+            off for gloo).
+        materialize: called on this rank's partition before it is moved to
+            ``device`` (e.g. to initialise layers built on the ``meta`` device).
     """
 
     def __init__(self, module: nn.Sequential, balance: Sequence[int], *,
@@ -149,6 +153,7 @@ class PipelineStage:
                  group: Optional[dist.ProcessGroup] = None,
                  ctrl_group: Optional[dist.ProcessGroup] = None,
                  deferred_batch_norm: bool = False, pack: bool = True,
+                 links: Optional[bool] = None,
                  materialize: Optional[Callable[[nn.Module], None]] = None) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
@@ -213,11 +218,37 @@ class PipelineStage:
             else:
                 ctrl_group = dist.new_group(ranks=self.ranks, backend='gloo')
         self.ctrl_group = ctrl_group
-        self.p2p = P2P(device, group=group, ctrl_group=ctrl_group, pack=pack)
+        self.p2p = P2P(device, group=group, ctrl_group=ctrl_group, pack=pack,
+                       link_groups=self._make_links(links) if distributed else None)
 
         self._cells: List[_Cell] = []
         self._sig: Optional[Signature] = None
         self._m = 0
+
+    def _make_links(self, enabled: Optional[bool]) -> Dict[int, dist.ProcessGroup]:
+        """Create one 2-rank process group per pipeline link this model uses.
+
+        ``new_group`` is collective over WORLD, so every rank creates every
+        link in the same (sorted) order, including links it is not part of.
+        Links are the adjacent-stage pairs plus every cross-partition skip route.
+        On ``gloo`` (CPU) the pipeline group itself is used.
+        """
+        if enabled is None:
+            enabled = dist.get_backend(self.group) != 'gloo'
+        if not enabled:
+            return {}
+        pairs = {(j, j + 1) for j in range(self.n - 1)}
+        for (src, dst) in self.layout.by_ns_name.values():
+            if src != dst:
+                pairs.add((min(src, dst), max(src, dst)))
+        links: Dict[int, dist.ProcessGroup] = {}
+        for a, b in sorted(pairs):
+            pg = dist.new_group(ranks=[self.ranks[a], self.ranks[b]])
+            if self.rank == a:
+                links[self.ranks[b]] = pg
+            elif self.rank == b:
+                links[self.ranks[a]] = pg
+        return links
 
     # -- module-like helpers ----------------------------------------------------------------
 
@@ -241,6 +272,7 @@ class PipelineStage:
         return self.rank == self.n - 1
 
     def checkpoint_stop(self, m: int) -> int:
+        # Like GPipe.checkpoint_stop: checkpointing only while training.
         if not (self.training and torch.is_grad_enabled()):
             return 0
         return {'always': m, 'except_last': m - 1, 'never': 0}[self.checkpoint]
@@ -374,6 +406,10 @@ class PipelineStage:
                 self.p2p.send(by_dst[dst], self.ranks[dst],
                               self._key('skip', i, self.ranks[self.rank]))
             outputs.append(act_out[0] if cell.out_atomic else tuple(act_out))
+        if not torch.is_grad_enabled():
+            # Inference: no backward will flush the sends; complete them now.
+            self.p2p.flush()
+            self._cells = []
         return outputs
 
     # -- backward ---------------------------------------------------------------------------
