@@ -31,12 +31,20 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 # Reference (Tesla P40) throughputs of the same experiments, BASELINE.md §1/§2.
+# Batch / chunks / reference balance are the reference's experiment tables.
+# ``tuned`` balances were re-derived for MI355X + MIOpen: per-layer device times
+# measured on MI355X (profiles/unet_layer_profile.json, benchmarks/layer_profile.py)
+# fed to the step simulator (torchgpipe_amd.balance.simulate.optimize, 60 GB/s
+# links); per-stage device times checked with benchmarks/stage_harness.py
+# (profiles/stage_harness_p8_{tuned,ref}.json: max stage 359 ms tuned vs 613 ms ref).
 UNET_EXPERIMENTS = {
-    1: dict(name='pipeline-1', batch=80, chunks=2, balance=[241], ref=24.456),
-    2: dict(name='pipeline-2', batch=512, chunks=32, balance=[104, 137], ref=35.502),
-    4: dict(name='pipeline-4', batch=512, chunks=16, balance=[30, 66, 84, 61], ref=67.042),
-    8: dict(name='pipeline-8', batch=640, chunks=40,
-            balance=[16, 27, 31, 44, 22, 57, 27, 17], ref=88.497),
+    1: dict(name='pipeline-1', batch=80, chunks=2, balance=[241], tuned=[241], ref=24.456),
+    2: dict(name='pipeline-2', batch=512, chunks=32, balance=[104, 137], tuned=[97, 144],
+            ref=35.502),
+    4: dict(name='pipeline-4', batch=512, chunks=16, balance=[30, 66, 84, 61],
+            tuned=[39, 54, 58, 90], ref=67.042),
+    8: dict(name='pipeline-8', batch=640, chunks=40, balance=[16, 27, 31, 44, 22, 57, 27, 17],
+            tuned=[18, 27, 29, 23, 25, 33, 44, 42], ref=88.497),
 }
 AMOEBA_EXPERIMENTS = {
     2: dict(name='n2m32', batch=1280, chunks=32, balance=[9, 15], ref=47.386),
@@ -57,6 +65,9 @@ def parse() -> argparse.Namespace:
     p.add_argument('--batch', type=int, default=None, help='override the global batch')
     p.add_argument('--chunks', type=int, default=None, help='override the micro-batch count')
     p.add_argument('--unfused', action='store_true', help='use the unfused PyTorch U-Net cells')
+    p.add_argument('--balance', default='tuned',
+                   help="'tuned' (MI355X-measured, default), 'ref' (reference table) or a "
+                        "comma-separated list")
     p.add_argument('--cudnn-benchmark', action='store_true',
                    help='MIOpen exhaustive find (slow first step, cached afterwards)')
     p.add_argument('--profile-steps', type=int, default=0,
@@ -112,6 +123,10 @@ def main() -> None:
         exp['batch'] = args.batch
     if args.chunks:
         exp['chunks'] = args.chunks
+    if args.balance == 'tuned':
+        exp['balance'] = exp.get('tuned', exp['balance'])
+    elif args.balance != 'ref':
+        exp['balance'] = [int(v) for v in args.balance.split(',')]
     batch, chunks, balance = exp['batch'], exp['chunks'], exp['balance']
 
     stage = PipelineStage(model, balance, device=device, chunks=chunks, checkpoint=checkpoint)
@@ -197,6 +212,7 @@ def main() -> None:
                 'input': 'x'.join(map(str, in_shape)),
                 'chunks': chunks,
                 'balance': balance,
+                'balance_source': args.balance,
                 'checkpoint': checkpoint,
                 'parallelism': f'pp{world}',
                 'fused_cells': args.model == 'unet' and not args.unfused,

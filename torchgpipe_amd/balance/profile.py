@@ -90,8 +90,19 @@ def profile_sizes(module: nn.Sequential, input: TensorOrTensors, chunks: int,
     for i, x in enumerate(batch):
         batch[i] = x[:1].detach().to(device).requires_grad_(x.requires_grad)
 
+    layers = list(layerwise_sandbox(module, device))
+
+    # Warm-up pass: the first GEMM/conv on a device lazily allocates library
+    # workspaces (hipBLASLt, MIOpen) through the caching allocator, which would
+    # otherwise be billed to whichever layer happens to run first.
+    warm = Batch(tuple(batch)) if not batch.atomic else Batch(batch.tensor)
+    with torch.no_grad():
+        for layer in layers:
+            warm = warm.call(layer)
+    del warm
+
     sizes: List[int] = []
-    for layer in layerwise_sandbox(module, device):
+    for layer in layers:
         detach(batch)
         before = torch.cuda.memory_allocated(device)
         batch = batch.call(layer)
