@@ -94,8 +94,9 @@ def main() -> None:
         torch.cuda.set_device(device)
         torch.backends.cudnn.benchmark = args.cudnn_benchmark
     if world > 1:
-        dist.init_process_group('nccl' if gpu else 'gloo', rank=rank, world_size=world,
-                                device_id=device if gpu else None)
+        # Lazy RCCL init: each pipeline link (peer pair) then gets its own
+        # communicator and stream on first use.
+        dist.init_process_group('nccl' if gpu else 'gloo', rank=rank, world_size=world)
 
     from torchgpipe_amd.models import amoebanetd, unet
     from torchgpipe_amd.parallel import PipelineStage

@@ -30,6 +30,7 @@ from torchgpipe_amd.pipeline import Pipeline
 from torchgpipe_amd.skip.layout import inspect_skip_layout
 from torchgpipe_amd.skip.skippable import verify_skippables
 from torchgpipe_amd.stream import AbstractStream, StreamPool
+from torchgpipe_amd.utils.meta import is_meta, materialize
 from torchgpipe_amd.worker import WorkerPool
 
 __all__ = ['GPipe', 'BalanceError', 'verify_module', 'split_module']
@@ -111,7 +112,11 @@ def split_module(module: nn.Sequential, balance: Iterable[int], devices: List[to
     partitions = []
     for group, device in zip(partition_layers(module, balance), devices):
         partition = nn.Sequential(group)
-        partition.to(device)
+        if is_meta(partition):
+            # Built on the meta device: allocate + initialise on the target GPU.
+            materialize(partition, device)
+        else:
+            partition.to(device)
         partitions.append(partition)
     del devices[len(balance):]
     return cast(List[nn.Sequential], nn.ModuleList(partitions)), balance, devices

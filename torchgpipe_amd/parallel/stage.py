@@ -45,6 +45,8 @@ from torchgpipe_amd.skip.namespace import Namespace
 from torchgpipe_amd.skip.skippable import Skippable, verify_skippables
 from torchgpipe_amd.skip.tracker import SkipTracker, use_skip_tracker
 from torchgpipe_amd.utils import trace
+from torchgpipe_amd.utils.meta import is_meta
+from torchgpipe_amd.utils.meta import materialize as meta_materialize
 
 __all__ = ['PipelineStage', 'signature_of']
 
@@ -193,6 +195,9 @@ class PipelineStage:
             partition = DeferredBatchNorm.convert_deferred_batch_norm(partition, chunks)
         if materialize is not None:
             materialize(partition)
+        if is_meta(partition):
+            # Whole model built on the meta device: only this rank's layers get memory.
+            meta_materialize(partition, device)
         self.partition = partition.to(device)
         self._has_dbn = any(isinstance(m, DeferredBatchNorm) for m in partition.modules())
 
@@ -234,7 +239,13 @@ class PipelineStage:
         On ``gloo`` (CPU) the pipeline group itself is used.
         """
         if enabled is None:
-            enabled = dist.get_backend(self.group) != 'gloo'
+            # Needed only when the group was eagerly initialised (``device_id``):
+            # then PyTorch runs unbatched P2P on the group's single communicator.
+            # Lazily initialised RCCL groups already give every peer pair its own
+            # communicator (and stream) on first use.
+            pg = self.group if self.group is not None else dist.group.WORLD
+            enabled = (dist.get_backend(self.group) != 'gloo'
+                       and getattr(pg, 'bound_device_id', None) is not None)
         if not enabled:
             return {}
         pairs = {(j, j + 1) for j in range(self.n - 1)}
