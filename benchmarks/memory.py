@@ -143,7 +143,8 @@ def main() -> None:
                    help='U-Net B (convs per cell) or AmoebaNet L (layers)')
     p.add_argument('--channels', '-C', type=int, default=None,
                    help='U-Net C (base channels) or AmoebaNet D (filters)')
-    p.add_argument('--balance', type=int, nargs='*', default=None)
+    p.add_argument('--balance', nargs='*', default=None,
+                   help="layers per stage, or 'params N' to split N ways by parameter bytes")
     p.add_argument('--chunks', type=int, default=None)
     p.add_argument('--batch', type=int, default=None)
     p.add_argument('--stages', type=int, nargs='*', default=None)
@@ -160,7 +161,14 @@ def main() -> None:
     shape = (3, 192, 192) if args.model == 'unet' else (3, 224, 224)
     model = build(args.model, depth, channels)
     layers = list(model)
-    balance = args.balance or cfg.get('balance') or [len(layers)]
+    if args.balance and args.balance[0] == 'params':
+        from torchgpipe_amd.balance.blockpartition import solve_splits
+        cost = [sum(p.numel() for p in layer.parameters()) + 1 for layer in layers]
+        balance = solve_splits(cost, int(args.balance[1]))
+    elif args.balance:
+        balance = [int(v) for v in args.balance]
+    else:
+        balance = cfg.get('balance') or [len(layers)]
     assert sum(balance) == len(layers), (sum(balance), len(layers))
     total_params = sum(p.numel() for p in model.parameters())
     device = torch.device('cuda', 0)
