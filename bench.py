@@ -46,11 +46,15 @@ UNET_EXPERIMENTS = {
     8: dict(name='pipeline-8', batch=640, chunks=40, balance=[16, 27, 31, 44, 22, 57, 27, 17],
             tuned=[18, 27, 29, 23, 25, 33, 44, 42], ref=88.497),
 }
+# AmoebaNet tuned balances: profiles/amoebanet_layer_profile.json (micro-batch 40) through
+# the same simulator (n2 535 vs 492, n4 851 vs 814, n8 1539 vs 1503 simulated samples/s).
 AMOEBA_EXPERIMENTS = {
-    2: dict(name='n2m32', batch=1280, chunks=32, balance=[9, 15], ref=47.386),
-    4: dict(name='n4m32', batch=1152, chunks=32, balance=[3, 6, 7, 8], ref=72.412),
-    8: dict(name='n8m32', batch=1280, chunks=32, balance=[2, 2, 2, 3, 3, 4, 4, 4], ref=132.413),
-    1: dict(name='n1m32', batch=640, chunks=32, balance=[24], ref=None),
+    1: dict(name='n1m32', batch=640, chunks=32, balance=[24], tuned=[24], ref=None),
+    2: dict(name='n2m32', batch=1280, chunks=32, balance=[9, 15], tuned=[10, 14], ref=47.386),
+    4: dict(name='n4m32', batch=1152, chunks=32, balance=[3, 6, 7, 8], tuned=[5, 5, 6, 8],
+            ref=72.412),
+    8: dict(name='n8m32', batch=1280, chunks=32, balance=[2, 2, 2, 3, 3, 4, 4, 4],
+            tuned=[2, 2, 3, 3, 3, 3, 4, 4], ref=132.413),
 }
 
 
