@@ -97,6 +97,7 @@ def run_speed(args: argparse.Namespace, experiment: Experiment,
         else:
             model = GPipe(model, balance, devices=devices, chunks=chunks, checkpoint=checkpoint)
             in_device, out_device = model.devices[0], model.devices[-1]
+            stage = None
             params = list(model.parameters())
         rank, world, first, last = 0, 1, True, True
         torch.cuda.set_device(in_device)

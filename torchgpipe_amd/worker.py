@@ -13,10 +13,12 @@ Kernel launches are asynchronous, so a worker thread only spends host time
 enqueueing HIP work; the device threads let PyTorch issue launches for
 different GPUs concurrently (PyTorch releases the GIL inside its C++ ops).
 """
+import atexit
 from contextlib import contextmanager
 from queue import Queue
 import sys
 from threading import Thread
+import weakref
 from types import TracebackType
 from typing import Callable, Dict, Generator, List, Optional, Tuple, Type, Union
 
@@ -97,12 +99,28 @@ def _drain_close(queues: Dict[torch.device, Tuple[InQueue, OutQueue]]) -> None:
         running[key] = out_q
 
 
+_live_pools: 'weakref.WeakSet[WorkerPool]' = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_pools() -> None:
+    # Join idle device threads before interpreter finalisation: a daemon thread
+    # that still owns a HIP context while C++ static destructors run aborts the
+    # process ("terminate called without an active exception").
+    for pool in list(_live_pools):
+        try:
+            pool.close(wait=True)
+        except Exception:  # pragma: no cover
+            pass
+
+
 class WorkerPool:
     """Persistent device threads shared by every forward of one ``GPipe``."""
 
     def __init__(self) -> None:
         self._workers: Dict[torch.device, Tuple[InQueue, OutQueue]] = {}
         self._threads: List[Thread] = []
+        _live_pools.add(self)
 
     def queues(self, devices: List[torch.device]) -> Tuple[List[InQueue], List[OutQueue]]:
         in_queues: List[InQueue] = []
@@ -124,6 +142,8 @@ class WorkerPool:
         if self._workers:
             if wait:
                 _drain_close(self._workers)
+                for t in self._threads:
+                    t.join(timeout=10)
             else:
                 for in_q, _ in self._workers.values():
                     in_q.put(None)
