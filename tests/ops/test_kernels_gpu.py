@@ -81,7 +81,8 @@ def test_drop_norm_act_module_replays_under_tape():
     assert not torch.equal(a, c)
 
 
-@pytest.mark.parametrize('shape', [(4, 16, 12, 12), (3, 7, 5, 5), (2, 64, 56, 56), (8, 3, 1)])
+@pytest.mark.parametrize('shape', [(4, 16, 12, 12), (3, 7, 5, 5), (2, 64, 56, 56), (8, 3, 1),
+                                   (2, 3, 80, 80), (3, 5, 67, 67), (40, 1024, 14, 14)])
 def test_dbn_track_and_commit(shape):
     x = torch.randn(shape, device=cuda) * 2 + 0.5
     c = shape[1]

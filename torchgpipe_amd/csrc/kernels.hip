@@ -108,6 +108,56 @@ __global__ __launch_bounds__(kTrackThreads) void dbn_track_kernel(
   }
 }
 
+// K1 for small spatial extents (S < one chunk): each block strides over the flattened
+// (n, s) index space of its channel so every lane has work even when S is 49 or 196.
+template <bool VEC>
+__global__ __launch_bounds__(kTrackThreads) void dbn_track_flat_kernel(
+    const float* __restrict__ x, float* __restrict__ sum, float* __restrict__ sumsq, int64_t n,
+    int64_t c, int64_t s, int nsplit) {
+  const int ch_idx = blockIdx.y;
+  const int tid = threadIdx.x;
+  float a = 0.f, b = 0.f;
+  if (VEC) {
+    const int64_t sv = s / 4;
+    const int64_t total = n * sv;
+    for (int64_t k = static_cast<int64_t>(blockIdx.x) * kTrackThreads + tid; k < total;
+         k += static_cast<int64_t>(nsplit) * kTrackThreads) {
+      const int64_t ni = k / sv;
+      const float4 v = reinterpret_cast<const float4*>(x + (ni * c + ch_idx) * s)[k - ni * sv];
+      a += (v.x + v.y) + (v.z + v.w);
+      b += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+    }
+  } else {
+    const int64_t total = n * s;
+    for (int64_t k = static_cast<int64_t>(blockIdx.x) * kTrackThreads + tid; k < total;
+         k += static_cast<int64_t>(nsplit) * kTrackThreads) {
+      const int64_t ni = k / s;
+      const float v = x[(ni * c + ch_idx) * s + (k - ni * s)];
+      a += v;
+      b += v * v;
+    }
+  }
+  __shared__ float red[2][kTrackThreads / kWave];
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int wave = tid / kWave;
+  if ((tid & (kWave - 1)) == 0) {
+    red[0][wave] = a;
+    red[1][wave] = b;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float ta = 0.f, tb = 0.f;
+#pragma unroll
+    for (int w = 0; w < kTrackThreads / kWave; ++w) {
+      ta += red[0][w];
+      tb += red[1][w];
+    }
+    atomicAdd(sum + ch_idx, ta);
+    atomicAdd(sumsq + ch_idx, tb);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K2: commit.  fp64 arithmetic for mean/variance (the sums are fp32).
 // ---------------------------------------------------------------------------------------------
@@ -482,12 +532,30 @@ constexpr int64_t kDnaMaxTile = 1024 * 9 * 4;
 void launch_dbn_track(const float* x, float* sum, float* sumsq, int64_t n, int64_t c, int64_t s,
                       hipStream_t stream) {
   if (n == 0 || c == 0 || s == 0) return;
+  const bool aligned = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (s < kTrackChunk) {
+    // Flattened (n, s) space per channel; >= 16 elements per lane, >= ~2048 blocks.
+    const bool vec_flat = (s % 4 == 0) && aligned;
+    const int64_t work = n * (vec_flat ? s / 4 : s);
+    int64_t nsplit = (work + kTrackThreads * 4 - 1) / (kTrackThreads * 4);
+    const int64_t want = (2048 + c - 1) / c;
+    if (nsplit > want) nsplit = want;
+    if (nsplit < 1) nsplit = 1;
+    const dim3 grid(static_cast<unsigned>(nsplit), static_cast<unsigned>(c));
+    if (vec_flat)
+      hipLaunchKernelGGL(dbn_track_flat_kernel<true>, grid, dim3(kTrackThreads), 0, stream, x,
+                         sum, sumsq, n, c, s, static_cast<int>(nsplit));
+    else
+      hipLaunchKernelGGL(dbn_track_flat_kernel<false>, grid, dim3(kTrackThreads), 0, stream, x,
+                         sum, sumsq, n, c, s, static_cast<int>(nsplit));
+    return;
+  }
   const int64_t chunks_per_n = (s + kTrackChunk - 1) / kTrackChunk;
   const int64_t items = n * chunks_per_n;
   int64_t nsplit = (2048 + c - 1) / c;  // aim for >= 2048 blocks (8 per CU)
   if (nsplit > items) nsplit = items;
   if (nsplit < 1) nsplit = 1;
-  const bool vec = (s % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  const bool vec = (s % 4 == 0) && aligned;
   const dim3 grid(static_cast<unsigned>(nsplit), static_cast<unsigned>(c));
   if (vec)
     hipLaunchKernelGGL(dbn_track_kernel<true>, grid, dim3(kTrackThreads), 0, stream, x, sum,
