@@ -74,6 +74,12 @@ def parse() -> argparse.Namespace:
                         "comma-separated list")
     p.add_argument('--cudnn-benchmark', action='store_true',
                    help='MIOpen exhaustive find (slow first step, cached afterwards)')
+    p.add_argument('--backend', choices=['auto', 'gloo'], default='auto',
+                   help="tensor transport: 'auto' = RCCL on GPUs (gloo on CPU); 'gloo' stages "
+                        "messages through host memory and lets several ranks share one GPU "
+                        "(functional rehearsal only, not a valid measurement)")
+    p.add_argument('--tiny', action='store_true',
+                   help='tiny model of the same family (CI smoke test of this script only)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -86,6 +92,13 @@ def even_balance(layers: int, parts: int) -> list:
 
 def main() -> None:
     args = parse()
+    # stdout carries exactly one JSON line (rank 0).  Libraries print to fd 1
+    # from native code (gloo's "[Gloo] Rank r is connected to ..." banner, RCCL
+    # info): point fd 1 at stderr for the whole run and keep a private handle
+    # on the real stdout for the result.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), 'w')
+    os.dup2(2, 1)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
@@ -93,14 +106,19 @@ def main() -> None:
         raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU')
 
     gpu = torch.cuda.is_available()
-    device = torch.device('cuda', local_rank) if gpu else torch.device('cpu')
+    rehearsal = args.backend == 'gloo' and gpu and world > 1
+    if gpu and not rehearsal and local_rank >= torch.cuda.device_count():
+        raise SystemExit(f'LOCAL_RANK {local_rank} but only {torch.cuda.device_count()} GPUs')
+    device = (torch.device('cuda', local_rank % torch.cuda.device_count()) if gpu
+              else torch.device('cpu'))
     if gpu:
         torch.cuda.set_device(device)
         torch.backends.cudnn.benchmark = args.cudnn_benchmark
     if world > 1:
         # Lazy RCCL init: each pipeline link (peer pair) then gets its own
         # communicator and stream on first use.
-        dist.init_process_group('nccl' if gpu else 'gloo', rank=rank, world_size=world)
+        backend = 'nccl' if gpu and not rehearsal else 'gloo'
+        dist.init_process_group(backend, rank=rank, world_size=world)
 
     from torchgpipe_amd.models import amoebanetd, unet
     from torchgpipe_amd.parallel import PipelineStage
@@ -110,15 +128,24 @@ def main() -> None:
         exp = dict(table.get(world) or dict(name=f'pipeline-{world}', batch=80 * world,
                                             chunks=4 * world, balance=even_balance(241, world),
                                             ref=None))
-        model = unet(depth=5, num_convs=5, base_channels=64, input_channels=3,
-                     output_channels=1, fused=not args.unfused)
+        if args.tiny:
+            model = unet(depth=2, num_convs=1, base_channels=4, input_channels=3,
+                         output_channels=1, fused=not args.unfused)
+            exp['balance'] = exp['tuned'] = even_balance(len(model), world)
+        else:
+            model = unet(depth=5, num_convs=5, base_channels=64, input_channels=3,
+                         output_channels=1, fused=not args.unfused)
         in_shape = (3, 192, 192)
         checkpoint = 'except_last'
         model_name = 'U-Net(5,64)'
     else:
         exp = dict(table.get(world) or dict(name=f'n{world}m32', batch=160 * world, chunks=32,
                                             balance=even_balance(24, world), ref=None))
-        model = amoebanetd(num_classes=1000, num_layers=18, num_filters=256)
+        if args.tiny:
+            model = amoebanetd(num_classes=10, num_layers=3, num_filters=8)
+            exp['balance'] = exp['tuned'] = even_balance(len(model), world)
+        else:
+            model = amoebanetd(num_classes=1000, num_layers=18, num_filters=256)
         in_shape = (3, 224, 224)
         checkpoint = 'except_last' if exp['chunks'] > 1 else 'always'
         model_name = 'AmoebaNet-D(18,256)'
@@ -144,7 +171,7 @@ def main() -> None:
         target = torch.ones(batch, 1, 192, 192, device=device) if stage.is_last else None
         loss_fn = F.binary_cross_entropy_with_logits
     else:
-        target = (torch.randint(1000, (batch,), device=device, generator=gen)
+        target = (torch.randint(10 if args.tiny else 1000, (batch,), device=device, generator=gen)
                   if stage.is_last else None)
         loss_fn = F.cross_entropy
     from torchgpipe_amd.parallel.stage import signature_of
@@ -194,7 +221,9 @@ def main() -> None:
 
     samples_per_s = batch * args.steps / elapsed
     if rank == 0:
-        ref = exp.get('ref')
+        ref = None if args.tiny else exp.get('ref')
+        if args.tiny:
+            model_name += ' TINY smoke-test variant (not a measurement)'
         mem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if gpu else 0.0
         print(json.dumps({
             'metric': f'{model_name} GPipe training throughput (samples/sec)',
@@ -220,12 +249,14 @@ def main() -> None:
                 'balance_source': args.balance,
                 'checkpoint': checkpoint,
                 'parallelism': f'pp{world}',
+                'transport': 'gloo-host-staged (rehearsal)' if rehearsal else
+                             ('rccl' if gpu and world > 1 else 'none'),
                 'fused_cells': args.model == 'unet' and not args.unfused,
                 'baseline_samples_per_sec_p40': ref,
                 'rank0_peak_mem_gib': round(mem, 2),
                 'warmup_s': round(warm_s, 1),
             },
-        }), flush=True)
+        }), file=result_out, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

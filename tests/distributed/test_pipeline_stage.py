@@ -160,3 +160,51 @@ def test_eval_forward_matches_plain_model(tmp_path):
     with torch.no_grad():
         want = model(X)
     torch.testing.assert_close(torch.cat(results[-1]), want)
+
+
+def build_unet():
+    from torchgpipe_amd.models import unet
+    torch.manual_seed(7)
+    model = unet(depth=3, num_convs=1, base_channels=4, input_channels=3, output_channels=1)
+    for m in model.modules():  # deterministic: compare against the plain model
+        if isinstance(getattr(m, 'p', None), float):
+            m.p = 0.0
+    return model
+
+
+UX = torch.rand(6, 3, 16, 16, generator=torch.Generator().manual_seed(8))
+UT = torch.rand(6, 1, 16, 16, generator=torch.Generator().manual_seed(9))
+
+
+def _unet_worker(rank, world, balance, checkpoint):
+    from torchgpipe_amd.parallel import PipelineStage
+    stage = PipelineStage(build_unet(), balance, chunks=3, checkpoint=checkpoint)
+    for _ in range(2):  # second step runs on cached message metadata
+        for p in stage.parameters():
+            p.grad = None
+        loss = stage.train_step(UX if rank == 0 else None, UT if rank == world - 1 else None,
+                                F.binary_cross_entropy_with_logits)
+    return {'grads': [p.grad.clone() for p in stage.parameters()],
+            'loss': None if loss is None else loss.item(),
+            'skip_dsts': sorted({d for d, _ in stage.out_skips}),
+            'skip_srcs': sorted({s for s, _ in stage.in_skips})}
+
+
+@pytest.mark.parametrize('checkpoint', ['except_last', 'never'])
+def test_unet_skips_fan_out_to_several_ranks(tmp_path, checkpoint):
+    """Rank 0 stashes skips popped by two different ranks and receives skip
+    gradients back from both: every (kind, micro-batch, src, dst) message has
+    its own metadata entry."""
+    model = build_unet()
+    balance = [17, 9, 6, 9]
+    assert sum(balance) == len(model)
+    results = run(_unet_worker, 4, tmp_path, balance, checkpoint)
+    assert len(results[0]['skip_dsts']) >= 2, results[0]['skip_dsts']
+    loss = F.binary_cross_entropy_with_logits(model(UX), UT)
+    loss.backward()
+    want = [p.grad for p in model.parameters()]
+    got = [g for r in results for g in r['grads']]
+    assert len(got) == len(want)
+    for a, b in zip(got, want):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    assert results[-1]['loss'] == pytest.approx(loss.item(), rel=1e-5)

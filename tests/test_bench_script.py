@@ -1,0 +1,52 @@
+"""The bench.py driver contract: one JSON line from rank 0, MAX-over-ranks timing.
+
+Runs the script end to end on CPU (gloo) with the ``--tiny`` model variant, at
+one rank and under ``torch.distributed.run`` with two ranks.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {'metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step',
+        'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'data', 'config'}
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _run(nproc: int, *extra: str) -> dict:
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='', OMP_NUM_THREADS='2')
+    args = ['bench.py', '--gpus', str(nproc), '--steps', '1', '--warmup', '1', '--tiny',
+            '--batch', '4', '--chunks', '2', *extra]
+    if nproc > 1:
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+               f'--nproc-per-node={nproc}', '--master-addr', '127.0.0.1',
+               '--master-port', str(_free_port()), *args]
+    else:
+        cmd = [sys.executable, *args]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout  # nothing but the JSON line on stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize('nproc,model', [(1, 'unet'), (2, 'unet'), (2, 'amoebanet')])
+def test_bench_json_contract(nproc, model):
+    rec = _run(nproc, '--model', model)
+    assert KEYS <= set(rec)
+    assert rec['n_gpus'] == nproc and rec['steps'] == 1 and rec['warmup'] == 1
+    assert rec['value'] > 0 and rec['higher_is_better'] is True
+    assert rec['config']['global_batch'] == 4
+    assert rec['config']['parallelism'] == f'pp{nproc}'
+    assert 'TINY' in rec['metric'] and rec['vs_baseline'] is None
+    # value is the whole-job aggregate: batch * steps / elapsed
+    assert rec['value'] == pytest.approx(4 * 1000 / rec['ms_per_step'], rel=1e-2)

@@ -87,15 +87,19 @@ def _align16(n: int) -> int:
 class Message:
     """Handle of a posted receive: ``wait()`` returns the received tensors."""
 
-    __slots__ = ('_works', '_tensors', '_buffer', '_metas', 'atomic')
+    __slots__ = ('_works', '_tensors', '_buffer', '_metas', 'atomic', '_device')
 
     def __init__(self, works: List[object], tensors: Optional[List[Tensor]],
-                 buffer: Optional[Tensor], metas: List[TensorMeta], atomic: bool) -> None:
+                 buffer: Optional[Tensor], metas: List[TensorMeta], atomic: bool,
+                 device: Optional[torch.device] = None) -> None:
         self._works = works
         self._tensors = tensors
         self._buffer = buffer
         self._metas = metas
         self.atomic = atomic
+        # Host-staged receive (gloo transport for device tensors): move the
+        # received host buffers onto this device after the wait.
+        self._device = device
 
     def wait(self) -> List[Tensor]:
         """Wait (stream-ordered on GPUs) and return detached leaf tensors.
@@ -106,6 +110,12 @@ class Message:
         for w in self._works:
             w.wait()  # type: ignore[attr-defined]
         self._works = []
+        if self._device is not None:
+            if self._tensors is not None:
+                self._tensors = [t.to(self._device, non_blocking=True) for t in self._tensors]
+            if self._buffer is not None:
+                self._buffer = self._buffer.to(self._device, non_blocking=True)
+            self._device = None
         if self._tensors is None:
             assert self._buffer is not None
             views: List[Tensor] = []
@@ -146,6 +156,11 @@ class P2P:
         self.link_groups = link_groups or {}
         self.ctrl_group = ctrl_group
         self.pack = pack
+        # gloo cannot move device memory: when the tensor transport is gloo and
+        # the stage runs on a GPU (single-GPU rehearsal of a multi-rank run),
+        # stage every message through host memory.
+        self.stage_host = (device.type == 'cuda' and dist.is_initialized()
+                           and dist.get_backend(group) == 'gloo')
         self._meta: Dict[Hashable, Tuple[List[TensorMeta], bool]] = {}
         self._pending_sends: List[object] = []
         self._pending_meta: List[object] = []
@@ -196,11 +211,15 @@ class P2P:
         self._prune()
         if len(tensors) == 1 or not self.pack:
             for t in tensors:
-                self._pending_sends.append(dist.isend(t.detach().contiguous(), dst,
-                                                      group=self._link(dst)))
+                t = t.detach().contiguous()
+                if self.stage_host:
+                    t = t.cpu()
+                self._pending_sends.append(dist.isend(t, dst, group=self._link(dst)))
             return
         buf = torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=tensors[0].device)
         misc.pack([t.detach() for t in tensors], buf)
+        if self.stage_host:
+            buf = buf.cpu()
         self._pending_sends.append(dist.isend(buf, dst, group=self._link(dst)))
 
     def recv(self, src: int, key: Hashable) -> Message:
@@ -212,12 +231,15 @@ class P2P:
         metas, atomic = cached
         if not metas:
             return Message([], [], None, metas, atomic)
+        where = torch.device('cpu') if self.stage_host else self.device
+        late = self.device if self.stage_host else None
         if len(metas) == 1 or not self.pack:
-            out = [torch.empty(m.shape, dtype=m.dtype, device=self.device) for m in metas]
+            out = [torch.empty(m.shape, dtype=m.dtype, device=where) for m in metas]
             works = [dist.irecv(t, src, group=self._link(src)) for t in out]
-            return Message(works, out, None, metas, atomic)
-        buf = torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=self.device)
-        return Message([dist.irecv(buf, src, group=self._link(src))], None, buf, metas, atomic)
+            return Message(works, out, None, metas, atomic, late)
+        buf = torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=where)
+        return Message([dist.irecv(buf, src, group=self._link(src))], None, buf, metas, atomic,
+                       late)
 
     def _link(self, peer: int) -> Optional[dist.ProcessGroup]:
         return self.link_groups.get(peer, self.group)

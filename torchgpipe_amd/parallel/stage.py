@@ -313,8 +313,11 @@ class PipelineStage:
         self.p2p.recv_control(payload, self.ranks[0])
         return _decode_signature(payload)
 
-    def _key(self, kind: str, i: int, peer: int) -> Hashable:
-        return (self._sig, self.training, torch.is_grad_enabled(), kind, i, peer)
+    def _key(self, kind: str, i: int, src: int, dst: int) -> Hashable:
+        # Metadata cache key of one message.  Both endpoints are part of it: a
+        # stage may send the same kind of message (skips, skip gradients) to
+        # several peers in one micro-batch, each with its own layout.
+        return (self._sig, self.training, torch.is_grad_enabled(), kind, i, src, dst)
 
     # -- forward ----------------------------------------------------------------------------
 
@@ -367,6 +370,7 @@ class PipelineStage:
             assert input is not None
             batches = microbatch.scatter(input, self.chunks)
 
+        me = self.ranks[self.rank]
         prev = self.ranks[self.rank - 1] if self.rank > 0 else None
         nxt = self.ranks[self.rank + 1] if not self.is_last else None
         self._cells = []
@@ -382,9 +386,9 @@ class PipelineStage:
                 in_atomic = b.atomic
                 act_msg = None
             else:
-                act_msg = self.p2p.recv(prev, self._key('act', i, prev))  # type: ignore[arg-type]
+                act_msg = self.p2p.recv(prev, self._key('act', i, prev, me))  # type: ignore[arg-type]
                 in_atomic = True
-            skip_msgs = [(self.p2p.recv(self.ranks[src], self._key('skip', i, self.ranks[src])))
+            skip_msgs = [(self.p2p.recv(self.ranks[src], self._key('skip', i, self.ranks[src], me)))
                          for src in sorted({s for s, _ in self.in_skips})]
             if act_msg is not None:
                 acts = act_msg.wait()
@@ -408,14 +412,14 @@ class PipelineStage:
             # 3. outputs: activation to the next stage, skips to their pop ranks
             act_out = out[:cell.n_act_out]
             if nxt is not None:
-                self.p2p.send(act_out, nxt, self._key('act', i, self.ranks[self.rank]),
+                self.p2p.send(act_out, nxt, self._key('act', i, me, nxt),
                               atomic=cell.out_atomic)
             by_dst: Dict[int, List[Tensor]] = OrderedDict()
             for (dst, _), t in zip(self.out_skips, out[cell.n_act_out:]):
                 by_dst.setdefault(dst, []).append(t)
             for dst in sorted(by_dst):
                 self.p2p.send(by_dst[dst], self.ranks[dst],
-                              self._key('skip', i, self.ranks[self.rank]))
+                              self._key('skip', i, me, self.ranks[dst]))
             outputs.append(act_out[0] if cell.out_atomic else tuple(act_out))
         if not torch.is_grad_enabled():
             # Inference: no backward will flush the sends; complete them now.
@@ -442,11 +446,11 @@ class PipelineStage:
             # 1. post the gradient receives first ...
             grad_msg = None
             if nxt is not None and any(t.requires_grad for t in cell.outputs[:cell.n_act_out]):
-                grad_msg = self.p2p.recv(nxt, self._key('gact', i, nxt))
+                grad_msg = self.p2p.recv(nxt, self._key('gact', i, nxt, me))
             skip_grad_msgs = []
             for dst in sorted({d for d, _ in self.out_skips}):
                 skip_grad_msgs.append(
-                    (dst, self.p2p.recv(self.ranks[dst], self._key('gskip', i, self.ranks[dst]))))
+                    (dst, self.p2p.recv(self.ranks[dst], self._key('gskip', i, self.ranks[dst], me))))
             # 2. ... then recompute while they are in flight
             if cell.chk is not None:
                 with trace.range(f'recompute mb{i} stage{self.rank}'):
@@ -484,13 +488,13 @@ class PipelineStage:
             n_in_act = len(cell.inputs) - len(self.in_skips)
             if prev is not None:
                 gin = [self._grad_of(t) for t in cell.inputs[:n_in_act] if t.requires_grad]
-                self.p2p.send(gin, prev, self._key('gact', i, me))
+                self.p2p.send(gin, prev, self._key('gact', i, me, prev))
             skip_in = cell.inputs[n_in_act:]
             by_src: Dict[int, List[Tensor]] = {}
             for (src, _), t in zip(self.in_skips, skip_in):
                 by_src.setdefault(src, []).append(self._grad_of(t))
             for src in sorted(by_src):
-                self.p2p.send(by_src[src], self.ranks[src], self._key('gskip', i, me))
+                self.p2p.send(by_src[src], self.ranks[src], self._key('gskip', i, me, self.ranks[src]))
             cell.inputs = []
             cell.outputs = []
             cell.chk = None
