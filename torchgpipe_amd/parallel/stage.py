@@ -229,6 +229,45 @@ class PipelineStage:
         self._cells: List[_Cell] = []
         self._sig: Optional[Signature] = None
         self._m = 0
+        if distributed and self.n > 1:
+            self.connect()
+
+    def _link_pairs(self) -> List[Tuple[int, int]]:
+        """Stage pairs that exchange messages: neighbours plus cross-rank skip routes."""
+        pairs = {(j, j + 1) for j in range(self.n - 1)}
+        for (src, dst) in self.layout.by_ns_name.values():
+            if src != dst:
+                pairs.add((min(src, dst), max(src, dst)))
+        return sorted(pairs)
+
+    def connect(self) -> None:
+        """Open every link this stage uses, in one global order.
+
+        RCCL creates a peer pair's communicator on the first send/recv between
+        them, and that creation blocks both hosts until the pair meets.  Left
+        to the training step, the order in which a rank meets its peers follows
+        its own message order (activations first, then skips), and stages with
+        skips to distant ranks could wait on each other in a cycle.  Here every
+        rank visits its pairs in the same sorted order, which cannot cycle, and
+        exchanges one element per pair, so all communicators exist before the
+        first step.
+        """
+        staged = self.p2p.stage_host or self.device.type != 'cuda'
+        where = torch.device('cpu') if staged else self.device
+        works = []
+        for a, b in self._link_pairs():
+            if self.rank not in (a, b):
+                continue
+            peer = self.ranks[b if self.rank == a else a]
+            buf = torch.zeros(1, device=where)
+            if self.rank == a:
+                works.append(dist.isend(buf, peer, group=self.p2p._link(peer)))
+            else:
+                dist.irecv(buf, peer, group=self.p2p._link(peer)).wait()
+        for w in works:
+            w.wait()
+        if where.type == 'cuda':
+            torch.cuda.synchronize(where)
 
     def _make_links(self, enabled: Optional[bool]) -> Dict[int, dist.ProcessGroup]:
         """Create one 2-rank process group per pipeline link this model uses.
@@ -248,12 +287,8 @@ class PipelineStage:
                        and getattr(pg, 'bound_device_id', None) is not None)
         if not enabled:
             return {}
-        pairs = {(j, j + 1) for j in range(self.n - 1)}
-        for (src, dst) in self.layout.by_ns_name.values():
-            if src != dst:
-                pairs.add((min(src, dst), max(src, dst)))
         links: Dict[int, dist.ProcessGroup] = {}
-        for a, b in sorted(pairs):
+        for a, b in self._link_pairs():
             pg = dist.new_group(ranks=[self.ranks[a], self.ranks[b]])
             if self.rank == a:
                 links[self.ranks[b]] = pg
