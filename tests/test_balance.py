@@ -160,3 +160,52 @@ def test_sandbox_during_profiling():
 def test_deprecated_torchgpipe_amd_balancing():
     with pytest.raises(ImportError, match="import 'torchgpipe_amd.balance' instead"):
         __import__('torchgpipe_amd_balancing')
+
+
+class _Twin(nn.Module):
+    def forward(self, x):
+        return x, x.detach()
+
+
+class _Add(nn.Module):
+    def forward(self, pair):
+        a, b = pair
+        return a + b
+
+
+def test_balance_by_time_tuple_boundaries():
+    model = nn.Sequential(_Twin(), _Add())
+    assert balance_by_time(1, model, torch.rand(1, requires_grad=True), device='cpu') == [2]
+
+
+@gpu
+def test_balance_by_size_tuple_boundaries():
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    model = nn.Sequential(_Twin(), _Add())
+    assert balance_by_size(1, model, torch.rand(1, requires_grad=True)) == [2]
+
+
+@gpu
+def test_balance_by_size_param_scale_tradeoff():
+    """param_scale weighs parameters against activations: with no weight the
+    activation-heavy front layers dominate, with a heavy weight the
+    parameter-heavy back layers do."""
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+
+    class Tradeoff(nn.Module):
+        def __init__(self, params, latents):
+            super().__init__()
+            self.fc = nn.Linear(params, params)
+            self.latents = latents
+
+        def forward(self, x):
+            for _ in range(self.latents):
+                x = x + torch.rand_like(x, requires_grad=True)
+            return x
+
+    model = nn.Sequential(*[Tradeoff(p, 7 - p) for p in range(1, 7)])
+    sample = torch.rand(1, requires_grad=True)
+    assert balance_by_size(2, model, sample, param_scale=0) == [2, 4]
+    assert balance_by_size(2, model, sample, param_scale=100) == [4, 2]

@@ -44,3 +44,12 @@ def test_wait_detaches():
     assert y is not x
     assert y.grad_fn is not None
     _ = current_stream(torch.device('cpu'))
+
+
+def test_wait_multiple_tensors_share_one_node():
+    a = torch.rand(2, requires_grad=True)
+    b = torch.rand(3, requires_grad=True)
+    a2, b2 = Wait.apply(CPUStream, CPUStream, a, b)
+    assert a2.grad_fn is b2.grad_fn
+    (a2.sum() + 2 * b2.sum()).backward()
+    assert torch.equal(a.grad, torch.ones(2)) and torch.equal(b.grad, torch.full((3,), 2.0))

@@ -86,6 +86,26 @@ class TestGPU:
         assert y.data_ptr() != ptr
         stream.synchronize()
 
+    def test_record_stream_shifted_view(self, gpu_sleep):
+        # A view that starts inside its allocation must still protect the block.
+        need_gpu()
+        alloc = new_stream(torch.device('cuda'))
+        with torch.cuda.stream(alloc):
+            x = torch.rand(2, device='cuda')
+        y = x[1:]
+        assert y.data_ptr() > x.data_ptr()
+        user = new_stream(torch.device('cuda'))
+        with use_stream(user):
+            gpu_sleep(0.3)
+        record_stream(y, user)
+        ptr = x.data_ptr()
+        del x, y
+        alloc.synchronize()
+        with torch.cuda.stream(alloc):
+            z = torch.rand(2, device='cuda')
+        assert z.data_ptr() != ptr
+        user.synchronize()
+
     def test_pool_ring(self):
         need_gpu()
         pool = StreamPool(2)
