@@ -1,0 +1,84 @@
+"""Winograd F(2x2,3x3) MFMA convolution vs the plain PyTorch fp32 convolution (GPU only)."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from torchgpipe_amd.ops import _ext
+from torchgpipe_amd.ops.conv import WinogradConv2d, winograd_conv2d
+
+pytestmark = pytest.mark.gpu
+cuda = torch.device('cuda', 0)
+
+
+@pytest.fixture(autouse=True)
+def need_ext():
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    assert _ext.available(), f'HIP extension must load on a GPU box: {_ext.load_error()!r}'
+
+
+SHAPES = [  # (N, C, K, H, W)
+    (2, 3, 64, 16, 16),     # C not a multiple of the 8-channel chunk (U-Net input conv)
+    (2, 64, 64, 24, 24),
+    (1, 5, 70, 7, 9),       # odd H/W, K not a multiple of 64
+    (3, 128, 256, 6, 6),
+    (2, 256, 128, 12, 12),
+    (1, 16, 8, 1, 1),
+    (4, 32, 32, 33, 2),
+]
+
+
+def _ref(x, w, b=None):
+    return F.conv2d(x.double(), w.double(), None if b is None else b.double(), padding=1)
+
+
+@pytest.mark.parametrize('shape', SHAPES)
+@pytest.mark.parametrize('bias', [False, True])
+def test_forward_backward_match_conv2d(shape, bias):
+    n, c, k, h, w = shape
+    torch.manual_seed(0)
+    x = torch.randn(n, c, h, w, device=cuda, requires_grad=True)
+    conv = WinogradConv2d(c, k, 3, padding=1, bias=bias).to(cuda)
+    y = conv(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+
+    xr = x.detach().double().requires_grad_(True)
+    wr = conv.weight.detach().double().requires_grad_(True)
+    br = conv.bias.detach().double().requires_grad_(True) if bias else None
+    yr = F.conv2d(xr, wr, br, padding=1)
+    yr.backward(dy.double())
+    scale = yr.abs().max().item() + 1
+    torch.testing.assert_close(y.double(), yr, rtol=1e-4, atol=2e-5 * scale)
+    torch.testing.assert_close(x.grad.double(), xr.grad, rtol=1e-4,
+                               atol=2e-5 * (xr.grad.abs().max().item() + 1))
+    torch.testing.assert_close(conv.weight.grad.double(), wr.grad, rtol=1e-4,
+                               atol=2e-5 * (wr.grad.abs().max().item() + 1))
+    if bias:
+        torch.testing.assert_close(conv.bias.grad.double(), br.grad, rtol=1e-4, atol=1e-3)
+
+
+def test_transform_cache_follows_weight_updates():
+    conv = WinogradConv2d(8, 16, 3, padding=1, bias=False).to(cuda)
+    x = torch.randn(2, 8, 10, 10, device=cuda)
+    a = conv(x)
+    with torch.no_grad():
+        conv.weight.mul_(2)  # in-place update bumps the version -> new transform
+    b = conv(x)
+    torch.testing.assert_close(b, 2 * a, rtol=1e-5, atol=1e-5)
+    clone = copy.deepcopy(conv)
+    torch.testing.assert_close(clone(x), b)
+
+
+def test_same_state_dict_as_conv2d():
+    conv = WinogradConv2d(4, 6, 3, padding=1)
+    plain = torch.nn.Conv2d(4, 6, 3, padding=1)
+    assert conv.state_dict().keys() == plain.state_dict().keys()
+
+
+def test_functional_falls_back_for_other_configs():
+    x = torch.randn(1, 4, 9, 9, device=cuda)
+    w = torch.randn(6, 4, 5, 5, device=cuda)
+    torch.testing.assert_close(winograd_conv2d(x, w), F.conv2d(x, w, padding=1))

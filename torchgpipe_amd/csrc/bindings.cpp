@@ -137,6 +137,55 @@ void copy_segments(at::TensorList srcs, at::TensorList dsts) {
   }
 }
 
+at::Tensor wino_weight(const at::Tensor& w, bool flip) {
+  check_f32_gpu(w, "weight");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "weight must be [K][C][3][3]");
+  const int64_t out_channels = flip ? w.size(1) : w.size(0);
+  const int64_t red_channels = flip ? w.size(0) : w.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  auto u = at::empty({wino_pad_reduction(red_channels), wino_pad_output(out_channels), 16},
+                     w.options());
+  launch_wino_weight(w.data_ptr<float>(), u.data_ptr<float>(), out_channels, red_channels, flip,
+                     stream_of(w));
+  return u;
+}
+
+at::Tensor wino_conv(const at::Tensor& x_in, const at::Tensor& u,
+                     const c10::optional<at::Tensor>& bias, int64_t out_channels,
+                     int64_t variant, int64_t splits) {
+  auto x = x_in.contiguous();
+  check_f32_gpu(x, "x");
+  check_f32_gpu(u, "u");
+  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+  const int64_t n = x.size(0), r = x.size(1), h = x.size(2), w = x.size(3);
+  TORCH_CHECK(u.dim() == 3 && u.size(2) == 16 && u.size(0) == wino_pad_reduction(r) &&
+                  u.size(1) == wino_pad_output(out_channels),
+              "transformed weight does not match the input/output channels");
+  TORCH_CHECK(u.device() == x.device(), "u must live on the input's device");
+  TORCH_CHECK(n * ((h + 1) / 2) * ((w + 1) / 2) < (int64_t{1} << 31) * 32,
+              "too many output tiles for one launch");
+  TORCH_CHECK(r * h * w < (int64_t{1} << 31) && out_channels < (1 << 24),
+              "plane too large for 32-bit channel offsets");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_f32_gpu(*bias, "bias");
+    TORCH_CHECK(bias->numel() == out_channels, "bias must have K elements");
+    bptr = bias->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(variant >= -1 && variant <= 1, "variant must be -1 (auto), 0 or 1");
+  auto y = at::empty({n, out_channels, h, w}, x.options());
+  if (y.numel() == 0) return y;
+  const WinoPlan plan = wino_plan(n, r, h, w, out_channels, static_cast<int>(variant),
+                                  static_cast<int>(splits));
+  at::Tensor ws;
+  if (plan.workspace > 0) ws = at::empty({plan.workspace}, x.options());
+  launch_wino_conv(x.data_ptr<float>(), u.data_ptr<float>(), bptr, y.data_ptr<float>(),
+                   plan.workspace > 0 ? ws.data_ptr<float>() : nullptr, n, r, h, w, out_channels,
+                   plan, stream_of(x));
+  return y;
+}
+
 }  // namespace
 }  // namespace tgpipe
 
@@ -152,6 +201,9 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("philox_uniform(int n, int seed, int offset, Device device) -> Tensor");
   m.def("spin(int ns, Device device) -> ()");
   m.def("copy_segments(Tensor[] srcs, Tensor(a!)[] dsts) -> ()");
+  m.def("wino_weight(Tensor w, bool flip) -> Tensor");
+  m.def("wino_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
+        "int splits=0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
@@ -161,6 +213,8 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("dna_backward", &tgpipe::dna_backward);
   m.impl("dropout", &tgpipe::dropout);
   m.impl("copy_segments", &tgpipe::copy_segments);
+  m.impl("wino_weight", &tgpipe::wino_weight);
+  m.impl("wino_conv", &tgpipe::wino_conv);
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CompositeExplicitAutograd, m) {

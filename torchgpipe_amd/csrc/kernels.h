@@ -48,4 +48,26 @@ struct Segment {
 constexpr int kMaxSegments = 16;
 void launch_segments_copy(const Segment* segs, int count, hipStream_t stream);
 
+// Winograd F(2x2,3x3) convolution (3x3, stride 1, pad 1, fp32 NCHW) on f32 MFMA.
+// Transformed weights: U[Rp][Op][16], Rp = wino_pad_reduction(R), Op = wino_pad_output(O).
+// flip = false: w is [O][R][3][3] (forward).  flip = true: w is [R][O][3][3] and the
+// kernel is rotated 180 degrees (backward-data: O = input channels, R = output channels).
+int64_t wino_pad_reduction(int64_t r);
+int64_t wino_pad_output(int64_t o);
+void launch_wino_weight(const float* w, float* u, int64_t out_channels, int64_t red_channels,
+                        bool flip, hipStream_t stream);
+// Launch plan: block-tile variant (0: 64 channels x 32 tiles, 1: 32 x 64) and the
+// number of reduction splits (> 1 needs a workspace of `workspace` floats).
+struct WinoPlan {
+  int variant = 0;
+  int splits = 1;
+  int64_t workspace = 0;
+};
+WinoPlan wino_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                   int variant, int splits);
+// y[N][O][H][W] = conv3x3(x[N][R][H][W]) (+ bias[O] if non-null).
+void launch_wino_conv(const float* x, const float* u, const float* bias, float* y, float* ws,
+                      int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                      const WinoPlan& plan, hipStream_t stream);
+
 }  // namespace tgpipe

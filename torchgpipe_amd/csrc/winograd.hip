@@ -1,0 +1,410 @@
+// Winograd F(2x2, 3x3) convolution on the fp32 MFMA pipes of CDNA4 (gfx950).
+//
+// The U-Net's 3x3 / stride 1 / pad 1 convolutions are ~60 % of its training
+// step.  MIOpen runs them with a VALU Winograd kernel at ~110 TFLOP/s
+// (direct-conv FLOP count); here the Winograd-domain products run on
+// v_mfma_f32_16x16x4_f32 instead, with the input transform fused in front of
+// the matrix core work and the output transform fused behind it:
+//
+//   for each block of 32 output tiles (2x2 pixels each) x 64 output channels:
+//     for each chunk of 8 input channels:
+//       V[xi][c][t] = (B^T d B)[xi]   4x4 input patch of tile t, channel c   (VALU -> LDS)
+//       U[xi][c][o]                   pre-transformed weights (G g G^T)     (global -> LDS)
+//       M[xi][o][t] += sum_c U[xi][c][o] * V[xi][c][t]   16 independent GEMMs (MFMA)
+//     Y[o][tile] = A^T M A                                     (registers -> global)
+//
+// Each wave owns 16 output channels x 32 tiles for ALL 16 Winograd positions
+// (32 accumulator tiles of 16x16), so the output transform needs no data
+// exchange: lane l holds positions 0..15 of the same (channel, tile) pair.
+// Numerics are exact f32 arithmetic (MFMA f32 is an fmaf chain); the Winograd
+// transform itself changes rounding relative to a direct convolution at the
+// 1e-6 relative level.
+//
+// Backward-data of a 3x3/s1/p1 convolution is the same convolution of dY with
+// the spatially flipped, in/out-transposed kernel: the weight transform takes a
+// `flip` flag, and the same main kernel runs it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "kernels.h"
+
+namespace tgpipe {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCB = 8;          // reduction channels per main-loop iteration
+constexpr int kOBMax = 64;      // output-channel padding granule of U
+constexpr int kThreads = 256;   // 4 waves
+
+__device__ const float kZeroTap = 0.f;  // load target of zero-padding taps
+
+// U[r][o][xi] = (G g G^T)[xi] for g = kernel of (output channel o, reduction
+// channel r), zero-padded to [Rp][Op][16].
+__global__ void wino_weight_kernel(const float* __restrict__ w, float* __restrict__ u, int O,
+                                   int R, int Op, int Rp, bool flip) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(Rp) * Op) return;
+  const int r = static_cast<int>(idx / Op);
+  const int o = static_cast<int>(idx % Op);
+  float g[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) g[i][j] = 0.f;
+  if (r < R && o < O) {
+    if (!flip) {  // w = [O][R][3][3]
+      const float* src = w + (static_cast<int64_t>(o) * R + r) * 9;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) g[i][j] = src[i * 3 + j];
+    } else {  // w = [R][O][3][3] (forward weights), rotated by 180 degrees
+      const float* src = w + (static_cast<int64_t>(r) * O + o) * 9;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) g[i][j] = src[(2 - i) * 3 + (2 - j)];
+    }
+  }
+  float t[4][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    t[0][j] = g[0][j];
+    t[1][j] = 0.5f * (g[0][j] + g[1][j] + g[2][j]);
+    t[2][j] = 0.5f * (g[0][j] - g[1][j] + g[2][j]);
+    t[3][j] = g[2][j];
+  }
+  // xi innermost: one (r, o) pair is 16 contiguous floats (4 x float4 stores).
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i * 4 + 0] = t[i][0];
+    v[i * 4 + 1] = 0.5f * (t[i][0] + t[i][1] + t[i][2]);
+    v[i * 4 + 2] = 0.5f * (t[i][0] - t[i][1] + t[i][2]);
+    v[i * 4 + 3] = t[i][2];
+  }
+  float4* dst = reinterpret_cast<float4*>(u + idx * 16);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dst[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+}
+
+// Block tile: (16*OW) output channels x (32*TW) output tiles; wave (wo, wt) owns
+// 16 channels x 32 tiles for all 16 Winograd positions (32 accumulator tiles).
+template <int OW, int TW>
+struct Tile {
+  static_assert(OW * TW == kThreads / 64, "four waves per block");
+  static constexpr int kOB = 16 * OW;
+  static constexpr int kTB = 32 * TW;
+  // LDS images keep the 16 Winograd positions of one (channel, o) / (channel, tile)
+  // pair contiguous, padded to 20 floats: a 16-lane group reading 16 B per lane at
+  // a 20-float stride covers all 64 banks once (ds_read_b128 conflict-free).
+  static constexpr int kXS = 20;
+  static constexpr int kUVec = kCB * kOB * 16 / 4 / kThreads;  // float4 of U per thread
+  static constexpr int kPairs = kCB * kTB / kThreads;          // (channel, tile) per thread
+};
+
+// Global -> registers staging of one reduction chunk (U slice + raw input patches).
+template <typename T>
+__device__ __forceinline__ void fetch_chunk(floatx4 (&ur)[T::kUVec], float (&xr)[T::kPairs][16],
+                                            const float* __restrict__ u,
+                                            const float* __restrict__ x,
+                                            const float* const (&xptr)[T::kPairs],
+                                            const uint32_t (&vmask)[T::kPairs], int c0, int Op,
+                                            int o0, int R, int W, int64_t HW, int tid) {
+#pragma unroll
+  for (int i = 0; i < T::kUVec; ++i) {
+    const int idx = i * kThreads + tid;       // float4 index inside the chunk
+    const int c = idx / (T::kOB * 4);
+    const int rest = idx - c * (T::kOB * 4);  // (o, xi/4) inside one channel row
+    ur[i] = *reinterpret_cast<const floatx4*>(
+        u + (static_cast<int64_t>(c0 + c) * Op + o0) * 16 + rest * 4);
+  }
+#pragma unroll
+  for (int k = 0; k < T::kPairs; ++k) {
+    const int c = c0 + (k * kThreads + tid) / T::kTB;
+    const uint32_t m = c < R ? vmask[k] : 0u;
+    const float* xp = xptr[k] + static_cast<int64_t>(c0) * HW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // Branch- and select-free: out-of-image taps read a zero word, so nothing
+        // consumes the loaded value before the MFMA phase that hides its latency.
+        const bool ok = (m >> (i * 4 + j)) & 1u;
+        xr[k][i * 4 + j] = *(ok ? xp + i * W + j : &kZeroTap);
+      }
+  }
+}
+
+template <int OW, int TW>
+__global__ __launch_bounds__(kThreads, 2) void wino_conv_kernel(
+    const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ bias,
+    float* __restrict__ y, int R, int H, int W, int O, int Rp, int Op, int TH, int TW_,
+    int64_t P, int tblocks, int oblocks, int splits) {
+  using T = Tile<OW, TW>;
+  __shared__ float Us[kCB * T::kOB * T::kXS];
+  __shared__ float Vs[kCB * T::kTB * T::kXS];
+
+  // XCD-aware bijective remap: consecutive logical blocks (same output-channel
+  // block, neighbouring tiles: they share every U chunk) land on one XCD's L2.
+  const int nwg = tblocks * oblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int q = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int tb = wgid % tblocks;
+  const int ob = (wgid / tblocks) % oblocks;
+  const int z = wgid / (tblocks * oblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wo = wave % OW;
+  const int wt = wave / OW;
+  const int64_t t0 = static_cast<int64_t>(tb) * T::kTB;
+  const int o0 = ob * T::kOB;
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int tiles_per_image = TH * TW_;
+
+  // Input-transform role: kPairs (channel, tile) pairs per thread and iteration.
+  const float* xptr[T::kPairs];
+  uint32_t vmask[T::kPairs];  // bit 4i+j: input pixel (i, j) of the patch is inside the image
+  int vofs[T::kPairs];        // LDS offset of the pair's 16 positions
+#pragma unroll
+  for (int k = 0; k < T::kPairs; ++k) {
+    const int pq = k * kThreads + tid;
+    const int tl = pq % T::kTB;
+    const int cl = pq / T::kTB;
+    const int64_t t = t0 + tl;
+    uint32_t m = 0;
+    int64_t n = 0;
+    int ty = 0, tx = 0;
+    if (t < P) {
+      n = t / tiles_per_image;
+      const int rem = static_cast<int>(t - n * tiles_per_image);
+      ty = rem / TW_;
+      tx = rem - ty * TW_;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int yy = 2 * ty - 1 + i, xx = 2 * tx - 1 + j;
+          if (yy >= 0 && yy < H && xx >= 0 && xx < W) m |= 1u << (i * 4 + j);
+        }
+    }
+    vmask[k] = m;
+    xptr[k] = x + (n * R + cl) * HW + static_cast<int64_t>(2 * ty - 1) * W + (2 * tx - 1);
+    vofs[k] = (cl * T::kTB + tl) * T::kXS;
+  }
+
+  floatx4 acc[16][2];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) {
+    acc[xi][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    acc[xi][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int nchunks = Rp / kCB;
+  const int c_begin = (z * nchunks / splits) * kCB;
+  const int c_end = ((z + 1) * nchunks / splits) * kCB;
+
+  // Register staging of the NEXT chunk (issued before the MFMA phase of the
+  // current one, consumed after it): global latency hides behind the matrix cores.
+  floatx4 ur[T::kUVec];
+  float xr[T::kPairs][16];
+  if (c_begin >= c_end) return;  // (never: every split owns >= 1 chunk)
+  fetch_chunk<T>(ur, xr, u, x, xptr, vmask, c_begin, Op, o0, R, W, HW, tid);
+  for (int c0 = c_begin; c0 < c_end; c0 += kCB) {
+    // -- staged registers -> LDS: U as is, input through V = B^T d B ------------------
+#pragma unroll
+    for (int i = 0; i < T::kUVec; ++i) {
+      const int idx = i * kThreads + tid;
+      const int c = idx / (T::kOB * 4);
+      const int rest = idx - c * (T::kOB * 4);
+      const int o = rest >> 2;
+      *reinterpret_cast<floatx4*>(&Us[(c * T::kOB + o) * T::kXS + (rest & 3) * 4]) = ur[i];
+    }
+#pragma unroll
+    for (int k = 0; k < T::kPairs; ++k) {
+      const float* d = xr[k];
+      float e[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[0][j] = d[0 * 4 + j] - d[2 * 4 + j];
+        e[1][j] = d[1 * 4 + j] + d[2 * 4 + j];
+        e[2][j] = d[2 * 4 + j] - d[1 * 4 + j];
+        e[3][j] = d[1 * 4 + j] - d[3 * 4 + j];
+      }
+      float4* vdst = reinterpret_cast<float4*>(&Vs[vofs[k]]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        vdst[i] = make_float4(e[i][0] - e[i][2], e[i][1] + e[i][2], e[i][2] - e[i][1],
+                              e[i][1] - e[i][3]);
+    }
+    __syncthreads();
+    // Unconditional (the last iteration re-reads its own chunk): a branch here makes
+    // the compiler wait for the loads on the spot instead of behind the MFMAs.
+    fetch_chunk<T>(ur, xr, u, x, xptr, vmask, min(c0 + kCB, c_end - kCB), Op, o0, R, W, HW,
+                        tid);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMA phase
+    // -- 16 GEMMs on the matrix cores: M[xi] += U[xi]^T V[xi] ----------------------------
+#pragma unroll
+    for (int ks = 0; ks < kCB / 4; ++ks) {
+      const int cr = ks * 4 + (lane >> 4);
+      const float4* ua =
+          reinterpret_cast<const float4*>(&Us[(cr * T::kOB + wo * 16 + (lane & 15)) * T::kXS]);
+      const float4* vb =
+          reinterpret_cast<const float4*>(&Vs[(cr * T::kTB + wt * 32 + (lane & 15)) * T::kXS]);
+      // Four positions at a time: 3 x ds_read_b128 feed 8 MFMAs (12 operand VGPRs).
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 a4 = ua[k];
+        const float4 b0 = vb[k];
+        const float4 b1 = vb[16 * T::kXS / 4 + k];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[4 * k + e][0] =
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b0[e], acc[4 * k + e][0], 0, 0, 0);
+          acc[4 * k + e][1] =
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b1[e], acc[4 * k + e][1], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // -- output transform Y = A^T M A, straight from the accumulators ---------------------
+  // Split-reduction partials go to slab z of the workspace (bias added by the reducer).
+  float* ydst = y + static_cast<int64_t>(z) * (P / tiles_per_image) * O * HW;
+  const bool add_bias = bias != nullptr && splits == 1;
+  const bool even_w = (W & 1) == 0;
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    const int64_t tp = t0 + wt * 32 + ph * 16 + (lane & 15);
+    if (tp >= P) continue;
+    const int64_t pn = tp / tiles_per_image;
+    const int prem = static_cast<int>(tp - pn * tiles_per_image);
+    const int pty = prem / TW_;
+    const int py = pty * 2;
+    const int px = (prem - pty * TW_) * 2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = o0 + wo * 16 + (lane >> 4) * 4 + r;
+      if (o >= O) continue;
+      float m[16];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) m[xi] = acc[xi][ph][r];
+      float s[2][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[0][j] = m[0 * 4 + j] + m[1 * 4 + j] + m[2 * 4 + j];
+        s[1][j] = m[1 * 4 + j] - m[2 * 4 + j] - m[3 * 4 + j];
+      }
+      const float b = add_bias ? bias[o] : 0.f;
+      float* yp = ydst + (pn * O + o) * HW + static_cast<int64_t>(py) * W + px;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (py + i >= H) break;
+        const float v0 = s[i][0] + s[i][1] + s[i][2] + b;
+        const float v1 = s[i][1] - s[i][2] - s[i][3] + b;
+        if (even_w) {
+          *reinterpret_cast<float2*>(yp + i * W) = make_float2(v0, v1);
+        } else {
+          yp[i * W] = v0;
+          if (px + 1 < W) yp[i * W + 1] = v1;
+        }
+      }
+    }
+  }
+}
+
+// y[i] = sum_z ws[z][i] (+ bias[o]) over the split-reduction partial slabs.
+__global__ void wino_split_reduce_kernel(const float* __restrict__ ws,
+                                         const float* __restrict__ bias, float* __restrict__ y,
+                                         int64_t numel, int64_t hw, int O, int splits) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= numel) return;
+  float v = bias ? bias[(i / hw) % O] : 0.f;
+  for (int z = 0; z < splits; ++z) v += ws[z * numel + i];
+  y[i] = v;
+}
+
+template <int OW, int TW>
+void launch_variant(const float* x, const float* u, const float* bias, float* y, float* ws,
+                    int64_t n, int64_t R, int64_t H, int64_t W, int64_t O, int splits,
+                    hipStream_t stream) {
+  using T = Tile<OW, TW>;
+  const int64_t Rp = wino_pad_reduction(R);
+  const int64_t Op = wino_pad_output(O);
+  const int64_t th = (H + 1) / 2, tw = (W + 1) / 2;
+  const int64_t P = n * th * tw;
+  const int tblocks = static_cast<int>((P + T::kTB - 1) / T::kTB);
+  const int oblocks = static_cast<int>((O + T::kOB - 1) / T::kOB);
+  const int64_t nwg = static_cast<int64_t>(tblocks) * oblocks * splits;
+  hipLaunchKernelGGL((wino_conv_kernel<OW, TW>), dim3(static_cast<unsigned>(nwg)),
+                     dim3(kThreads), 0, stream, x, u, bias, splits > 1 ? ws : y,
+                     static_cast<int>(R), static_cast<int>(H), static_cast<int>(W),
+                     static_cast<int>(O), static_cast<int>(Rp), static_cast<int>(Op),
+                     static_cast<int>(th), static_cast<int>(tw), P, tblocks, oblocks, splits);
+  if (splits > 1) {
+    const int64_t numel = n * O * H * W;
+    hipLaunchKernelGGL(wino_split_reduce_kernel, dim3(static_cast<unsigned>((numel + 255) / 256)),
+                       dim3(256), 0, stream, ws, bias, y, numel, H * W, static_cast<int>(O),
+                       splits);
+  }
+}
+
+}  // namespace
+
+int64_t wino_pad_reduction(int64_t r) { return (r + kCB - 1) / kCB * kCB; }
+int64_t wino_pad_output(int64_t o) { return (o + kOBMax - 1) / kOBMax * kOBMax; }
+
+void launch_wino_weight(const float* w, float* u, int64_t out_channels, int64_t red_channels,
+                        bool flip, hipStream_t stream) {
+  const int64_t Op = wino_pad_output(out_channels);
+  const int64_t Rp = wino_pad_reduction(red_channels);
+  const int64_t total = Rp * Op;
+  const int blocks = static_cast<int>((total + 255) / 256);
+  hipLaunchKernelGGL(wino_weight_kernel, dim3(blocks), dim3(256), 0, stream, w, u,
+                     static_cast<int>(out_channels), static_cast<int>(red_channels),
+                     static_cast<int>(Op), static_cast<int>(Rp), flip);
+}
+
+WinoPlan wino_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                   int variant, int splits) {
+  WinoPlan plan;
+  plan.variant = variant >= 0 ? variant : (out_channels <= 32 ? 1 : 0);
+  const int ob = plan.variant == 0 ? 64 : 32;
+  const int tbk = plan.variant == 0 ? 32 : 64;
+  const int64_t P = n * ((h + 1) / 2) * ((w + 1) / 2);
+  const int64_t blocks = ((P + tbk - 1) / tbk) * ((out_channels + ob - 1) / ob);
+  const int64_t chunks = wino_pad_reduction(red_channels) / kCB;
+  if (splits > 0) {
+    plan.splits = static_cast<int>(std::min<int64_t>(splits, chunks));
+  } else {
+    // Fill the chip: aim for >= 1024 blocks (2 per CU, 2 rounds), keeping >= 16
+    // channel chunks per split so the pipeline prologue stays amortised.
+    int64_t s = 1;
+    while (blocks * s < 1024 && chunks / (s * 2) >= 16) s *= 2;
+    plan.splits = static_cast<int>(s);
+  }
+  plan.workspace = plan.splits > 1 ? plan.splits * n * out_channels * h * w : 0;
+  return plan;
+}
+
+void launch_wino_conv(const float* x, const float* u, const float* bias, float* y, float* ws,
+                      int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                      const WinoPlan& plan, hipStream_t stream) {
+  if (plan.variant == 1) {
+    launch_variant<2, 2>(x, u, bias, y, ws, n, red_channels, h, w, out_channels, plan.splits,
+                         stream);
+  } else {
+    launch_variant<4, 1>(x, u, bias, y, ws, n, red_channels, h, w, out_channels, plan.splits,
+                         stream);
+  }
+}
+
+}  // namespace tgpipe

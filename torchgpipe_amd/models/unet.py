@@ -11,8 +11,10 @@ parameters, so the reference balance tables (e.g. p8 =
 
 ``fused=True`` (default) keeps the 241-layer structure but makes the
 ``dropout`` layer a :class:`~torchgpipe_amd.ops.fused.DropNormAct` HIP kernel
-(Dropout2d + InstanceNorm2d + LeakyReLU in one pass) and the ``norm`` /
-``relu`` layers identities.  Because every layer stays in place, any balance
+(Dropout2d + InstanceNorm2d + LeakyReLU in one pass), the ``norm`` /
+``relu`` layers identities, and the 3×3 convolutions
+:class:`~torchgpipe_amd.ops.conv.WinogradConv2d` (Winograd F(2,3) on the f32
+matrix cores; same parameters as ``nn.Conv2d``).  Because every layer stays in place, any balance
 that splits a cell between partitions still computes the same function, and
 the state-dict is identical (those layers have no parameters).
 """
@@ -24,6 +26,7 @@ from torch import Tensor, nn
 import torch.nn.functional as F
 
 from torchgpipe_amd.models.flatten import flatten_sequential
+from torchgpipe_amd.ops.conv import WinogradConv2d
 from torchgpipe_amd.ops.fused import DropNormAct
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
@@ -51,7 +54,8 @@ class PopCat(nn.Module):
 
 def conv_block(in_channels: int, out_channels: int, fused: bool) -> nn.Sequential:
     layers: 'OrderedDict[str, nn.Module]' = OrderedDict()
-    layers['conv'] = nn.Conv2d(in_channels, out_channels, kernel_size=3, padding=1, bias=False)
+    conv = WinogradConv2d if fused else nn.Conv2d
+    layers['conv'] = conv(in_channels, out_channels, kernel_size=3, padding=1, bias=False)
     if fused:
         layers['dropout'] = DropNormAct(p=0.1, eps=1e-5, negative_slope=1e-2)
         layers['norm'] = nn.Identity()
