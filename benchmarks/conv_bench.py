@@ -59,6 +59,9 @@ def main() -> None:
             t_mb = timeit(lambda: torch.ops.aten.convolution_backward(
                 dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
             t_wt = timeit(lambda: ops.wino_weight(w, False))
+            t_ww = timeit(lambda: ops.wino_wgrad(x, dy, 0))
+            t_mw = timeit(lambda: torch.ops.aten.convolution_backward(
+                dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
             sweep = {}
             if args.sweep:
                 for var in (0, 1):
@@ -70,6 +73,7 @@ def main() -> None:
                    'wino_fwd_ms': round(t_wf, 4), 'miopen_fwd_ms': round(t_mf, 4),
                    'wino_bwd_data_ms': round(t_wb, 4), 'miopen_bwd_data_ms': round(t_mb, 4),
                    'weight_transform_ms': round(t_wt, 4),
+                   'wino_wgrad_ms': round(t_ww, 4), 'miopen_wgrad_ms': round(t_mw, 4),
                    'wino_fwd_TFs': round(flop / t_wf / 1e9, 1),
                    'miopen_fwd_TFs': round(flop / t_mf / 1e9, 1),
                    'max_abs_err': err, 'sweep_fwd_ms': sweep}

@@ -82,3 +82,29 @@ def test_functional_falls_back_for_other_configs():
     x = torch.randn(1, 4, 9, 9, device=cuda)
     w = torch.randn(6, 4, 5, 5, device=cuda)
     torch.testing.assert_close(winograd_conv2d(x, w), F.conv2d(x, w, padding=1))
+
+
+@pytest.mark.parametrize('shape', SHAPES + [(2, 70, 40, 10, 12), (1, 8, 8, 2, 2)])
+def test_weight_gradient_kernel(shape):
+    n, c, k, h, w = shape
+    torch.manual_seed(1)
+    x = torch.randn(n, c, h, w, device=cuda)
+    dy = torch.randn(n, k, h, w, device=cuda)
+    ops = _ext.require(x)
+    want = torch.ops.aten.convolution_backward(
+        dy.double(), x.double(), torch.zeros(k, c, 3, 3, device=cuda, dtype=torch.float64), None,
+        [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    for splits in (0, 1, 3):
+        got = ops.wino_wgrad(x, dy, splits)
+        torch.testing.assert_close(got.double(), want, rtol=1e-4,
+                                   atol=2e-5 * (want.abs().max().item() + 1))
+
+
+def test_direct_ops_small_channels():
+    # the module routes C < 8 to MIOpen; the kernel itself must still be right there
+    x = torch.randn(2, 5, 9, 7, device=cuda)
+    w = torch.randn(70, 5, 3, 3, device=cuda)
+    ops = _ext.require(x)
+    for variant in (0, 1):
+        y = ops.wino_conv(x, ops.wino_weight(w, False), None, 70, variant, 0)
+        torch.testing.assert_close(y.double(), _ref(x, w), rtol=1e-4, atol=1e-4)

@@ -186,6 +186,29 @@ at::Tensor wino_conv(const at::Tensor& x_in, const at::Tensor& u,
   return y;
 }
 
+at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits) {
+  auto x = x_in.contiguous();
+  auto dy = dy_in.contiguous();
+  check_f32_gpu(x, "x");
+  check_f32_gpu(dy, "dy");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "x and dy must be NCHW");
+  const int64_t n = x.size(0), c = x.size(1), h = x.size(2), w = x.size(3), k = dy.size(1);
+  TORCH_CHECK(dy.size(0) == n && dy.size(2) == h && dy.size(3) == w,
+              "dy must be [N][K][H][W] of a 3x3/s1/p1 convolution of x");
+  TORCH_CHECK(dy.device() == x.device(), "x and dy must share a device");
+  TORCH_CHECK(c * h * w < (int64_t{1} << 31) && k * h * w < (int64_t{1} << 31),
+              "plane too large for 32-bit channel offsets");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto dw = at::empty({k, c, 3, 3}, x.options());
+  if (n == 0 || h == 0 || w == 0) return dw.zero_();
+  const int s = splits > 0 ? static_cast<int>(splits) : wino_wgrad_splits(n, c, k, h, w);
+  at::Tensor ws;
+  if (s > 1) ws = at::empty({s * k * c * 9}, x.options());
+  launch_wino_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), dw.data_ptr<float>(),
+                    s > 1 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s, stream_of(x));
+  return dw;
+}
+
 }  // namespace
 }  // namespace tgpipe
 
@@ -202,6 +225,7 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("spin(int ns, Device device) -> ()");
   m.def("copy_segments(Tensor[] srcs, Tensor(a!)[] dsts) -> ()");
   m.def("wino_weight(Tensor w, bool flip) -> Tensor");
+  m.def("wino_wgrad(Tensor x, Tensor dy, int splits=0) -> Tensor");
   m.def("wino_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
 }
@@ -215,6 +239,7 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("copy_segments", &tgpipe::copy_segments);
   m.impl("wino_weight", &tgpipe::wino_weight);
   m.impl("wino_conv", &tgpipe::wino_conv);
+  m.impl("wino_wgrad", &tgpipe::wino_wgrad);
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CompositeExplicitAutograd, m) {

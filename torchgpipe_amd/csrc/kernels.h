@@ -70,4 +70,11 @@ void launch_wino_conv(const float* x, const float* u, const float* bias, float* 
                       int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                       const WinoPlan& plan, hipStream_t stream);
 
+// Weight gradient of the same convolution: dw[K][C][3][3] from x[N][C][H][W] and
+// dy[N][K][H][W]; `splits` > 1 needs a workspace of splits*K*C*9 floats.
+int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
+void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
+                       int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                       hipStream_t stream);
+
 }  // namespace tgpipe

@@ -39,7 +39,7 @@ constexpr int kCB = 8;          // reduction channels per main-loop iteration
 constexpr int kOBMax = 64;      // output-channel padding granule of U
 constexpr int kThreads = 256;   // 4 waves
 
-__device__ const float kZeroTap = 0.f;  // load target of zero-padding taps
+__device__ float kZeroTap = 0.f;  // load target of zero-padding taps (never written)
 
 // U[r][o][xi] = (G g G^T)[xi] for g = kernel of (output channel o, reduction
 // channel r), zero-padded to [Rp][Op][16].
@@ -357,6 +357,234 @@ void launch_variant(const float* x, const float* u, const float* bias, float* y,
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Weight gradient.  With V_t = B^T d_t B (input patch of tile t) and
+// M'_t = A dY_t A^T (output-gradient tile lifted to the 4x4 Winograd domain):
+//   dU[xi][c][k] = sum_t V_t[xi][c] * M'_t[xi][k]     16 GEMMs reducing over tiles
+//   dW[k][c]     = G^T dU[k][c] G                     (in-register, per lane)
+// Block: 64 input channels x 32 output channels; wave w owns channels 16w..16w+15
+// for both 16-wide k halves and all 16 positions.  The tile range is split over
+// gridDim (deterministic: per-split partial dW slabs, summed by a reduce kernel).
+constexpr int kWC = 64;   // input channels per block
+constexpr int kWK = 32;   // output channels per block
+constexpr int kWT = 8;    // tiles per main-loop iteration
+constexpr int kWS = 20;   // padded LDS stride of one (tile, channel) position vector
+
+// Registers <- global for one wgrad iteration: two 4x4 input patches and one 2x2
+// output-gradient patch per thread.  Out-of-range taps load from the tensor base
+// and are zeroed later through `xmask` / `ymask` (applied in the staging phase, so
+// nothing consumes a load before the MFMA phase that hides its latency).
+__device__ __forceinline__ void wgrad_fetch(float (&xr)[2][16], float (&yr)[4], uint32_t& xmask,
+                                            uint32_t& ymask, const float* __restrict__ x,
+                                            const float* __restrict__ dy, int64_t it, int xt,
+                                            int xc, int yt, int yk, int c0, int k0, int C, int K,
+                                            int H, int W, int TW_, int tiles_per_image,
+                                            int64_t P, int64_t HW) {
+  xmask = 0;
+  ymask = 0;
+  {
+    // 32-bit tile arithmetic (the host guarantees P < 2^31).
+    const int t = static_cast<int>(it) * kWT + xt;
+    const bool tv = t < P;
+    const int tt = tv ? t : 0;
+    const int n = tt / tiles_per_image;
+    const int rem = tt - n * tiles_per_image;
+    const int ty = rem / TW_;
+    const int tx = rem - ty * TW_;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int c = c0 + xc + pr * 32;
+      const bool cv = tv && c < C;
+      const float* xp =
+          x + (static_cast<int64_t>(n) * C + c) * HW + static_cast<int64_t>(2 * ty - 1) * W +
+          (2 * tx - 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool rok = cv && 2 * ty - 1 + i >= 0 && 2 * ty - 1 + i < H;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = rok && 2 * tx - 1 + j >= 0 && 2 * tx - 1 + j < W;
+          xmask |= static_cast<uint32_t>(ok) << (pr * 16 + i * 4 + j);
+          xr[pr][i * 4 + j] = *(ok ? xp + i * W + j : x);
+        }
+      }
+    }
+  }
+  {
+    const int t = static_cast<int>(it) * kWT + yt;
+    const bool tv = t < P;
+    const int tt = tv ? t : 0;
+    const int n = tt / tiles_per_image;
+    const int rem = tt - n * tiles_per_image;
+    const int ty = rem / TW_;
+    const int tx = rem - ty * TW_;
+    const int k = k0 + yk;
+    const bool kv = tv && k < K;
+    const float* yp =
+        dy + (static_cast<int64_t>(n) * K + k) * HW + static_cast<int64_t>(2 * ty) * W + 2 * tx;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool ok = kv && 2 * ty + i < H && 2 * tx + j < W;
+        ymask |= static_cast<uint32_t>(ok) << (i * 2 + j);
+        yr[i * 2 + j] = *(ok ? yp + i * W + j : dy);
+      }
+  }
+}
+
+__global__ __launch_bounds__(kThreads, 2) void wino_wgrad_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dw, int C,
+    int K, int H, int W, int TH, int TW_, int64_t P, int cblocks, int kblocks, int splits) {
+  __shared__ float Vs[kWT * kWC * kWS];
+  __shared__ float Ms[kWT * kWK * kWS];
+
+  const int nwg = cblocks * kblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int q = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int cb = wgid % cblocks;
+  const int kb = (wgid / cblocks) % kblocks;
+  const int z = wgid / (cblocks * kblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int c0 = cb * kWC;
+  const int k0 = kb * kWK;
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int tiles_per_image = TH * TW_;
+  const int64_t iters_total = (P + kWT - 1) / kWT;
+  const int64_t it_begin = z * iters_total / splits;
+  const int64_t it_end = (z + 1) * iters_total / splits;
+
+  // roles: two (channel, tile) input pairs and one (k, tile) gradient pair per thread
+  const int xt = tid % kWT;          // tile slot of both input pairs
+  const int xc = tid / kWT;          // channel of pair 0 (pair 1: + 32)
+  const int yt = tid % kWT;
+  const int yk = tid / kWT;          // 0..31
+
+  floatx4 acc[16][2];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) {
+    acc[xi][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    acc[xi][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  float xr[2][16];
+  float yr[4];
+  uint32_t xmask = 0, ymask = 0;
+  if (it_begin < it_end)
+    wgrad_fetch(xr, yr, xmask, ymask, x, dy, it_begin, xt, xc, yt, yk, c0, k0, C, K, H, W, TW_,
+                tiles_per_image, P, HW);
+  for (int64_t it = it_begin; it < it_end; ++it) {
+    // -- stage: V = B^T d B for both input pairs, M' = A dY A^T for the gradient pair ---
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      float d[16];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) d[b] = (xmask >> (pr * 16 + b)) & 1u ? xr[pr][b] : 0.f;
+      float e[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[0][j] = d[0 * 4 + j] - d[2 * 4 + j];
+        e[1][j] = d[1 * 4 + j] + d[2 * 4 + j];
+        e[2][j] = d[2 * 4 + j] - d[1 * 4 + j];
+        e[3][j] = d[1 * 4 + j] - d[3 * 4 + j];
+      }
+      floatx4* vdst = reinterpret_cast<floatx4*>(&Vs[(xt * kWC + xc + pr * 32) * kWS]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        vdst[i] = floatx4{e[i][0] - e[i][2], e[i][1] + e[i][2], e[i][2] - e[i][1],
+                          e[i][1] - e[i][3]};
+    }
+    {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) yr[b] = (ymask >> b) & 1u ? yr[b] : 0.f;
+      float r[4][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        r[0][j] = yr[0 * 2 + j];
+        r[1][j] = yr[0 * 2 + j] + yr[1 * 2 + j];
+        r[2][j] = yr[0 * 2 + j] - yr[1 * 2 + j];
+        r[3][j] = -yr[1 * 2 + j];
+      }
+      floatx4* mdst = reinterpret_cast<floatx4*>(&Ms[(yt * kWK + yk) * kWS]);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        mdst[a] = floatx4{r[a][0], r[a][0] + r[a][1], r[a][0] - r[a][1], -r[a][1]};
+    }
+    __syncthreads();
+    wgrad_fetch(xr, yr, xmask, ymask, x, dy, it + 1 < it_end ? it + 1 : it, xt, xc, yt, yk, c0, k0, C, K, H,
+                W, TW_, tiles_per_image, P, HW);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < kWT / 4; ++ks) {
+      const int tr = ks * 4 + (lane >> 4);
+      const floatx4* va =
+          reinterpret_cast<const floatx4*>(&Vs[(tr * kWC + wave * 16 + (lane & 15)) * kWS]);
+      const floatx4* mb = reinterpret_cast<const floatx4*>(&Ms[(tr * kWK + (lane & 15)) * kWS]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const floatx4 a4 = va[k];
+        const floatx4 b0 = mb[k];
+        const floatx4 b1 = mb[16 * kWS / 4 + k];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[4 * k + e][0] =
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b0[e], acc[4 * k + e][0], 0, 0, 0);
+          acc[4 * k + e][1] =
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b1[e], acc[4 * k + e][1], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // -- dW = G^T dU G per (c, k) pair; partial slab z of [splits][K][C][9] --------------
+  float* out = dw + static_cast<int64_t>(z) * K * C * 9;
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    const int k = k0 + ph * 16 + (lane & 15);
+    if (k >= K) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = c0 + wave * 16 + (lane >> 4) * 4 + r;
+      if (c >= C) continue;
+      float u[16];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) u[xi] = acc[xi][ph][r];
+      float t[3][4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float s12 = 0.5f * (u[1 * 4 + b] + u[2 * 4 + b]);
+        t[0][b] = u[0 * 4 + b] + s12;
+        t[1][b] = 0.5f * (u[1 * 4 + b] - u[2 * 4 + b]);
+        t[2][b] = s12 + u[3 * 4 + b];
+      }
+      float* o = out + (static_cast<int64_t>(k) * C + c) * 9;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const float s12 = 0.5f * (t[i][1] + t[i][2]);
+        o[i * 3 + 0] = t[i][0] + s12;
+        o[i * 3 + 1] = 0.5f * (t[i][1] - t[i][2]);
+        o[i * 3 + 2] = s12 + t[i][3];
+      }
+    }
+  }
+}
+
+__global__ void wino_wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
+                                         int64_t numel, int splits) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= numel) return;
+  float v = 0.f;
+  for (int z = 0; z < splits; ++z) v += ws[z * numel + i];
+  dw[i] = v;
+}
+
 }  // namespace
 
 int64_t wino_pad_reduction(int64_t r) { return (r + kCB - 1) / kCB * kCB; }
@@ -404,6 +632,36 @@ void launch_wino_conv(const float* x, const float* u, const float* bias, float* 
   } else {
     launch_variant<4, 1>(x, u, bias, y, ws, n, red_channels, h, w, out_channels, plan.splits,
                          stream);
+  }
+}
+
+int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
+  const int64_t P = n * ((h + 1) / 2) * ((w + 1) / 2);
+  const int64_t tiles_blocks = ((c + kWC - 1) / kWC) * ((k + kWK - 1) / kWK);
+  const int64_t iters = (P + kWT - 1) / kWT;
+  int64_t s = (1024 + tiles_blocks - 1) / tiles_blocks;
+  s = std::min<int64_t>(s, std::max<int64_t>(1, iters / 16));  // >= 16 iterations per split
+  s = std::min<int64_t>(s, 256);
+  return static_cast<int>(std::max<int64_t>(s, 1));
+}
+
+void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
+                       int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                       hipStream_t stream) {
+  const int64_t th = (h + 1) / 2, tw = (w + 1) / 2;
+  const int64_t P = n * th * tw;
+  const int cblocks = static_cast<int>((c + kWC - 1) / kWC);
+  const int kblocks = static_cast<int>((k + kWK - 1) / kWK);
+  const int64_t nwg = static_cast<int64_t>(cblocks) * kblocks * splits;
+  hipLaunchKernelGGL(wino_wgrad_kernel, dim3(static_cast<unsigned>(nwg)), dim3(kThreads), 0,
+                     stream, x, dy, splits > 1 ? ws : dw, static_cast<int>(c),
+                     static_cast<int>(k), static_cast<int>(h), static_cast<int>(w),
+                     static_cast<int>(th), static_cast<int>(tw), P, cblocks, kblocks, splits);
+  if (splits > 1) {
+    const int64_t numel = k * c * 9;
+    hipLaunchKernelGGL(wino_wgrad_reduce_kernel,
+                       dim3(static_cast<unsigned>((numel + 255) / 256)), dim3(256), 0, stream,
+                       ws, dw, numel, splits);
   }
 }
 

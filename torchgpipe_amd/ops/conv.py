@@ -3,7 +3,8 @@
 :class:`WinogradConv2d` is a drop-in ``nn.Conv2d`` (same parameters, same
 state-dict keys) whose 3×3 / stride 1 / pad 1 / fp32 GPU forward and
 backward-data run the fused HIP kernel of ``csrc/winograd.hip``; the weight
-gradient stays on MIOpen's implicit-GEMM (already ≈ 140 TFLOP/s-equivalent).
+gradient runs the Winograd wgrad kernel on large planes and MIOpen's
+implicit GEMM elsewhere (see ``_wgrad_on_mfma``).
 Other configurations, CPU tensors and non-fp32 dtypes use ``F.conv2d``.
 
 The Winograd-domain weights ``U = G g Gᵀ`` (and the rotated/transposed ``U'``
@@ -64,12 +65,26 @@ class _WinogradConv(torch.autograd.Function):
             dx = _ext.require(dy).wino_conv(dy, ctx.cache.get(weight, True), None,
                                              weight.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(
-                dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                [False, True, False])[1]
+            if _wgrad_on_mfma(x, weight):
+                dw = _ext.require(dy).wino_wgrad(x, dy, 0)
+            else:
+                dw = torch.ops.aten.convolution_backward(
+                    dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                    [False, True, False])[1]
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum((0, 2, 3))
         return dx, dw, db, None
+
+
+def _wgrad_on_mfma(x: Tensor, weight: Tensor) -> bool:
+    """Weight gradient on the Winograd MFMA kernel where it beats MIOpen's wrw.
+
+    benchmarks/conv_bench.py (profiles/conv_bench.json): the Winograd wgrad wins
+    on large planes (64->64 @192²: 1.05 vs 1.42 ms, 128->32 @192²: 1.18 vs 1.74 ms
+    at N=40) and ties or loses below 96² where MIOpen's implicit GEMM has
+    enough channels to fill its tiles.
+    """
+    return x.shape[2] * x.shape[3] >= 96 * 96 and weight.shape[1] >= 64
 
 
 # Below this many input channels the 8-channel reduction chunk is mostly padding
