@@ -251,26 +251,50 @@ __global__ __launch_bounds__(kThreads, 2) void wino_conv_kernel(
                         tid);
     __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMA phase
     // -- 16 GEMMs on the matrix cores: M[xi] += U[xi]^T V[xi] ----------------------------
+    // 8 operand groups (2 channel quads x 4 position quads), each 3 x ds_read_b128
+    // feeding 8 MFMAs; group g+1 is read while group g's MFMAs issue, so the LDS
+    // latency hides behind the matrix pipe instead of stalling it.
+    {
+      const float4* ua0 =
+          reinterpret_cast<const float4*>(&Us[((lane >> 4) * T::kOB + wo * 16 + (lane & 15)) *
+                                              T::kXS]);
+      const float4* vb0 =
+          reinterpret_cast<const float4*>(&Vs[((lane >> 4) * T::kTB + wt * 32 + (lane & 15)) *
+                                              T::kXS]);
+      constexpr int kUQuad = 4 * T::kOB * T::kXS / 4;  // float4 stride of 4 channels in Us
+      constexpr int kVQuad = 4 * T::kTB * T::kXS / 4;
+      constexpr int kVHalf = 16 * T::kXS / 4;           // second 16-tile half
+      floatx4 a_c = *reinterpret_cast<const floatx4*>(ua0);
+      floatx4 b0_c = *reinterpret_cast<const floatx4*>(vb0);
+      floatx4 b1_c = *reinterpret_cast<const floatx4*>(vb0 + kVHalf);
 #pragma unroll
-    for (int ks = 0; ks < kCB / 4; ++ks) {
-      const int cr = ks * 4 + (lane >> 4);
-      const float4* ua =
-          reinterpret_cast<const float4*>(&Us[(cr * T::kOB + wo * 16 + (lane & 15)) * T::kXS]);
-      const float4* vb =
-          reinterpret_cast<const float4*>(&Vs[(cr * T::kTB + wt * 32 + (lane & 15)) * T::kXS]);
-      // Four positions at a time: 3 x ds_read_b128 feed 8 MFMAs (12 operand VGPRs).
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float4 a4 = ua[k];
-        const float4 b0 = vb[k];
-        const float4 b1 = vb[16 * T::kXS / 4 + k];
+      for (int g = 0; g < (kCB / 4) * 4; ++g) {
+        floatx4 a_n = a_c, b0_n = b0_c, b1_n = b1_c;
+        if (g + 1 < (kCB / 4) * 4) {
+          const int ks = (g + 1) >> 2, k = (g + 1) & 3;
+          a_n = *reinterpret_cast<const floatx4*>(ua0 + ks * kUQuad + k);
+          b0_n = *reinterpret_cast<const floatx4*>(vb0 + ks * kVQuad + k);
+          b1_n = *reinterpret_cast<const floatx4*>(vb0 + ks * kVQuad + kVHalf + k);
+        }
+        const int k = g & 3;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           acc[4 * k + e][0] =
-              __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b0[e], acc[4 * k + e][0], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a_c[e], b0_c[e], acc[4 * k + e][0], 0, 0, 0);
           acc[4 * k + e][1] =
-              __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b1[e], acc[4 * k + e][1], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a_c[e], b1_c[e], acc[4 * k + e][1], 0, 0, 0);
         }
+        a_c = a_n;
+        b0_c = b0_n;
+        b1_c = b1_n;
+      }
+      // Pin the interleave for the machine scheduler: group 0's reads, then per group
+      // the next group's 3 LDS reads ahead of this group's 8 MFMAs.
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+      for (int g = 0; g < (kCB / 4) * 4; ++g) {
+        if (g + 1 < (kCB / 4) * 4) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
       }
     }
     __syncthreads();
@@ -520,24 +544,42 @@ __global__ __launch_bounds__(kThreads, 2) void wino_wgrad_kernel(
     wgrad_fetch(xr, yr, xmask, ymask, x, dy, it + 1 < it_end ? it + 1 : it, xt, xc, yt, yk, c0, k0, C, K, H,
                 W, TW_, tiles_per_image, P, HW);
     __builtin_amdgcn_sched_barrier(0);
+    {
+      // same software-pipelined operand groups as the forward kernel
+      const floatx4* va0 =
+          reinterpret_cast<const floatx4*>(&Vs[((lane >> 4) * kWC + wave * 16 + (lane & 15)) * kWS]);
+      const floatx4* mb0 = reinterpret_cast<const floatx4*>(&Ms[((lane >> 4) * kWK + (lane & 15)) * kWS]);
+      constexpr int kVQuad = 4 * kWC * kWS / 4;
+      constexpr int kMQuad = 4 * kWK * kWS / 4;
+      constexpr int kMHalf = 16 * kWS / 4;
+      constexpr int kGroups = (kWT / 4) * 4;
+      floatx4 a_c = va0[0], b0_c = mb0[0], b1_c = mb0[kMHalf];
 #pragma unroll
-    for (int ks = 0; ks < kWT / 4; ++ks) {
-      const int tr = ks * 4 + (lane >> 4);
-      const floatx4* va =
-          reinterpret_cast<const floatx4*>(&Vs[(tr * kWC + wave * 16 + (lane & 15)) * kWS]);
-      const floatx4* mb = reinterpret_cast<const floatx4*>(&Ms[(tr * kWK + (lane & 15)) * kWS]);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const floatx4 a4 = va[k];
-        const floatx4 b0 = mb[k];
-        const floatx4 b1 = mb[16 * kWS / 4 + k];
+      for (int g = 0; g < kGroups; ++g) {
+        floatx4 a_n = a_c, b0_n = b0_c, b1_n = b1_c;
+        if (g + 1 < kGroups) {
+          const int ks = (g + 1) >> 2, k = (g + 1) & 3;
+          a_n = va0[ks * kVQuad + k];
+          b0_n = mb0[ks * kMQuad + k];
+          b1_n = mb0[ks * kMQuad + kMHalf + k];
+        }
+        const int k = g & 3;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           acc[4 * k + e][0] =
-              __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b0[e], acc[4 * k + e][0], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a_c[e], b0_c[e], acc[4 * k + e][0], 0, 0, 0);
           acc[4 * k + e][1] =
-              __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b1[e], acc[4 * k + e][1], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a_c[e], b1_c[e], acc[4 * k + e][1], 0, 0, 0);
         }
+        a_c = a_n;
+        b0_c = b0_n;
+        b1_c = b1_n;
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+      for (int g = 0; g < kGroups; ++g) {
+        if (g + 1 < kGroups) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
       }
     }
     __syncthreads();
