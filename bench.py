@@ -32,19 +32,21 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 # Reference (Tesla P40) throughputs of the same experiments, BASELINE.md §1/§2.
 # Batch / chunks / reference balance are the reference's experiment tables.
-# ``tuned`` balances were re-derived for MI355X + MIOpen: per-layer device times
-# measured on MI355X (profiles/unet_layer_profile.json, benchmarks/layer_profile.py)
-# fed to the step simulator (torchgpipe_amd.balance.simulate.optimize, 60 GB/s
-# links); per-stage device times checked with benchmarks/stage_harness.py
-# (profiles/stage_harness_p8_{tuned,ref}.json: max stage 359 ms tuned vs 613 ms ref).
+# ``tuned`` balances were re-derived for MI355X with the Winograd-MFMA convolutions:
+# per-layer device times measured on MI355X (profiles/unet_layer_profile_wino.json,
+# benchmarks/layer_profile.py) fed to the step simulator (scripts/tune_balance.py →
+# torchgpipe_amd.balance.simulate.optimize, 60 GB/s links), then corrected with the
+# per-stage device times of benchmarks/stage_harness.py
+# (profiles/stage_harness_p8_wino.json: max stage 327 ms before moving one conv cell
+# from stage 4 to stage 3; the reference's P40 balance has a 613 ms max stage).
 UNET_EXPERIMENTS = {
     1: dict(name='pipeline-1', batch=80, chunks=2, balance=[241], tuned=[241], ref=24.456),
-    2: dict(name='pipeline-2', batch=512, chunks=32, balance=[104, 137], tuned=[97, 144],
+    2: dict(name='pipeline-2', batch=512, chunks=32, balance=[104, 137], tuned=[96, 145],
             ref=35.502),
     4: dict(name='pipeline-4', batch=512, chunks=16, balance=[30, 66, 84, 61],
-            tuned=[39, 54, 58, 90], ref=67.042),
+            tuned=[39, 57, 62, 83], ref=67.042),
     8: dict(name='pipeline-8', batch=640, chunks=40, balance=[16, 27, 31, 44, 22, 57, 27, 17],
-            tuned=[18, 27, 29, 23, 25, 33, 44, 42], ref=88.497),
+            tuned=[20, 26, 25, 29, 19, 37, 45, 40], ref=88.497),
 }
 # AmoebaNet tuned balances: profiles/amoebanet_layer_profile.json (micro-batch 40) through
 # the same simulator (n2 535 vs 492, n4 851 vs 814, n8 1539 vs 1503 simulated samples/s).
