@@ -105,6 +105,25 @@ def test_direct_ops_small_channels():
     x = torch.randn(2, 5, 9, 7, device=cuda)
     w = torch.randn(70, 5, 3, 3, device=cuda)
     ops = _ext.require(x)
-    for variant in (0, 1):
+    for variant in (0, 1, 2):
         y = ops.wino_conv(x, ops.wino_weight(w, False), None, 70, variant, 0)
         torch.testing.assert_close(y.double(), _ref(x, w), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('variant', [0, 1, 2])
+@pytest.mark.parametrize('shape', [(2, 64, 64, 24, 24), (1, 24, 130, 14, 10), (3, 16, 96, 9, 12),
+                                   (2, 40, 64, 8, 8)])
+@pytest.mark.parametrize('splits', [0, 1, 3])
+def test_forward_variants_and_splits(variant, shape, splits):
+    # variant 2 = double-buffered one-workgroup-per-CU kernel (paired 16-byte stores when
+    # W % 4 == 0 and H is even; plain stores otherwise)
+    n, c, k, h, w = shape
+    torch.manual_seed(2)
+    x = torch.randn(n, c, h, w, device=cuda)
+    wt = torch.randn(k, c, 3, 3, device=cuda)
+    b = torch.randn(k, device=cuda)
+    ops = _ext.require(x)
+    y = ops.wino_conv(x, ops.wino_weight(wt, False), b, k, variant, splits)
+    want = _ref(x, wt, b)
+    torch.testing.assert_close(y.double(), want, rtol=1e-4,
+                               atol=2e-5 * (want.abs().max().item() + 1))

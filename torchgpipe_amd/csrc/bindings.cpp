@@ -173,7 +173,7 @@ at::Tensor wino_conv(const at::Tensor& x_in, const at::Tensor& u,
     bptr = bias->data_ptr<float>();
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  TORCH_CHECK(variant >= -1 && variant <= 1, "variant must be -1 (auto), 0 or 1");
+  TORCH_CHECK(variant >= -1 && variant <= 2, "variant must be -1 (auto), 0, 1 or 2");
   auto y = at::empty({n, out_channels, h, w}, x.options());
   if (y.numel() == 0) return y;
   const WinoPlan plan = wino_plan(n, r, h, w, out_channels, static_cast<int>(variant),

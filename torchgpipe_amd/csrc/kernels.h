@@ -56,7 +56,8 @@ int64_t wino_pad_reduction(int64_t r);
 int64_t wino_pad_output(int64_t o);
 void launch_wino_weight(const float* w, float* u, int64_t out_channels, int64_t red_channels,
                         bool flip, hipStream_t stream);
-// Launch plan: block-tile variant (0: 64 channels x 32 tiles, 1: 32 x 64) and the
+// Launch plan: block-tile variant (0: 64 channels x 32 tiles, 1: 32 x 64, 2: 64 x 64
+// double-buffered, one workgroup per CU) and the
 // number of reduction splits (> 1 needs a workspace of `workspace` floats).
 struct WinoPlan {
   int variant = 0;

@@ -383,6 +383,362 @@ void launch_variant(const float* x, const float* u, const float* bias, float* y,
 
 
 // ---------------------------------------------------------------------------------------
+// Variant 2: 64 output channels x 64 tiles per workgroup of 8 waves, ONE workgroup per
+// CU (two waves per SIMD), LDS double-buffered so one barrier per channel chunk
+// suffices, and the staging of chunk c+1 (global -> registers -> input transform ->
+// LDS) cut into small slots that ride between the MFMAs of chunk c.
+//
+// Why: with two 4-wave workgroups per CU (variants 0/1) both blocks' MFMA phases and
+// both blocks' staging phases fall into step through their barriers, so the matrix
+// pipe idles during staging (rocprofv3: SQ_VALU_MFMA_BUSY_CYCLES = 41 % of the SIMD
+// cycles on 40x64x192^2).  Here staging never has a phase of its own: an f32 MFMA
+// holds the SIMD's issue for 8 of its 32 cycles, the rest carries the loads, the LDS
+// stores and the transform, and the partner wave on the SIMD fills what is left.
+//
+// Wave (wo, wt) = (wave & 1, wave >> 1) owns 32 channels x 16 tiles for all 16
+// Winograd positions (2 accumulator tiles of 16 x 16 per position, 128 registers).
+// Each (channel quad, position quad) operand group is 3 ds_read_b128 feeding 8 MFMAs.
+constexpr int kDBT = 64;                      // tiles per workgroup
+constexpr int kDBO = 64;                      // output channels per workgroup
+constexpr int kDBThreads = 512;
+constexpr int kDBImg = kCB * 64 * 20;         // floats per LDS operand image
+
+struct DbStage {
+  floatx4 ur[4];   // U of the staged chunk: channel 2i + (tid >> 8), float4 (tid & 255)
+  float xr[16];    // raw 4x4 patch: channel tid >> 6, tile tid & 63
+};
+
+struct DbCtx {
+  float* Us_next;          // LDS images being filled (the other buffer)
+  float* Vs_next;
+  const float* u_next;     // this thread's U float4 in channel row 0 of the prefetch
+  const float* xp_next;    // this thread's (channel, image) plane of the prefetch
+  int64_t u_row;           // 2 * Op * 16: float stride between this thread's U rows
+  uint32_t vmask;
+  int tid;
+};
+
+// Staging work of one pipeline step, in slots (slot S runs after MFMA 2S + 1): the 4 U
+// stores, the input transform of the (channel, tile) pair and its 4 V stores, then the
+// prefetch loads of the chunk after next, which overwrite the registers the earlier
+// slots consumed.
+template <int S>
+__device__ __forceinline__ void db_slot(DbStage& s, float (&d)[16], float (&e)[4][4],
+                                        const DbCtx& c, const uint32_t (&toff)[16]) {
+  if constexpr (S < 4) {
+    *reinterpret_cast<floatx4*>(
+        &c.Us_next[((2 * S + (c.tid >> 8)) * 64 + ((c.tid & 255) >> 2)) * 20 +
+                   (c.tid & 3) * 4]) = s.ur[S];
+  } else if constexpr (S < 8) {  // zero the padding taps of patch row S - 4
+    constexpr int r = S - 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      d[r * 4 + j] = (c.vmask >> (r * 4 + j)) & 1u ? s.xr[r * 4 + j] : 0.f;
+  } else if constexpr (S < 12) {  // column j of B^T d
+    constexpr int j = S - 8;
+    e[0][j] = d[0 * 4 + j] - d[2 * 4 + j];
+    e[1][j] = d[1 * 4 + j] + d[2 * 4 + j];
+    e[2][j] = d[2 * 4 + j] - d[1 * 4 + j];
+    e[3][j] = d[1 * 4 + j] - d[3 * 4 + j];
+  } else if constexpr (S < 16) {  // row i of (B^T d) B -> LDS
+    constexpr int i = S - 12;
+    floatx4* vdst =
+        reinterpret_cast<floatx4*>(&c.Vs_next[((c.tid >> 6) * 64 + (c.tid & 63)) * 20]);
+    vdst[i] = floatx4{e[i][0] - e[i][2], e[i][1] + e[i][2], e[i][2] - e[i][1],
+                      e[i][1] - e[i][3]};
+  } else if constexpr (S < 20) {  // U prefetch
+    s.ur[S - 16] = *reinterpret_cast<const floatx4*>(c.u_next + (S - 16) * c.u_row);
+  } else if constexpr (S < 28) {  // x prefetch, two taps per slot
+    constexpr int t = S - 20;
+    s.xr[2 * t] = c.xp_next[toff[2 * t]];
+    s.xr[2 * t + 1] = c.xp_next[toff[2 * t + 1]];
+  }
+}
+
+__device__ __forceinline__ void db_fetch(DbStage& s, const float* __restrict__ u,
+                                         const float* __restrict__ x,
+                                         const uint32_t (&toff)[16], int64_t tile_base, int c0,
+                                         int R, int Op, int o0, int64_t HW, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    s.ur[i] = *reinterpret_cast<const floatx4*>(
+        u + (static_cast<int64_t>(c0 + 2 * i + (tid >> 8)) * Op + o0) * 16 + (tid & 255) * 4);
+  // Channels >= R (padding of the last chunk) re-read channel R-1: their U rows are
+  // zero, any finite value works.
+  const float* p =
+      x + tile_base + static_cast<int64_t>(min(c0 + (tid >> 6), R - 1)) * HW;
+#pragma unroll
+  for (int ij = 0; ij < 16; ++ij) s.xr[ij] = p[toff[ij]];
+}
+
+__device__ __forceinline__ void db_stage_all(const DbStage& s, float* Us, float* Vs,
+                                             uint32_t vmask, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    *reinterpret_cast<floatx4*>(
+        &Us[((2 * i + (tid >> 8)) * 64 + ((tid & 255) >> 2)) * 20 + (tid & 3) * 4]) = s.ur[i];
+  float d[16];
+#pragma unroll
+  for (int ij = 0; ij < 16; ++ij) d[ij] = (vmask >> ij) & 1u ? s.xr[ij] : 0.f;
+  float e[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    e[0][j] = d[0 * 4 + j] - d[2 * 4 + j];
+    e[1][j] = d[1 * 4 + j] + d[2 * 4 + j];
+    e[2][j] = d[2 * 4 + j] - d[1 * 4 + j];
+    e[3][j] = d[1 * 4 + j] - d[3 * 4 + j];
+  }
+  floatx4* vdst = reinterpret_cast<floatx4*>(&Vs[((tid >> 6) * 64 + (tid & 63)) * 20]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    vdst[i] = floatx4{e[i][0] - e[i][2], e[i][1] + e[i][2], e[i][2] - e[i][1],
+                      e[i][1] - e[i][3]};
+}
+
+template <int G, int M>
+__device__ __forceinline__ void db_group_tail(floatx4 (&acc)[16][2], DbStage& s,
+                                              float (&d)[16], float (&e)[4][4],
+                                              const DbCtx& c, const uint32_t (&toff)[16],
+                                              const floatx4& a0, const floatx4& a1,
+                                              const floatx4& b0) {
+  if constexpr (M < 8) {
+    constexpr int ep = M >> 1;
+    constexpr int i = M & 1;
+    acc[4 * (G & 3) + ep][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+        (i ? a1 : a0)[ep], b0[ep], acc[4 * (G & 3) + ep][i], 0, 0, 0);
+    if constexpr ((M & 1) == 1) db_slot<(G * 8 + M) / 2>(s, d, e, c, toff);
+    __builtin_amdgcn_sched_barrier(0);
+    db_group_tail<G, M + 1>(acc, s, d, e, c, toff, a0, a1, b0);
+  }
+}
+
+template <int G>
+__device__ __forceinline__ void db_groups(floatx4 (&acc)[16][2], DbStage& s, float (&d)[16],
+                                          float (&e)[4][4], const DbCtx& c,
+                                          const uint32_t (&toff)[16], const floatx4* ua,
+                                          const floatx4* vb, floatx4 a0, floatx4 a1,
+                                          floatx4 b0) {
+  if constexpr (G < 8) {
+    constexpr int kQuad = 4 * 64 * 20 / 4;  // float4 stride of 4 channels
+    constexpr int kHalf = 16 * 20 / 4;      // float4 stride of 16 rows (second sub-tile)
+    floatx4 na0 = a0, na1 = a1, nb0 = b0;
+    if constexpr (G + 1 < 8) {
+      constexpr int off = ((G + 1) >> 2) * kQuad + ((G + 1) & 3);
+      na0 = ua[off];
+      na1 = ua[off + kHalf];
+      nb0 = vb[off];
+    }
+    db_group_tail<G, 0>(acc, s, d, e, c, toff, a0, a1, b0);
+    db_groups<G + 1>(acc, s, d, e, c, toff, ua, vb, na0, na1, nb0);
+  }
+}
+
+// One pipeline step: the 64 MFMAs of buffer BUF, with the staging of the prefetched
+// chunk into buffer BUF^1 and the prefetch of the chunk after it in their issue gaps.
+template <int BUF>
+__device__ __forceinline__ void db_step(floatx4 (&acc)[16][2], DbStage& s, float* lds,
+                                        const float* __restrict__ u,
+                                        const float* __restrict__ x,
+                                        const uint32_t (&toff)[16], int64_t tile_base,
+                                        uint32_t vmask, int next_c, int R, int Op, int o0,
+                                        int64_t HW, int tid, int lane, int wo, int wt) {
+  DbCtx c;
+  c.Us_next = lds + (BUF ^ 1) * 2 * kDBImg;
+  c.Vs_next = c.Us_next + kDBImg;
+  c.u_row = static_cast<int64_t>(Op) * 32;
+  c.u_next = u + (static_cast<int64_t>(next_c + (tid >> 8)) * Op + o0) * 16 + (tid & 255) * 4;
+  c.xp_next = x + tile_base + static_cast<int64_t>(min(next_c + (tid >> 6), R - 1)) * HW;
+  c.vmask = vmask;
+  c.tid = tid;
+
+  const float* Us = lds + BUF * 2 * kDBImg;
+  const float* Vs = Us + kDBImg;
+  const floatx4* ua = reinterpret_cast<const floatx4*>(
+      &Us[((lane >> 4) * 64 + wo * 32 + (lane & 15)) * 20]);
+  const floatx4* vb = reinterpret_cast<const floatx4*>(
+      &Vs[((lane >> 4) * 64 + wt * 16 + (lane & 15)) * 20]);
+  constexpr int kHalf = 16 * 20 / 4;
+  float d[16];
+  float e[4][4];
+  db_groups<0>(acc, s, d, e, c, toff, ua, vb, ua[0], ua[kHalf], vb[0]);
+}
+
+__global__ __launch_bounds__(kDBThreads, 1) void wino_conv_db_kernel(
+    const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ bias,
+    float* __restrict__ y, int R, int H, int W, int O, int Rp, int Op, int TH, int TW_,
+    int64_t P, int tblocks, int oblocks, int splits) {
+  __shared__ float lds[2 * 2 * kDBImg];  // [buffer][U | V][8 channels][64][20]: 160 KiB
+
+  const int nwg = tblocks * oblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int tb = wgid % tblocks;
+  const int ob = (wgid / tblocks) % oblocks;
+  const int z = wgid / (tblocks * oblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wo = wave & 1;
+  const int wt = wave >> 1;
+  const int64_t t0 = static_cast<int64_t>(tb) * kDBT;
+  const int o0 = ob * kDBO;
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int tiles_per_image = TH * TW_;
+
+  // Staging role: tile t0 + (tid & 63), channel tid >> 6 of each chunk.  Padding taps
+  // read the tile's always-valid pixel (2ty, 2tx) and are zeroed through `vmask`.
+  uint32_t vmask = 0;
+  uint32_t toff[16];
+  int64_t tile_base = 0;
+  {
+    const int64_t t = t0 + (tid & 63);
+    int ty = 0, tx = 0;
+    if (t < P) {
+      const int64_t n = t / tiles_per_image;
+      const int rem = static_cast<int>(t - n * tiles_per_image);
+      ty = rem / TW_;
+      tx = rem - ty * TW_;
+      tile_base = n * R * HW;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int yy = 2 * ty - 1 + i, xx = 2 * tx - 1 + j;
+        const bool ok = t < P && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        vmask |= static_cast<uint32_t>(ok) << (i * 4 + j);
+        toff[i * 4 + j] = static_cast<uint32_t>(ok ? yy * W + xx : 2 * ty * W + 2 * tx);
+      }
+  }
+
+  floatx4 acc[16][2];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) {
+    acc[xi][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    acc[xi][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int nchunks = Rp / kCB;
+  const int c_begin = (z * nchunks / splits) * kCB;
+  const int c_end = ((z + 1) * nchunks / splits) * kCB;
+
+  DbStage s;
+  db_fetch(s, u, x, toff, tile_base, c_begin, R, Op, o0, HW, tid);
+  db_stage_all(s, lds, lds + kDBImg, vmask, tid);
+  __syncthreads();
+  db_fetch(s, u, x, toff, tile_base, min(c_begin + kCB, c_end - kCB), R, Op, o0, HW, tid);
+  // Two steps per trip so the buffer index is a compile-time constant (the compiler
+  // then sees that the staging stores and the MFMA operand reads never alias).  The
+  // last step stages a clamped (repeated) chunk into the idle buffer: harmless.
+  for (int c0 = c_begin;;) {
+    db_step<0>(acc, s, lds, u, x, toff, tile_base, vmask, min(c0 + 2 * kCB, c_end - kCB), R,
+               Op, o0, HW, tid, lane, wo, wt);
+    __syncthreads();
+    c0 += kCB;
+    if (c0 >= c_end) break;
+    db_step<1>(acc, s, lds, u, x, toff, tile_base, vmask, min(c0 + 2 * kCB, c_end - kCB), R,
+               Op, o0, HW, tid, lane, wo, wt);
+    __syncthreads();
+    c0 += kCB;
+    if (c0 >= c_end) break;
+  }
+
+  // -- output transform Y = A^T M A from the accumulators ------------------------------
+  // Lane (wt*16 + j) holds tile t0 + wt*16 + j: a 2x2 output patch per channel.  When
+  // W % 4 == 0 and H is even, tiles 2m and 2m+1 are horizontal neighbours; lanes 2m
+  // and 2m+1 trade one patch row (DPP quad_perm [1,0,3,2]) so each stores one 16-byte
+  // row segment instead of two 8-byte ones: the epilogue is store-issue bound.
+  float* ydst = y + static_cast<int64_t>(z) * (P / tiles_per_image) * O * HW;
+  const bool add_bias = bias != nullptr && splits == 1;
+  const int64_t tp = t0 + wt * 16 + (lane & 15);
+  const bool paired = (W & 3) == 0 && (H & 1) == 0;
+  if (tp >= P) return;  // (paired: P is even and tile pairs are valid together)
+  const int64_t pn = tp / tiles_per_image;
+  const int prem = static_cast<int>(tp - pn * tiles_per_image);
+  const int pty = prem / TW_;
+  const int py = pty * 2;
+  const int px = (prem - pty * TW_) * 2;
+  const bool odd = lane & 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = o0 + wo * 32 + i * 16 + (lane >> 4) * 4 + r;
+      float m[16];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) m[xi] = acc[xi][i][r];
+      float sr[2][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sr[0][c] = m[0 * 4 + c] + m[1 * 4 + c] + m[2 * 4 + c];
+        sr[1][c] = m[1 * 4 + c] - m[2 * 4 + c] - m[3 * 4 + c];
+      }
+      const float b = add_bias && o < O ? bias[o] : 0.f;
+      float v[2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        v[a][0] = sr[a][0] + sr[a][1] + sr[a][2] + b;
+        v[a][1] = sr[a][1] - sr[a][2] - sr[a][3] + b;
+      }
+      if (paired) {
+        // even lane sends row 1, odd lane sends row 0 (all lanes take part in the DPP)
+        const float s0 = odd ? v[0][0] : v[1][0];
+        const float s1 = odd ? v[0][1] : v[1][1];
+        const float r0 = __int_as_float(
+            __builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xF, 0xF, false));
+        const float r1 = __int_as_float(
+            __builtin_amdgcn_mov_dpp(__float_as_int(s1), 0xB1, 0xF, 0xF, false));
+        if (o >= O) continue;
+        const floatx4 out = odd ? floatx4{r0, r1, v[1][0], v[1][1]}
+                                : floatx4{v[0][0], v[0][1], r0, r1};
+        float* yp = ydst + (pn * O + o) * HW + static_cast<int64_t>(py + odd) * W +
+                    (px - 2 * odd);
+        *reinterpret_cast<floatx4*>(yp) = out;
+      } else {
+        if (o >= O) continue;
+        float* yp = ydst + (pn * O + o) * HW + static_cast<int64_t>(py) * W + px;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          if (py + a >= H) break;
+          if ((W & 1) == 0) {
+            *reinterpret_cast<float2*>(yp + a * W) = make_float2(v[a][0], v[a][1]);
+          } else {
+            yp[a * W] = v[a][0];
+            if (px + 1 < W) yp[a * W + 1] = v[a][1];
+          }
+        }
+      }
+    }
+}
+
+void launch_db(const float* x, const float* u, const float* bias, float* y, float* ws,
+               int64_t n, int64_t R, int64_t H, int64_t W, int64_t O, int splits,
+               hipStream_t stream) {
+  const int64_t Rp = wino_pad_reduction(R);
+  const int64_t Op = wino_pad_output(O);
+  const int64_t th = (H + 1) / 2, tw = (W + 1) / 2;
+  const int64_t P = n * th * tw;
+  const int tblocks = static_cast<int>((P + kDBT - 1) / kDBT);
+  const int oblocks = static_cast<int>((O + kDBO - 1) / kDBO);
+  const int64_t nwg = static_cast<int64_t>(tblocks) * oblocks * splits;
+  hipLaunchKernelGGL(wino_conv_db_kernel, dim3(static_cast<unsigned>(nwg)), dim3(kDBThreads),
+                     0, stream, x, u, bias, splits > 1 ? ws : y, static_cast<int>(R),
+                     static_cast<int>(H), static_cast<int>(W), static_cast<int>(O),
+                     static_cast<int>(Rp), static_cast<int>(Op), static_cast<int>(th),
+                     static_cast<int>(tw), P, tblocks, oblocks, splits);
+  if (splits > 1) {
+    const int64_t numel = n * O * H * W;
+    hipLaunchKernelGGL(wino_split_reduce_kernel, dim3(static_cast<unsigned>((numel + 255) / 256)),
+                       dim3(256), 0, stream, ws, bias, y, numel, H * W, static_cast<int>(O),
+                       splits);
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------
 // Weight gradient.  With V_t = B^T d_t B (input patch of tile t) and
 // M'_t = A dY_t A^T (output-gradient tile lifted to the 4x4 Winograd domain):
 //   dU[xi][c][k] = sum_t V_t[xi][c] * M'_t[xi][k]     16 GEMMs reducing over tiles
@@ -646,8 +1002,8 @@ void launch_wino_weight(const float* w, float* u, int64_t out_channels, int64_t 
 WinoPlan wino_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                    int variant, int splits) {
   WinoPlan plan;
-  plan.variant = variant >= 0 ? variant : (out_channels <= 32 ? 1 : 0);
-  const int ob = plan.variant == 0 ? 64 : 32;
+  plan.variant = variant >= 0 ? variant : (out_channels <= 32 ? 1 : 2);
+  const int ob = plan.variant == 1 ? 32 : 64;
   const int tbk = plan.variant == 0 ? 32 : 64;
   const int64_t P = n * ((h + 1) / 2) * ((w + 1) / 2);
   const int64_t blocks = ((P + tbk - 1) / tbk) * ((out_channels + ob - 1) / ob);
@@ -655,10 +1011,13 @@ WinoPlan wino_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_
   if (splits > 0) {
     plan.splits = static_cast<int>(std::min<int64_t>(splits, chunks));
   } else {
-    // Fill the chip: aim for >= 1024 blocks (2 per CU, 2 rounds), keeping >= 16
-    // channel chunks per split so the pipeline prologue stays amortised.
+    // Fill the chip: >= 2 rounds of workgroups over the CUs (variant 2 runs one per CU,
+    // variants 0/1 two), keeping enough channel chunks per split to amortise the
+    // pipeline prologue.
+    const int64_t target = plan.variant == 2 ? 512 : 1024;
+    const int64_t min_chunks = plan.variant == 2 ? 8 : 16;
     int64_t s = 1;
-    while (blocks * s < 1024 && chunks / (s * 2) >= 16) s *= 2;
+    while (blocks * s < target && chunks / (s * 2) >= min_chunks) s *= 2;
     plan.splits = static_cast<int>(s);
   }
   plan.workspace = plan.splits > 1 ? plan.splits * n * out_channels * h * w : 0;
@@ -668,7 +1027,9 @@ WinoPlan wino_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_
 void launch_wino_conv(const float* x, const float* u, const float* bias, float* y, float* ws,
                       int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                       const WinoPlan& plan, hipStream_t stream) {
-  if (plan.variant == 1) {
+  if (plan.variant == 2) {
+    launch_db(x, u, bias, y, ws, n, red_channels, h, w, out_channels, plan.splits, stream);
+  } else if (plan.variant == 1) {
     launch_variant<2, 2>(x, u, bias, y, ws, n, red_channels, h, w, out_channels, plan.splits,
                          stream);
   } else {
