@@ -94,10 +94,11 @@ def test_weight_gradient_kernel(shape):
     want = torch.ops.aten.convolution_backward(
         dy.double(), x.double(), torch.zeros(k, c, 3, 3, device=cuda, dtype=torch.float64), None,
         [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
-    for splits in (0, 1, 3):
-        got = ops.wino_wgrad(x, dy, splits)
-        torch.testing.assert_close(got.double(), want, rtol=1e-4,
-                                   atol=2e-5 * (want.abs().max().item() + 1))
+    for variant in (0, 2):
+        for splits in (0, 1, 3):
+            got = ops.wino_wgrad(x, dy, splits, variant)
+            torch.testing.assert_close(got.double(), want, rtol=1e-4,
+                                       atol=2e-5 * (want.abs().max().item() + 1))
 
 
 def test_direct_ops_small_channels():

@@ -1,5 +1,6 @@
 // ATen bindings: registers the framework kernels as torch.ops.tgpipe.* (CUDA == HIP
 // dispatch key on ROCm builds) and validates shapes / dtypes / devices before launching.
+#include <algorithm>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -186,7 +187,8 @@ at::Tensor wino_conv(const at::Tensor& x_in, const at::Tensor& u,
   return y;
 }
 
-at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits) {
+at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits,
+                      int64_t variant) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   check_f32_gpu(x, "x");
@@ -201,11 +203,21 @@ at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t s
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto dw = at::empty({k, c, 3, 3}, x.options());
   if (n == 0 || h == 0 || w == 0) return dw.zero_();
-  const int s = splits > 0 ? static_cast<int>(splits) : wino_wgrad_splits(n, c, k, h, w);
+  TORCH_CHECK(variant == -1 || variant == 0 || variant == 2, "variant must be -1, 0 or 2");
+  // auto: the 64 x 64 double-buffered kernel, except for <= 32 output channels where
+  // half of its 64-wide k block would idle (benchmarks/wgrad_variants.py).  Variant 2
+  // decodes tile indices through a float reciprocal: exact below 2^24 tiles.
+  const int64_t tiles = n * ((h + 1) / 2) * ((w + 1) / 2);
+  int v = variant >= 0 ? static_cast<int>(variant) : (k <= 32 ? 0 : 2);
+  if (v == 2 && tiles >= (int64_t{1} << 24)) v = 0;
+  // every split must own >= 1 step of 8 tiles (both variants step 8 tiles)
+  const int64_t steps = (tiles + 7) / 8;
+  const int s = static_cast<int>(std::min<int64_t>(
+      splits > 0 ? splits : wino_wgrad_splits(n, c, k, h, w, v), steps));
   at::Tensor ws;
   if (s > 1) ws = at::empty({s * k * c * 9}, x.options());
   launch_wino_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), dw.data_ptr<float>(),
-                    s > 1 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s, stream_of(x));
+                    s > 1 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s, v, stream_of(x));
   return dw;
 }
 
@@ -225,7 +237,7 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("spin(int ns, Device device) -> ()");
   m.def("copy_segments(Tensor[] srcs, Tensor(a!)[] dsts) -> ()");
   m.def("wino_weight(Tensor w, bool flip) -> Tensor");
-  m.def("wino_wgrad(Tensor x, Tensor dy, int splits=0) -> Tensor");
+  m.def("wino_wgrad(Tensor x, Tensor dy, int splits=0, int variant=-1) -> Tensor");
   m.def("wino_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
 }

@@ -73,9 +73,11 @@ void launch_wino_conv(const float* x, const float* u, const float* bias, float* 
 
 // Weight gradient of the same convolution: dw[K][C][3][3] from x[N][C][H][W] and
 // dy[N][K][H][W]; `splits` > 1 needs a workspace of splits*K*C*9 floats.
-int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
+// variant 0: 64 x 32 (c x k) blocks, two workgroups per CU; variant 2: 64 x 64 blocks,
+// one 8-wave workgroup per CU, double-buffered LDS (the forward variant 2 structure).
+int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int variant);
 void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
-                       int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                       int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
                        hipStream_t stream);
 
 }  // namespace tgpipe

@@ -455,6 +455,14 @@ __device__ __forceinline__ void db_slot(DbStage& s, float (&d)[16], float (&e)[4
   }
 }
 
+// Fake use of the prefetch registers after the loop (see wd_keep).
+__device__ __forceinline__ void db_keep(const DbStage& s) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(s.ur[i]));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(s.xr[i]));
+}
+
 __device__ __forceinline__ void db_fetch(DbStage& s, const float* __restrict__ u,
                                          const float* __restrict__ x,
                                          const uint32_t (&toff)[16], int64_t tile_base, int c0,
@@ -533,17 +541,18 @@ __device__ __forceinline__ void db_groups(floatx4 (&acc)[16][2], DbStage& s, flo
   }
 }
 
-// One pipeline step: the 64 MFMAs of buffer BUF, with the staging of the prefetched
-// chunk into buffer BUF^1 and the prefetch of the chunk after it in their issue gaps.
-template <int BUF>
-__device__ __forceinline__ void db_step(floatx4 (&acc)[16][2], DbStage& s, float* lds,
+// One pipeline step: the 64 MFMAs of buffer `buf`, with the staging of the prefetched
+// chunk into buffer buf^1 and the prefetch of the chunk after it in their issue gaps.
+// (A runtime buffer index: the pinned slot order already orders the staging stores and
+// the operand reads, and a single-step loop body keeps the accumulators in place.)
+__device__ __forceinline__ void db_step(floatx4 (&acc)[16][2], DbStage& s, float* lds, int buf,
                                         const float* __restrict__ u,
                                         const float* __restrict__ x,
                                         const uint32_t (&toff)[16], int64_t tile_base,
                                         uint32_t vmask, int next_c, int R, int Op, int o0,
                                         int64_t HW, int tid, int lane, int wo, int wt) {
   DbCtx c;
-  c.Us_next = lds + (BUF ^ 1) * 2 * kDBImg;
+  c.Us_next = lds + (buf ^ 1) * 2 * kDBImg;
   c.Vs_next = c.Us_next + kDBImg;
   c.u_row = static_cast<int64_t>(Op) * 32;
   c.u_next = u + (static_cast<int64_t>(next_c + (tid >> 8)) * Op + o0) * 16 + (tid & 255) * 4;
@@ -551,7 +560,7 @@ __device__ __forceinline__ void db_step(floatx4 (&acc)[16][2], DbStage& s, float
   c.vmask = vmask;
   c.tid = tid;
 
-  const float* Us = lds + BUF * 2 * kDBImg;
+  const float* Us = lds + buf * 2 * kDBImg;
   const float* Vs = Us + kDBImg;
   const floatx4* ua = reinterpret_cast<const floatx4*>(
       &Us[((lane >> 4) * 64 + wo * 32 + (lane & 15)) * 20]);
@@ -630,21 +639,13 @@ __global__ __launch_bounds__(kDBThreads, 1) void wino_conv_db_kernel(
   db_stage_all(s, lds, lds + kDBImg, vmask, tid);
   __syncthreads();
   db_fetch(s, u, x, toff, tile_base, min(c_begin + kCB, c_end - kCB), R, Op, o0, HW, tid);
-  // Two steps per trip so the buffer index is a compile-time constant (the compiler
-  // then sees that the staging stores and the MFMA operand reads never alias).  The
-  // last step stages a clamped (repeated) chunk into the idle buffer: harmless.
-  for (int c0 = c_begin;;) {
-    db_step<0>(acc, s, lds, u, x, toff, tile_base, vmask, min(c0 + 2 * kCB, c_end - kCB), R,
-               Op, o0, HW, tid, lane, wo, wt);
+  // The last step stages a clamped (repeated) chunk into the idle buffer: harmless.
+  for (int c0 = c_begin; c0 < c_end; c0 += kCB) {
+    db_step(acc, s, lds, ((c0 - c_begin) / kCB) & 1, u, x, toff, tile_base, vmask,
+            min(c0 + 2 * kCB, c_end - kCB), R, Op, o0, HW, tid, lane, wo, wt);
     __syncthreads();
-    c0 += kCB;
-    if (c0 >= c_end) break;
-    db_step<1>(acc, s, lds, u, x, toff, tile_base, vmask, min(c0 + 2 * kCB, c_end - kCB), R,
-               Op, o0, HW, tid, lane, wo, wt);
-    __syncthreads();
-    c0 += kCB;
-    if (c0 >= c_end) break;
   }
+  db_keep(s);
 
   // -- output transform Y = A^T M A from the accumulators ------------------------------
   // Lane (wt*16 + j) holds tile t0 + wt*16 + j: a 2x2 output patch per channel.  When
@@ -974,6 +975,343 @@ __global__ __launch_bounds__(kThreads, 2) void wino_wgrad_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Weight gradient, variant 2: the structure of the forward variant 2 applied to
+//   dU[xi][c][k] = sum_t V_t[xi][c] * M'_t[xi][k]
+// 64 input channels x 64 output channels per 8-wave workgroup (one per CU), 8 tiles per
+// pipeline step, LDS double-buffered, staging interleaved into the MFMA stream.  Wave
+// (wc, wk) = (wave & 1, wave >> 1) owns 32 channels x 16 output channels for all 16
+// positions.  Staging role of a thread: tile slot t = tid & 7 of the step, channel
+// (and output channel) tid >> 3.  In LDS, tile row t stores channel c at c ^ t: the
+// 8 lanes of one ds_write_b128 group (8 tiles, one channel) then hit 8 different bank
+// groups, while the MFMA reads (16 consecutive channels of one tile) stay a conflict-free
+// permutation of their 16-channel group.
+constexpr int kWDT = 8;                        // tiles per pipeline step
+constexpr int kWDImg = kWDT * 64 * 20;         // floats per LDS operand image
+
+struct WdStage {
+  float xr[16];      // 4x4 input patch of (tile slot, channel), zero-padded; transformed
+                     // in place while it is staged
+  float yr[4];       // 2x2 output-gradient patch of (tile slot, output channel)
+};
+
+// a / d for 0 <= a < 2^24 through a float reciprocal (exact after one correction).
+__device__ __forceinline__ int wd_div(int a, int d, float inv) {
+  int q = static_cast<int>(static_cast<float>(a) * inv);
+  const int r = a - q * d;
+  q += (r >= d) - (r < 0);
+  return q;
+}
+
+// Per-thread tile geometry of one step: image, top-left input pixel of the 4x4 patch.
+struct WdGeo {
+  int n, y0, x0;
+  bool tv;
+};
+
+struct WdShape {
+  int C, K, H, W, TW_, tpi;
+  float inv_tw, inv_tpi;
+  int64_t P, HW;
+};
+
+__device__ __forceinline__ WdGeo wd_geo(int64_t t, const WdShape& sh) {
+  WdGeo g;
+  g.tv = t >= 0 && t < sh.P;
+  const int tt = g.tv ? static_cast<int>(t) : 0;
+  g.n = wd_div(tt, sh.tpi, sh.inv_tpi);
+  const int rem = tt - g.n * sh.tpi;
+  const int ty = wd_div(rem, sh.TW_, sh.inv_tw);
+  g.y0 = 2 * ty - 1;
+  g.x0 = 2 * (rem - ty * sh.TW_) - 1;
+  return g;
+}
+
+// Global -> registers for one step, in parts: part i < 4 loads input patch row i
+// (part 0 also resets the mask), part 4 the 2x2 output-gradient patch.
+template <int PART>
+__device__ __forceinline__ void wd_fetch_part(WdStage& s, const WdGeo& g,
+                                              const float* __restrict__ x,
+                                              const float* __restrict__ dy, int c, int k,
+                                              const WdShape& sh) {
+  // Padding taps, padding tiles and padding channels load the zero word kZeroTap.
+  if constexpr (PART < 4) {
+    const bool cv = g.tv && c < sh.C;
+    const float* xp = x + (static_cast<int64_t>(g.n) * sh.C + (cv ? c : 0)) * sh.HW;
+    const int yy = g.y0 + PART;
+    const bool rok = cv && yy >= 0 && yy < sh.H;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int xx = g.x0 + j;
+      const bool ok = rok && xx >= 0 && xx < sh.W;
+      s.xr[PART * 4 + j] = *(ok ? xp + yy * sh.W + xx : &kZeroTap);
+    }
+  } else {
+    const bool kv = g.tv && k < sh.K;
+    const float* yp = dy + (static_cast<int64_t>(g.n) * sh.K + (kv ? k : 0)) * sh.HW;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int yy = g.y0 + 1 + i, xx = g.x0 + 1 + j;
+        const bool ok = kv && yy < sh.H && xx < sh.W;
+        s.yr[i * 2 + j] = *(ok ? yp + yy * sh.W + xx : &kZeroTap);
+      }
+  }
+}
+
+// Fake use of the prefetch registers on a loop exit: otherwise MachineSink moves the
+// prefetch loads of a step past the exit branch into the next step (it sees them used
+// only there), which serialises them and doubles the live patch registers.
+__device__ __forceinline__ void wd_keep(const WdStage& s) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(s.xr[i]));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(s.yr[i]));
+}
+
+__device__ __forceinline__ void wd_fetch(WdStage& s, int64_t t, const float* __restrict__ x,
+                                         const float* __restrict__ dy, int c, int k,
+                                         const WdShape& sh) {
+  const WdGeo g = wd_geo(t, sh);
+  wd_fetch_part<0>(s, g, x, dy, c, k, sh);
+  wd_fetch_part<1>(s, g, x, dy, c, k, sh);
+  wd_fetch_part<2>(s, g, x, dy, c, k, sh);
+  wd_fetch_part<3>(s, g, x, dy, c, k, sh);
+  wd_fetch_part<4>(s, g, x, dy, c, k, sh);
+}
+
+// V = B^T d B of the staged input patch and M' = A dY A^T of the staged gradient patch
+// into LDS image pair (Vs, Ms).
+__device__ __forceinline__ void wd_stage_all(const WdStage& s, float* Vs, float* Ms, int tid) {
+  const int t = tid & 7, ch = tid >> 3;
+  const float* d = s.xr;
+  float e[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    e[0][j] = d[0 * 4 + j] - d[2 * 4 + j];
+    e[1][j] = d[1 * 4 + j] + d[2 * 4 + j];
+    e[2][j] = d[2 * 4 + j] - d[1 * 4 + j];
+    e[3][j] = d[1 * 4 + j] - d[3 * 4 + j];
+  }
+  floatx4* vdst = reinterpret_cast<floatx4*>(&Vs[(t * 64 + (ch ^ t)) * 20]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    vdst[i] = floatx4{e[i][0] - e[i][2], e[i][1] + e[i][2], e[i][2] - e[i][1],
+                      e[i][1] - e[i][3]};
+  const float* y = s.yr;
+  float r[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    r[0][j] = y[0 * 2 + j];
+    r[1][j] = y[0 * 2 + j] + y[1 * 2 + j];
+    r[2][j] = y[0 * 2 + j] - y[1 * 2 + j];
+    r[3][j] = -y[1 * 2 + j];
+  }
+  floatx4* mdst = reinterpret_cast<floatx4*>(&Ms[(t * 64 + (ch ^ t)) * 20]);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+    mdst[a] = floatx4{r[a][0], r[a][0] + r[a][1], r[a][0] - r[a][1], -r[a][1]};
+}
+
+struct WdCtx {
+  float* Vs_next;
+  float* Ms_next;
+  const float* x;
+  const float* dy;
+  int64_t t_next;    // this thread's tile of the step being prefetched
+  WdGeo geo;         // its geometry (computed in slot 17)
+  int c, k;
+  int tid;
+};
+
+// Slot S (after MFMA 2S + 1) of one wgrad step: stage the prefetched patches into the
+// idle buffer (S 0-11), then fetch the patches of the step after next (S 13-22).
+template <int S>
+__device__ __forceinline__ void wd_slot(WdStage& s, WdCtx& c, const WdShape& sh) {
+  const int t = c.tid & 7, ch = c.tid >> 3;
+  float* d = s.xr;
+  if constexpr (S < 4) {  // column j = S of B^T d, in place
+    constexpr int j = S;
+    const float e0 = d[0 * 4 + j] - d[2 * 4 + j];
+    const float e1 = d[1 * 4 + j] + d[2 * 4 + j];
+    const float e2 = d[2 * 4 + j] - d[1 * 4 + j];
+    const float e3 = d[1 * 4 + j] - d[3 * 4 + j];
+    d[0 * 4 + j] = e0;
+    d[1 * 4 + j] = e1;
+    d[2 * 4 + j] = e2;
+    d[3 * 4 + j] = e3;
+  } else if constexpr (S < 8) {  // row i of (B^T d) B -> LDS
+    constexpr int i = S - 4;
+    floatx4* vdst = reinterpret_cast<floatx4*>(&c.Vs_next[(t * 64 + (ch ^ t)) * 20]);
+    vdst[i] = floatx4{d[i * 4 + 0] - d[i * 4 + 2], d[i * 4 + 1] + d[i * 4 + 2],
+                      d[i * 4 + 2] - d[i * 4 + 1], d[i * 4 + 1] - d[i * 4 + 3]};
+  } else if constexpr (S < 12) {  // row a of A dY A^T -> LDS
+    constexpr int a = S - 8;
+    const float* y = s.yr;
+    // rows of A dY: [y0, y1], [y0 + y2, y1 + y3], [y0 - y2, y1 - y3], [-y2, -y3]
+    const float r0 = a == 0 ? y[0] : a == 1 ? y[0] + y[2] : a == 2 ? y[0] - y[2] : -y[2];
+    const float r1 = a == 0 ? y[1] : a == 1 ? y[1] + y[3] : a == 2 ? y[1] - y[3] : -y[3];
+    floatx4* mdst = reinterpret_cast<floatx4*>(&c.Ms_next[(t * 64 + (ch ^ t)) * 20]);
+    mdst[a] = floatx4{r0, r0 + r1, r0 - r1, -r1};
+  } else if constexpr (S == 13) {
+    c.geo = wd_geo(c.t_next, sh);
+  } else if constexpr (S >= 14 && S < 24 && (S & 1) == 0) {  // prefetch parts 0-4
+    wd_fetch_part<(S - 14) / 2>(s, c.geo, c.x, c.dy, c.c, c.k, sh);
+  }
+}
+
+template <int G, int M>
+__device__ __forceinline__ void wd_group_tail(floatx4 (&acc)[16][2], WdStage& s, WdCtx& c,
+                                              const WdShape& sh,
+                                              const floatx4& a0,
+                                              const floatx4& a1, const floatx4& b0) {
+  if constexpr (M < 8) {
+    constexpr int ep = M >> 1;
+    constexpr int i = M & 1;
+    acc[4 * (G & 3) + ep][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+        (i ? a1 : a0)[ep], b0[ep], acc[4 * (G & 3) + ep][i], 0, 0, 0);
+    if constexpr ((M & 1) == 1) wd_slot<(G * 8 + M) / 2>(s, c, sh);
+    __builtin_amdgcn_sched_barrier(0);
+    wd_group_tail<G, M + 1>(acc, s, c, sh, a0, a1, b0);
+  }
+}
+
+// The A operand of tile quad ks, lane quarter q = lane >> 4: channel (cb + (lane & 15))
+// of tile t = 4ks + q sits at position (cb + (lane & 15)) ^ t of row t.
+template <int G>
+__device__ __forceinline__ void wd_groups(floatx4 (&acc)[16][2], WdStage& s, WdCtx& c,
+                                          const WdShape& sh, const float* Vs, const float* Ms,
+                                          int lane, int wc,
+                                          int wk, floatx4 a0, floatx4 a1, floatx4 b0) {
+  if constexpr (G < 8) {
+    floatx4 na0 = a0, na1 = a1, nb0 = b0;
+    if constexpr (G + 1 < 8) {
+      constexpr int ks = (G + 1) >> 2, q4 = (G + 1) & 3;
+      const int t = 4 * ks + (lane >> 4);
+      const int cA = wc * 32 + (lane & 15);
+      const int kB = wk * 16 + (lane & 15);
+      na0 = *reinterpret_cast<const floatx4*>(&Vs[(t * 64 + (cA ^ t)) * 20 + q4 * 4]);
+      na1 = *reinterpret_cast<const floatx4*>(&Vs[(t * 64 + ((cA + 16) ^ t)) * 20 + q4 * 4]);
+      nb0 = *reinterpret_cast<const floatx4*>(&Ms[(t * 64 + (kB ^ t)) * 20 + q4 * 4]);
+    }
+    wd_group_tail<G, 0>(acc, s, c, sh, a0, a1, b0);
+    wd_groups<G + 1>(acc, s, c, sh, Vs, Ms, lane, wc, wk, na0, na1, nb0);
+  }
+}
+
+// (a runtime buffer index: the pinned slot order already orders the staging stores
+// and operand reads, and a single-step loop body keeps the accumulators in place)
+__device__ __forceinline__ void wd_step(floatx4 (&acc)[16][2], WdStage& s, float* lds, int buf,
+                                        WdCtx& c, const WdShape& sh, int lane, int wc, int wk) {
+  c.Vs_next = lds + (buf ^ 1) * 2 * kWDImg;
+  c.Ms_next = c.Vs_next + kWDImg;
+  const float* Vs = lds + buf * 2 * kWDImg;
+  const float* Ms = Vs + kWDImg;
+  const int t = lane >> 4;
+  const int cA = wc * 32 + (lane & 15);
+  const int kB = wk * 16 + (lane & 15);
+  const floatx4 a0 = *reinterpret_cast<const floatx4*>(&Vs[(t * 64 + (cA ^ t)) * 20]);
+  const floatx4 a1 = *reinterpret_cast<const floatx4*>(&Vs[(t * 64 + ((cA + 16) ^ t)) * 20]);
+  const floatx4 b0 = *reinterpret_cast<const floatx4*>(&Ms[(t * 64 + (kB ^ t)) * 20]);
+  wd_groups<0>(acc, s, c, sh, Vs, Ms, lane, wc, wk, a0, a1, b0);
+}
+
+__global__ __launch_bounds__(kDBThreads, 1) void wino_wgrad_db_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dw, int C,
+    int K, int H, int W, int TH, int TW_, int64_t P, int cblocks, int kblocks, int splits) {
+  __shared__ float lds[2 * 2 * kWDImg];  // [buffer][V | M'][8 tiles][64][20]: 160 KiB
+
+  const int nwg = cblocks * kblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int cb = wgid % cblocks;
+  const int kb = (wgid / cblocks) % kblocks;
+  const int z = wgid / (cblocks * kblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wc = wave & 1;
+  const int wk = wave >> 1;
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int64_t steps_total = (P + kWDT - 1) / kWDT;
+  const int64_t st_begin = z * steps_total / splits;
+  const int64_t st_end = (z + 1) * steps_total / splits;
+
+  floatx4 acc[16][2];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) {
+    acc[xi][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    acc[xi][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // (every split owns >= 1 step: the host caps splits at the step count)
+  WdShape sh;
+  sh.C = C;
+  sh.K = K;
+  sh.H = H;
+  sh.W = W;
+  sh.TW_ = TW_;
+  sh.tpi = TH * TW_;
+  sh.inv_tw = 1.f / static_cast<float>(TW_);
+  sh.inv_tpi = 1.f / static_cast<float>(sh.tpi);
+  sh.P = P;
+  sh.HW = HW;
+  WdCtx c;
+  c.x = x;
+  c.dy = dy;
+  c.c = cb * 64 + (tid >> 3);
+  c.k = kb * 64 + (tid >> 3);
+  c.tid = tid;
+  const int slot = tid & 7;
+  WdStage s;
+  wd_fetch(s, st_begin * kWDT + slot, x, dy, c.c, c.k, sh);
+  wd_stage_all(s, lds, lds + kWDImg, tid);
+  __syncthreads();
+  // Prefetches past the split's last step re-read its last step (staged, never read).
+  wd_fetch(s, min(st_begin + 1, st_end - 1) * kWDT + slot, x, dy, c.c, c.k, sh);
+  for (int64_t st = st_begin; st < st_end; ++st) {
+    c.t_next = min(st + 2, st_end - 1) * kWDT + slot;
+    wd_step(acc, s, lds, static_cast<int>((st - st_begin) & 1), c, sh, lane, wc, wk);
+    __syncthreads();
+  }
+  wd_keep(s);
+
+  // -- dW = G^T dU G per (c, k) pair; partial slab z of [splits][K][C][9] --------------
+  float* out = dw + static_cast<int64_t>(z) * K * C * 9;
+  const int k = kb * 64 + wk * 16 + (lane & 15);
+  if (k >= K) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ch = cb * 64 + wc * 32 + i * 16 + (lane >> 4) * 4 + r;
+      if (ch >= C) continue;
+      float u[16];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) u[xi] = acc[xi][i][r];
+      float t[3][4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float s12 = 0.5f * (u[1 * 4 + b] + u[2 * 4 + b]);
+        t[0][b] = u[0 * 4 + b] + s12;
+        t[1][b] = 0.5f * (u[1 * 4 + b] - u[2 * 4 + b]);
+        t[2][b] = s12 + u[3 * 4 + b];
+      }
+      float* o = out + (static_cast<int64_t>(k) * C + ch) * 9;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const float s12 = 0.5f * (t[a][1] + t[a][2]);
+        o[a * 3 + 0] = t[a][0] + s12;
+        o[a * 3 + 1] = 0.5f * (t[a][1] - t[a][2]);
+        o[a * 3 + 2] = s12 + t[a][3];
+      }
+    }
+}
+
 __global__ void wino_wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
                                          int64_t numel, int splits) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1038,8 +1376,17 @@ void launch_wino_conv(const float* x, const float* u, const float* bias, float* 
   }
 }
 
-int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
+int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int variant) {
   const int64_t P = n * ((h + 1) / 2) * ((w + 1) / 2);
+  if (variant == 2) {
+    // one workgroup per CU: >= 2 rounds of 256, >= 8 steps of 8 tiles per split
+    const int64_t tiles_blocks = ((c + 63) / 64) * ((k + 63) / 64);
+    const int64_t steps = (P + kWDT - 1) / kWDT;
+    int64_t s = (512 + tiles_blocks - 1) / tiles_blocks;
+    s = std::min<int64_t>(s, std::max<int64_t>(1, steps / 8));
+    s = std::min<int64_t>(s, 256);
+    return static_cast<int>(std::max<int64_t>(s, 1));
+  }
   const int64_t tiles_blocks = ((c + kWC - 1) / kWC) * ((k + kWK - 1) / kWK);
   const int64_t iters = (P + kWT - 1) / kWT;
   int64_t s = (1024 + tiles_blocks - 1) / tiles_blocks;
@@ -1049,17 +1396,29 @@ int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
 }
 
 void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
-                       int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                       int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
                        hipStream_t stream) {
   const int64_t th = (h + 1) / 2, tw = (w + 1) / 2;
   const int64_t P = n * th * tw;
-  const int cblocks = static_cast<int>((c + kWC - 1) / kWC);
-  const int kblocks = static_cast<int>((k + kWK - 1) / kWK);
-  const int64_t nwg = static_cast<int64_t>(cblocks) * kblocks * splits;
-  hipLaunchKernelGGL(wino_wgrad_kernel, dim3(static_cast<unsigned>(nwg)), dim3(kThreads), 0,
-                     stream, x, dy, splits > 1 ? ws : dw, static_cast<int>(c),
-                     static_cast<int>(k), static_cast<int>(h), static_cast<int>(w),
-                     static_cast<int>(th), static_cast<int>(tw), P, cblocks, kblocks, splits);
+  if (variant == 2) {
+    const int cblocks = static_cast<int>((c + 63) / 64);
+    const int kblocks = static_cast<int>((k + 63) / 64);
+    const int64_t nwg = static_cast<int64_t>(cblocks) * kblocks * splits;
+    hipLaunchKernelGGL(wino_wgrad_db_kernel, dim3(static_cast<unsigned>(nwg)),
+                       dim3(kDBThreads), 0, stream, x, dy, splits > 1 ? ws : dw,
+                       static_cast<int>(c), static_cast<int>(k), static_cast<int>(h),
+                       static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw), P,
+                       cblocks, kblocks, splits);
+  } else {
+    const int cblocks = static_cast<int>((c + kWC - 1) / kWC);
+    const int kblocks = static_cast<int>((k + kWK - 1) / kWK);
+    const int64_t nwg = static_cast<int64_t>(cblocks) * kblocks * splits;
+    hipLaunchKernelGGL(wino_wgrad_kernel, dim3(static_cast<unsigned>(nwg)), dim3(kThreads), 0,
+                       stream, x, dy, splits > 1 ? ws : dw, static_cast<int>(c),
+                       static_cast<int>(k), static_cast<int>(h), static_cast<int>(w),
+                       static_cast<int>(th), static_cast<int>(tw), P, cblocks, kblocks,
+                       splits);
+  }
   if (splits > 1) {
     const int64_t numel = k * c * 9;
     hipLaunchKernelGGL(wino_wgrad_reduce_kernel,

@@ -3,8 +3,8 @@
 :class:`WinogradConv2d` is a drop-in ``nn.Conv2d`` (same parameters, same
 state-dict keys) whose 3×3 / stride 1 / pad 1 / fp32 GPU forward and
 backward-data run the fused HIP kernel of ``csrc/winograd.hip``; the weight
-gradient runs the Winograd wgrad kernel on large planes and MIOpen's
-implicit GEMM elsewhere (see ``_wgrad_on_mfma``).
+gradient runs the Winograd wgrad kernels wherever they beat MIOpen's wrw (see
+``_wgrad_on_mfma``).
 Other configurations, CPU tensors and non-fp32 dtypes use ``F.conv2d``.
 
 The Winograd-domain weights ``U = G g Gᵀ`` (and the rotated/transposed ``U'``
@@ -77,14 +77,18 @@ class _WinogradConv(torch.autograd.Function):
 
 
 def _wgrad_on_mfma(x: Tensor, weight: Tensor) -> bool:
-    """Weight gradient on the Winograd MFMA kernel where it beats MIOpen's wrw.
+    """Weight gradient on the Winograd MFMA kernels where they beat MIOpen's wrw.
 
-    benchmarks/conv_bench.py (profiles/conv_bench.json): the Winograd wgrad wins
-    on large planes (64->64 @192²: 1.05 vs 1.42 ms, 128->32 @192²: 1.18 vs 1.74 ms
-    at N=40) and ties or loses below 96² where MIOpen's implicit GEMM has
-    enough channels to fill its tiles.
+    benchmarks/wgrad_variants.py (profiles/wgrad_variants.json): the double-buffered
+    64x64 kernel (variant 2) runs 133-170 TFLOP/s direct-equivalent on every U-Net
+    shape with > 32 output channels (MIOpen wrw: 75-107); with <= 32 output channels
+    the 64x32 kernel (variant 0) still wins on large planes with >= 64 input channels
+    (128->32 @192^2: 1.13 vs 1.72 ms) and MIOpen wins the rest (32->32 @192^2).
     """
-    return x.shape[2] * x.shape[3] >= 96 * 96 and weight.shape[1] >= 64
+    k, c = weight.shape[0], weight.shape[1]
+    if k > 32:
+        return c >= 16
+    return c >= 64 and x.shape[2] * x.shape[3] >= 96 * 96
 
 
 # Below this many input channels the 8-channel reduction chunk is mostly padding
