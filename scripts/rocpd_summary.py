@@ -14,7 +14,7 @@ import sqlite3
 
 GROUPS = [
     ('tgpipe Winograd F(2,3) conv fwd/bwd-data on MFMA (HIP)',
-     ('wino_conv_kernel', 'wino_split_reduce')),
+     ('wino_conv', 'wino_split_reduce')),
     ('tgpipe Winograd weight gradient on MFMA (HIP)', ('wino_wgrad',)),
     ('tgpipe Winograd weight transform (HIP)', ('wino_weight_kernel',)),
     ('tgpipe fused Dropout2d+InstanceNorm+LeakyReLU (HIP)', ('dna_forward', 'dna_backward')),

@@ -418,40 +418,46 @@ struct DbCtx {
   int tid;
 };
 
-// Staging work of one pipeline step, in slots (slot S runs after MFMA 2S + 1): the 4 U
-// stores, the input transform of the (channel, tile) pair and its 4 V stores, then the
-// prefetch loads of the chunk after next, which overwrite the registers the earlier
-// slots consumed.
+// Staging work of one pipeline step, in slots (slot S runs after MFMA 2S + 1), all on
+// the staging registers in place: zero the padding taps (S 0-3), B^T d by columns
+// (S 4-7), (B^T d) B rows -> LDS (S 8-11); then the patch registers are free and the
+// x prefetch of the chunk after next goes out early (S 12-19, latency-critical: it
+// misses to HBM), then the U stores (S 20-23) and the U prefetch (S 24-27, L2-hot).
 template <int S>
-__device__ __forceinline__ void db_slot(DbStage& s, float (&d)[16], float (&e)[4][4],
-                                        const DbCtx& c, const uint32_t (&toff)[16]) {
+__device__ __forceinline__ void db_slot(DbStage& s, const DbCtx& c,
+                                        const uint32_t (&toff)[16]) {
+  float* d = s.xr;
   if constexpr (S < 4) {
-    *reinterpret_cast<floatx4*>(
-        &c.Us_next[((2 * S + (c.tid >> 8)) * 64 + ((c.tid & 255) >> 2)) * 20 +
-                   (c.tid & 3) * 4]) = s.ur[S];
-  } else if constexpr (S < 8) {  // zero the padding taps of patch row S - 4
-    constexpr int r = S - 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      d[r * 4 + j] = (c.vmask >> (r * 4 + j)) & 1u ? s.xr[r * 4 + j] : 0.f;
-  } else if constexpr (S < 12) {  // column j of B^T d
-    constexpr int j = S - 8;
-    e[0][j] = d[0 * 4 + j] - d[2 * 4 + j];
-    e[1][j] = d[1 * 4 + j] + d[2 * 4 + j];
-    e[2][j] = d[2 * 4 + j] - d[1 * 4 + j];
-    e[3][j] = d[1 * 4 + j] - d[3 * 4 + j];
-  } else if constexpr (S < 16) {  // row i of (B^T d) B -> LDS
-    constexpr int i = S - 12;
+      d[S * 4 + j] = (c.vmask >> (S * 4 + j)) & 1u ? d[S * 4 + j] : 0.f;
+  } else if constexpr (S < 8) {
+    constexpr int j = S - 4;
+    const float e0 = d[0 * 4 + j] - d[2 * 4 + j];
+    const float e1 = d[1 * 4 + j] + d[2 * 4 + j];
+    const float e2 = d[2 * 4 + j] - d[1 * 4 + j];
+    const float e3 = d[1 * 4 + j] - d[3 * 4 + j];
+    d[0 * 4 + j] = e0;
+    d[1 * 4 + j] = e1;
+    d[2 * 4 + j] = e2;
+    d[3 * 4 + j] = e3;
+  } else if constexpr (S < 12) {
+    constexpr int i = S - 8;
     floatx4* vdst =
         reinterpret_cast<floatx4*>(&c.Vs_next[((c.tid >> 6) * 64 + (c.tid & 63)) * 20]);
-    vdst[i] = floatx4{e[i][0] - e[i][2], e[i][1] + e[i][2], e[i][2] - e[i][1],
-                      e[i][1] - e[i][3]};
-  } else if constexpr (S < 20) {  // U prefetch
-    s.ur[S - 16] = *reinterpret_cast<const floatx4*>(c.u_next + (S - 16) * c.u_row);
-  } else if constexpr (S < 28) {  // x prefetch, two taps per slot
-    constexpr int t = S - 20;
+    vdst[i] = floatx4{d[i * 4 + 0] - d[i * 4 + 2], d[i * 4 + 1] + d[i * 4 + 2],
+                      d[i * 4 + 2] - d[i * 4 + 1], d[i * 4 + 1] - d[i * 4 + 3]};
+  } else if constexpr (S < 20) {  // x prefetch, two taps per slot
+    constexpr int t = S - 12;
     s.xr[2 * t] = c.xp_next[toff[2 * t]];
     s.xr[2 * t + 1] = c.xp_next[toff[2 * t + 1]];
+  } else if constexpr (S < 24) {
+    constexpr int i = S - 20;
+    *reinterpret_cast<floatx4*>(
+        &c.Us_next[((2 * i + (c.tid >> 8)) * 64 + ((c.tid & 255) >> 2)) * 20 +
+                   (c.tid & 3) * 4]) = s.ur[i];
+  } else if constexpr (S < 28) {  // U prefetch
+    s.ur[S - 24] = *reinterpret_cast<const floatx4*>(c.u_next + (S - 24) * c.u_row);
   }
 }
 
@@ -505,7 +511,6 @@ __device__ __forceinline__ void db_stage_all(const DbStage& s, float* Us, float*
 
 template <int G, int M>
 __device__ __forceinline__ void db_group_tail(floatx4 (&acc)[16][2], DbStage& s,
-                                              float (&d)[16], float (&e)[4][4],
                                               const DbCtx& c, const uint32_t (&toff)[16],
                                               const floatx4& a0, const floatx4& a1,
                                               const floatx4& b0) {
@@ -514,15 +519,14 @@ __device__ __forceinline__ void db_group_tail(floatx4 (&acc)[16][2], DbStage& s,
     constexpr int i = M & 1;
     acc[4 * (G & 3) + ep][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(
         (i ? a1 : a0)[ep], b0[ep], acc[4 * (G & 3) + ep][i], 0, 0, 0);
-    if constexpr ((M & 1) == 1) db_slot<(G * 8 + M) / 2>(s, d, e, c, toff);
+    if constexpr ((M & 1) == 1) db_slot<(G * 8 + M) / 2>(s, c, toff);
     __builtin_amdgcn_sched_barrier(0);
-    db_group_tail<G, M + 1>(acc, s, d, e, c, toff, a0, a1, b0);
+    db_group_tail<G, M + 1>(acc, s, c, toff, a0, a1, b0);
   }
 }
 
 template <int G>
-__device__ __forceinline__ void db_groups(floatx4 (&acc)[16][2], DbStage& s, float (&d)[16],
-                                          float (&e)[4][4], const DbCtx& c,
+__device__ __forceinline__ void db_groups(floatx4 (&acc)[16][2], DbStage& s, const DbCtx& c,
                                           const uint32_t (&toff)[16], const floatx4* ua,
                                           const floatx4* vb, floatx4 a0, floatx4 a1,
                                           floatx4 b0) {
@@ -536,8 +540,8 @@ __device__ __forceinline__ void db_groups(floatx4 (&acc)[16][2], DbStage& s, flo
       na1 = ua[off + kHalf];
       nb0 = vb[off];
     }
-    db_group_tail<G, 0>(acc, s, d, e, c, toff, a0, a1, b0);
-    db_groups<G + 1>(acc, s, d, e, c, toff, ua, vb, na0, na1, nb0);
+    db_group_tail<G, 0>(acc, s, c, toff, a0, a1, b0);
+    db_groups<G + 1>(acc, s, c, toff, ua, vb, na0, na1, nb0);
   }
 }
 
@@ -567,9 +571,7 @@ __device__ __forceinline__ void db_step(floatx4 (&acc)[16][2], DbStage& s, float
   const floatx4* vb = reinterpret_cast<const floatx4*>(
       &Vs[((lane >> 4) * 64 + wt * 16 + (lane & 15)) * 20]);
   constexpr int kHalf = 16 * 20 / 4;
-  float d[16];
-  float e[4][4];
-  db_groups<0>(acc, s, d, e, c, toff, ua, vb, ua[0], ua[kHalf], vb[0]);
+  db_groups<0>(acc, s, c, toff, ua, vb, ua[0], ua[kHalf], vb[0]);
 }
 
 __global__ __launch_bounds__(kDBThreads, 1) void wino_conv_db_kernel(
