@@ -82,6 +82,8 @@ def parse() -> argparse.Namespace:
                         "(functional rehearsal only, not a valid measurement)")
     p.add_argument('--tiny', action='store_true',
                    help='tiny model of the same family (CI smoke test of this script only)')
+    p.add_argument('--channels-last', action='store_true',
+                   help='NHWC activations and weights (MIOpen NHWC kernels; AmoebaNet)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -165,10 +167,14 @@ def main() -> None:
 
     stage = PipelineStage(model, balance, device=device, chunks=chunks, checkpoint=checkpoint)
     del model
+    if args.channels_last:
+        stage.partition.to(memory_format=torch.channels_last)
     optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
 
     gen = torch.Generator(device=device).manual_seed(0)
     x = torch.rand(batch, *in_shape, device=device, generator=gen) if stage.is_first else None
+    if x is not None and args.channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
     if args.model == 'unet':
         target = torch.ones(batch, 1, 192, 192, device=device) if stage.is_last else None
         loss_fn = F.binary_cross_entropy_with_logits

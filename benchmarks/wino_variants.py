@@ -16,7 +16,8 @@ from torchgpipe_amd.ops import _ext  # noqa: E402
 SHAPES = [  # N, C, K, H
     (40, 64, 64, 192), (16, 64, 64, 192), (16, 128, 128, 96), (16, 256, 256, 48),
     (16, 512, 512, 24), (16, 1024, 1024, 12), (16, 2048, 2048, 6), (16, 2048, 1024, 6),
-    (16, 128, 64, 192), (40, 128, 32, 192), (3, 70, 130, 13),
+    (16, 128, 64, 192), (40, 128, 32, 192), (40, 32, 32, 192), (16, 128, 32, 192),
+    (16, 32, 32, 192), (3, 70, 130, 13),
 ]
 
 
