@@ -34,17 +34,23 @@ def main() -> None:
         x = torch.randn(n, c, h, h, device='cuda')
         w = torch.randn(k, c, 3, 3, device='cuda') / (3 * c ** 0.5)
         u = ops.wino_weight(w, False)
+        u4 = ops.wino4_weight(w, False) if max(a.variants) >= 4 else None
         ref = F.conv2d(x.double(), w.double(), padding=1)
         row = {'shape': [n, c, k, h]}
         for v in a.variants:
-            y = ops.wino_conv(x, u, None, k, v, 0)
+            # variants 4/5 = Winograd F(4x4,3x3) (winograd_f4.hip), the rest F(2x2,3x3)
+            def run():  # noqa: E306
+                if v >= 4:
+                    return ops.wino4_conv(x, u4, None, k, v, 0)
+                return ops.wino_conv(x, u, None, k, v, 0)
+            y = run()
             err = ((y.double() - ref).abs().max() / (ref.abs().max() + 1e-12)).item()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             for _ in range(3):
-                ops.wino_conv(x, u, None, k, v, 0)
+                run()
             s.record()
             for _ in range(a.iters):
-                ops.wino_conv(x, u, None, k, v, 0)
+                run()
             e.record()
             e.synchronize()
             ms = s.elapsed_time(e) / a.iters

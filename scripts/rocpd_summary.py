@@ -13,6 +13,9 @@ import csv
 import sqlite3
 
 GROUPS = [
+    ('tgpipe Winograd F(4,3) conv fwd/bwd-data on MFMA (HIP)',
+     ('f4_conv_kernel', 'f4_split_reduce')),
+    ('tgpipe Winograd weight transform (HIP)', ('wino_weight_kernel', 'f4_weight_kernel')),
     ('tgpipe Winograd F(2,3) conv fwd/bwd-data on MFMA (HIP)',
      ('wino_conv', 'wino_split_reduce')),
     ('tgpipe Winograd weight gradient on MFMA (HIP)', ('wino_wgrad',)),

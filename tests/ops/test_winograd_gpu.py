@@ -111,6 +111,34 @@ def test_direct_ops_small_channels():
         torch.testing.assert_close(y.double(), _ref(x, w), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize('shape', [(2, 64, 64, 24, 24), (1, 24, 130, 14, 10), (3, 16, 96, 9, 12),
+                                   (2, 40, 64, 8, 8), (1, 3, 64, 16, 16), (2, 5, 70, 7, 9),
+                                   (1, 16, 8, 1, 1), (4, 32, 32, 33, 2), (2, 256, 128, 12, 12),
+                                   (1, 64, 192, 20, 36)])
+@pytest.mark.parametrize('splits', [0, 1, 3])
+@pytest.mark.parametrize('variant', [4, 5])
+def test_f4_forward_and_flip(shape, splits, variant):
+    # Winograd F(4x4,3x3): edge tiles (H, W not multiples of 4), padded channels, split-K,
+    # and backward-data through the flipped weight transform
+    n, c, k, h, w = shape
+    torch.manual_seed(3)
+    x = torch.randn(n, c, h, w, device=cuda)
+    wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
+    b = torch.randn(k, device=cuda)
+    ops = _ext.require(x)
+    y = ops.wino4_conv(x, ops.wino4_weight(wt, False), b, k, variant, splits)
+    want = _ref(x, wt, b)
+    torch.testing.assert_close(y.double(), want, rtol=1e-4,
+                               atol=5e-5 * (want.abs().max().item() + 1))
+    dy = torch.randn(n, k, h, w, device=cuda)
+    dx = ops.wino4_conv(dy, ops.wino4_weight(wt, True), None, c, variant, splits)
+    want_dx = torch.ops.aten.convolution_backward(
+        dy.double(), x.double(), wt.double(), None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+        [True, False, False])[0]
+    torch.testing.assert_close(dx.double(), want_dx, rtol=1e-4,
+                               atol=5e-5 * (want_dx.abs().max().item() + 1))
+
+
 @pytest.mark.parametrize('variant', [0, 1, 2])
 @pytest.mark.parametrize('shape', [(2, 64, 64, 24, 24), (1, 24, 130, 14, 10), (3, 16, 96, 9, 12),
                                    (2, 40, 64, 8, 8)])

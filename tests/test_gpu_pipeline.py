@@ -56,20 +56,30 @@ def test_gpipe_training_gradients_match_reference_with_dropout(checkpoint):
 
 
 def test_fused_unet_matches_unfused_training_without_dropout():
+    # Both fp32 models are judged against an fp64 copy of the plain model: the fused one
+    # runs Winograd F(4x4,3x3) / F(2x2,3x3) whose fp32 rounding (~1e-5 relative per conv)
+    # is amplified by the instance norms of the 4x4 bottom planes, so elementwise
+    # fused-vs-plain tolerances would test MIOpen's rounding as much as ours.
     fused = small_unet(fused=True).cuda()
     plain = small_unet(fused=False).cuda()
     plain.load_state_dict(fused.state_dict())
-    for m in list(fused.modules()) + list(plain.modules()):
+    ref = copy.deepcopy(plain).double()
+    for m in list(fused.modules()) + list(plain.modules()) + list(ref.modules()):
         if hasattr(m, 'p'):
             m.p = 0.0
     x = torch.rand(2, 3, 32, 32, device='cuda')
     a = fused(x)
     b = plain(x)
+    c = ref(x.double())
     torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
     a.sum().backward()
     b.sum().backward()
-    for p, q in zip(fused.parameters(), plain.parameters()):
-        torch.testing.assert_close(p.grad, q.grad, rtol=1e-3, atol=1e-3)
+    c.sum().backward()
+    for p, q, r in zip(fused.parameters(), plain.parameters(), ref.parameters()):
+        scale = r.grad.norm().item() + 1e-6
+        err_fused = (p.grad.double() - r.grad).norm().item() / scale
+        err_plain = (q.grad.double() - r.grad).norm().item() / scale
+        assert err_fused < max(1e-3, 10 * err_plain), (p.shape, err_fused, err_plain)
 
 
 def test_deferred_batch_norm_on_gpu_matches_bn():

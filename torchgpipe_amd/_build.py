@@ -26,7 +26,7 @@ TARGET = os.path.join(HERE, '_C.so')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
 ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 
-KERNEL_SOURCES = ['kernels.hip', 'winograd.hip']
+KERNEL_SOURCES = ['kernels.hip', 'winograd.hip', 'winograd_f4.hip']
 HOST_SOURCES = ['bindings.cpp']
 HEADERS = ['kernels.h', 'philox.h']
 

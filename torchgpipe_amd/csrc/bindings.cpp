@@ -187,6 +187,54 @@ at::Tensor wino_conv(const at::Tensor& x_in, const at::Tensor& u,
   return y;
 }
 
+at::Tensor wino4_weight(const at::Tensor& w, bool flip) {
+  check_f32_gpu(w, "weight");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "weight must be [K][C][3][3]");
+  const int64_t out_channels = flip ? w.size(1) : w.size(0);
+  const int64_t red_channels = flip ? w.size(0) : w.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  auto u = at::empty({wino4_pad_reduction(red_channels), wino4_pad_output(out_channels), 36},
+                     w.options());
+  launch_wino4_weight(w.data_ptr<float>(), u.data_ptr<float>(), out_channels, red_channels, flip,
+                      stream_of(w));
+  return u;
+}
+
+at::Tensor wino4_conv(const at::Tensor& x_in, const at::Tensor& u,
+                      const c10::optional<at::Tensor>& bias, int64_t out_channels,
+                      int64_t variant, int64_t splits) {
+  auto x = x_in.contiguous();
+  check_f32_gpu(x, "x");
+  check_f32_gpu(u, "u");
+  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+  const int64_t n = x.size(0), r = x.size(1), h = x.size(2), w = x.size(3);
+  // the kernel's 36-float weight rows, channel padding and index ranges
+  TORCH_CHECK(u.dim() == 3 && u.size(2) == 36 && u.size(0) == wino4_pad_reduction(r) &&
+                  u.size(1) == wino4_pad_output(out_channels),
+              "F(4x4) transformed weight does not match the input/output channels");
+  TORCH_CHECK(u.device() == x.device(), "u must live on the input's device");
+  TORCH_CHECK(wino4_supported(n, r, h, w, out_channels),
+              "input too large for the F(4x4) kernel (needs < 1 GiB); use wino_conv");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_f32_gpu(*bias, "bias");
+    TORCH_CHECK(bias->numel() == out_channels, "bias must have K elements");
+    bptr = bias->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({n, out_channels, h, w}, x.options());
+  if (y.numel() == 0) return y;
+  TORCH_CHECK(variant == -1 || variant == 4 || variant == 5, "variant must be -1, 4 or 5");
+  const WinoPlan plan = wino4_plan(n, r, h, w, out_channels, static_cast<int>(variant),
+                                   static_cast<int>(splits));
+  at::Tensor ws;
+  if (plan.workspace > 0) ws = at::empty({plan.workspace}, x.options());
+  launch_wino4_conv(x.data_ptr<float>(), u.data_ptr<float>(), bptr, y.data_ptr<float>(),
+                    plan.workspace > 0 ? ws.data_ptr<float>() : nullptr, n, r, h, w,
+                    out_channels, plan, stream_of(x));
+  return y;
+}
+
 at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits,
                       int64_t variant) {
   auto x = x_in.contiguous();
@@ -240,6 +288,9 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("wino_wgrad(Tensor x, Tensor dy, int splits=0, int variant=-1) -> Tensor");
   m.def("wino_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
+  m.def("wino4_weight(Tensor w, bool flip) -> Tensor");
+  m.def("wino4_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
+        "int splits=0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
@@ -252,6 +303,8 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("wino_weight", &tgpipe::wino_weight);
   m.impl("wino_conv", &tgpipe::wino_conv);
   m.impl("wino_wgrad", &tgpipe::wino_wgrad);
+  m.impl("wino4_weight", &tgpipe::wino4_weight);
+  m.impl("wino4_conv", &tgpipe::wino4_conv);
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CompositeExplicitAutograd, m) {

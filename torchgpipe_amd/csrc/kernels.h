@@ -71,6 +71,22 @@ void launch_wino_conv(const float* x, const float* u, const float* bias, float* 
                       int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                       const WinoPlan& plan, hipStream_t stream);
 
+// Winograd F(4x4,3x3) (winograd_f4.hip): same convolution, 36 MFMA multiplies per 16
+// output pixels.  Transformed weights U4[Rp4/4][Op4/16][4][16][36] (Rp4 = multiple of 4,
+// Op4 = multiple of 64).  Variant 4: 64 output channels x 32 tiles per 8-wave workgroup
+// (one per CU); variant 5: 32 x 32 per 4-wave workgroup (two per CU); -1: auto.
+// wino4_supported(): input < 1 GiB etc.
+int64_t wino4_pad_reduction(int64_t r);
+int64_t wino4_pad_output(int64_t o);
+bool wino4_supported(int64_t n, int64_t r, int64_t h, int64_t w, int64_t o);
+void launch_wino4_weight(const float* w, float* u, int64_t out_channels, int64_t red_channels,
+                         bool flip, hipStream_t stream);
+WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                    int variant, int splits);
+void launch_wino4_conv(const float* x, const float* u, const float* bias, float* y, float* ws,
+                       int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                       const WinoPlan& plan, hipStream_t stream);
+
 // Weight gradient of the same convolution: dw[K][C][3][3] from x[N][C][H][W] and
 // dy[N][K][H][W]; `splits` > 1 needs a workspace of splits*K*C*9 floats.
 // variant 0: 64 x 32 (c x k) blocks, two workgroups per CU; variant 2: 64 x 64 blocks,

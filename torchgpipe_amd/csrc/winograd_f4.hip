@@ -1,0 +1,463 @@
+// Winograd F(4x4, 3x3) convolution on the fp32 MFMA pipes of CDNA4 (gfx950).
+//
+// The F(2x2,3x3) kernels of winograd.hip spend 16 matrix-core multiplies per 4 output
+// pixels (4 per pixel, 2.25x fewer than a direct 3x3); F(4x4,3x3) spends 36 per 16
+// (2.25 per pixel, 4x fewer), so the same matrix-core time covers 1.78x the output.
+// The price is a 6x6 input patch per tile and transforms with coefficients up to 8
+// (fp32 rounding at the 1e-6..1e-5 relative level, what cuDNN/MIOpen's F(4x4) fp32
+// kernels give as well).
+//
+//   V[xi][c][t] = (B^T d B)[xi]   6x6 input patch of tile t, channel c       (VALU -> LDS)
+//   U[xi][c][o] = (G g G^T)[xi]   pre-transformed weights                     (global -> LDS)
+//   M[xi][o][t] = sum_c U[xi][c][o] V[xi][c][t]   36 independent GEMMs        (MFMA 16x16x4)
+//   Y[o][t]     = A^T M A                         4x4 output patch            (registers -> HBM)
+//
+// Workgroup: 8 waves, 64 output channels x 32 tiles (512 output pixels per channel);
+// wave (wo, wt) = (wave & 3, wave >> 2) owns 16 channels x 16 tiles for all 36
+// positions (36 accumulator tiles, 144 registers), so the output transform runs in
+// registers with no exchange.  One pipeline step = 4 reduction channels (the MFMA K):
+// 36 MFMAs per wave, operands from a double-buffered LDS image (one barrier per step).
+// Staging is split by wave: waves 0-1 load and transform the 128 input patches of the
+// step (one per lane), waves 2-7 copy the step's 36 KiB weight slab -- the wave-to-SIMD
+// order puts one patch wave and one slab wave on two of the four SIMDs and slab waves
+// on the other two, so no SIMD carries two transform streams.
+//
+// Padding taps (image borders, tiles past the end) are raw buffer loads with an
+// out-of-range offset: the hardware returns 0, so no select sits between a load and
+// the transform, and no address ever leaves the tensor.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "kernels.h"
+
+namespace tgpipe {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kP = 36;                  // Winograd positions of a 6x6 tile
+constexpr int kC = 4;                   // reduction channels per step (MFMA K)
+constexpr int kOPad = 64;               // output-channel padding of U4
+constexpr int kT = 32;                  // output tiles per workgroup
+constexpr int kVImg = kC * kT * kP;     // 4608 floats: [4 c][32 t][36]
+
+// Workgroup of OG 16-channel output groups x 2 tile groups = 2*OG waves.
+//   OG = 4: 64 channels, 512 threads, 108 KiB LDS -> one workgroup per CU
+//   OG = 2: 32 channels, 256 threads,  72 KiB LDS -> two workgroups per CU, whose
+//           prologues / epilogues / barriers overlap the other's MFMAs
+template <int OG>
+struct F4Cfg {
+  static constexpr int kO = 16 * OG;
+  static constexpr int kThreads = 128 * OG;
+  static constexpr int kUImg = kC * kO * kP;            // [OG][4 c][16 o][36]
+  static constexpr int kBuf = kUImg + kVImg;            // one LDS buffer; two of them
+  static constexpr int kSlabThreads = kThreads - 128;   // waves 2.. copy the weight slab
+  static constexpr int kUVec = kUImg / 4 / kSlabThreads;  // float4 per slab thread (6 / 9)
+  static_assert(kUVec * 4 * kSlabThreads == kUImg, "slab waves copy the slab evenly");
+};
+// Buffer offsets of padding taps.  Row, channel (< 2^30) and column terms are added per
+// tap; any sum with a bad term is >= 2^30 - 4 >= the tensor's byte size (host-checked:
+// < 2^30 - 64), without wrapping past 2^32.  A valid row term of -4 (tap (-1, -1) of the
+// first plane) wraps back into range only together with a valid column term >= 4.
+constexpr uint32_t kBadRow = 0x80000000u;
+constexpr uint32_t kBadCol = 0x40000000u;
+
+// U4[Rp/4][Op/16][4 c][16 o][36] = G g G^T of (output channel o, reduction channel r).
+__global__ void f4_weight_kernel(const float* __restrict__ w, float* __restrict__ u, int O,
+                                 int R, int Op, int Rp, bool flip) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(Rp) * Op) return;
+  const int r = static_cast<int>(idx / Op);
+  const int o = static_cast<int>(idx % Op);
+  float g[3][3] = {};
+  if (r < R && o < O) {
+    if (!flip) {  // w = [O][R][3][3]
+      const float* src = w + (static_cast<int64_t>(o) * R + r) * 9;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) g[i][j] = src[i * 3 + j];
+    } else {      // w = [R][O][3][3] (forward weights), rotated by 180 degrees
+      const float* src = w + (static_cast<int64_t>(r) * O + o) * 9;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) g[i][j] = src[(2 - i) * 3 + (2 - j)];
+    }
+  }
+  // G: rows (1/4, 0, 0), -(1,1,1)/6, -(1,-1,1)/6, (1/24, 1/12, 1/6), (1/24, -1/12, 1/6), (0,0,1)
+  auto lift = [](float a, float b, float c, float (&out)[6]) {
+    out[0] = 0.25f * a;
+    out[1] = -(a + b + c) / 6.f;
+    out[2] = -(a - b + c) / 6.f;
+    out[3] = a / 24.f + b / 12.f + c / 6.f;
+    out[4] = a / 24.f - b / 12.f + c / 6.f;
+    out[5] = c;
+  };
+  float t[6][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float col[6];
+    lift(g[0][j], g[1][j], g[2][j], col);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) t[i][j] = col[i];
+  }
+  float v[kP];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float row[6];
+    lift(t[i][0], t[i][1], t[i][2], row);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) v[i * 6 + j] = row[j];
+  }
+  float* dst = u + (static_cast<int64_t>(r / kC) * (Op / 16) + o / 16) * (kC * 16 * kP) +
+               ((r % kC) * 16 + o % 16) * kP;
+#pragma unroll
+  for (int k = 0; k < kP / 4; ++k)
+    *reinterpret_cast<floatx4*>(dst + 4 * k) =
+        floatx4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+}
+
+// B^T of one 6-vector, in place.
+__device__ __forceinline__ void bt6(float& d0, float& d1, float& d2, float& d3, float& d4,
+                                    float& d5) {
+  const float p = d4 - 4.f * d2, q = d3 - 4.f * d1;
+  const float s = d4 - d2, t = 2.f * (d3 - d1);
+  const float r0 = 4.f * d0 - 5.f * d2 + d4;
+  const float r5 = 4.f * d1 - 5.f * d3 + d5;
+  d0 = r0;
+  d1 = p + q;
+  d2 = p - q;
+  d3 = s + t;
+  d4 = s - t;
+  d5 = r5;
+}
+
+// Patch-wave state: raw 6x6 patch (transformed in place) and its tap offsets.
+struct F4Patch {
+  float d[kP];
+  uint32_t row[6];   // byte offset of (row i, column x0) of channel 0, or kBadRow
+  uint32_t col[6];   // 4*j, or kBadCol for columns outside the image
+};
+
+__device__ __forceinline__ void f4_load_patch(F4Patch& p, __amdgpu_buffer_rsrc_t xr,
+                                              uint32_t chan_bytes) {
+  // Opaque per call: otherwise LICM hoists the 36 loop-invariant row+column sums out of
+  // the step loop and keeps them live (36 registers -> spills next to 144 accumulators).
+#pragma unroll
+  for (int i = 0; i < 6; ++i) asm volatile("" : "+v"(p.row[i]), "+v"(p.col[i]));
+  // The channel advance goes into the range-checked VGPR offset, not soffset (which the
+  // gfx9 raw-buffer range check ignores): padding channels of the last image then read
+  // zeros instead of past the tensor.
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const uint32_t rb = p.row[i] + chan_bytes;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      p.d[i * 6 + j] =
+          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rb + p.col[j], 0, 0));
+  }
+}
+
+// V = B^T d B into the lane's 36 contiguous LDS floats.
+__device__ __forceinline__ void f4_transform_store(F4Patch& p, float* vdst) {
+  float* d = p.d;
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    bt6(d[0 * 6 + j], d[1 * 6 + j], d[2 * 6 + j], d[3 * 6 + j], d[4 * 6 + j], d[5 * 6 + j]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+    bt6(d[i * 6 + 0], d[i * 6 + 1], d[i * 6 + 2], d[i * 6 + 3], d[i * 6 + 4], d[i * 6 + 5]);
+#pragma unroll
+  for (int k = 0; k < kP / 4; ++k)
+    reinterpret_cast<floatx4*>(vdst)[k] = floatx4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
+}
+
+template <typename Cfg>
+__device__ __forceinline__ void f4_load_slab(floatx4 (&ur)[Cfg::kUVec],
+                                             const float* __restrict__ u, int64_t slab, int stid) {
+#pragma unroll
+  for (int i = 0; i < Cfg::kUVec; ++i)
+    ur[i] = *reinterpret_cast<const floatx4*>(u + slab + 4 * (i * Cfg::kSlabThreads + stid));
+}
+
+template <typename Cfg>
+__device__ __forceinline__ void f4_store_slab(const floatx4 (&ur)[Cfg::kUVec], float* us,
+                                              int stid) {
+#pragma unroll
+  for (int i = 0; i < Cfg::kUVec; ++i)
+    *reinterpret_cast<floatx4*>(us + 4 * (i * Cfg::kSlabThreads + stid)) = ur[i];
+}
+
+// 36 MFMAs of one step: M[xi] += U[xi]^T V[xi] over the step's 4 channels.
+template <typename Cfg>
+__device__ __forceinline__ void f4_mfma(floatx4 (&acc)[kP], const float* buf, int lane, int wo,
+                                        int wt) {
+  const floatx4* ua =
+      reinterpret_cast<const floatx4*>(buf + ((wo * kC + (lane >> 4)) * 16 + (lane & 15)) * kP);
+  const floatx4* vb = reinterpret_cast<const floatx4*>(
+      buf + Cfg::kUImg + ((lane >> 4) * kT + wt * 16 + (lane & 15)) * kP);
+  // operand quad q+1 is read while quad q's 4 MFMAs issue
+  floatx4 a = ua[0], b = vb[0];
+#pragma unroll
+  for (int q = 0; q < kP / 4; ++q) {
+    floatx4 an = a, bn = b;
+    if (q + 1 < kP / 4) {
+      an = ua[q + 1];
+      bn = vb[q + 1];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      acc[4 * q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], b[e], acc[4 * q + e], 0, 0, 0);
+    a = an;
+    b = bn;
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+  for (int q = 0; q < kP / 4; ++q) {
+    if (q + 1 < kP / 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+  }
+}
+
+template <int OG>
+__global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
+    const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ bias,
+    float* __restrict__ y, int R, int H, int W, int O, int Rp, int Op, int TH, int TW, int P,
+    int tblocks, int oblocks, int splits, uint32_t x_bytes) {
+  using Cfg = F4Cfg<OG>;
+  constexpr int kO = Cfg::kO;
+  constexpr int kBuf = Cfg::kBuf;
+  __shared__ float lds[2 * kBuf];  // 108 KiB (OG 4) / 72 KiB (OG 2)
+
+  // XCD-aware bijective remap; output-channel blocks of one tile block are adjacent, so
+  // they share the block's input patches in one XCD's L2.
+  const int nwg = tblocks * oblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int ob = wgid % oblocks;
+  const int tb = (wgid / oblocks) % tblocks;
+  const int z = wgid / (oblocks * tblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wo = wave % OG;
+  const int wt = wave / OG;
+  const int t0 = tb * kT;
+  const int o0 = ob * kO;
+  const int HW = H * W;
+  const int tpi = TH * TW;
+
+  const int nsteps = Rp / kC;
+  const int s_begin = z * nsteps / splits;
+  const int s_end = (z + 1) * nsteps / splits;
+  floatx4 acc[kP];
+#pragma unroll
+  for (int i = 0; i < kP; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (wave < 2) {
+    // -- patch waves: tile t0 + 16*wave + (lane & 15), channel (lane >> 4) of each step --
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                          static_cast<int>(x_bytes), 0x00020000);
+    F4Patch p;
+    {
+      const int t = t0 + wave * 16 + (lane & 15);
+      const bool tv = t < P;
+      const int tt = tv ? t : 0;
+      const int n = tt / tpi;
+      const int rem = tt - n * tpi;
+      const int ty = rem / TW;
+      const int tx = rem - ty * TW;
+      const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
+      // element index of (row y0, column x0) of channel (lane >> 4); may be -1 (wraps)
+      const int64_t base = (static_cast<int64_t>(n) * R + (lane >> 4)) * HW +
+                           static_cast<int64_t>(y0) * W + x0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const bool ok = tv && y0 + i >= 0 && y0 + i < H;
+        p.row[i] = ok ? static_cast<uint32_t>((base + static_cast<int64_t>(i) * W) * 4) : kBadRow;
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const bool ok = x0 + j >= 0 && x0 + j < W;
+        p.col[j] = ok ? static_cast<uint32_t>(4 * j) : kBadCol;
+      }
+    }
+    float* vmine = lds + Cfg::kUImg + ((lane >> 4) * kT + wave * 16 + (lane & 15)) * kP;
+    const uint32_t step_bytes = static_cast<uint32_t>(kC) * HW * 4;
+    f4_load_patch(p, xr, s_begin * step_bytes);
+    f4_transform_store(p, vmine);
+    __syncthreads();
+    f4_load_patch(p, xr, min(s_begin + 1, s_end - 1) * step_bytes);
+    // Per step: transform the patch loaded one step ago into the idle buffer, send the
+    // loads of the step after next (a whole step of MFMAs hides them), then the MFMAs.
+    for (int s = s_begin; s < s_end; ++s) {
+      const int buf = (s - s_begin) & 1;
+      f4_transform_store(p, vmine + (buf ^ 1) * kBuf);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_load_patch(p, xr, min(s + 2, s_end - 1) * step_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+      __syncthreads();
+    }
+  } else {
+    // -- slab waves: the step's [OG o-groups][4 c][16 o][36] weight slab --
+    const int stid = tid - 128;
+    const int64_t slab_stride = static_cast<int64_t>(Op / 16) * (kC * 16 * kP);
+    const float* ubase = u + static_cast<int64_t>(o0 / 16) * (kC * 16 * kP);
+    floatx4 ur[Cfg::kUVec];
+    f4_load_slab<Cfg>(ur, ubase, s_begin * slab_stride, stid);
+    f4_store_slab<Cfg>(ur, lds, stid);
+    __syncthreads();
+    f4_load_slab<Cfg>(ur, ubase, min(s_begin + 1, s_end - 1) * slab_stride, stid);
+    for (int s = s_begin; s < s_end; ++s) {
+      const int buf = (s - s_begin) & 1;
+      f4_store_slab<Cfg>(ur, lds + (buf ^ 1) * kBuf, stid);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_load_slab<Cfg>(ur, ubase, min(s + 2, s_end - 1) * slab_stride, stid);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+      __syncthreads();
+    }
+  }
+
+  // -- output transform Y = A^T M A from the accumulators --------------------------------
+  // Lane (wt*16 + j) holds tile t0 + wt*16 + j; register r of accumulator xi holds output
+  // channel o0 + wo*16 + 4*(lane >> 4) + r.  Split-K partials go to slab z of y.
+  const int tp = t0 + wt * 16 + (lane & 15);
+  if (tp >= P) return;
+  float* ydst = y + static_cast<int64_t>(z) * (P / tpi) * O * HW;
+  const bool add_bias = bias != nullptr && splits == 1;
+  const int pn = tp / tpi;
+  const int prem = tp - pn * tpi;
+  const int pty = prem / TW;
+  const int py = 4 * pty;
+  const int px = 4 * (prem - pty * TW);
+  const bool full = (W & 3) == 0 && py + 4 <= H;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = o0 + wo * 16 + 4 * (lane >> 4) + r;
+    if (o >= O) continue;
+    // A^T along rows (i), for every column j
+    float s[4][6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const float m0 = acc[0 * 6 + j][r], m1 = acc[1 * 6 + j][r], m2 = acc[2 * 6 + j][r];
+      const float m3 = acc[3 * 6 + j][r], m4 = acc[4 * 6 + j][r], m5 = acc[5 * 6 + j][r];
+      const float a = m1 + m2, b = m1 - m2, c = m3 + m4, d = m3 - m4;
+      s[0][j] = m0 + a + c;
+      s[1][j] = b + 2.f * d;
+      s[2][j] = a + 4.f * c;
+      s[3][j] = b + 8.f * d + m5;
+    }
+    const float bv = add_bias ? bias[o] : 0.f;
+    float* yp = ydst + (static_cast<int64_t>(pn) * O + o) * HW + static_cast<int64_t>(py) * W + px;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a = s[k][1] + s[k][2], b = s[k][1] - s[k][2];
+      const float c = s[k][3] + s[k][4], d = s[k][3] - s[k][4];
+      const floatx4 out{s[k][0] + a + c + bv, b + 2.f * d + bv, a + 4.f * c + bv,
+                        b + 8.f * d + s[k][5] + bv};
+      if (full) {
+        *reinterpret_cast<floatx4*>(yp + k * W) = out;
+      } else if (py + k < H) {
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+          if (px + l < W) yp[k * W + l] = out[l];
+      }
+    }
+  }
+}
+
+// y[i] = sum_z ws[z][i] (+ bias[o]) over the split-K partial slabs.
+__global__ void f4_split_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ bias,
+                                       float* __restrict__ y, int64_t numel, int64_t hw, int O,
+                                       int splits) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= numel) return;
+  float v = bias ? bias[(i / hw) % O] : 0.f;
+  for (int z = 0; z < splits; ++z) v += ws[z * numel + i];
+  y[i] = v;
+}
+
+}  // namespace
+
+int64_t wino4_pad_reduction(int64_t r) { return (r + kC - 1) / kC * kC; }
+int64_t wino4_pad_output(int64_t o) { return (o + kOPad - 1) / kOPad * kOPad; }
+
+bool wino4_supported(int64_t n, int64_t r, int64_t h, int64_t w, int64_t o) {
+  // 32-bit tile / offset arithmetic and the padding-tap encoding need the input below
+  // 1 GiB; every split keeps >= 1 step.
+  const int64_t x_bytes = n * r * h * w * 4;
+  const int64_t tiles = n * ((h + 3) / 4) * ((w + 3) / 4);
+  return x_bytes > 0 && x_bytes < (int64_t{1} << 30) - 64 && tiles < (int64_t{1} << 30) &&
+         n * o * h * w < (int64_t{1} << 31) && o < (1 << 24);
+}
+
+void launch_wino4_weight(const float* w, float* u, int64_t out_channels, int64_t red_channels,
+                         bool flip, hipStream_t stream) {
+  const int64_t Op = wino4_pad_output(out_channels);
+  const int64_t Rp = wino4_pad_reduction(red_channels);
+  const int64_t total = Rp * Op;
+  hipLaunchKernelGGL(f4_weight_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256),
+                     0, stream, w, u, static_cast<int>(out_channels),
+                     static_cast<int>(red_channels), static_cast<int>(Op), static_cast<int>(Rp),
+                     flip);
+}
+
+WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                    int variant, int splits) {
+  WinoPlan plan;
+  plan.variant = variant == 4 || variant == 5 ? variant : 5;
+  const int og = plan.variant == 4 ? 4 : 2;
+  const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
+  const int64_t blocks = ((P + kT - 1) / kT) * ((out_channels + 16 * og - 1) / (16 * og));
+  const int64_t steps = wino4_pad_reduction(red_channels) / kC;
+  if (splits > 0) {
+    plan.splits = static_cast<int>(std::min<int64_t>(splits, steps));
+  } else {
+    // >= 2 rounds of workgroups over the 256 CUs (4 - og... one or two per CU), >= 16
+    // steps per split to amortise the pipeline prologue and the output transform
+    const int64_t target = og == 4 ? 512 : 1024;
+    int64_t s = 1;
+    while (blocks * s < target && steps / (s * 2) >= 16) s *= 2;
+    plan.splits = static_cast<int>(s);
+  }
+  plan.workspace = plan.splits > 1 ? plan.splits * n * out_channels * h * w : 0;
+  return plan;
+}
+
+void launch_wino4_conv(const float* x, const float* u, const float* bias, float* y, float* ws,
+                       int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                       const WinoPlan& plan, hipStream_t stream) {
+  const int64_t Rp = wino4_pad_reduction(red_channels);
+  const int64_t Op = wino4_pad_output(out_channels);
+  const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
+  const int64_t P = n * th * tw;
+  const int og = plan.variant == 4 ? 4 : 2;
+  const int tblocks = static_cast<int>((P + kT - 1) / kT);
+  const int oblocks = static_cast<int>((out_channels + 16 * og - 1) / (16 * og));
+  const int splits = plan.splits;
+  const int64_t nwg = static_cast<int64_t>(tblocks) * oblocks * splits;
+  auto kernel = og == 4 ? f4_conv_kernel<4> : f4_conv_kernel<2>;
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(128 * og), 0, stream,
+                     x, u, bias, splits > 1 ? ws : y, static_cast<int>(red_channels),
+                     static_cast<int>(h), static_cast<int>(w), static_cast<int>(out_channels),
+                     static_cast<int>(Rp), static_cast<int>(Op), static_cast<int>(th),
+                     static_cast<int>(tw), static_cast<int>(P), tblocks, oblocks, splits,
+                     static_cast<uint32_t>(n * red_channels * h * w * 4));
+  if (splits > 1) {
+    const int64_t numel = n * out_channels * h * w;
+    hipLaunchKernelGGL(f4_split_reduce_kernel, dim3(static_cast<unsigned>((numel + 255) / 256)),
+                       dim3(256), 0, stream, ws, bias, y, numel, h * w,
+                       static_cast<int>(out_channels), splits);
+  }
+}
+
+}  // namespace tgpipe

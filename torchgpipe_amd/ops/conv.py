@@ -1,8 +1,9 @@
-"""3×3 convolution on the CDNA4 matrix cores: Winograd F(2×2, 3×3) with f32 MFMA.
+"""3×3 convolution on the CDNA4 matrix cores: Winograd F(4×4, 3×3) / F(2×2, 3×3) with f32 MFMA.
 
 :class:`WinogradConv2d` is a drop-in ``nn.Conv2d`` (same parameters, same
 state-dict keys) whose 3×3 / stride 1 / pad 1 / fp32 GPU forward and
-backward-data run the fused HIP kernel of ``csrc/winograd.hip``; the weight
+backward-data run the fused HIP kernels of ``csrc/winograd_f4.hip`` (planes ≥ 8²)
+and ``csrc/winograd.hip`` (smaller planes); the weight
 gradient runs the Winograd wgrad kernels wherever they beat MIOpen's wrw (see
 ``_wgrad_on_mfma``).
 Other configurations, CPU tensors and non-fp32 dtypes use ``F.conv2d``.
@@ -24,33 +25,62 @@ __all__ = ['WinogradConv2d', 'winograd_conv2d', 'wino_eligible']
 
 
 class _TransformCache:
-    """Winograd-domain weights keyed by (storage, version, device) of the parameter."""
+    """Winograd-domain weights keyed by (storage, version, device) of the parameter.
+
+    Entries per (flip, f4): F(2x2) ``U[Rp][Op][16]`` and F(4x4) ``U4[Rp/4][Op/16][4][16][36]``.
+    """
 
     __slots__ = ('_entries',)
 
     def __init__(self) -> None:
-        self._entries: Dict[bool, Tuple[Tuple[int, int, torch.device], Tensor]] = {}
+        self._entries: Dict[Tuple[bool, bool], Tuple[Tuple[int, int, torch.device], Tensor]] = {}
 
-    def get(self, weight: Tensor, flip: bool) -> Tensor:
+    def get(self, weight: Tensor, flip: bool, f4: bool = False) -> Tensor:
         key = (weight.data_ptr(), weight._version, weight.device)
-        hit = self._entries.get(flip)
+        hit = self._entries.get((flip, f4))
         if hit is not None and hit[0] == key:
             return hit[1]
+        ops = _ext.require(weight)
         with torch.no_grad():
-            u = _ext.require(weight).wino_weight(weight.detach().contiguous(), flip)
-        self._entries[flip] = (key, u)
+            w = weight.detach().contiguous()
+            u = ops.wino4_weight(w, flip) if f4 else ops.wino_weight(w, flip)
+        self._entries[(flip, f4)] = (key, u)
         return u
 
     def clear(self) -> None:
         self._entries.clear()
 
 
+# Winograd F(4x4,3x3) (csrc/winograd_f4.hip) on planes of at least this size; F(2x2) on
+# smaller ones.  benchmarks/wino_variants.py (profiles/wino_f4_variants.json): F(4x4)
+# 1.17-1.45x faster than F(2x2) from 12^2 up, slower at 6^2 (a 4x4 tile wastes 5/9 of a
+# 6-pixel plane).  The F(4x4) kernel's 32-bit offsets need the input below 1 GiB.
+F4_MIN_PLANE = 8
+F4_MAX_BYTES = (1 << 30) - 64
+
+
+def _use_f4(x: Tensor) -> bool:
+    return (min(x.shape[2], x.shape[3]) >= F4_MIN_PLANE
+            and x.numel() * x.element_size() < F4_MAX_BYTES)
+
+
+def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tensor],
+          flip: bool) -> Tensor:
+    """One Winograd convolution launch: forward (flip=False) or backward-data (flip=True)."""
+    ops = _ext.require(x)
+    out_channels = weight.shape[1] if flip else weight.shape[0]
+    if _use_f4(x):
+        # 32-channel workgroups when a 64-channel one would idle half its waves
+        variant = 5 if out_channels <= 32 else 4
+        return ops.wino4_conv(x, cache.get(weight, flip, True), bias, out_channels, variant)
+    return ops.wino_conv(x, cache.get(weight, flip), bias, out_channels)
+
+
 class _WinogradConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: Tensor, weight: Tensor, bias: Optional[Tensor],  # type: ignore[override]
                 cache: _TransformCache) -> Tensor:
-        ops = _ext.require(x)
-        y = ops.wino_conv(x, cache.get(weight, False), bias, weight.shape[0])
+        y = _conv(x.contiguous(), cache, weight, bias, False)
         ctx.save_for_backward(x, weight)
         ctx.cache = cache
         ctx.has_bias = bias is not None
@@ -62,8 +92,7 @@ class _WinogradConv(torch.autograd.Function):
         dy = dy.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _ext.require(dy).wino_conv(dy, ctx.cache.get(weight, True), None,
-                                             weight.shape[1])
+            dx = _conv(dy, ctx.cache, weight, None, True)
         if ctx.needs_input_grad[1]:
             if _wgrad_on_mfma(x, weight):
                 dw = _ext.require(dy).wino_wgrad(x, dy, 0)
