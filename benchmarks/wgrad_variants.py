@@ -1,4 +1,4 @@
-"""Time the Winograd weight-gradient kernels (variant 0 / 2) against MIOpen's wrw.
+"""Time the Winograd weight-gradient kernels (F(2x2) variants 0 / 2, F(4x4)) against MIOpen's wrw.
 
     python benchmarks/wgrad_variants.py --out gpurun_out/wgrad_variants.json
 """
@@ -60,6 +60,12 @@ def main() -> None:
             ms = timed(lambda: ops.wino_wgrad(x, dy, 0, v), a.iters)
             row[f'v{v}'] = {'ms': round(ms, 4), 'direct_tflops': round(flops / ms / 1e9, 1),
                             'rel_err': err}
+        if min(h, h) >= 8:
+            got = ops.wino4_wgrad(x, dy, 0)
+            err = ((got.double() - ref).abs().max() / ref.abs().max()).item()
+            ms = timed(lambda: ops.wino4_wgrad(x, dy, 0), a.iters)
+            row['f4'] = {'ms': round(ms, 4), 'direct_tflops': round(flops / ms / 1e9, 1),
+                         'rel_err': err}
         rows.append(row)
         print(json.dumps(row), flush=True)
     if a.out:

@@ -18,6 +18,9 @@ SHAPES = [  # N, C, K, H
     (16, 512, 512, 24), (16, 1024, 1024, 12), (16, 2048, 2048, 6), (16, 2048, 1024, 6),
     (16, 128, 64, 192), (40, 128, 32, 192), (40, 32, 32, 192), (16, 128, 32, 192),
     (16, 32, 32, 192), (3, 70, 130, 13),
+    # the micro-batch of the 1-GPU bench (B=80, 2 chunks)
+    (40, 128, 128, 96), (40, 256, 256, 48), (40, 512, 512, 24), (40, 1024, 1024, 12),
+    (40, 2048, 2048, 6),
 ]
 
 

@@ -32,11 +32,36 @@ def skip_routes(model, out_bytes):
     return routes
 
 
+def calibrate(fwd, bwd, m, paths):
+    """Per-layer times scaled so every stage measured by the stage harness at this
+    micro-batch count matches its measured device time (forward + recompute + backward
+    of all micro-batches); layers no harness covers keep their profiled times."""
+    fwd, bwd = list(fwd), list(bwd)
+    for path in paths:
+        run = json.load(open(path))
+        if run['args']['chunks'] != m:
+            continue
+        ck = run['args'].get('checkpoint', 'except_last')
+        for st in run['stages']:
+            lo, hi = st['layers']
+            f, b = sum(fwd[lo:hi]), sum(bwd[lo:hi])
+            recompute = f * (m - 1 if ck == 'except_last' else m if ck == 'always' else 0)
+            predicted = (f + b) * m + recompute
+            scale = st['device_ms'] / predicted
+            for i in range(lo, hi):
+                fwd[i] *= scale
+                bwd[i] *= scale
+    return fwd, bwd
+
+
 def main() -> None:
     p = argparse.ArgumentParser()
     p.add_argument('--profile', required=True)
     p.add_argument('--model', choices=['unet', 'amoebanet'], default='unet')
     p.add_argument('--link-gbps', type=float, default=60.0)
+    p.add_argument('--calibrate', nargs='*', default=[],
+                   help='benchmarks/stage_harness.py outputs: scale the layers of each '
+                        'measured stage by measured / profiled stage time before searching')
     args = p.parse_args()
     import bench
     prof = json.load(open(args.profile))
@@ -57,6 +82,7 @@ def main() -> None:
         bwd = [b * scale for b in pr['bwd_ms']]
         ob = [b * scale for b in pr['out_bytes']]
         skips = skip_routes(model, ob)
+        fwd, bwd = calibrate(fwd, bwd, m, args.calibrate)
         kw = dict(out_bytes=ob, skips=skips, link_gbps=args.link_gbps)
         ck = 'except_last' if m > 1 else 'always'
         t_ref = step_time(fwd, bwd, exp['balance'], m, ck, **kw)

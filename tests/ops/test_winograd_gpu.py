@@ -139,6 +139,26 @@ def test_f4_forward_and_flip(shape, splits, variant):
                                atol=5e-5 * (want_dx.abs().max().item() + 1))
 
 
+@pytest.mark.parametrize('shape', [(2, 64, 64, 24, 24), (1, 24, 130, 14, 10), (3, 16, 96, 9, 12),
+                                   (2, 40, 64, 8, 8), (1, 3, 64, 16, 16), (2, 5, 70, 7, 9),
+                                   (1, 16, 8, 1, 1), (4, 32, 32, 33, 2), (2, 256, 128, 12, 12),
+                                   (5, 64, 33, 20, 36)])
+@pytest.mark.parametrize('splits', [0, 1, 3, 1000])
+def test_f4_wgrad(shape, splits):
+    # F(4x4,3x3) weight gradient: edge tiles, channel blocks past C / K, split tiles
+    # (1000 is capped at the step count)
+    n, c, k, h, w = shape
+    torch.manual_seed(5)
+    x = torch.randn(n, c, h, w, device=cuda)
+    dy = torch.randn(n, k, h, w, device=cuda)
+    got = _ext.require(x).wino4_wgrad(x, dy, splits)
+    want = torch.ops.aten.convolution_backward(
+        dy.double(), x.double(), torch.zeros(k, c, 3, 3, device=cuda, dtype=torch.double), None,
+        [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    torch.testing.assert_close(got.double(), want, rtol=1e-4,
+                               atol=5e-5 * (want.abs().max().item() + 1))
+
+
 @pytest.mark.parametrize('variant', [0, 1, 2])
 @pytest.mark.parametrize('shape', [(2, 64, 64, 24, 24), (1, 24, 130, 14, 10), (3, 16, 96, 9, 12),
                                    (2, 40, 64, 8, 8)])

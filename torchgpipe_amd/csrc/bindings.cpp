@@ -269,6 +269,34 @@ at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t s
   return dw;
 }
 
+at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits) {
+  auto x = x_in.contiguous();
+  auto dy = dy_in.contiguous();
+  check_f32_gpu(x, "x");
+  check_f32_gpu(dy, "dy");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "x and dy must be NCHW");
+  const int64_t n = x.size(0), c = x.size(1), h = x.size(2), w = x.size(3), k = dy.size(1);
+  TORCH_CHECK(dy.size(0) == n && dy.size(2) == h && dy.size(3) == w,
+              "dy must be [N][K][H][W] of a 3x3/s1/p1 convolution of x");
+  TORCH_CHECK(dy.device() == x.device(), "x and dy must share a device");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto dw = at::empty({k, c, 3, 3}, x.options());
+  if (n == 0 || h == 0 || w == 0 || c == 0 || k == 0) return dw.zero_();
+  // 32-bit buffer offsets and tile indices
+  TORCH_CHECK(wino4_wgrad_supported(n, c, k, h, w),
+              "input too large for the F(4x4) weight-gradient kernel (needs < 1 GiB); "
+              "use wino_wgrad");
+  // every split owns >= 1 step of 4 tiles
+  const int64_t steps = (n * ((h + 3) / 4) * ((w + 3) / 4) + 3) / 4;
+  const int s = static_cast<int>(std::min<int64_t>(
+      splits > 0 ? splits : wino4_wgrad_splits(n, c, k, h, w), steps));
+  at::Tensor ws;
+  if (s > 1) ws = at::empty({s * k * c * 9}, x.options());
+  launch_wino4_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), dw.data_ptr<float>(),
+                     s > 1 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s, stream_of(x));
+  return dw;
+}
+
 }  // namespace
 }  // namespace tgpipe
 
@@ -289,6 +317,7 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("wino_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
   m.def("wino4_weight(Tensor w, bool flip) -> Tensor");
+  m.def("wino4_wgrad(Tensor x, Tensor dy, int splits=0) -> Tensor");
   m.def("wino4_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
 }
@@ -305,6 +334,7 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("wino_wgrad", &tgpipe::wino_wgrad);
   m.impl("wino4_weight", &tgpipe::wino4_weight);
   m.impl("wino4_conv", &tgpipe::wino4_conv);
+  m.impl("wino4_wgrad", &tgpipe::wino4_wgrad);
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CompositeExplicitAutograd, m) {

@@ -87,6 +87,15 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
                        int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                        const WinoPlan& plan, hipStream_t stream);
 
+// F(4x4,3x3) weight gradient (winograd_f4.hip): dw[K][C][3][3], 36 MFMA multiplies per
+// 16 output pixels of each (k, c) pair; 64 k x 32 c per 8-wave workgroup, tiles split
+// over `splits` workgroups (> 1 needs a workspace of splits*K*C*9 floats).
+bool wino4_wgrad_supported(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
+int wino4_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
+void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
+                        int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                        hipStream_t stream);
+
 // Weight gradient of the same convolution: dw[K][C][3][3] from x[N][C][H][W] and
 // dy[N][K][H][W]; `splits` > 1 needs a workspace of splits*K*C*9 floats.
 // variant 0: 64 x 32 (c x k) blocks, two workgroups per CU; variant 2: 64 x 64 blocks,

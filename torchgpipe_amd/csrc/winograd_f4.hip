@@ -142,6 +142,9 @@ struct F4Patch {
   uint32_t col[6];   // 4*j, or kBadCol for columns outside the image
 };
 
+// kVec (W % 4 == 0): the 4 centre columns of a patch row are one aligned 16-byte load
+// (valid whenever the row is), the two halo columns dword loads -- 18 loads, not 36.
+template <bool kVec>
 __device__ __forceinline__ void f4_load_patch(F4Patch& p, __amdgpu_buffer_rsrc_t xr,
                                               uint32_t chan_bytes) {
   // Opaque per call: otherwise LICM hoists the 36 loop-invariant row+column sums out of
@@ -154,10 +157,20 @@ __device__ __forceinline__ void f4_load_patch(F4Patch& p, __amdgpu_buffer_rsrc_t
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const uint32_t rb = p.row[i] + chan_bytes;
+    if constexpr (kVec) {
+      p.d[i * 6 + 0] =
+          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rb + p.col[0], 0, 0));
+      const auto mid = __builtin_amdgcn_raw_buffer_load_b128(xr, rb + 4, 0, 0);
 #pragma unroll
-    for (int j = 0; j < 6; ++j)
-      p.d[i * 6 + j] =
-          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rb + p.col[j], 0, 0));
+      for (int j = 0; j < 4; ++j) p.d[i * 6 + 1 + j] = __uint_as_float(mid[j]);
+      p.d[i * 6 + 5] =
+          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rb + p.col[5], 0, 0));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        p.d[i * 6 + j] =
+            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, rb + p.col[j], 0, 0));
+    }
   }
 }
 
@@ -222,7 +235,7 @@ __device__ __forceinline__ void f4_mfma(floatx4 (&acc)[kP], const float* buf, in
   }
 }
 
-template <int OG>
+template <int OG, bool kVec>
 __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
     const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ bias,
     float* __restrict__ y, int R, int H, int W, int O, int Rp, int Op, int TH, int TW, int P,
@@ -291,17 +304,17 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
     }
     float* vmine = lds + Cfg::kUImg + ((lane >> 4) * kT + wave * 16 + (lane & 15)) * kP;
     const uint32_t step_bytes = static_cast<uint32_t>(kC) * HW * 4;
-    f4_load_patch(p, xr, s_begin * step_bytes);
+    f4_load_patch<kVec>(p, xr, s_begin * step_bytes);
     f4_transform_store(p, vmine);
     __syncthreads();
-    f4_load_patch(p, xr, min(s_begin + 1, s_end - 1) * step_bytes);
+    f4_load_patch<kVec>(p, xr, min(s_begin + 1, s_end - 1) * step_bytes);
     // Per step: transform the patch loaded one step ago into the idle buffer, send the
     // loads of the step after next (a whole step of MFMAs hides them), then the MFMAs.
     for (int s = s_begin; s < s_end; ++s) {
       const int buf = (s - s_begin) & 1;
       f4_transform_store(p, vmine + (buf ^ 1) * kBuf);
       __builtin_amdgcn_sched_barrier(0);
-      f4_load_patch(p, xr, min(s + 2, s_end - 1) * step_bytes);
+      f4_load_patch<kVec>(p, xr, min(s + 2, s_end - 1) * step_bytes);
       __builtin_amdgcn_sched_barrier(0);
       f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
       __syncthreads();
@@ -386,6 +399,271 @@ __global__ void f4_split_reduce_kernel(const float* __restrict__ ws, const float
   y[i] = v;
 }
 
+
+// ---- weight gradient: dW = G^T [ sum_t (A dY_t A^T) (.) (B^T d_t B) ] G ------------------
+//
+// The trilinear form of F(4x4,3x3), sum_xi (G g)_xi (B^T d)_xi (A y)_xi = sum y_i g_j d_{i+j},
+// read the other way round: the correlation of a 6x6 input patch d with the 4x4 output
+// gradient tile dY is the 3x3 weight gradient, G^T [(A dY A^T) (.) (B^T d B)] G.  Summed
+// over all tiles t: 36 independent GEMMs dU[xi][k][c] = sum_t M'[xi][k][t] V[xi][c][t]
+// with the tiles as the reduction (MFMA K), then one output transform per (k, c).
+//
+// Workgroup: 8 waves, 64 output channels (k, MFMA rows) x 32 input channels (c, MFMA
+// columns), all 36 positions in accumulators (the forward's f4_mfma on the same LDS
+// image shapes).  One step = 4 tiles.  Staging by wave: waves 0-1 load and transform the
+// step's 128 input patches (4 tiles x 32 channels, one per lane), waves 2, 3, 6, 7 the 256
+// gradient tiles (4 tiles x 64 channels) -- SIMDs 0/1 carry one patch wave each, SIMDs
+// 2/3 two gradient waves each -- and waves 4-5 only multiply.  Lanes of one channel take 4
+// horizontally adjacent tiles, so a load instruction touches 16 channel planes.
+
+// A of one 4-vector: (y0, y0+y1+y2+y3, y0-y1+y2-y3, y0+2y1+4y2+8y3, y0-2y1+4y2-8y3, y3).
+__device__ __forceinline__ void a6(float y0, float y1, float y2, float y3, float (&o)[6]) {
+  const float e = y0 + y2, od = y1 + y3;
+  const float e2 = y0 + 4.f * y2, o2 = 2.f * y1 + 8.f * y3;
+  o[0] = y0;
+  o[1] = e + od;
+  o[2] = e - od;
+  o[3] = e2 + o2;
+  o[4] = e2 - o2;
+  o[5] = y3;
+}
+
+// Running tile position of a staging lane: advanced by 4 tiles per fetched step.
+struct F4TileCursor {
+  int n, ty, tx;
+};
+
+__device__ __forceinline__ void f4_cursor_advance(F4TileCursor& cur, int TH, int TW) {
+  cur.tx += 4;
+  while (cur.tx >= TW) {
+    cur.tx -= TW;
+    if (++cur.ty == TH) {
+      cur.ty = 0;
+      ++cur.n;
+    }
+  }
+}
+
+// 6x6 input patch of (tile at cur, channel ch) -> p.row / p.col; zeros past N or C.
+__device__ __forceinline__ void f4_patch_offsets(F4Patch& p, const F4TileCursor& cur, int ch,
+                                                 int N, int C, int H, int W) {
+  const bool tv = cur.n < N && ch < C;
+  const int y0 = 4 * cur.ty - 1, x0 = 4 * cur.tx - 1;
+  const int64_t base =
+      (static_cast<int64_t>(tv ? cur.n : 0) * C + (tv ? ch : 0)) * H * W +
+      static_cast<int64_t>(y0) * W + x0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const bool ok = tv && y0 + i >= 0 && y0 + i < H;
+    p.row[i] = ok ? static_cast<uint32_t>((base + static_cast<int64_t>(i) * W) * 4) : kBadRow;
+  }
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const bool ok = x0 + j >= 0 && x0 + j < W;
+    p.col[j] = ok ? static_cast<uint32_t>(4 * j) : kBadCol;
+  }
+}
+
+// 4x4 gradient tile of (tile at cur, channel k): zeros outside; kVec (W % 4 == 0): one
+// 16-byte load per row.
+template <bool kVec>
+__device__ __forceinline__ void f4_load_dy(float (&g)[16], __amdgpu_buffer_rsrc_t dyr,
+                                           const F4TileCursor& cur, int k, int N, int K, int H,
+                                           int W) {
+  const bool tv = cur.n < N && k < K;
+  const int y0 = 4 * cur.ty, x0 = 4 * cur.tx;
+  const int64_t base =
+      (static_cast<int64_t>(tv ? cur.n : 0) * K + (tv ? k : 0)) * H * W +
+      static_cast<int64_t>(y0) * W + x0;
+  uint32_t col[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) col[j] = x0 + j < W ? static_cast<uint32_t>(4 * j) : kBadCol;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t rb = tv && y0 + i < H
+                            ? static_cast<uint32_t>((base + static_cast<int64_t>(i) * W) * 4)
+                            : kBadRow;
+    if constexpr (kVec) {
+      const auto row = __builtin_amdgcn_raw_buffer_load_b128(dyr, rb, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[i * 4 + j] = __uint_as_float(row[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        g[i * 4 + j] =
+            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(dyr, rb + col[j], 0, 0));
+    }
+  }
+}
+
+// M' = A g A^T into the lane's 36 contiguous LDS floats.
+__device__ __forceinline__ void f4_dy_transform_store(const float (&g)[16], float* mdst) {
+  float t[6][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float col[6];
+    a6(g[0 * 4 + j], g[1 * 4 + j], g[2 * 4 + j], g[3 * 4 + j], col);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) t[i][j] = col[i];
+  }
+  float m[kP];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float row[6];
+    a6(t[i][0], t[i][1], t[i][2], t[i][3], row);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) m[i * 6 + j] = row[j];
+  }
+#pragma unroll
+  for (int q = 0; q < kP / 4; ++q)
+    reinterpret_cast<floatx4*>(mdst)[q] = floatx4{m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]};
+}
+
+// G^T of one 6-vector: 3 outputs.
+__device__ __forceinline__ void gt6(const float (&u)[6], float (&w)[3]) {
+  const float a = u[1] + u[2], b = u[3] + u[4];
+  w[0] = 0.25f * u[0] - a * (1.f / 6.f) + b * (1.f / 24.f);
+  w[1] = (u[2] - u[1]) * (1.f / 6.f) + (u[3] - u[4]) * (1.f / 12.f);
+  w[2] = (b - a) * (1.f / 6.f) + u[5];
+}
+
+constexpr int kWgThreads = 512;
+
+template <bool kVec>
+__global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dw, int N,
+    int C, int K, int H, int W, int TH, int TW, int P, int cblocks, int kblocks, int splits,
+    uint32_t x_bytes, uint32_t dy_bytes) {
+  using Cfg = F4Cfg<4>;
+  constexpr int kBuf = Cfg::kBuf;
+  __shared__ float lds[2 * kBuf];  // [buffer][M' 64k x 4t x 36 | V 4t x 32c x 36]: 108 KiB
+
+  const int nwg = cblocks * kblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int cb = wgid % cblocks;
+  const int kb = (wgid / cblocks) % kblocks;
+  const int z = wgid / (cblocks * kblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wo = wave & 3;   // 16 k rows
+  const int wt = wave >> 2;  // 16 c columns
+  const int c0 = cb * 32;
+  const int k0 = kb * 64;
+
+  const int nsteps = (P + 3) / 4;
+  const int s_begin = static_cast<int>(static_cast<int64_t>(z) * nsteps / splits);
+  const int s_end = static_cast<int>(static_cast<int64_t>(z + 1) * nsteps / splits);
+  floatx4 acc[kP];
+#pragma unroll
+  for (int i = 0; i < kP; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // staging lane's tile cursor: tile 4*s_begin + (lane >> 4)
+  F4TileCursor cur;
+  {
+    const int t = 4 * s_begin + (lane >> 4);
+    const int tpi = TH * TW;
+    cur.n = t / tpi;
+    const int rem = t - cur.n * tpi;
+    cur.ty = rem / TW;
+    cur.tx = rem - cur.ty * TW;
+  }
+  const bool dy_wave = (wave & 2) != 0;  // waves 2, 3, 6, 7
+
+  if (wave < 2) {
+    // -- input patches: channel c0 + 16*wave + (lane & 15), tile (lane >> 4) of the step --
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                          static_cast<int>(x_bytes), 0x00020000);
+    const int ch = c0 + 16 * wave + (lane & 15);
+    float* vmine = lds + Cfg::kUImg + ((lane >> 4) * kT + 16 * wave + (lane & 15)) * kP;
+    F4Patch p;
+    f4_patch_offsets(p, cur, ch, N, C, H, W);
+    f4_load_patch<kVec>(p, xr, 0);
+    f4_transform_store(p, vmine);
+    __syncthreads();
+    f4_cursor_advance(cur, TH, TW);
+    f4_patch_offsets(p, cur, ch, N, C, H, W);
+    f4_load_patch<kVec>(p, xr, 0);
+    for (int s = s_begin; s < s_end; ++s) {
+      const int buf = (s - s_begin) & 1;
+      f4_transform_store(p, vmine + (buf ^ 1) * kBuf);
+      __builtin_amdgcn_sched_barrier(0);
+      // the step after next (past the split's end: staged, never read)
+      f4_cursor_advance(cur, TH, TW);
+      f4_patch_offsets(p, cur, ch, N, C, H, W);
+      f4_load_patch<kVec>(p, xr, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+      __syncthreads();
+    }
+  } else if (dy_wave) {
+    // -- gradient tiles: channel k0 + 16*d + (lane & 15), tile (lane >> 4) of the step --
+    const __amdgpu_buffer_rsrc_t dyr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), static_cast<short>(0),
+                                          static_cast<int>(dy_bytes), 0x00020000);
+    const int d = (wave & 1) | ((wave >> 2) << 1);
+    const int k = k0 + 16 * d + (lane & 15);
+    float* mmine = lds + ((d * kC + (lane >> 4)) * 16 + (lane & 15)) * kP;
+    float g[16];
+    f4_load_dy<kVec>(g, dyr, cur, k, N, K, H, W);
+    f4_dy_transform_store(g, mmine);
+    __syncthreads();
+    f4_cursor_advance(cur, TH, TW);
+    f4_load_dy<kVec>(g, dyr, cur, k, N, K, H, W);
+    for (int s = s_begin; s < s_end; ++s) {
+      const int buf = (s - s_begin) & 1;
+      f4_dy_transform_store(g, mmine + (buf ^ 1) * kBuf);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_cursor_advance(cur, TH, TW);
+      f4_load_dy<kVec>(g, dyr, cur, k, N, K, H, W);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+      __syncthreads();
+    }
+  } else {
+    __syncthreads();
+    for (int s = s_begin; s < s_end; ++s) {
+      const int buf = (s - s_begin) & 1;
+      f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+      __syncthreads();
+    }
+  }
+
+  // -- dW = G^T dU G; lane holds c = c0 + wt*16 + (lane & 15), k = k0 + wo*16 + 4(lane>>4) + r
+  const int c = c0 + wt * 16 + (lane & 15);
+  if (c >= C) return;
+  float* out = dw + static_cast<int64_t>(z) * K * C * 9;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = k0 + wo * 16 + 4 * (lane >> 4) + r;
+    if (k >= K) continue;
+    float t[3][6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float u[6], w3[3];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) u[i] = acc[i * 6 + j][r];
+      gt6(u, w3);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) t[a][j] = w3[a];
+    }
+    float* o = out + (static_cast<int64_t>(k) * C + c) * 9;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      float w3[3];
+      gt6(t[a], w3);
+      o[a * 3 + 0] = w3[0];
+      o[a * 3 + 1] = w3[1];
+      o[a * 3 + 2] = w3[2];
+    }
+  }
+}
+
 }  // namespace
 
 int64_t wino4_pad_reduction(int64_t r) { return (r + kC - 1) / kC * kC; }
@@ -445,7 +723,11 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
   const int oblocks = static_cast<int>((out_channels + 16 * og - 1) / (16 * og));
   const int splits = plan.splits;
   const int64_t nwg = static_cast<int64_t>(tblocks) * oblocks * splits;
-  auto kernel = og == 4 ? f4_conv_kernel<4> : f4_conv_kernel<2>;
+  // 16-byte centre loads (W % 4 == 0) pay off in the 4-wave variant only: the 8-wave one
+  // ran 4-16 % slower with them (benchmarks/wino_variants.py, profiles/wino_f4_variants.json)
+  const bool vec = og == 2 && (w & 3) == 0;
+  auto kernel = og == 4 ? f4_conv_kernel<4, false>
+                        : (vec ? f4_conv_kernel<2, true> : f4_conv_kernel<2, false>);
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(128 * og), 0, stream,
                      x, u, bias, splits > 1 ? ws : y, static_cast<int>(red_channels),
                      static_cast<int>(h), static_cast<int>(w), static_cast<int>(out_channels),
@@ -457,6 +739,47 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
     hipLaunchKernelGGL(f4_split_reduce_kernel, dim3(static_cast<unsigned>((numel + 255) / 256)),
                        dim3(256), 0, stream, ws, bias, y, numel, h * w,
                        static_cast<int>(out_channels), splits);
+  }
+}
+
+bool wino4_wgrad_supported(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
+  const int64_t lim = (int64_t{1} << 30) - 64;
+  const int64_t tiles = n * ((h + 3) / 4) * ((w + 3) / 4);
+  return n * c * h * w * 4 < lim && n * k * h * w * 4 < lim && n * c * h * w > 0 &&
+         n * k * h * w > 0 && tiles + 64 < (int64_t{1} << 30);
+}
+
+int wino4_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
+  // one 8-wave workgroup per CU: >= 2 rounds of 256, >= 32 steps of 4 tiles per split
+  const int64_t blocks = ((c + 31) / 32) * ((k + 63) / 64);
+  const int64_t steps = (n * ((h + 3) / 4) * ((w + 3) / 4) + 3) / 4;
+  int64_t s = (512 + blocks - 1) / blocks;
+  s = std::min<int64_t>(s, std::max<int64_t>(1, steps / 32));
+  s = std::min<int64_t>(s, 512);
+  return static_cast<int>(std::max<int64_t>(s, 1));
+}
+
+void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
+                        int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                        hipStream_t stream) {
+  const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
+  const int64_t P = n * th * tw;
+  const int cblocks = static_cast<int>((c + 31) / 32);
+  const int kblocks = static_cast<int>((k + 63) / 64);
+  const int64_t nwg = static_cast<int64_t>(cblocks) * kblocks * splits;
+  auto kernel = (w & 3) == 0 ? f4_wgrad_kernel<true> : f4_wgrad_kernel<false>;
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(kWgThreads), 0,
+                     stream, x, dy, splits > 1 ? ws : dw, static_cast<int>(n),
+                     static_cast<int>(c), static_cast<int>(k), static_cast<int>(h),
+                     static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw),
+                     static_cast<int>(P), cblocks, kblocks, splits,
+                     static_cast<uint32_t>(n * c * h * w * 4),
+                     static_cast<uint32_t>(n * k * h * w * 4));
+  if (splits > 1) {
+    const int64_t numel = k * c * 9;
+    hipLaunchKernelGGL(f4_split_reduce_kernel, dim3(static_cast<unsigned>((numel + 255) / 256)),
+                       dim3(256), 0, stream, ws, nullptr, dw, numel, int64_t{9},
+                       static_cast<int>(k), splits);
   }
 }
 

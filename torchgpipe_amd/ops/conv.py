@@ -4,8 +4,8 @@
 state-dict keys) whose 3×3 / stride 1 / pad 1 / fp32 GPU forward and
 backward-data run the fused HIP kernels of ``csrc/winograd_f4.hip`` (planes ≥ 8²)
 and ``csrc/winograd.hip`` (smaller planes); the weight
-gradient runs the Winograd wgrad kernels wherever they beat MIOpen's wrw (see
-``_wgrad_on_mfma``).
+gradient runs the F(4x4) / F(2x2) Winograd wgrad kernels wherever they beat MIOpen's
+wrw (see ``_wgrad_f4`` and ``_wgrad_on_mfma``).
 Other configurations, CPU tensors and non-fp32 dtypes use ``F.conv2d``.
 
 The Winograd-domain weights ``U = G g Gᵀ`` (and the rotated/transposed ``U'``
@@ -70,8 +70,14 @@ def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tens
     ops = _ext.require(x)
     out_channels = weight.shape[1] if flip else weight.shape[0]
     if _use_f4(x):
-        # 32-channel workgroups when a 64-channel one would idle half its waves
-        variant = 5 if out_channels <= 32 else 4
+        # 32-channel workgroups (variant 5) when a 64-channel one would idle half its
+        # waves, or when the 64-channel grid covers well under one workgroup per CU
+        # (before split-K): profiles/wino_f4_variants.json, 16 images at 12^2 / 24^2
+        # (80 / 144 blocks) 12 % / 10 % faster on variant 5; 40 images at 12^2 (192
+        # blocks) and every larger grid 3-14 % faster on variant 4.
+        tiles = x.shape[0] * ((x.shape[2] + 3) // 4) * ((x.shape[3] + 3) // 4)
+        blocks = -(-tiles // 32) * -(-out_channels // 64)
+        variant = 5 if out_channels <= 32 or blocks < 160 else 4
         return ops.wino4_conv(x, cache.get(weight, flip, True), bias, out_channels, variant)
     return ops.wino_conv(x, cache.get(weight, flip), bias, out_channels)
 
@@ -94,7 +100,9 @@ class _WinogradConv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _conv(dy, ctx.cache, weight, None, True)
         if ctx.needs_input_grad[1]:
-            if _wgrad_on_mfma(x, weight):
+            if _wgrad_f4(x, dy, weight):
+                dw = _ext.require(dy).wino4_wgrad(x, dy, 0)
+            elif _wgrad_on_mfma(x, weight):
                 dw = _ext.require(dy).wino_wgrad(x, dy, 0)
             else:
                 dw = torch.ops.aten.convolution_backward(
@@ -103,6 +111,20 @@ class _WinogradConv(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum((0, 2, 3))
         return dx, dw, db, None
+
+
+def _wgrad_f4(x: Tensor, dy: Tensor, weight: Tensor) -> bool:
+    """Weight gradient on the F(4x4,3x3) kernel (csrc/winograd_f4.hip).
+
+    benchmarks/wgrad_variants.py (profiles/wgrad_f4_variants.json): 1.25-1.6x faster than
+    the F(2x2) kernel and 1.6-2.4x faster than MIOpen's wrw on every U-Net shape from
+    12^2 up (74-251 TFLOP/s direct-equivalent), on 32-channel layers too.  Below 16
+    input channels the 32-wide channel block is mostly padding (the 3-channel input conv
+    stays on MIOpen); 32-bit buffer offsets need both operands below 1 GiB.
+    """
+    return (weight.shape[1] >= 16 and min(x.shape[2], x.shape[3]) >= F4_MIN_PLANE
+            and x.numel() * x.element_size() < F4_MAX_BYTES
+            and dy.numel() * dy.element_size() < F4_MAX_BYTES)
 
 
 def _wgrad_on_mfma(x: Tensor, weight: Tensor) -> bool:
