@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -388,17 +389,63 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
   }
 }
 
-// y[i] = sum_z ws[z][i] (+ bias[o]) over the split-K partial slabs.
-__global__ void f4_split_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ bias,
-                                       float* __restrict__ y, int64_t numel, int64_t hw, int O,
-                                       int splits) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= numel) return;
-  float v = bias ? bias[(i / hw) % O] : 0.f;
-  for (int z = 0; z < splits; ++z) v += ws[z * numel + i];
-  y[i] = v;
+// y[i] = sum_z ws[z][i] (+ bias[o]) over the split-K partial slabs.  A 256-thread block
+// owns 64 columns (float4 each with kVec) and sums the slabs in 4 interleaved z-lanes,
+// combined through LDS: the weight-gradient partials are short rows of up to 512 slabs,
+// which one thread per column walked serially (29 us per call in the p1 step).
+template <bool kVec>
+__global__ __launch_bounds__(256) void f4_split_reduce_kernel(
+    const float* __restrict__ ws, const float* __restrict__ bias, float* __restrict__ y,
+    int64_t numel, int64_t hw, int O, int splits) {
+  typedef std::conditional_t<kVec, floatx4, float> T;
+  constexpr int kW = kVec ? 4 : 1;
+  __shared__ T part[3][64];
+  const int col = threadIdx.x & 63;
+  const int zl = threadIdx.x >> 6;
+  const int64_t i = (static_cast<int64_t>(blockIdx.x) * 64 + col) * kW;  // first element
+  const bool ok = i < numel;
+  T v{};
+  if (ok) {
+    const T* src = reinterpret_cast<const T*>(ws + i);
+    const int64_t stride = numel / kW;
+    int z = zl;
+    for (; z + 4 < splits; z += 8) {
+      const T a = src[z * stride], b = src[(z + 4) * stride];
+      v += a;
+      v += b;
+    }
+    if (z < splits) v += src[z * stride];
+  }
+  if (zl > 0) part[zl - 1][col] = v;
+  __syncthreads();
+  if (zl > 0 || !ok) return;
+  v += part[0][col];
+  v += part[1][col];
+  v += part[2][col];
+  if constexpr (kVec) {
+    if (bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += bias[((i + e) / hw) % O];
+    }
+    *reinterpret_cast<floatx4*>(y + i) = v;
+  } else {
+    if (bias) v += bias[(i / hw) % O];
+    y[i] = v;
+  }
 }
 
+void launch_split_reduce(const float* ws, const float* bias, float* y, int64_t numel, int64_t hw,
+                         int O, int splits, hipStream_t stream) {
+  const bool vec = (numel & 3) == 0;
+  const int64_t cols = vec ? numel / 4 : numel;
+  const dim3 grid(static_cast<unsigned>((cols + 63) / 64));
+  if (vec)
+    hipLaunchKernelGGL(f4_split_reduce_kernel<true>, grid, dim3(256), 0, stream, ws, bias, y,
+                       numel, hw, O, splits);
+  else
+    hipLaunchKernelGGL(f4_split_reduce_kernel<false>, grid, dim3(256), 0, stream, ws, bias, y,
+                       numel, hw, O, splits);
+}
 
 // ---- weight gradient: dW = G^T [ sum_t (A dY_t A^T) (.) (B^T d_t B) ] G ------------------
 //
@@ -735,10 +782,8 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
                      static_cast<int>(tw), static_cast<int>(P), tblocks, oblocks, splits,
                      static_cast<uint32_t>(n * red_channels * h * w * 4));
   if (splits > 1) {
-    const int64_t numel = n * out_channels * h * w;
-    hipLaunchKernelGGL(f4_split_reduce_kernel, dim3(static_cast<unsigned>((numel + 255) / 256)),
-                       dim3(256), 0, stream, ws, bias, y, numel, h * w,
-                       static_cast<int>(out_channels), splits);
+    launch_split_reduce(ws, bias, y, n * out_channels * h * w, h * w,
+                        static_cast<int>(out_channels), splits, stream);
   }
 }
 
@@ -776,10 +821,7 @@ void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, i
                      static_cast<uint32_t>(n * c * h * w * 4),
                      static_cast<uint32_t>(n * k * h * w * 4));
   if (splits > 1) {
-    const int64_t numel = k * c * 9;
-    hipLaunchKernelGGL(f4_split_reduce_kernel, dim3(static_cast<unsigned>((numel + 255) / 256)),
-                       dim3(256), 0, stream, ws, nullptr, dw, numel, int64_t{9},
-                       static_cast<int>(k), splits);
+    launch_split_reduce(ws, nullptr, dw, k * c * 9, 9, static_cast<int>(k), splits, stream);
   }
 }
 
