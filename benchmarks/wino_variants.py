@@ -29,10 +29,12 @@ def main() -> None:
     p.add_argument('--variants', type=int, nargs='+', default=[0, 2])
     p.add_argument('--iters', type=int, default=20)
     p.add_argument('--out', default=None)
+    p.add_argument('--shape', type=int, nargs=4, action='append', default=None,
+                   help='N C K H (repeatable; default: the built-in table)')
     a = p.parse_args()
     ops = _ext.require()
     rows = []
-    for n, c, k, h in SHAPES:
+    for n, c, k, h in (a.shape or SHAPES):
         torch.manual_seed(0)
         x = torch.randn(n, c, h, h, device='cuda')
         w = torch.randn(k, c, 3, 3, device='cuda') / (3 * c ** 0.5)
@@ -41,7 +43,8 @@ def main() -> None:
         ref = F.conv2d(x.double(), w.double(), padding=1)
         row = {'shape': [n, c, k, h]}
         for v in a.variants:
-            # variants 4/5 = Winograd F(4x4,3x3) (winograd_f4.hip), the rest F(2x2,3x3)
+            # variants >= 4 = Winograd F(4x4,3x3) (winograd_f4.hip; 8-10 are timing
+            # ablations with wrong results), the rest F(2x2,3x3)
             def run():  # noqa: E306
                 if v >= 4:
                     return ops.wino4_conv(x, u4, None, k, v, 0)

@@ -236,7 +236,56 @@ __device__ __forceinline__ void f4_mfma(floatx4 (&acc)[kP], const float* buf, in
   }
 }
 
-template <int OG, bool kVec>
+// Tap offsets of the 6x6 input patch of output tile t, channel c of the first step.
+__device__ __forceinline__ void f4_fwd_offsets(F4Patch& p, int t, int c, int P, int tpi, int TW,
+                                               int R, int H, int W) {
+  const bool tv = t < P;
+  const int tt = tv ? t : 0;
+  const int n = tt / tpi;
+  const int rem = tt - n * tpi;
+  const int ty = rem / TW;
+  const int tx = rem - ty * TW;
+  const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
+  // element index of (row y0, column x0) of channel c; may be -1 (wraps)
+  const int64_t base = (static_cast<int64_t>(n) * R + c) * H * W +
+                       static_cast<int64_t>(y0) * W + x0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const bool ok = tv && y0 + i >= 0 && y0 + i < H;
+    p.row[i] = ok ? static_cast<uint32_t>((base + static_cast<int64_t>(i) * W) * 4) : kBadRow;
+  }
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const bool ok = x0 + j >= 0 && x0 + j < W;
+    p.col[j] = ok ? static_cast<uint32_t>(4 * j) : kBadCol;
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glob_void_t;
+
+// One step's weight slab straight into LDS (global_load_lds_dwordx4, no VGPR staging):
+// the slab U4[s][o0/16 .. +OG][4][16][36] is contiguous and so is its LDS image, in
+// 1 KiB pieces of one wave-instruction each, dealt round-robin over the slab waves.
+template <typename Cfg, int kWaves>
+__device__ __forceinline__ void f4_glds_slab(const float* __restrict__ src, float* dst, int sw,
+                                             int lane) {
+  constexpr int kPieces = Cfg::kUImg / 256;
+  static_assert(kPieces % kWaves == 0, "slab waves copy the slab evenly");
+#pragma unroll
+  for (int i = 0; i < kPieces / kWaves; ++i) {
+    const int piece = i * kWaves + sw;
+    __builtin_amdgcn_global_load_lds((glob_void_t*)(src + piece * 256 + lane * 4),
+                                     (lds_void_t*)(dst + piece * 256), 16, 0, 0);
+  }
+}
+
+// kAblate (timing ablations only, wrong results; variants 8-10): 1 = no in-loop patch
+// loads, 2 = no in-loop B^T d B (raw patch stored), 3 = neither.
+// kTouch (with kGlds, OG 4): slab waves 2-3 copy no slab but touch the input patches of
+// the step after next into L2 (one load at each end of every patch row), so the patch
+// waves' own loads of that step hit; waves 4-7 copy the slab.
+template <int OG, bool kVec, bool kGlds = false, int kAblate = 0, bool kTouch = false>
 __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
     const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ bias,
     float* __restrict__ y, int R, int H, int W, int O, int Rp, int Op, int TH, int TW, int P,
@@ -280,29 +329,7 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
                                           static_cast<int>(x_bytes), 0x00020000);
     F4Patch p;
-    {
-      const int t = t0 + wave * 16 + (lane & 15);
-      const bool tv = t < P;
-      const int tt = tv ? t : 0;
-      const int n = tt / tpi;
-      const int rem = tt - n * tpi;
-      const int ty = rem / TW;
-      const int tx = rem - ty * TW;
-      const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
-      // element index of (row y0, column x0) of channel (lane >> 4); may be -1 (wraps)
-      const int64_t base = (static_cast<int64_t>(n) * R + (lane >> 4)) * HW +
-                           static_cast<int64_t>(y0) * W + x0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const bool ok = tv && y0 + i >= 0 && y0 + i < H;
-        p.row[i] = ok ? static_cast<uint32_t>((base + static_cast<int64_t>(i) * W) * 4) : kBadRow;
-      }
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const bool ok = x0 + j >= 0 && x0 + j < W;
-        p.col[j] = ok ? static_cast<uint32_t>(4 * j) : kBadCol;
-      }
-    }
+    f4_fwd_offsets(p, t0 + wave * 16 + (lane & 15), lane >> 4, P, tpi, TW, R, H, W);
     float* vmine = lds + Cfg::kUImg + ((lane >> 4) * kT + wave * 16 + (lane & 15)) * kP;
     const uint32_t step_bytes = static_cast<uint32_t>(kC) * HW * 4;
     f4_load_patch<kVec>(p, xr, s_begin * step_bytes);
@@ -313,9 +340,17 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
     // loads of the step after next (a whole step of MFMAs hides them), then the MFMAs.
     for (int s = s_begin; s < s_end; ++s) {
       const int buf = (s - s_begin) & 1;
-      f4_transform_store(p, vmine + (buf ^ 1) * kBuf);
+      if constexpr ((kAblate & 2) == 0) {
+        f4_transform_store(p, vmine + (buf ^ 1) * kBuf);
+      } else {
+#pragma unroll
+        for (int q = 0; q < kP / 4; ++q)
+          reinterpret_cast<floatx4*>(vmine + (buf ^ 1) * kBuf)[q] =
+              floatx4{p.d[4 * q], p.d[4 * q + 1], p.d[4 * q + 2], p.d[4 * q + 3]};
+      }
       __builtin_amdgcn_sched_barrier(0);
-      f4_load_patch<kVec>(p, xr, min(s + 2, s_end - 1) * step_bytes);
+      if constexpr ((kAblate & 1) == 0)
+        f4_load_patch<kVec>(p, xr, min(s + 2, s_end - 1) * step_bytes);
       __builtin_amdgcn_sched_barrier(0);
       f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
       __syncthreads();
@@ -325,19 +360,67 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
     const int stid = tid - 128;
     const int64_t slab_stride = static_cast<int64_t>(Op / 16) * (kC * 16 * kP);
     const float* ubase = u + static_cast<int64_t>(o0 / 16) * (kC * 16 * kP);
-    floatx4 ur[Cfg::kUVec];
-    f4_load_slab<Cfg>(ur, ubase, s_begin * slab_stride, stid);
-    f4_store_slab<Cfg>(ur, lds, stid);
-    __syncthreads();
-    f4_load_slab<Cfg>(ur, ubase, min(s_begin + 1, s_end - 1) * slab_stride, stid);
-    for (int s = s_begin; s < s_end; ++s) {
-      const int buf = (s - s_begin) & 1;
-      f4_store_slab<Cfg>(ur, lds + (buf ^ 1) * kBuf, stid);
-      __builtin_amdgcn_sched_barrier(0);
-      f4_load_slab<Cfg>(ur, ubase, min(s + 2, s_end - 1) * slab_stride, stid);
-      __builtin_amdgcn_sched_barrier(0);
-      f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+    if constexpr (kGlds) {
+      constexpr int kGldsWaves = kTouch ? 4 : Cfg::kSlabThreads / 64;
+      const int sw = (stid >> 6) - (kTouch ? 2 : 0);
+      if (kTouch && sw < 0) {
+        // -- L2 touch waves: the patches wave (sw + 2) loads, two steps ahead of it --
+        const __amdgpu_buffer_rsrc_t xr =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                              static_cast<int>(x_bytes), 0x00020000);
+        F4Patch p;
+        f4_fwd_offsets(p, t0 + (sw + 2) * 16 + (lane & 15), lane >> 4, P, tpi, TW, R, H, W);
+        const uint32_t step_bytes = static_cast<uint32_t>(kC) * HW * 4;
+        float held[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) held[i] = 0.f;
+        __syncthreads();
+        for (int s = s_begin; s < s_end; ++s) {
+          const int buf = (s - s_begin) & 1;
+          // retire the previous step's touches (a step ago), then touch step s + 3
+#pragma unroll
+          for (int i = 0; i < 12; ++i) asm volatile("" ::"v"(held[i]));
+          if (s + 3 < s_end) {
+            const uint32_t cb = (s + 3) * step_bytes;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              held[2 * i] = __uint_as_float(
+                  __builtin_amdgcn_raw_buffer_load_b32(xr, p.row[i] + cb + p.col[0], 0, 0));
+              held[2 * i + 1] = __uint_as_float(
+                  __builtin_amdgcn_raw_buffer_load_b32(xr, p.row[i] + cb + p.col[5], 0, 0));
+            }
+          }
+          f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+          __syncthreads();
+        }
+      } else {
+        // LDS-DMA one step ahead; __syncthreads drains it (vmcnt(0)) before the buffer's use
+        f4_glds_slab<Cfg, kGldsWaves>(ubase + s_begin * slab_stride, lds, sw, lane);
+        __syncthreads();
+        for (int s = s_begin; s < s_end; ++s) {
+          const int buf = (s - s_begin) & 1;
+          if (s + 1 < s_end)
+            f4_glds_slab<Cfg, kGldsWaves>(ubase + (s + 1) * slab_stride, lds + (buf ^ 1) * kBuf,
+                                          sw, lane);
+          f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+          __syncthreads();
+        }
+      }
+    } else {
+      floatx4 ur[Cfg::kUVec];
+      f4_load_slab<Cfg>(ur, ubase, s_begin * slab_stride, stid);
+      f4_store_slab<Cfg>(ur, lds, stid);
       __syncthreads();
+      f4_load_slab<Cfg>(ur, ubase, min(s_begin + 1, s_end - 1) * slab_stride, stid);
+      for (int s = s_begin; s < s_end; ++s) {
+        const int buf = (s - s_begin) & 1;
+        f4_store_slab<Cfg>(ur, lds + (buf ^ 1) * kBuf, stid);
+        __builtin_amdgcn_sched_barrier(0);
+        f4_load_slab<Cfg>(ur, ubase, min(s + 2, s_end - 1) * slab_stride, stid);
+        __builtin_amdgcn_sched_barrier(0);
+        f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+        __syncthreads();
+      }
     }
   }
 
@@ -739,8 +822,8 @@ void launch_wino4_weight(const float* w, float* u, int64_t out_channels, int64_t
 WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                     int variant, int splits) {
   WinoPlan plan;
-  plan.variant = variant == 4 || variant == 5 ? variant : 5;
-  const int og = plan.variant == 4 ? 4 : 2;
+  plan.variant = variant >= 4 && variant <= 12 ? variant : 5;
+  const int og = plan.variant == 5 || plan.variant == 7 ? 2 : 4;
   const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
   const int64_t blocks = ((P + kT - 1) / kT) * ((out_channels + 16 * og - 1) / (16 * og));
   const int64_t steps = wino4_pad_reduction(red_channels) / kC;
@@ -765,16 +848,23 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
   const int64_t Op = wino4_pad_output(out_channels);
   const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
   const int64_t P = n * th * tw;
-  const int og = plan.variant == 4 ? 4 : 2;
+  const int og = plan.variant == 5 || plan.variant == 7 ? 2 : 4;
   const int tblocks = static_cast<int>((P + kT - 1) / kT);
   const int oblocks = static_cast<int>((out_channels + 16 * og - 1) / (16 * og));
   const int splits = plan.splits;
   const int64_t nwg = static_cast<int64_t>(tblocks) * oblocks * splits;
   // 16-byte centre loads (W % 4 == 0) pay off in the 4-wave variant only: the 8-wave one
   // ran 4-16 % slower with them (benchmarks/wino_variants.py, profiles/wino_f4_variants.json)
-  const bool vec = og == 2 && (w & 3) == 0;
+  const bool vec = (w & 3) == 0;
   auto kernel = og == 4 ? f4_conv_kernel<4, false>
                         : (vec ? f4_conv_kernel<2, true> : f4_conv_kernel<2, false>);
+  if (plan.variant == 6) kernel = f4_conv_kernel<4, false, true>;
+  if (plan.variant == 8) kernel = f4_conv_kernel<4, false, true, 1>;
+  if (plan.variant == 9) kernel = f4_conv_kernel<4, false, true, 2>;
+  if (plan.variant == 10) kernel = f4_conv_kernel<4, false, true, 3>;
+  if (plan.variant == 11) kernel = f4_conv_kernel<4, false, true, 0, true>;
+  if (plan.variant == 12) kernel = vec ? f4_conv_kernel<4, true, true> : f4_conv_kernel<4, false, true>;
+  if (plan.variant == 7) kernel = vec ? f4_conv_kernel<2, true, true> : f4_conv_kernel<2, false, true>;
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(128 * og), 0, stream,
                      x, u, bias, splits > 1 ? ws : y, static_cast<int>(red_channels),
                      static_cast<int>(h), static_cast<int>(w), static_cast<int>(out_channels),

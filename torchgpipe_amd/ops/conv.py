@@ -70,14 +70,15 @@ def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tens
     ops = _ext.require(x)
     out_channels = weight.shape[1] if flip else weight.shape[0]
     if _use_f4(x):
-        # 32-channel workgroups (variant 5) when a 64-channel one would idle half its
-        # waves, or when the 64-channel grid covers well under one workgroup per CU
-        # (before split-K): profiles/wino_f4_variants.json, 16 images at 12^2 / 24^2
-        # (80 / 144 blocks) 12 % / 10 % faster on variant 5; 40 images at 12^2 (192
-        # blocks) and every larger grid 3-14 % faster on variant 4.
+        # 32-channel workgroups (variant 7) when a 64-channel one (variant 6) would idle
+        # half its waves, or when the 64-channel grid covers well under one workgroup per
+        # CU (before split-K): profiles/wino_f4_variants.json, 16 images at 12^2 / 24^2
+        # (80 / 144 blocks) 12 % / 10 % faster on 32 channels; 40 images at 12^2 (192
+        # blocks) and every larger grid 3-14 % faster on 64.  Both copy the weight slab
+        # with LDS-DMA (variants 4 / 5 stage it through registers: 2-12 % slower).
         tiles = x.shape[0] * ((x.shape[2] + 3) // 4) * ((x.shape[3] + 3) // 4)
         blocks = -(-tiles // 32) * -(-out_channels // 64)
-        variant = 5 if out_channels <= 32 or blocks < 160 else 4
+        variant = 7 if out_channels <= 32 or blocks < 160 else 6
         return ops.wino4_conv(x, cache.get(weight, flip, True), bias, out_channels, variant)
     return ops.wino_conv(x, cache.get(weight, flip), bias, out_channels)
 
