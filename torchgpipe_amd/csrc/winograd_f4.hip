@@ -282,10 +282,7 @@ __device__ __forceinline__ void f4_glds_slab(const float* __restrict__ src, floa
 
 // kAblate (timing ablations only, wrong results; variants 8-10): 1 = no in-loop patch
 // loads, 2 = no in-loop B^T d B (raw patch stored), 3 = neither.
-// kTouch (with kGlds, OG 4): slab waves 2-3 copy no slab but touch the input patches of
-// the step after next into L2 (one load at each end of every patch row), so the patch
-// waves' own loads of that step hit; waves 4-7 copy the slab.
-template <int OG, bool kVec, bool kGlds = false, int kAblate = 0, bool kTouch = false>
+template <int OG, bool kVec, bool kGlds = false, int kAblate = 0>
 __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
     const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ bias,
     float* __restrict__ y, int R, int H, int W, int O, int Rp, int Op, int TH, int TW, int P,
@@ -361,39 +358,9 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
     const int64_t slab_stride = static_cast<int64_t>(Op / 16) * (kC * 16 * kP);
     const float* ubase = u + static_cast<int64_t>(o0 / 16) * (kC * 16 * kP);
     if constexpr (kGlds) {
-      constexpr int kGldsWaves = kTouch ? 4 : Cfg::kSlabThreads / 64;
-      const int sw = (stid >> 6) - (kTouch ? 2 : 0);
-      if (kTouch && sw < 0) {
-        // -- L2 touch waves: the patches wave (sw + 2) loads, two steps ahead of it --
-        const __amdgpu_buffer_rsrc_t xr =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
-                                              static_cast<int>(x_bytes), 0x00020000);
-        F4Patch p;
-        f4_fwd_offsets(p, t0 + (sw + 2) * 16 + (lane & 15), lane >> 4, P, tpi, TW, R, H, W);
-        const uint32_t step_bytes = static_cast<uint32_t>(kC) * HW * 4;
-        float held[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) held[i] = 0.f;
-        __syncthreads();
-        for (int s = s_begin; s < s_end; ++s) {
-          const int buf = (s - s_begin) & 1;
-          // retire the previous step's touches (a step ago), then touch step s + 3
-#pragma unroll
-          for (int i = 0; i < 12; ++i) asm volatile("" ::"v"(held[i]));
-          if (s + 3 < s_end) {
-            const uint32_t cb = (s + 3) * step_bytes;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-              held[2 * i] = __uint_as_float(
-                  __builtin_amdgcn_raw_buffer_load_b32(xr, p.row[i] + cb + p.col[0], 0, 0));
-              held[2 * i + 1] = __uint_as_float(
-                  __builtin_amdgcn_raw_buffer_load_b32(xr, p.row[i] + cb + p.col[5], 0, 0));
-            }
-          }
-          f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
-          __syncthreads();
-        }
-      } else {
+      constexpr int kGldsWaves = Cfg::kSlabThreads / 64;
+      const int sw = stid >> 6;
+      {
         // LDS-DMA one step ahead; __syncthreads drains it (vmcnt(0)) before the buffer's use
         f4_glds_slab<Cfg, kGldsWaves>(ubase + s_begin * slab_stride, lds, sw, lane);
         __syncthreads();
@@ -822,7 +789,7 @@ void launch_wino4_weight(const float* w, float* u, int64_t out_channels, int64_t
 WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                     int variant, int splits) {
   WinoPlan plan;
-  plan.variant = variant >= 4 && variant <= 12 ? variant : 5;
+  plan.variant = variant >= 4 && variant <= 12 && variant != 11 ? variant : 5;
   const int og = plan.variant == 5 || plan.variant == 7 ? 2 : 4;
   const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
   const int64_t blocks = ((P + kT - 1) / kT) * ((out_channels + 16 * og - 1) / (16 * og));
@@ -862,7 +829,6 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
   if (plan.variant == 8) kernel = f4_conv_kernel<4, false, true, 1>;
   if (plan.variant == 9) kernel = f4_conv_kernel<4, false, true, 2>;
   if (plan.variant == 10) kernel = f4_conv_kernel<4, false, true, 3>;
-  if (plan.variant == 11) kernel = f4_conv_kernel<4, false, true, 0, true>;
   if (plan.variant == 12) kernel = vec ? f4_conv_kernel<4, true, true> : f4_conv_kernel<4, false, true>;
   if (plan.variant == 7) kernel = vec ? f4_conv_kernel<2, true, true> : f4_conv_kernel<2, false, true>;
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(128 * og), 0, stream,
