@@ -14,7 +14,7 @@ import sqlite3
 
 GROUPS = [
     ('tgpipe Winograd F(4,3) conv fwd/bwd-data on MFMA (HIP)',
-     ('f4_conv_kernel', 'f4_split_reduce')),
+     ('f4_conv_kernel', 'f4_split_reduce', 'f4_gemm_kernel', 'f4_input_transform')),
     ('tgpipe Winograd weight transform (HIP)', ('wino_weight_kernel', 'f4_weight_kernel')),
     ('tgpipe Winograd F(2,3) conv fwd/bwd-data on MFMA (HIP)',
      ('wino_conv', 'wino_split_reduce')),

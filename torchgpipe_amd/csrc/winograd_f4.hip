@@ -261,6 +261,55 @@ __device__ __forceinline__ void f4_fwd_offsets(F4Patch& p, int t, int c, int P, 
   }
 }
 
+// Y = A^T M A of one lane's tile tp from its 36 accumulators; register r of each holds
+// output channel obase + r.  Writes the 4x4 output patch (+ bias), clipped at the edges.
+__device__ __forceinline__ void f4_output_transform(const floatx4 (&acc)[kP],
+                                                    float* __restrict__ ydst,
+                                                    const float* __restrict__ bias, int tp,
+                                                    int tpi, int TW, int H, int W, int O,
+                                                    int obase) {
+  const int HW = H * W;
+  const int pn = tp / tpi;
+  const int prem = tp - pn * tpi;
+  const int pty = prem / TW;
+  const int py = 4 * pty;
+  const int px = 4 * (prem - pty * TW);
+  const bool full = (W & 3) == 0 && py + 4 <= H;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = obase + r;
+    if (o >= O) continue;
+    // A^T along rows (i), for every column j
+    float s[4][6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const float m0 = acc[0 * 6 + j][r], m1 = acc[1 * 6 + j][r], m2 = acc[2 * 6 + j][r];
+      const float m3 = acc[3 * 6 + j][r], m4 = acc[4 * 6 + j][r], m5 = acc[5 * 6 + j][r];
+      const float a = m1 + m2, b = m1 - m2, c = m3 + m4, d = m3 - m4;
+      s[0][j] = m0 + a + c;
+      s[1][j] = b + 2.f * d;
+      s[2][j] = a + 4.f * c;
+      s[3][j] = b + 8.f * d + m5;
+    }
+    const float bv = bias ? bias[o] : 0.f;
+    float* yp = ydst + (static_cast<int64_t>(pn) * O + o) * HW + static_cast<int64_t>(py) * W + px;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a = s[k][1] + s[k][2], b = s[k][1] - s[k][2];
+      const float c = s[k][3] + s[k][4], d = s[k][3] - s[k][4];
+      const floatx4 out{s[k][0] + a + c + bv, b + 2.f * d + bv, a + 4.f * c + bv,
+                        b + 8.f * d + s[k][5] + bv};
+      if (full) {
+        *reinterpret_cast<floatx4*>(yp + k * W) = out;
+      } else if (py + k < H) {
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+          if (px + l < W) yp[k * W + l] = out[l];
+      }
+    }
+  }
+}
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glob_void_t;
 
@@ -397,46 +446,122 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
   const int tp = t0 + wt * 16 + (lane & 15);
   if (tp >= P) return;
   float* ydst = y + static_cast<int64_t>(z) * (P / tpi) * O * HW;
-  const bool add_bias = bias != nullptr && splits == 1;
-  const int pn = tp / tpi;
-  const int prem = tp - pn * tpi;
-  const int pty = prem / TW;
-  const int py = 4 * pty;
-  const int px = 4 * (prem - pty * TW);
-  const bool full = (W & 3) == 0 && py + 4 <= H;
+  f4_output_transform(acc, ydst, bias != nullptr && splits == 1 ? bias : nullptr, tp, tpi, TW,
+                      H, W, O, o0 + wo * 16 + 4 * (lane >> 4));
+}
+
+// ---- non-fused variant: input transform pass + two-operand LDS-DMA GEMM ----------------
+// Variants 14 / 15 take the input transform out of the GEMM kernel (cuDNN's
+// WINOGRAD_NONFUSED split): f4_input_transform_kernel writes V = B^T d B of every (tile,
+// channel) once, in the exact LDS image order of the GEMM -- V4[P/32][Rp/4][4 c][32 t][36]
+// -- so the GEMM kernel copies both operands per step by LDS-DMA and its eight waves only
+// multiply.  The ablation that drove it: without patch staging the fused kernel is 30-37 %
+// faster (profiles/wino_f4_glds_ablation.json); the pass costs 2.25x the input in writes.
+
+// One thread per (tile, channel) of the padded grid (tiles to a multiple of 32, channels
+// to a multiple of 4; the padding is written as zeros).
+__global__ __launch_bounds__(256) void f4_input_transform_kernel(
+    const float* __restrict__ x, float* __restrict__ v, int R, int H, int W, int TW, int tpi,
+    int P, int Rp, int64_t total, uint32_t x_bytes) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  // idx = ((tb * (Rp/4) + s) * 4 + c4) * 32 + tt  (consecutive threads: consecutive tiles)
+  const int tt = static_cast<int>(idx & 31);
+  const int64_t rest = idx >> 5;
+  const int c4 = static_cast<int>(rest & 3);
+  const int64_t sb = rest >> 2;  // tb * (Rp/4) + s
+  const int steps = Rp / kC;
+  const int s = static_cast<int>(sb % steps);
+  const int tb = static_cast<int>(sb / steps);
+  const int t = tb * kT + tt;
+  const int c = s * kC + c4;
+  float* dst = v + idx * kP;
+  F4Patch p;
+  if (t >= P || c >= R) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int o = o0 + wo * 16 + 4 * (lane >> 4) + r;
-    if (o >= O) continue;
-    // A^T along rows (i), for every column j
-    float s[4][6];
+    for (int q = 0; q < kP / 4; ++q) reinterpret_cast<floatx4*>(dst)[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                        static_cast<int>(x_bytes), 0x00020000);
+  // f4_fwd_offsets with image n's channel c (R channels per image)
+  f4_fwd_offsets(p, t, c, P, tpi, TW, R, H, W);
+  f4_load_patch<false>(p, xr, 0);
+  f4_transform_store(p, dst);
+}
+
+// GEMM on the transformed operands: per step both the weight slab and the V slab of the
+// tile block arrive by LDS-DMA (1 KiB pieces dealt round-robin over all waves).
+template <int OG>
+__global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_gemm_kernel(
+    const float* __restrict__ v, const float* __restrict__ u, const float* __restrict__ bias,
+    float* __restrict__ y, int H, int W, int O, int Rp, int Op, int TH, int TW, int P,
+    int tblocks, int oblocks, int splits) {
+  using Cfg = F4Cfg<OG>;
+  constexpr int kO = Cfg::kO;
+  constexpr int kBuf = Cfg::kBuf;
+  constexpr int kUPieces = Cfg::kUImg / 256;
+  constexpr int kPieces = kBuf / 256;
+  constexpr int kWaves = Cfg::kThreads / 64;
+  __shared__ float lds[2 * kBuf];
+
+  const int nwg = tblocks * oblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int ob = wgid % oblocks;
+  const int tb = (wgid / oblocks) % tblocks;
+  const int z = wgid / (oblocks * tblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wo = wave % OG;
+  const int wt = wave / OG;
+  const int t0 = tb * kT;
+  const int o0 = ob * kO;
+  const int HW = H * W;
+  const int tpi = TH * TW;
+
+  const int nsteps = Rp / kC;
+  const int s_begin = z * nsteps / splits;
+  const int s_end = (z + 1) * nsteps / splits;
+  floatx4 acc[kP];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const float m0 = acc[0 * 6 + j][r], m1 = acc[1 * 6 + j][r], m2 = acc[2 * 6 + j][r];
-      const float m3 = acc[3 * 6 + j][r], m4 = acc[4 * 6 + j][r], m5 = acc[5 * 6 + j][r];
-      const float a = m1 + m2, b = m1 - m2, c = m3 + m4, d = m3 - m4;
-      s[0][j] = m0 + a + c;
-      s[1][j] = b + 2.f * d;
-      s[2][j] = a + 4.f * c;
-      s[3][j] = b + 8.f * d + m5;
-    }
-    const float bv = add_bias ? bias[o] : 0.f;
-    float* yp = ydst + (static_cast<int64_t>(pn) * O + o) * HW + static_cast<int64_t>(py) * W + px;
+  for (int i = 0; i < kP; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t slab_stride = static_cast<int64_t>(Op / 16) * (kC * 16 * kP);
+  const float* ubase = u + static_cast<int64_t>(o0 / 16) * (kC * 16 * kP);
+  const float* vbase = v + static_cast<int64_t>(tb) * nsteps * kVImg;
+  auto issue = [&](int step, float* dst) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float a = s[k][1] + s[k][2], b = s[k][1] - s[k][2];
-      const float c = s[k][3] + s[k][4], d = s[k][3] - s[k][4];
-      const floatx4 out{s[k][0] + a + c + bv, b + 2.f * d + bv, a + 4.f * c + bv,
-                        b + 8.f * d + s[k][5] + bv};
-      if (full) {
-        *reinterpret_cast<floatx4*>(yp + k * W) = out;
-      } else if (py + k < H) {
-#pragma unroll
-        for (int l = 0; l < 4; ++l)
-          if (px + l < W) yp[k * W + l] = out[l];
+    for (int i = 0; i < (kPieces + kWaves - 1) / kWaves; ++i) {
+      const int piece = i * kWaves + wave;
+      if (piece < kPieces) {
+        const float* src = piece < kUPieces
+                               ? ubase + step * slab_stride + piece * 256
+                               : vbase + static_cast<int64_t>(step) * kVImg + (piece - kUPieces) * 256;
+        __builtin_amdgcn_global_load_lds((glob_void_t*)(src + lane * 4),
+                                         (lds_void_t*)(dst + piece * 256), 16, 0, 0);
       }
     }
+  };
+  issue(s_begin, lds);
+  __syncthreads();
+  for (int s = s_begin; s < s_end; ++s) {
+    const int buf = (s - s_begin) & 1;
+    if (s + 1 < s_end) issue(s + 1, lds + (buf ^ 1) * kBuf);
+    f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+    __syncthreads();
   }
+
+  const int tp = t0 + wt * 16 + (lane & 15);
+  if (tp >= P) return;
+  float* ydst = y + static_cast<int64_t>(z) * (P / tpi) * O * HW;
+  f4_output_transform(acc, ydst, bias != nullptr && splits == 1 ? bias : nullptr, tp, tpi,
+                          TW, H, W, O, o0 + wo * 16 + 4 * (lane >> 4));
 }
 
 // y[i] = sum_z ws[z][i] (+ bias[o]) over the split-K partial slabs.  A 256-thread block
@@ -789,8 +914,8 @@ void launch_wino4_weight(const float* w, float* u, int64_t out_channels, int64_t
 WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                     int variant, int splits) {
   WinoPlan plan;
-  plan.variant = variant >= 4 && variant <= 12 && variant != 11 ? variant : 5;
-  const int og = plan.variant == 5 || plan.variant == 7 ? 2 : 4;
+  plan.variant = (variant >= 4 && variant <= 12 && variant != 11) || variant == 14 || variant == 15 ? variant : 5;
+  const int og = plan.variant == 5 || plan.variant == 7 || plan.variant == 15 ? 2 : 4;
   const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
   const int64_t blocks = ((P + kT - 1) / kT) * ((out_channels + 16 * og - 1) / (16 * og));
   const int64_t steps = wino4_pad_reduction(red_channels) / kC;
@@ -805,6 +930,9 @@ WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64
     plan.splits = static_cast<int>(s);
   }
   plan.workspace = plan.splits > 1 ? plan.splits * n * out_channels * h * w : 0;
+  if (plan.variant >= 14) {  // + the transformed input V4[P/32][Rp/4][4][32][36], first
+    plan.workspace += ((P + kT - 1) / kT) * kT * wino4_pad_reduction(red_channels) * kP;
+  }
   return plan;
 }
 
@@ -815,11 +943,31 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
   const int64_t Op = wino4_pad_output(out_channels);
   const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
   const int64_t P = n * th * tw;
-  const int og = plan.variant == 5 || plan.variant == 7 ? 2 : 4;
+  const int og = plan.variant == 5 || plan.variant == 7 || plan.variant == 15 ? 2 : 4;
   const int tblocks = static_cast<int>((P + kT - 1) / kT);
   const int oblocks = static_cast<int>((out_channels + 16 * og - 1) / (16 * og));
   const int splits = plan.splits;
   const int64_t nwg = static_cast<int64_t>(tblocks) * oblocks * splits;
+  if (plan.variant >= 14) {
+    float* vbuf = ws;
+    const int64_t vtotal = static_cast<int64_t>(tblocks) * kT * Rp;  // threads
+    float* split_ws = ws + vtotal * kP;
+    hipLaunchKernelGGL(f4_input_transform_kernel, dim3(static_cast<unsigned>((vtotal + 255) / 256)),
+                       dim3(256), 0, stream, x, vbuf, static_cast<int>(red_channels),
+                       static_cast<int>(h), static_cast<int>(w), static_cast<int>(tw),
+                       static_cast<int>(th * tw), static_cast<int>(P), static_cast<int>(Rp),
+                       vtotal, static_cast<uint32_t>(n * red_channels * h * w * 4));
+    auto gemm = og == 4 ? f4_gemm_kernel<4> : f4_gemm_kernel<2>;
+    hipLaunchKernelGGL(gemm, dim3(static_cast<unsigned>(nwg)), dim3(128 * og), 0, stream, vbuf, u,
+                       bias, splits > 1 ? split_ws : y, static_cast<int>(h), static_cast<int>(w),
+                       static_cast<int>(out_channels), static_cast<int>(Rp), static_cast<int>(Op),
+                       static_cast<int>(th), static_cast<int>(tw), static_cast<int>(P), tblocks,
+                       oblocks, splits);
+    if (splits > 1)
+      launch_split_reduce(split_ws, bias, y, n * out_channels * h * w, h * w,
+                          static_cast<int>(out_channels), splits, stream);
+    return;
+  }
   // 16-byte centre loads (W % 4 == 0) pay off in the 4-wave variant only: the 8-wave one
   // ran 4-16 % slower with them (benchmarks/wino_variants.py, profiles/wino_f4_variants.json)
   const bool vec = (w & 3) == 0;

@@ -76,9 +76,17 @@ def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tens
         # (80 / 144 blocks) 12 % / 10 % faster on 32 channels; 40 images at 12^2 (192
         # blocks) and every larger grid 3-14 % faster on 64.  Both copy the weight slab
         # with LDS-DMA (variants 4 / 5 stage it through registers: 2-12 % slower).
+        # From 512 output channels the input transform runs as its own pass (variants 14 /
+        # 15: V written once, then a GEMM kernel with both operands by LDS-DMA): 20-28 %
+        # faster at 512-2048 channels, where V is re-read by >= 8 channel blocks; slower
+        # on the wide planes with few channels (64 @ 192^2: 0.75 vs 0.52 ms).
         tiles = x.shape[0] * ((x.shape[2] + 3) // 4) * ((x.shape[3] + 3) // 4)
         blocks = -(-tiles // 32) * -(-out_channels // 64)
-        variant = 7 if out_channels <= 32 or blocks < 160 else 6
+        small = out_channels <= 32 or blocks < 160
+        if out_channels >= 512:
+            variant = 15 if small else 14
+        else:
+            variant = 7 if small else 6
         return ops.wino4_conv(x, cache.get(weight, flip, True), bias, out_channels, variant)
     return ops.wino_conv(x, cache.get(weight, flip), bias, out_channels)
 
