@@ -16,6 +16,7 @@ SHAPES = [  # N, C, K, H
     (40, 64, 64, 192), (16, 64, 64, 192), (16, 128, 128, 96), (16, 256, 256, 48),
     (16, 512, 512, 24), (16, 1024, 1024, 12), (16, 2048, 2048, 6), (16, 2048, 1024, 6),
     (40, 128, 32, 192), (40, 32, 32, 192), (40, 256, 256, 48), (40, 1024, 1024, 12),
+    (40, 128, 128, 96), (40, 512, 512, 24),
     (3, 70, 130, 13),
 ]
 
@@ -61,11 +62,12 @@ def main() -> None:
             row[f'v{v}'] = {'ms': round(ms, 4), 'direct_tflops': round(flops / ms / 1e9, 1),
                             'rel_err': err}
         if min(h, h) >= 8:
-            got = ops.wino4_wgrad(x, dy, 0)
-            err = ((got.double() - ref).abs().max() / ref.abs().max()).item()
-            ms = timed(lambda: ops.wino4_wgrad(x, dy, 0), a.iters)
-            row['f4'] = {'ms': round(ms, 4), 'direct_tflops': round(flops / ms / 1e9, 1),
-                         'rel_err': err}
+            for name, var in (('f4', 0), ('f4nf', 1)):
+                got = ops.wino4_wgrad(x, dy, 0, var)
+                err = ((got.double() - ref).abs().max() / ref.abs().max()).item()
+                ms = timed(lambda: ops.wino4_wgrad(x, dy, 0, var), a.iters)
+                row[name] = {'ms': round(ms, 4), 'direct_tflops': round(flops / ms / 1e9, 1),
+                             'rel_err': err}
         rows.append(row)
         print(json.dumps(row), flush=True)
     if a.out:

@@ -18,7 +18,7 @@ GROUPS = [
     ('tgpipe Winograd weight transform (HIP)', ('wino_weight_kernel', 'f4_weight_kernel')),
     ('tgpipe Winograd F(2,3) conv fwd/bwd-data on MFMA (HIP)',
      ('wino_conv', 'wino_split_reduce')),
-    ('tgpipe Winograd weight gradient on MFMA (HIP)', ('wino_wgrad', 'f4_wgrad')),
+    ('tgpipe Winograd weight gradient on MFMA (HIP)', ('wino_wgrad', 'f4_wgrad', 'f4_wg_')),
     ('tgpipe Winograd weight transform (HIP)', ('wino_weight_kernel',)),
     ('tgpipe fused Dropout2d+InstanceNorm+LeakyReLU (HIP)', ('dna_forward', 'dna_backward')),
     ('tgpipe other (HIP)', ('tgpipe::',)),

@@ -144,14 +144,15 @@ def test_f4_forward_and_flip(shape, splits, variant):
                                    (1, 16, 8, 1, 1), (4, 32, 32, 33, 2), (2, 256, 128, 12, 12),
                                    (5, 64, 33, 20, 36)])
 @pytest.mark.parametrize('splits', [0, 1, 3, 1000])
-def test_f4_wgrad(shape, splits):
+@pytest.mark.parametrize('variant', [0, 1])
+def test_f4_wgrad(shape, splits, variant):
     # F(4x4,3x3) weight gradient: edge tiles, channel blocks past C / K, split tiles
     # (1000 is capped at the step count)
     n, c, k, h, w = shape
     torch.manual_seed(5)
     x = torch.randn(n, c, h, w, device=cuda)
     dy = torch.randn(n, k, h, w, device=cuda)
-    got = _ext.require(x).wino4_wgrad(x, dy, splits)
+    got = _ext.require(x).wino4_wgrad(x, dy, splits, variant)
     want = torch.ops.aten.convolution_backward(
         dy.double(), x.double(), torch.zeros(k, c, 3, 3, device=cuda, dtype=torch.double), None,
         [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]

@@ -270,7 +270,8 @@ at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t s
   return dw;
 }
 
-at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits) {
+at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits,
+                       int64_t variant) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   check_f32_gpu(x, "x");
@@ -291,10 +292,13 @@ at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t 
   const int64_t steps = (n * ((h + 3) / 4) * ((w + 3) / 4) + 3) / 4;
   const int s = static_cast<int>(std::min<int64_t>(
       splits > 0 ? splits : wino4_wgrad_splits(n, c, k, h, w), steps));
+  TORCH_CHECK(variant == 0 || variant == 1, "variant must be 0 (fused) or 1 (non-fused)");
+  const int64_t wsize = wino4_wgrad_workspace(n, c, k, h, w, s, static_cast<int>(variant));
   at::Tensor ws;
-  if (s > 1) ws = at::empty({s * k * c * 9}, x.options());
+  if (wsize > 0) ws = at::empty({wsize}, x.options());
   launch_wino4_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), dw.data_ptr<float>(),
-                     s > 1 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s, stream_of(x));
+                     wsize > 0 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s,
+                     static_cast<int>(variant), stream_of(x));
   return dw;
 }
 
@@ -318,7 +322,7 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("wino_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
   m.def("wino4_weight(Tensor w, bool flip) -> Tensor");
-  m.def("wino4_wgrad(Tensor x, Tensor dy, int splits=0) -> Tensor");
+  m.def("wino4_wgrad(Tensor x, Tensor dy, int splits=0, int variant=0) -> Tensor");
   m.def("wino4_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
 }

@@ -92,8 +92,13 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
 // over `splits` workgroups (> 1 needs a workspace of splits*K*C*9 floats).
 bool wino4_wgrad_supported(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
 int wino4_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
+// variant 0: fused (patch / gradient-tile staging inside the GEMM kernel); 1: non-fused
+// (transform passes into the GEMM's LDS image order, then an LDS-DMA GEMM).  The workspace
+// holds the split-K partials (splits > 1) and, for variant 1, the transformed operands.
+int64_t wino4_wgrad_workspace(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                              int variant);
 void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
-                        int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                        int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
                         hipStream_t stream);
 
 // Weight gradient of the same convolution: dw[K][C][3][3] from x[N][C][H][W] and

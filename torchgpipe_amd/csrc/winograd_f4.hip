@@ -751,6 +751,152 @@ __device__ __forceinline__ void gt6(const float (&u)[6], float (&w)[3]) {
 
 constexpr int kWgThreads = 512;
 
+// dW[k][c] = G^T dU G for the lane's column c and rows kbase + r of its 36 accumulators.
+__device__ __forceinline__ void f4_wgrad_epilogue(const floatx4 (&acc)[kP], float* __restrict__ out,
+                                                  int c, int kbase, int C, int K) {
+  if (c >= C) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = kbase + r;
+    if (k >= K) continue;
+    float t[3][6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      float u[6], w3[3];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) u[i] = acc[i * 6 + j][r];
+      gt6(u, w3);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) t[a][j] = w3[a];
+    }
+    float* o = out + (static_cast<int64_t>(k) * C + c) * 9;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      float w3[3];
+      gt6(t[a], w3);
+      o[a * 3 + 0] = w3[0];
+      o[a * 3 + 1] = w3[1];
+      o[a * 3 + 2] = w3[2];
+    }
+  }
+}
+
+// ---- non-fused weight gradient (variant 1) ----------------------------------------------
+// Both operands transformed by their own passes into the GEMM's per-step LDS images:
+//   Vx[P/4][C/32][4 t][32 c][36] = B^T d B     M[P/4][K/64][4 og][4 t][16 k][36] = A dY A^T
+// then a GEMM whose eight waves copy 54 KiB per step by LDS-DMA and only multiply.
+
+// One thread per (channel, tile) of the padded grid; consecutive threads: consecutive tiles.
+__global__ __launch_bounds__(256) void f4_wg_vx_kernel(const float* __restrict__ x,
+                                                      float* __restrict__ vx, int N, int C,
+                                                      int H, int W, int TH, int TW, int Ppad,
+                                                      int cblocks, int64_t total,
+                                                      uint32_t x_bytes) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int t = static_cast<int>(idx % Ppad);
+  const int ch = static_cast<int>(idx / Ppad);
+  float* dst = vx + ((((static_cast<int64_t>(t >> 2) * cblocks + (ch >> 5)) * 4 + (t & 3)) * 32) +
+                     (ch & 31)) * kP;
+  F4TileCursor cur;
+  const int tpi = TH * TW;
+  cur.n = t / tpi;
+  const int rem = t - cur.n * tpi;
+  cur.ty = rem / TW;
+  cur.tx = rem - cur.ty * TW;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                        static_cast<int>(x_bytes), 0x00020000);
+  F4Patch p;
+  f4_patch_offsets(p, cur, ch, N, C, H, W);  // zeros past N or C
+  f4_load_patch<false>(p, xr, 0);
+  f4_transform_store(p, dst);
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(256) void f4_wg_mdy_kernel(const float* __restrict__ dy,
+                                                       float* __restrict__ m, int N, int K,
+                                                       int H, int W, int TH, int TW, int Ppad,
+                                                       int kblocks, int64_t total,
+                                                       uint32_t dy_bytes) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int t = static_cast<int>(idx % Ppad);
+  const int k = static_cast<int>(idx / Ppad);
+  // [s][kb][og][t4][k16][36]
+  float* dst = m + ((((static_cast<int64_t>(t >> 2) * kblocks + (k >> 6)) * 4 + ((k >> 4) & 3)) * 4 +
+                     (t & 3)) * 16 + (k & 15)) * kP;
+  F4TileCursor cur;
+  const int tpi = TH * TW;
+  cur.n = t / tpi;
+  const int rem = t - cur.n * tpi;
+  cur.ty = rem / TW;
+  cur.tx = rem - cur.ty * TW;
+  const __amdgpu_buffer_rsrc_t dyr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), static_cast<short>(0),
+                                        static_cast<int>(dy_bytes), 0x00020000);
+  float g[16];
+  f4_load_dy<kVec>(g, dyr, cur, k, N, K, H, W);
+  f4_dy_transform_store(g, dst);
+}
+
+__global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_gemm_kernel(
+    const float* __restrict__ vx, const float* __restrict__ m, float* __restrict__ dw, int C,
+    int K, int nsteps, int cblocks, int kblocks, int splits) {
+  using Cfg = F4Cfg<4>;
+  constexpr int kBuf = Cfg::kBuf;
+  constexpr int kMPieces = Cfg::kUImg / 256;  // 36
+  constexpr int kPieces = kBuf / 256;          // 54
+  constexpr int kWaves = kWgThreads / 64;
+  __shared__ float lds[2 * kBuf];
+
+  const int nwg = cblocks * kblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int cb = wgid % cblocks;
+  const int kb = (wgid / cblocks) % kblocks;
+  const int z = wgid / (cblocks * kblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wo = wave & 3;
+  const int wt = wave >> 2;
+  const int s_begin = static_cast<int>(static_cast<int64_t>(z) * nsteps / splits);
+  const int s_end = static_cast<int>(static_cast<int64_t>(z + 1) * nsteps / splits);
+  floatx4 acc[kP];
+#pragma unroll
+  for (int i = 0; i < kP; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int step, float* dst) {
+    const float* msrc = m + (static_cast<int64_t>(step) * kblocks + kb) * Cfg::kUImg;
+    const float* vsrc = vx + (static_cast<int64_t>(step) * cblocks + cb) * kVImg;
+#pragma unroll
+    for (int i = 0; i < (kPieces + kWaves - 1) / kWaves; ++i) {
+      const int piece = i * kWaves + wave;
+      if (piece < kPieces) {
+        const float* src = piece < kMPieces ? msrc + piece * 256 : vsrc + (piece - kMPieces) * 256;
+        __builtin_amdgcn_global_load_lds((glob_void_t*)(src + lane * 4),
+                                         (lds_void_t*)(dst + piece * 256), 16, 0, 0);
+      }
+    }
+  };
+  issue(s_begin, lds);
+  __syncthreads();
+  for (int s = s_begin; s < s_end; ++s) {
+    const int buf = (s - s_begin) & 1;
+    if (s + 1 < s_end) issue(s + 1, lds + (buf ^ 1) * kBuf);
+    f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+    __syncthreads();
+  }
+  f4_wgrad_epilogue(acc, dw + static_cast<int64_t>(z) * K * C * 9, cb * 32 + wt * 16 + (lane & 15),
+                    kb * 64 + wo * 16 + 4 * (lane >> 4), C, K);
+}
+
+
+
 template <bool kVec>
 __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dw, int N,
@@ -857,33 +1003,8 @@ __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_kernel(
   }
 
   // -- dW = G^T dU G; lane holds c = c0 + wt*16 + (lane & 15), k = k0 + wo*16 + 4(lane>>4) + r
-  const int c = c0 + wt * 16 + (lane & 15);
-  if (c >= C) return;
-  float* out = dw + static_cast<int64_t>(z) * K * C * 9;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k = k0 + wo * 16 + 4 * (lane >> 4) + r;
-    if (k >= K) continue;
-    float t[3][6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      float u[6], w3[3];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) u[i] = acc[i * 6 + j][r];
-      gt6(u, w3);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) t[a][j] = w3[a];
-    }
-    float* o = out + (static_cast<int64_t>(k) * C + c) * 9;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      float w3[3];
-      gt6(t[a], w3);
-      o[a * 3 + 0] = w3[0];
-      o[a * 3 + 1] = w3[1];
-      o[a * 3 + 2] = w3[2];
-    }
-  }
+  f4_wgrad_epilogue(acc, dw + static_cast<int64_t>(z) * K * C * 9, c0 + wt * 16 + (lane & 15),
+                    k0 + wo * 16 + 4 * (lane >> 4), C, K);
 }
 
 }  // namespace
@@ -1008,24 +1129,56 @@ int wino4_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
   return static_cast<int>(std::max<int64_t>(s, 1));
 }
 
+int64_t wino4_wgrad_workspace(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                              int variant) {
+  int64_t total = splits > 1 ? splits * k * c * 9 : 0;
+  if (variant == 1) {
+    const int64_t ppad = ((n * ((h + 3) / 4) * ((w + 3) / 4) + 3) / 4) * 4;
+    total += ppad * (((c + 31) / 32) * 32 + ((k + 63) / 64) * 64) * kP;
+  }
+  return total;
+}
+
 void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
-                        int64_t c, int64_t k, int64_t h, int64_t w, int splits,
+                        int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
                         hipStream_t stream) {
   const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
   const int64_t P = n * th * tw;
   const int cblocks = static_cast<int>((c + 31) / 32);
   const int kblocks = static_cast<int>((k + 63) / 64);
   const int64_t nwg = static_cast<int64_t>(cblocks) * kblocks * splits;
-  auto kernel = (w & 3) == 0 ? f4_wgrad_kernel<true> : f4_wgrad_kernel<false>;
-  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(kWgThreads), 0,
-                     stream, x, dy, splits > 1 ? ws : dw, static_cast<int>(n),
-                     static_cast<int>(c), static_cast<int>(k), static_cast<int>(h),
-                     static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw),
-                     static_cast<int>(P), cblocks, kblocks, splits,
-                     static_cast<uint32_t>(n * c * h * w * 4),
-                     static_cast<uint32_t>(n * k * h * w * 4));
+  const uint32_t x_bytes = static_cast<uint32_t>(n * c * h * w * 4);
+  const uint32_t dy_bytes = static_cast<uint32_t>(n * k * h * w * 4);
+  float* partial = ws;
+  if (variant == 1) {
+    const int64_t nsteps = (P + 3) / 4;
+    const int64_t ppad = nsteps * 4;
+    float* vx = ws;
+    float* m = vx + ppad * cblocks * 32 * kP;
+    partial = m + ppad * kblocks * 64 * kP;
+    const int64_t vt = ppad * cblocks * 32, mt = ppad * kblocks * 64;
+    hipLaunchKernelGGL(f4_wg_vx_kernel, dim3(static_cast<unsigned>((vt + 255) / 256)), dim3(256), 0,
+                       stream, x, vx, static_cast<int>(n), static_cast<int>(c), static_cast<int>(h),
+                       static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw),
+                       static_cast<int>(ppad), cblocks, vt, x_bytes);
+    auto mk = (w & 3) == 0 ? f4_wg_mdy_kernel<true> : f4_wg_mdy_kernel<false>;
+    hipLaunchKernelGGL(mk, dim3(static_cast<unsigned>((mt + 255) / 256)), dim3(256), 0, stream, dy,
+                       m, static_cast<int>(n), static_cast<int>(k), static_cast<int>(h),
+                       static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw),
+                       static_cast<int>(ppad), kblocks, mt, dy_bytes);
+    hipLaunchKernelGGL(f4_wgrad_gemm_kernel, dim3(static_cast<unsigned>(nwg)), dim3(kWgThreads), 0,
+                       stream, vx, m, splits > 1 ? partial : dw, static_cast<int>(c),
+                       static_cast<int>(k), static_cast<int>(nsteps), cblocks, kblocks, splits);
+  } else {
+    auto kernel = (w & 3) == 0 ? f4_wgrad_kernel<true> : f4_wgrad_kernel<false>;
+    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(kWgThreads), 0,
+                       stream, x, dy, splits > 1 ? partial : dw, static_cast<int>(n),
+                       static_cast<int>(c), static_cast<int>(k), static_cast<int>(h),
+                       static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw),
+                       static_cast<int>(P), cblocks, kblocks, splits, x_bytes, dy_bytes);
+  }
   if (splits > 1) {
-    launch_split_reduce(ws, nullptr, dw, k * c * 9, 9, static_cast<int>(k), splits, stream);
+    launch_split_reduce(partial, nullptr, dw, k * c * 9, 9, static_cast<int>(k), splits, stream);
   }
 }
 

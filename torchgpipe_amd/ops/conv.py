@@ -110,7 +110,11 @@ class _WinogradConv(torch.autograd.Function):
             dx = _conv(dy, ctx.cache, weight, None, True)
         if ctx.needs_input_grad[1]:
             if _wgrad_f4(x, dy, weight):
-                dw = _ext.require(dy).wino4_wgrad(x, dy, 0)
+                # non-fused (transform passes + LDS-DMA GEMM) from 512 channels on both
+                # sides: 11-23 % faster there, 1.2-3.6x slower on the wide shallow planes
+                # (profiles/wgrad_f4_variants.json)
+                nonfused = min(weight.shape[0], weight.shape[1]) >= 512
+                dw = _ext.require(dy).wino4_wgrad(x, dy, 0, 1 if nonfused else 0)
             elif _wgrad_on_mfma(x, weight):
                 dw = _ext.require(dy).wino_wgrad(x, dy, 0)
             else:
