@@ -37,10 +37,13 @@ def main() -> None:
     p = argparse.ArgumentParser()
     p.add_argument('--iters', type=int, default=10)
     p.add_argument('--out', default=None)
+    p.add_argument('--shape', type=int, nargs=4, action='append', default=None,
+                   help='N C K H (repeatable; default: the built-in table)')
+    p.add_argument('--all-f4', action='store_true', help='time F(4x4) below 8x8 planes too')
     a = p.parse_args()
     ops = _ext.require()
     rows = []
-    for n, c, k, h in SHAPES:
+    for n, c, k, h in (a.shape or SHAPES):
         torch.manual_seed(0)
         x = torch.randn(n, c, h, h, device='cuda')
         dy = torch.randn(n, k, h, h, device='cuda')
@@ -61,7 +64,7 @@ def main() -> None:
             ms = timed(lambda: ops.wino_wgrad(x, dy, 0, v), a.iters)
             row[f'v{v}'] = {'ms': round(ms, 4), 'direct_tflops': round(flops / ms / 1e9, 1),
                             'rel_err': err}
-        if min(h, h) >= 8:
+        if h >= 8 or a.all_f4:
             for name, var in (('f4', 0), ('f4nf', 1)):
                 got = ops.wino4_wgrad(x, dy, 0, var)
                 err = ((got.double() - ref).abs().max() / ref.abs().max()).item()

@@ -59,9 +59,19 @@ F4_MIN_PLANE = 8
 F4_MAX_BYTES = (1 << 30) - 64
 
 
-def _use_f4(x: Tensor) -> bool:
-    return (min(x.shape[2], x.shape[3]) >= F4_MIN_PLANE
-            and x.numel() * x.element_size() < F4_MAX_BYTES)
+# 6x6 planes (U-Net's bottom level) waste 5/9 of a 4x4-tile grid, so F(4x4) spends as
+# many multiplies there as F(2x2); with >= 512 channels its non-fused GEMM still wins
+# (profiles/wino_f4_6x6.json: forward 0-15 %, weight gradient 10-17 %).
+F4_MIN_PLANE_WIDE = 6
+F4_WIDE_CHANNELS = 512
+
+
+def _use_f4(x: Tensor, out_channels: int = 0) -> bool:
+    plane = min(x.shape[2], x.shape[3])
+    # forward at 6x6: ahead at 16 images (0.30 vs 0.36 ms), even at 40 (0.67 vs 0.66)
+    wide = (plane >= F4_MIN_PLANE_WIDE and out_channels >= F4_WIDE_CHANNELS
+            and x.shape[1] >= F4_WIDE_CHANNELS and x.shape[0] <= 24)
+    return (plane >= F4_MIN_PLANE or wide) and x.numel() * x.element_size() < F4_MAX_BYTES
 
 
 def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tensor],
@@ -69,7 +79,7 @@ def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tens
     """One Winograd convolution launch: forward (flip=False) or backward-data (flip=True)."""
     ops = _ext.require(x)
     out_channels = weight.shape[1] if flip else weight.shape[0]
-    if _use_f4(x):
+    if _use_f4(x, out_channels):
         # 32-channel workgroups (variant 7) when a 64-channel one (variant 6) would idle
         # half its waves, or when the 64-channel grid covers well under one workgroup per
         # CU (before split-K): profiles/wino_f4_variants.json, 16 images at 12^2 / 24^2
@@ -82,11 +92,12 @@ def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tens
         # on the wide planes with few channels (64 @ 192^2: 0.75 vs 0.52 ms).
         tiles = x.shape[0] * ((x.shape[2] + 3) // 4) * ((x.shape[3] + 3) // 4)
         blocks = -(-tiles // 32) * -(-out_channels // 64)
-        small = out_channels <= 32 or blocks < 160
         if out_channels >= 512:
+            # 6x6 planes: the 32-channel GEMM (0.67 vs 0.73 ms at 40 images)
+            small = blocks < 160 or min(x.shape[2], x.shape[3]) < F4_MIN_PLANE
             variant = 15 if small else 14
         else:
-            variant = 7 if small else 6
+            variant = 7 if out_channels <= 32 or blocks < 160 else 6
         return ops.wino4_conv(x, cache.get(weight, flip, True), bias, out_channels, variant)
     return ops.wino_conv(x, cache.get(weight, flip), bias, out_channels)
 
@@ -105,25 +116,34 @@ class _WinogradConv(torch.autograd.Function):
     def backward(ctx, dy: Tensor):  # type: ignore[override]
         x, weight = ctx.saved_tensors
         dy = dy.contiguous()
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = _conv(dy, ctx.cache, weight, None, True)
-        if ctx.needs_input_grad[1]:
-            if _wgrad_f4(x, dy, weight):
-                # non-fused (transform passes + LDS-DMA GEMM) from 512 channels on both
-                # sides: 11-23 % faster there, 1.2-3.6x slower on the wide shallow planes
-                # (profiles/wgrad_f4_variants.json)
-                nonfused = min(weight.shape[0], weight.shape[1]) >= 512
-                dw = _ext.require(dy).wino4_wgrad(x, dy, 0, 1 if nonfused else 0)
-            elif _wgrad_on_mfma(x, weight):
-                dw = _ext.require(dy).wino_wgrad(x, dy, 0)
-            else:
-                dw = torch.ops.aten.convolution_backward(
-                    dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                    [False, True, False])[1]
+        dx, dw = _conv_grads(x, weight, dy, ctx.cache, ctx.needs_input_grad[0],
+                             ctx.needs_input_grad[1])
+        db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum((0, 2, 3))
         return dx, dw, db, None
+
+
+def _conv_grads(x: Tensor, weight: Tensor, dy: Tensor, cache: _TransformCache, need_x: bool,
+                need_w: bool) -> Tuple[Optional[Tensor], Optional[Tensor]]:
+    """Backward-data and weight gradient of the 3x3 / stride 1 / pad 1 convolution."""
+    dx = dw = None
+    if need_x:
+        dx = _conv(dy, cache, weight, None, True)
+    if need_w:
+        if _wgrad_f4(x, dy, weight):
+            # non-fused (transform passes + LDS-DMA GEMM) from 512 channels on both
+            # sides: 11-23 % faster there, 1.2-3.6x slower on the wide shallow planes
+            # (profiles/wgrad_f4_variants.json)
+            nonfused = min(weight.shape[0], weight.shape[1]) >= 512
+            dw = _ext.require(dy).wino4_wgrad(x, dy, 0, 1 if nonfused else 0)
+        elif _wgrad_on_mfma(x, weight):
+            dw = _ext.require(dy).wino_wgrad(x, dy, 0)
+        else:
+            dw = torch.ops.aten.convolution_backward(
+                dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                [False, True, False])[1]
+    return dx, dw
 
 
 def _wgrad_f4(x: Tensor, dy: Tensor, weight: Tensor) -> bool:
@@ -135,7 +155,10 @@ def _wgrad_f4(x: Tensor, dy: Tensor, weight: Tensor) -> bool:
     input channels the 32-wide channel block is mostly padding (the 3-channel input conv
     stays on MIOpen); 32-bit buffer offsets need both operands below 1 GiB.
     """
-    return (weight.shape[1] >= 16 and min(x.shape[2], x.shape[3]) >= F4_MIN_PLANE
+    plane = min(x.shape[2], x.shape[3])
+    wide = min(weight.shape[0], weight.shape[1]) >= F4_WIDE_CHANNELS
+    return (weight.shape[1] >= 16
+            and (plane >= F4_MIN_PLANE or (plane >= F4_MIN_PLANE_WIDE and wide))
             and x.numel() * x.element_size() < F4_MAX_BYTES
             and dy.numel() * dy.element_size() < F4_MAX_BYTES)
 
