@@ -13,6 +13,7 @@ of backward-data) are cached per parameter version: a pipeline step runs the
 same weights over every micro-batch (forward, recompute, backward), so the
 transform runs once per optimizer step instead of once per call.
 """
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -66,7 +67,19 @@ F4_MIN_PLANE_WIDE = 6
 F4_WIDE_CHANNELS = 512
 
 
+# The F(4x4) weight cache holds 36 floats per (in, out) channel pair and direction (8x
+# the weight, vs 3.6x for F(2x2)): layers whose cache would pass this stay on F(2x2), so
+# memory-bound giant models (benchmarks/memory.py: U-Net(48,576)'s 18432-channel
+# bottleneck, 49 GB per direction in F(4x4)) keep their measured footprint.
+F4_MAX_CACHE_BYTES = 2 << 30
+# TGPIPE_WINOGRAD_F4=0 keeps every layer on F(2x2) (the memory benchmarks of
+# profiles/MEMORY.md were measured that way).
+F4_ENABLED = os.environ.get('TGPIPE_WINOGRAD_F4', '1') != '0'
+
+
 def _use_f4(x: Tensor, out_channels: int = 0) -> bool:
+    if not F4_ENABLED or x.shape[1] * out_channels * 36 * 4 > F4_MAX_CACHE_BYTES:
+        return False
     plane = min(x.shape[2], x.shape[3])
     # forward at 6x6: ahead at 16 images (0.30 vs 0.36 ms), even at 40 (0.67 vs 0.66)
     wide = (plane >= F4_MIN_PLANE_WIDE and out_channels >= F4_WIDE_CHANNELS
@@ -157,7 +170,7 @@ def _wgrad_f4(x: Tensor, dy: Tensor, weight: Tensor) -> bool:
     """
     plane = min(x.shape[2], x.shape[3])
     wide = min(weight.shape[0], weight.shape[1]) >= F4_WIDE_CHANNELS
-    return (weight.shape[1] >= 16
+    return (F4_ENABLED and weight.shape[1] >= 16
             and (plane >= F4_MIN_PLANE or (plane >= F4_MIN_PLANE_WIDE and wide))
             and x.numel() * x.element_size() < F4_MAX_BYTES
             and dy.numel() * dy.element_size() < F4_MAX_BYTES)
