@@ -72,8 +72,7 @@ F4_WIDE_CHANNELS = 512
 # memory-bound giant models (benchmarks/memory.py: U-Net(48,576)'s 18432-channel
 # bottleneck, 49 GB per direction in F(4x4)) keep their measured footprint.
 F4_MAX_CACHE_BYTES = 2 << 30
-# TGPIPE_WINOGRAD_F4=0 keeps every layer on F(2x2) (the memory benchmarks of
-# profiles/MEMORY.md were measured that way).
+# TGPIPE_WINOGRAD_F4=0 keeps every layer on F(2x2).
 F4_ENABLED = os.environ.get('TGPIPE_WINOGRAD_F4', '1') != '0'
 
 
@@ -196,10 +195,14 @@ def _wgrad_on_mfma(x: Tensor, weight: Tensor) -> bool:
 MIN_CHANNELS = 8
 
 
+# TGPIPE_WINOGRAD=0: every convolution on MIOpen (F.conv2d), no weight-transform caches.
+WINOGRAD_ENABLED = os.environ.get('TGPIPE_WINOGRAD', '1') != '0'
+
+
 def wino_eligible(x: Tensor, weight: Tensor, stride=(1, 1), padding=(1, 1), dilation=(1, 1),
                   groups: int = 1) -> bool:
     """Whether the HIP Winograd kernel computes this convolution."""
-    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
+    return (WINOGRAD_ENABLED and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
             and weight.shape[1] >= MIN_CHANNELS
             and weight.dtype == torch.float32 and tuple(weight.shape[2:]) == (3, 3)
             and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
