@@ -34,10 +34,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # Batch / chunks / reference balance are the reference's experiment tables.
 # ``tuned`` balances were re-derived for MI355X with the Winograd F(4x4) MFMA kernels
 # (fused and non-fused): candidates from the per-layer device times
-# (profiles/unet_layer_profile_nf.json, benchmarks/layer_profile.py), then rounds of
+# (profiles/unet_layer_profile_m1.json, benchmarks/layer_profile.py), then rounds of
 # benchmarks/stage_harness.py measurements fed back through
 # scripts/balance_from_harness.py (profiles/stage_harness_nf_p{2,4,8}.json): measured max
-# stage p8 210 ms, p4 283 ms, p2 641 ms (the reference's P40 balances measured a 613 ms
+# stage p8 206 ms, p4 283 ms, p2 643 ms (the reference's P40 balances measured a 613 ms
 # max stage at p8 with the earlier kernels).
 UNET_EXPERIMENTS = {
     1: dict(name='pipeline-1', batch=80, chunks=2, balance=[241], tuned=[241], ref=24.456),
@@ -46,7 +46,7 @@ UNET_EXPERIMENTS = {
     4: dict(name='pipeline-4', batch=512, chunks=16, balance=[30, 66, 84, 61],
             tuned=[45, 55, 59, 82], ref=67.042),
     8: dict(name='pipeline-8', batch=640, chunks=40, balance=[16, 27, 31, 44, 22, 57, 27, 17],
-            tuned=[22, 23, 25, 30, 22, 36, 44, 39], ref=88.497),
+            tuned=[22, 23, 26, 30, 22, 37, 43, 38], ref=88.497),
 }
 # AmoebaNet tuned balances: profiles/amoebanet_layer_profile.json (micro-batch 40) through
 # the same simulator (n2 535 vs 492, n4 851 vs 814, n8 1539 vs 1503 simulated samples/s).
