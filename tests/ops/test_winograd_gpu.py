@@ -1,4 +1,4 @@
-"""Winograd F(2x2,3x3) MFMA convolution vs the plain PyTorch fp32 convolution (GPU only)."""
+"""Winograd F(4x4,3x3) / F(2x2,3x3) MFMA convolutions vs an fp64 PyTorch convolution (GPU only)."""
 import copy
 
 import pytest
@@ -27,6 +27,9 @@ SHAPES = [  # (N, C, K, H, W)
     (2, 256, 128, 12, 12),
     (1, 16, 8, 1, 1),
     (4, 32, 32, 33, 2),
+    (2, 64, 96, 40, 40),    # fused F(4x4) forward / weight gradient
+    (2, 512, 640, 12, 12),  # non-fused F(4x4) forward, backward-data and weight gradient
+    (2, 512, 512, 6, 6),    # 6x6 with >= 512 channels: F(4x4) non-fused at <= 24 images
 ]
 
 
