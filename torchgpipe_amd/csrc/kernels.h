@@ -74,7 +74,10 @@ void launch_wino_conv(const float* x, const float* u, const float* bias, float* 
 // Winograd F(4x4,3x3) (winograd_f4.hip): same convolution, 36 MFMA multiplies per 16
 // output pixels.  Transformed weights U4[Rp4/4][Op4/16][4][16][36] (Rp4 = multiple of 4,
 // Op4 = multiple of 64).  Variant 4: 64 output channels x 32 tiles per 8-wave workgroup
-// (one per CU); variant 5: 32 x 32 per 4-wave workgroup (two per CU); -1: auto.
+// (one per CU); variant 5: 32 x 32 per 4-wave workgroup (two per CU); 6 / 7: the same with
+// the weight slab by LDS-DMA; 14 / 15: non-fused (input-transform pass, then a GEMM with
+// both operands by LDS-DMA; the plan's workspace then includes V); 8-10: timing
+// ablations; 12: 6 with 16-byte patch rows; -1: auto (5).
 // wino4_supported(): input < 1 GiB etc.
 int64_t wino4_pad_reduction(int64_t r);
 int64_t wino4_pad_output(int64_t o);

@@ -22,6 +22,15 @@
 // order puts one patch wave and one slab wave on two of the four SIMDs and slab waves
 // on the other two, so no SIMD carries two transform streams.
 //
+// Forward / backward-data variants (host `variant`, ops/conv.py picks):
+//    4 / 5   fused, weight slab staged through registers (64 / 32 output channels)
+//    6 / 7   fused, weight slab by LDS-DMA (global_load_lds_dwordx4)      <- < 512 channels
+//   14 / 15  non-fused: f4_input_transform_kernel writes V in the GEMM's LDS-image order,
+//            f4_gemm_kernel copies both operands by LDS-DMA               <- >= 512 channels
+//    8-10    timing ablations of the fused patch staging (wrong results)
+//   12       6 with 16-byte patch-row loads
+// Weight gradient: f4_wgrad_kernel (fused) and f4_wg_vx/_mdy + f4_wgrad_gemm (non-fused).
+//
 // Padding taps (image borders, tiles past the end) are raw buffer loads with an
 // out-of-range offset: the hardware returns 0, so no select sits between a load and
 // the transform, and no address ever leaves the tensor.
