@@ -245,6 +245,41 @@ __device__ __forceinline__ void f4_mfma(floatx4 (&acc)[kP], const float* buf, in
   }
 }
 
+// f4_mfma with the LDS operand quads read kAhead quads before their MFMAs (kAhead = 1 is
+// f4_mfma); for the GEMM kernels, whose waves hold no staging registers.  kAhead = 2 ran
+// the non-fused GEMMs 1-10 % faster than 1 (3: no further gain; wino_f4_glds_ablation.json).
+template <typename Cfg, int kAhead>
+__device__ __forceinline__ void f4_mfma_ahead(floatx4 (&acc)[kP], const float* buf, int lane,
+                                              int wo, int wt) {
+  constexpr int kQ = kP / 4;
+  const floatx4* ua =
+      reinterpret_cast<const floatx4*>(buf + ((wo * kC + (lane >> 4)) * 16 + (lane & 15)) * kP);
+  const floatx4* vb = reinterpret_cast<const floatx4*>(
+      buf + Cfg::kUImg + ((lane >> 4) * kT + wt * 16 + (lane & 15)) * kP);
+  floatx4 a[kQ], b[kQ];
+#pragma unroll
+  for (int q = 0; q < kAhead; ++q) {
+    a[q] = ua[q];
+    b[q] = vb[q];
+  }
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    if (q + kAhead < kQ) {
+      a[q + kAhead] = ua[q + kAhead];
+      b[q + kAhead] = vb[q + kAhead];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      acc[4 * q + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][e], b[q][e], acc[4 * q + e], 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * kAhead, 0);
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    if (q + kAhead < kQ) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+  }
+}
+
 // Tap offsets of the 6x6 input patch of output tile t, channel c of the first step.
 __device__ __forceinline__ void f4_fwd_offsets(F4Patch& p, int t, int c, int P, int tpi, int TW,
                                                int R, int H, int W) {
@@ -502,7 +537,7 @@ __global__ __launch_bounds__(256) void f4_input_transform_kernel(
 
 // GEMM on the transformed operands: per step both the weight slab and the V slab of the
 // tile block arrive by LDS-DMA (1 KiB pieces dealt round-robin over all waves).
-template <int OG>
+template <int OG, int kAhead = 2>
 __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_gemm_kernel(
     const float* __restrict__ v, const float* __restrict__ u, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int O, int Rp, int Op, int TH, int TW, int P,
@@ -562,7 +597,7 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_gemm_kernel(
   for (int s = s_begin; s < s_end; ++s) {
     const int buf = (s - s_begin) & 1;
     if (s + 1 < s_end) issue(s + 1, lds + (buf ^ 1) * kBuf);
-    f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+    f4_mfma_ahead<Cfg, kAhead>(acc, lds + buf * kBuf, lane, wo, wt);
     __syncthreads();
   }
 
@@ -849,6 +884,7 @@ __global__ __launch_bounds__(256) void f4_wg_mdy_kernel(const float* __restrict_
   f4_dy_transform_store(g, dst);
 }
 
+template <int kAhead = 2>
 __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_gemm_kernel(
     const float* __restrict__ vx, const float* __restrict__ m, float* __restrict__ dw, int C,
     int K, int nsteps, int cblocks, int kblocks, int splits) {
@@ -897,7 +933,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_gemm_kernel(
   for (int s = s_begin; s < s_end; ++s) {
     const int buf = (s - s_begin) & 1;
     if (s + 1 < s_end) issue(s + 1, lds + (buf ^ 1) * kBuf);
-    f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
+    f4_mfma_ahead<Cfg, kAhead>(acc, lds + buf * kBuf, lane, wo, wt);
     __syncthreads();
   }
   f4_wgrad_epilogue(acc, dw + static_cast<int64_t>(z) * K * C * 9, cb * 32 + wt * 16 + (lane & 15),
@@ -1175,7 +1211,7 @@ void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, i
                        m, static_cast<int>(n), static_cast<int>(k), static_cast<int>(h),
                        static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw),
                        static_cast<int>(ppad), kblocks, mt, dy_bytes);
-    hipLaunchKernelGGL(f4_wgrad_gemm_kernel, dim3(static_cast<unsigned>(nwg)), dim3(kWgThreads), 0,
+    hipLaunchKernelGGL(f4_wgrad_gemm_kernel<>, dim3(static_cast<unsigned>(nwg)), dim3(kWgThreads), 0,
                        stream, vx, m, splits > 1 ? partial : dw, static_cast<int>(c),
                        static_cast<int>(k), static_cast<int>(nsteps), cblocks, kblocks, splits);
   } else {
