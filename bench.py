@@ -19,10 +19,19 @@ stages; fp32 like the reference.  Rank 0 prints one JSON line.
         bench.py --gpus 8
 """
 import argparse
+import datetime
 import json
 import os
 import sys
 import time
+
+if int(os.environ.get('WORLD_SIZE', '1')) > 1:
+    # One HIP hardware queue per stream: a rank runs its compute stream plus one RCCL
+    # stream per pipeline link (up to 6 on U-Net p8 with long skips).  With HIP's
+    # default of 4 queues, streams beyond that share a queue and their kernels
+    # serialise, so a spinning RCCL receive could hold up unrelated work.  Set before
+    # the HIP runtime initialises (first CUDA call).
+    os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
 
 import torch
 import torch.distributed as dist
@@ -71,9 +80,15 @@ def parse() -> argparse.Namespace:
     p.add_argument('--batch', type=int, default=None, help='override the global batch')
     p.add_argument('--chunks', type=int, default=None, help='override the micro-batch count')
     p.add_argument('--unfused', action='store_true', help='use the unfused PyTorch U-Net cells')
-    p.add_argument('--balance', default='tuned',
-                   help="'tuned' (MI355X-measured, default), 'ref' (reference table) or a "
-                        "comma-separated list")
+    p.add_argument('--balance', default='ref',
+                   help="'ref' (the reference's experiment table, default), 'tuned' "
+                        "(MI355X-measured) or a comma-separated list")
+    p.add_argument('--also-tuned', choices=['auto', 'yes', 'no'], default='auto',
+                   help="after the headline timing, time the MI355X-tuned balance too and "
+                        "report it as the 'tuned' field (auto: when N > 1 and it differs)")
+    p.add_argument('--timeout', type=float, default=300.0,
+                   help='seconds any pipeline wait may take before the run fails (RCCL '
+                        'watchdog and gloo waits): a dead or stuck rank ends the job')
     p.add_argument('--cudnn-benchmark', action='store_true',
                    help='MIOpen exhaustive find (slow first step, cached afterwards)')
     p.add_argument('--backend', choices=['auto', 'gloo'], default='auto',
@@ -122,73 +137,56 @@ def main() -> None:
         # Lazy RCCL init: each pipeline link (peer pair) then gets its own
         # communicator and stream on first use.
         backend = 'nccl' if gpu and not rehearsal else 'gloo'
-        dist.init_process_group(backend, rank=rank, world_size=world)
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=args.timeout))
 
     from torchgpipe_amd.models import amoebanetd, unet
     from torchgpipe_amd.parallel import PipelineStage
 
     table = UNET_EXPERIMENTS if args.model == 'unet' else AMOEBA_EXPERIMENTS
+
+    def build_model() -> torch.nn.Sequential:
+        # Built on the meta device: each rank materialises (random-initialises) only
+        # its own partition inside PipelineStage.
+        with torch.device('meta'):
+            if args.model == 'unet':
+                if args.tiny:
+                    return unet(depth=2, num_convs=1, base_channels=4, input_channels=3,
+                                output_channels=1, fused=not args.unfused)
+                return unet(depth=5, num_convs=5, base_channels=64, input_channels=3,
+                            output_channels=1, fused=not args.unfused)
+            if args.tiny:
+                return amoebanetd(num_classes=10, num_layers=3, num_filters=8)
+            return amoebanetd(num_classes=1000, num_layers=18, num_filters=256)
+
+    n_layers = len(build_model())
     if args.model == 'unet':
         exp = dict(table.get(world) or dict(name=f'pipeline-{world}', batch=80 * world,
-                                            chunks=4 * world, balance=even_balance(241, world),
-                                            ref=None))
-        if args.tiny:
-            model = unet(depth=2, num_convs=1, base_channels=4, input_channels=3,
-                         output_channels=1, fused=not args.unfused)
-            exp['balance'] = exp['tuned'] = even_balance(len(model), world)
-        else:
-            model = unet(depth=5, num_convs=5, base_channels=64, input_channels=3,
-                         output_channels=1, fused=not args.unfused)
+                                            chunks=4 * world,
+                                            balance=even_balance(n_layers, world), ref=None))
         in_shape = (3, 192, 192)
         checkpoint = 'except_last'
         model_name = 'U-Net(5,64)'
     else:
         exp = dict(table.get(world) or dict(name=f'n{world}m32', batch=160 * world, chunks=32,
-                                            balance=even_balance(24, world), ref=None))
-        if args.tiny:
-            model = amoebanetd(num_classes=10, num_layers=3, num_filters=8)
-            exp['balance'] = exp['tuned'] = even_balance(len(model), world)
-        else:
-            model = amoebanetd(num_classes=1000, num_layers=18, num_filters=256)
+                                            balance=even_balance(n_layers, world), ref=None))
         in_shape = (3, 224, 224)
         checkpoint = 'except_last' if exp['chunks'] > 1 else 'always'
         model_name = 'AmoebaNet-D(18,256)'
+    if args.tiny:
+        exp['balance'] = exp['tuned'] = even_balance(n_layers, world)
     if args.checkpoint:
         checkpoint = args.checkpoint
     if args.batch:
         exp['batch'] = args.batch
     if args.chunks:
         exp['chunks'] = args.chunks
+    tuned_balance = list(exp.get('tuned', exp['balance']))
     if args.balance == 'tuned':
-        exp['balance'] = exp.get('tuned', exp['balance'])
+        exp['balance'] = tuned_balance
     elif args.balance != 'ref':
         exp['balance'] = [int(v) for v in args.balance.split(',')]
-    batch, chunks, balance = exp['batch'], exp['chunks'], exp['balance']
-
-    stage = PipelineStage(model, balance, device=device, chunks=chunks, checkpoint=checkpoint)
-    del model
-    if args.channels_last:
-        stage.partition.to(memory_format=torch.channels_last)
-    optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
-
-    gen = torch.Generator(device=device).manual_seed(0)
-    x = torch.rand(batch, *in_shape, device=device, generator=gen) if stage.is_first else None
-    if x is not None and args.channels_last:
-        x = x.contiguous(memory_format=torch.channels_last)
-    if args.model == 'unet':
-        target = torch.ones(batch, 1, 192, 192, device=device) if stage.is_last else None
-        loss_fn = F.binary_cross_entropy_with_logits
-    else:
-        target = (torch.randint(10 if args.tiny else 1000, (batch,), device=device, generator=gen)
-                  if stage.is_last else None)
-        loss_fn = F.cross_entropy
-    from torchgpipe_amd.parallel.stage import signature_of
-    signature = signature_of(torch.empty(batch, *in_shape, device='meta'))
-
-    def step() -> None:
-        stage.train_step(x, target, loss_fn, signature=signature)
-        optimizer.step()
-        optimizer.zero_grad(set_to_none=True)
+    batch, chunks, balance = exp['batch'], exp['chunks'], list(exp['balance'])
 
     def sync() -> None:
         if world > 1:
@@ -196,43 +194,92 @@ def main() -> None:
         if gpu:
             torch.cuda.synchronize(device)
 
-    t0 = time.time()
-    for k in range(args.warmup):
-        step()
-        sync()
-        if rank == 0:
-            print(f'[bench] warmup step {k + 1}/{args.warmup} done at {time.time() - t0:.1f}s',
-                  file=sys.stderr, flush=True)
-    warm_s = time.time() - t0
+    def measure(balance: list, tag: str) -> dict:
+        """Build the stage for ``balance``, warm up, time ``--steps`` full SGD steps."""
+        stage = PipelineStage(build_model(), balance, device=device, chunks=chunks,
+                              checkpoint=checkpoint, timeout=args.timeout)
+        if args.channels_last:
+            stage.partition.to(memory_format=torch.channels_last)
+        optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
 
-    sync()
-    start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    elapsed = time.perf_counter() - start
+        gen = torch.Generator(device=device).manual_seed(0)
+        x = torch.rand(batch, *in_shape, device=device, generator=gen) if stage.is_first else None
+        if x is not None and args.channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
+        if args.model == 'unet':
+            target = torch.ones(batch, 1, 192, 192, device=device) if stage.is_last else None
+            loss_fn = F.binary_cross_entropy_with_logits
+        else:
+            target = (torch.randint(10 if args.tiny else 1000, (batch,), device=device,
+                                    generator=gen) if stage.is_last else None)
+            loss_fn = F.cross_entropy
+        from torchgpipe_amd.parallel.stage import signature_of
+        signature = signature_of(torch.empty(batch, *in_shape, device='meta'))
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        def step() -> None:
+            stage.train_step(x, target, loss_fn, signature=signature)
+            optimizer.step()
+            optimizer.zero_grad(set_to_none=True)
 
-    if args.profile_steps and rank == 0:
-        from torch.profiler import ProfilerActivity, profile
-        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if gpu else [])
-        with profile(activities=acts) as prof:
-            for _ in range(args.profile_steps):
-                step()
+        if gpu:
+            torch.cuda.reset_peak_memory_stats(device)
+        t0 = time.time()
+        first_s = 0.0
+        for k in range(args.warmup):
+            step()
             sync()
-        print(prof.key_averages().table(sort_by='cuda_time_total' if gpu else 'cpu_time_total',
-                                        row_limit=30), file=sys.stderr)
+            if k == 0:
+                first_s = time.time() - t0
+            if rank == 0:
+                print(f'[bench] {tag} warmup step {k + 1}/{args.warmup} done at '
+                      f'{time.time() - t0:.1f}s', file=sys.stderr, flush=True)
+        warm_s = time.time() - t0
+
+        sync()
+        start = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync()
+        elapsed = time.perf_counter() - start
+
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+
+        if args.profile_steps and rank == 0 and tag == 'headline':
+            from torch.profiler import ProfilerActivity, profile
+            acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if gpu else [])
+            with profile(activities=acts) as prof:
+                for _ in range(args.profile_steps):
+                    step()
+                sync()
+            print(prof.key_averages().table(
+                sort_by='cuda_time_total' if gpu else 'cpu_time_total', row_limit=30),
+                file=sys.stderr)
+        mem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if gpu else 0.0
+        del stage, optimizer, x, target
+        if gpu:
+            torch.cuda.empty_cache()
+        return {'elapsed': elapsed, 'warm_s': warm_s, 'first_step_s': first_s, 'mem': mem}
+
+    main_run = measure(balance, 'headline')
+    elapsed, warm_s = main_run['elapsed'], main_run['warm_s']
+    tuned = None
+    also = args.also_tuned == 'yes' or (args.also_tuned == 'auto' and world > 1
+                                         and args.balance == 'ref' and tuned_balance != balance)
+    if also:
+        t = measure(tuned_balance, 'tuned')
+        tuned = {'balance': tuned_balance,
+                 'value': round(batch * args.steps / t['elapsed'], 3),
+                 'ms_per_step': round(1000 * t['elapsed'] / args.steps, 3)}
 
     samples_per_s = batch * args.steps / elapsed
     if rank == 0:
         ref = None if args.tiny else exp.get('ref')
         if args.tiny:
             model_name += ' TINY smoke-test variant (not a measurement)'
-        mem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if gpu else 0.0
+        mem = main_run['mem']
         print(json.dumps({
             'metric': f'{model_name} GPipe training throughput (samples/sec)',
             'value': round(samples_per_s, 3),
@@ -263,7 +310,10 @@ def main() -> None:
                 'baseline_samples_per_sec_p40': ref,
                 'rank0_peak_mem_gib': round(mem, 2),
                 'warmup_s': round(warm_s, 1),
+                'first_step_s': round(main_run['first_step_s'], 2),
+                'timeout_s': args.timeout,
             },
+            'tuned': tuned,
         }), file=result_out, flush=True)
     if world > 1:
         dist.barrier()

@@ -1,0 +1,109 @@
+"""Gradient-parity harness of the multi-process pipeline against one process.
+
+The same worker runs on gloo CPU ranks (every CPU test run) and on RCCL with one
+GPU per rank (``tests/distributed/test_rccl_multigpu.py``).  The oracle is the
+unpartitioned model run in one process on one device with the *same
+micro-batching*: the per-micro-batch losses, weighted by micro-batch size, are
+back-propagated one by one.  That is exactly GPipe's semantics (BatchNorm sees
+micro-batch statistics), so every parameter gradient of every rank and the
+loss must match the oracle.  Models run with dropout disabled (``p = 0``) so no
+RNG stream has to line up across processes.
+"""
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+MODELS = ('unet', 'amoebanet')
+
+
+def build(kind: str) -> nn.Sequential:
+    torch.manual_seed(7)
+    if kind == 'unet':
+        from torchgpipe_amd.models import unet
+        model = unet(depth=3, num_convs=1, base_channels=8, input_channels=3, output_channels=1)
+    elif kind == 'amoebanet':
+        from torchgpipe_amd.models import amoebanetd
+        model = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
+    else:
+        raise ValueError(kind)
+    for m in model.modules():
+        if isinstance(getattr(m, 'p', None), float):
+            m.p = 0.0
+    return model
+
+
+def data(kind: str, device: torch.device):
+    gen = torch.Generator().manual_seed(11)
+    if kind == 'unet':
+        x = torch.rand(6, 3, 16, 16, generator=gen)
+        t = torch.rand(6, 1, 16, 16, generator=gen)
+    else:
+        x = torch.rand(6, 3, 224, 224, generator=gen)
+        t = torch.randint(10, (6,), generator=gen)
+    return x.to(device), t.to(device)
+
+
+def loss_fn(kind: str):
+    return F.binary_cross_entropy_with_logits if kind == 'unet' else F.cross_entropy
+
+
+def balance(kind: str, world: int) -> list:
+    """Splits that put skips and tuple boundaries across ranks."""
+    n = len(build(kind))
+    table = {
+        ('unet', 2): [11, n - 11],          # skips of the two top levels cross ranks
+        ('unet', 4): [8, 10, 6, n - 24],     # rank 0 stashes for two different ranks
+        ('amoebanet', 2): [3, n - 3],        # (x, skip) tuple boundary
+        ('amoebanet', 4): [2, 2, 2, n - 6],
+    }
+    return table[(kind, world)]
+
+
+def reference(kind: str, device: torch.device, chunks: int):
+    """Gradients and loss of the whole model on one device, same micro-batching."""
+    model = build(kind).to(device)
+    x, t = data(kind, device)
+    fn = loss_fn(kind)
+    total = float(x.size(0))
+    loss_sum = 0.0
+    pairs = list(zip(x.chunk(chunks), t.chunk(chunks)))
+    outputs = [model(xc) for xc, _ in pairs]
+    for out, (_, tc) in reversed(list(zip(outputs, pairs))):
+        loss = fn(out, tc) * (tc.size(0) / total)
+        loss.backward()
+        loss_sum += loss.item()
+    return [p.grad.detach().cpu().clone() for p in model.parameters()], loss_sum
+
+
+def stage_worker(rank: int, world: int, kind: str, chunks: int, checkpoint: str,
+                 device_type: str):
+    """One rank: two training steps (the second on cached message metadata)."""
+    from torchgpipe_amd.parallel import PipelineStage
+    device = torch.device('cuda', rank) if device_type == 'cuda' else torch.device('cpu')
+    stage = PipelineStage(build(kind), balance(kind, world), device=device, chunks=chunks,
+                          checkpoint=checkpoint, timeout=60)
+    x, t = data(kind, device)
+    loss = None
+    for _ in range(2):
+        for p in stage.parameters():
+            p.grad = None
+        loss = stage.train_step(x if stage.is_first else None, t if stage.is_last else None,
+                                loss_fn(kind))
+    if device.type == 'cuda':
+        torch.cuda.synchronize(device)
+    return {'grads': [p.grad.detach().cpu().clone() for p in stage.parameters()],
+            'loss': None if loss is None else loss.item(),
+            'skip_peers': sorted({d for d, _ in stage.out_skips} | {s for s, _ in stage.in_skips})}
+
+
+def assert_parity(results, want_grads, want_loss, rel: float) -> None:
+    got = [g for r in results for g in r['grads']]
+    assert len(got) == len(want_grads), (len(got), len(want_grads))
+    for i, (a, b) in enumerate(zip(got, want_grads)):
+        assert a.shape == b.shape, (i, a.shape, b.shape)
+        scale = b.norm().item() + 1e-12
+        err = (a.double() - b.double()).norm().item() / scale
+        assert err <= rel, f'parameter {i} {tuple(b.shape)}: relative gradient error {err:.3e}'
+    assert results[-1]['loss'] is not None
+    assert abs(results[-1]['loss'] - want_loss) <= rel * max(1.0, abs(want_loss)), \
+        (results[-1]['loss'], want_loss)

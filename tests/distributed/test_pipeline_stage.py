@@ -208,3 +208,70 @@ def test_unet_skips_fan_out_to_several_ranks(tmp_path, checkpoint):
     for a, b in zip(got, want):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
     assert results[-1]['loss'] == pytest.approx(loss.item(), rel=1e-5)
+
+
+# -- gradient parity of U-Net / AmoebaNet against one process (same harness as RCCL) ------
+
+from tests.distributed import parity  # noqa: E402
+
+
+@pytest.mark.parametrize('world', [2, 4])
+@pytest.mark.parametrize('kind', parity.MODELS)
+def test_model_gradients_match_one_process(tmp_path, kind, world):
+    """Every rank's gradients and the loss equal the one-process run (gloo twin of
+    tests/distributed/test_rccl_multigpu.py)."""
+    chunks = 3
+    results = run(parity.stage_worker, world, tmp_path, kind, chunks, 'except_last', 'cpu')
+    grads, loss = parity.reference(kind, torch.device('cpu'), chunks)
+    parity.assert_parity(results, grads, loss, rel=1e-5)
+    if kind == 'unet':
+        assert any(r['skip_peers'] for r in results)
+
+
+# -- failure detection: a dead or mis-ordered peer raises within the timeout --------------
+
+def _dead_peer_worker(rank, world):
+    import time
+    from torchgpipe_amd.parallel import PipelineStage
+    from torchgpipe_amd.parallel.p2p import PipelineTimeout
+    stage = PipelineStage(build(), BALANCE, chunks=2, timeout=2.0)
+    if rank != 1:
+        time.sleep(5.0)  # rank 0 never sends; rank 2 idles too
+        return {'raised': None, 'elapsed': 0.0}
+    start = time.monotonic()
+    try:
+        stage.forward(None)
+    except PipelineTimeout as exc:
+        return {'raised': type(exc).__name__, 'elapsed': time.monotonic() - start,
+                'msg': str(exc)}
+    return {'raised': None, 'elapsed': time.monotonic() - start}
+
+
+def test_dead_peer_raises_pipeline_timeout(tmp_path):
+    results = run(_dead_peer_worker, 3, tmp_path, barrier=False)
+    assert results[1]['raised'] == 'PipelineTimeout', results[1]
+    assert results[1]['elapsed'] < 4.5, results[1]
+    assert 'rank 0' in results[1]['msg']
+
+
+def _misordered_worker(rank, world):
+    import time
+    from torchgpipe_amd.parallel.p2p import P2P, PipelineTimeout
+    p2p = P2P(torch.device('cpu'), timeout=2.0)
+    start = time.monotonic()
+    try:
+        # Both ranks receive first: the classic mis-ordered exchange that hangs forever
+        # under the reference's blocking mailboxes.
+        p2p.recv(1 - rank, ('act', 0)).wait()
+    except PipelineTimeout as exc:
+        return {'raised': type(exc).__name__, 'elapsed': time.monotonic() - start,
+                'msg': str(exc)}
+    return {'raised': None, 'elapsed': time.monotonic() - start}
+
+
+def test_misordered_exchange_raises_pipeline_timeout(tmp_path):
+    results = run(_misordered_worker, 2, tmp_path, barrier=False)
+    for r in results:
+        assert r['raised'] == 'PipelineTimeout', r
+        assert r['elapsed'] < 4.5, r
+        assert "'act'" in r['msg']

@@ -50,3 +50,21 @@ def test_bench_json_contract(nproc, model):
     assert 'TINY' in rec['metric'] and rec['vs_baseline'] is None
     # value is the whole-job aggregate: batch * steps / elapsed
     assert rec['value'] == pytest.approx(4 * 1000 / rec['ms_per_step'], rel=1e-2)
+
+
+def test_bench_headline_uses_reference_balance_and_reports_tuned():
+    """N > 1: the headline runs the reference balance; --also-tuned adds the MI355X one."""
+    rec = _run(2, '--model', 'unet', '--also-tuned', 'yes')
+    assert rec['config']['balance_source'] == 'ref'
+    tuned = rec['tuned']
+    assert tuned is not None and tuned['value'] > 0 and sum(tuned['balance']) == sum(
+        rec['config']['balance'])
+
+
+def test_bench_reference_balance_tables():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.UNET_EXPERIMENTS[8]['balance'] == [16, 27, 31, 44, 22, 57, 27, 17]
+    assert bench.UNET_EXPERIMENTS[4]['balance'] == [30, 66, 84, 61]
+    assert bench.UNET_EXPERIMENTS[2]['balance'] == [104, 137]
+    assert bench.AMOEBA_EXPERIMENTS[8]['balance'] == [2, 2, 2, 3, 3, 4, 4, 4]

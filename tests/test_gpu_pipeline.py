@@ -117,3 +117,26 @@ def test_gpipe_multi_gpu_if_available():
     x = torch.rand(8, 3, 32, 32, device='cuda:0')
     with torch.no_grad():
         torch.testing.assert_close(gpipe(x).cuda(0), ref(x), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('kind', ['unet', 'amoebanet'])
+@pytest.mark.parametrize('checkpoint', ['always', 'except_last', 'never'])
+@pytest.mark.parametrize('devices', [[0, 0], [0, 1]], ids=['1gpu', '2gpu'])
+def test_gpipe_training_gradients_match_one_device(devices, checkpoint, kind):
+    """Transparency (reference tests/test_transparency.py:7-42) on GPUs: a training step
+    of GPipe equals the unpartitioned model with the same micro-batching, including the
+    cross-device peer copies of activations, gradients and U-Net's portal skips."""
+    from tests.distributed import parity
+    if max(devices) >= torch.cuda.device_count():
+        pytest.skip(f'needs {max(devices) + 1} GPUs')
+    chunks = 3
+    model = parity.build(kind)
+    balance = parity.balance(kind, 2)
+    gpipe = GPipe(model, balance, devices=devices, chunks=chunks, checkpoint=checkpoint)
+    x, t = parity.data(kind, torch.device('cuda', devices[0]))
+    out = gpipe(x)
+    loss = parity.loss_fn(kind)(out, t.to(out.device))
+    loss.backward()
+    want, want_loss = parity.reference(kind, torch.device('cuda', 0), chunks)
+    got = [p.grad.detach().cpu() for p in gpipe.parameters()]
+    parity.assert_parity([{'grads': got, 'loss': loss.item()}], want, want_loss, rel=1e-4)

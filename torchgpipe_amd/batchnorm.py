@@ -57,6 +57,20 @@ class DeferredBatchNorm(_BatchNorm):
         self.chunks = chunks
         self.expected_chunks: Optional[int] = None
 
+    def reset_running_stats(self) -> None:
+        """Reset running statistics *and* the deferred accumulators.
+
+        ``_BatchNorm.reset_running_stats`` does not know ``sum`` / ``sum_squares``;
+        without this, a DeferredBatchNorm materialised from the meta device
+        (``utils.meta.materialize``) would commit allocator garbage.
+        """
+        super().reset_running_stats()
+        if hasattr(self, 'sum'):
+            self.sum.zero_()
+            self.sum_squares.zero_()
+        self.counter = 0
+        self.tracked = 0
+
     def _check_input_dim(self, input: Tensor) -> None:
         if input.dim() <= 2:
             raise ValueError('expected at least 3D input (got %dD input)' % input.dim())

@@ -54,7 +54,8 @@ class DistributedGPipe:
     def __init__(self, module: nn.Sequential, rank: int, workers: Optional[Dict[int, str]] = None,
                  balance: Optional[Iterable[int]] = None, microbatch_chunks: int = chunks, *,
                  device: Optional[torch.device] = None, deferred_batch_norm: bool = False,
-                 checkpoint: str = 'never', group: Optional[dist.ProcessGroup] = None) -> None:
+                 checkpoint: str = 'never', group: Optional[dist.ProcessGroup] = None,
+                 timeout: Optional[float] = None) -> None:
         microbatch_chunks = int(microbatch_chunks)
         if balance is None:
             raise ValueError(recommend_auto_balance('balance is required'))
@@ -75,7 +76,7 @@ class DistributedGPipe:
         self.device = device if device is not None else torch.device('cpu')
         self.stage = PipelineStage(module, balance, rank=rank, device=self.device,
                                    chunks=microbatch_chunks, checkpoint=checkpoint, group=group,
-                                   deferred_batch_norm=deferred_batch_norm)
+                                   deferred_batch_norm=deferred_batch_norm, timeout=timeout)
         self.module = self.stage.partition
         self._outputs: List[TensorOrTensors] = []
 
@@ -145,7 +146,7 @@ class DistributedGPipeDataLoader:
         for it, (data, target) in zip(range(self._num_iterations), self._data_loader):
             if self._last_rank != self._rank:
                 p2p = self._transport()
-                p2p.send([target.to(self._device)], self._last_rank, ('target', it))
+                p2p.send([target.to(self._device)], self._last_rank, ('target', it), cache=False)
                 # Complete the hand-off before handing control back: a send still
                 # pending when its transport is released would be dropped.
                 p2p.flush()
@@ -155,9 +156,9 @@ class DistributedGPipeDataLoader:
 
     def _last_stage_iter(self) -> Iterator[Tuple[Optional[Tensor], Optional[Tensor]]]:
         for it in range(self._num_iterations):
-            # The key carries the iteration index: the first message of each
-            # iteration always carries metadata, so target shapes may vary.
-            msg = self._transport().recv(0, ('target', it))
+            # One-shot key: every target carries its own metadata (shapes may
+            # vary per iteration) and nothing accumulates in the metadata cache.
+            msg = self._transport().recv(0, ('target', it), cache=False)
             (target,) = msg.wait()
             yield None, target.detach()
 

@@ -19,7 +19,17 @@ Metadata.  Receivers must allocate buffers before posting a receive.
 Shapes are exchanged once per (step signature, micro-batch, link, direction)
 over a CPU ``gloo`` control group — so no GPU→host synchronisation is ever
 needed — and cached afterwards.
+
+Failure detection.  The reference blocks forever on a rank that died or sent
+out of order (``torchgpipe/distributed/context.py:37``, "TODO: error
+handling").  Here every host-side wait is bounded: gloo waits (metadata,
+control payloads, host-staged tensors) take ``timeout`` and raise
+:class:`PipelineTimeout` naming the peer and message, and RCCL waits are
+stream-ordered, so a missing peer is caught by the process group's watchdog
+(``init_process_group(timeout=...)``), which aborts the rank instead of
+hanging the job.
 """
+import datetime
 from dataclasses import dataclass
 from typing import Dict, Hashable, List, Optional, Sequence, Tuple
 
@@ -29,7 +39,7 @@ from torch import Tensor
 
 from torchgpipe_amd.ops import misc
 
-__all__ = ['TensorMeta', 'P2P', 'Message']
+__all__ = ['TensorMeta', 'P2P', 'Message', 'PipelineTimeout']
 
 _DTYPES = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64,
            torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool]
@@ -80,6 +90,25 @@ def decode_metas(header: Tensor) -> Tuple[List[TensorMeta], bool]:
     return metas, atomic
 
 
+class PipelineTimeout(RuntimeError):
+    """A point-to-point wait exceeded the pipeline's timeout (dead or mis-ordered peer)."""
+
+
+def _wait(work: object, timeout: Optional[datetime.timedelta], what: str) -> None:
+    """``work.wait()`` bounded by ``timeout`` (host-blocking gloo works only)."""
+    try:
+        if timeout is None:
+            work.wait()  # type: ignore[attr-defined]
+        else:
+            work.wait(timeout)  # type: ignore[attr-defined]
+    except RuntimeError as exc:
+        msg = str(exc)
+        if 'imeout' in msg or 'imed out' in msg:
+            raise PipelineTimeout(f'{what}: no matching peer operation within {timeout} '
+                                  f'(peer dead or messages out of order): {msg}') from exc
+        raise
+
+
 def _align16(n: int) -> int:
     return (n + 15) // 16 * 16
 
@@ -87,12 +116,16 @@ def _align16(n: int) -> int:
 class Message:
     """Handle of a posted receive: ``wait()`` returns the received tensors."""
 
-    __slots__ = ('_works', '_tensors', '_buffer', '_metas', 'atomic', '_device')
+    __slots__ = ('_works', '_tensors', '_buffer', '_metas', 'atomic', '_device', '_timeout',
+                 '_what')
 
     def __init__(self, works: List[object], tensors: Optional[List[Tensor]],
                  buffer: Optional[Tensor], metas: List[TensorMeta], atomic: bool,
-                 device: Optional[torch.device] = None) -> None:
+                 device: Optional[torch.device] = None,
+                 timeout: Optional[datetime.timedelta] = None, what: str = '') -> None:
         self._works = works
+        self._timeout = timeout
+        self._what = what
         self._tensors = tensors
         self._buffer = buffer
         self._metas = metas
@@ -108,7 +141,7 @@ class Message:
         activations become the roots of this rank's backward graph.
         """
         for w in self._works:
-            w.wait()  # type: ignore[attr-defined]
+            _wait(w, self._timeout, self._what)
         self._works = []
         if self._device is not None:
             if self._tensors is not None:
@@ -141,13 +174,17 @@ class P2P:
         device: the device tensors are received on.
         group: process group for tensor traffic (``nccl`` = RCCL on GPUs).
         ctrl_group: ``gloo`` group for metadata (may equal ``group`` on CPU).
+        timeout: bound (seconds) of every host-blocking wait; ``None`` = the
+            process group's own timeout.
     """
 
     def __init__(self, device: torch.device, group: Optional[dist.ProcessGroup] = None,
                  ctrl_group: Optional[dist.ProcessGroup] = None,
                  pack: bool = True,
-                 link_groups: Optional[Dict[int, dist.ProcessGroup]] = None) -> None:
+                 link_groups: Optional[Dict[int, dist.ProcessGroup]] = None,
+                 timeout: Optional[float] = None) -> None:
         self.device = device
+        self.timeout = None if timeout is None else datetime.timedelta(seconds=timeout)
         self.group = group
         # One 2-rank communicator per peer ("link"): RCCL then runs every link on
         # its own stream, so a send waiting for a slow peer never holds back
@@ -161,6 +198,9 @@ class P2P:
         # stage every message through host memory.
         self.stage_host = (device.type == 'cuda' and dist.is_initialized()
                            and dist.get_backend(group) == 'gloo')
+        # Tensor works block the host only on gloo (RCCL waits are stream-ordered).
+        self._host_waits = not dist.is_initialized() or dist.get_backend(group) == 'gloo' \
+            or device.type != 'cuda'
         self._meta: Dict[Hashable, Tuple[List[TensorMeta], bool]] = {}
         self._pending_sends: List[object] = []
         self._pending_meta: List[object] = []
@@ -173,9 +213,10 @@ class P2P:
         self._pending_meta.append(dist.isend(encode_metas(metas, atomic), dst,
                                              group=self.ctrl_group))
 
-    def _recv_meta(self, src: int) -> Tuple[List[TensorMeta], bool]:
+    def _recv_meta(self, src: int, key: Hashable) -> Tuple[List[TensorMeta], bool]:
         header = torch.empty(_HEADER_LEN, dtype=torch.int64)
-        dist.recv(header, src, group=self.ctrl_group)
+        _wait(dist.irecv(header, src, group=self.ctrl_group), self.timeout,
+              f'metadata of message {key!r} from rank {src}')
         return decode_metas(header)
 
     def send_control(self, payload: Tensor, dst: int) -> None:
@@ -183,7 +224,8 @@ class P2P:
         self._pending_meta.append(dist.isend(payload, dst, group=self.ctrl_group))
 
     def recv_control(self, payload: Tensor, src: int) -> Tensor:
-        dist.recv(payload, src, group=self.ctrl_group)
+        _wait(dist.irecv(payload, src, group=self.ctrl_group), self.timeout,
+              f'control message from rank {src}')
         return payload
 
     def known(self, key: Hashable) -> Optional[Tuple[List[TensorMeta], bool]]:
@@ -195,15 +237,20 @@ class P2P:
     # -- tensors ----------------------------------------------------------------------------
 
     def send(self, tensors: Sequence[Tensor], dst: int, key: Hashable,
-             atomic: bool = False) -> None:
-        """Send ``tensors`` to ``dst``.  Asynchronous for the host (RCCL)."""
+             atomic: bool = False, cache: bool = True) -> None:
+        """Send ``tensors`` to ``dst``.  Asynchronous for the host (RCCL).
+
+        ``cache=False`` is for one-shot keys (e.g. per-iteration targets): the
+        metadata travels with this message and is not remembered.
+        """
         if not tensors:
             return
         metas = [TensorMeta.of(t) for t in tensors]
         cached = self._meta.get(key)
         if cached is None:
             self._send_meta(metas, atomic, dst)
-            self._meta[key] = (metas, atomic)
+            if cache:
+                self._meta[key] = (metas, atomic)
         elif cached != (metas, atomic):
             raise RuntimeError(
                 f'message {key!r} changed shape/dtype under the same step signature '
@@ -222,24 +269,27 @@ class P2P:
             buf = buf.cpu()
         self._pending_sends.append(dist.isend(buf, dst, group=self._link(dst)))
 
-    def recv(self, src: int, key: Hashable) -> Message:
+    def recv(self, src: int, key: Hashable, cache: bool = True) -> Message:
         """Post a receive from ``src``; the returned handle's ``wait()`` yields tensors."""
         cached = self._meta.get(key)
         if cached is None:
-            cached = self._recv_meta(src)
-            self._meta[key] = cached
+            cached = self._recv_meta(src, key)
+            if cache:
+                self._meta[key] = cached
         metas, atomic = cached
         if not metas:
             return Message([], [], None, metas, atomic)
         where = torch.device('cpu') if self.stage_host else self.device
         late = self.device if self.stage_host else None
+        timeout = self.timeout if self._host_waits else None
+        what = f'message {key!r} from rank {src}'
         if len(metas) == 1 or not self.pack:
             out = [torch.empty(m.shape, dtype=m.dtype, device=where) for m in metas]
             works = [dist.irecv(t, src, group=self._link(src)) for t in out]
-            return Message(works, out, None, metas, atomic, late)
+            return Message(works, out, None, metas, atomic, late, timeout, what)
         buf = torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=where)
         return Message([dist.irecv(buf, src, group=self._link(src))], None, buf, metas, atomic,
-                       late)
+                       late, timeout, what)
 
     def _link(self, peer: int) -> Optional[dist.ProcessGroup]:
         return self.link_groups.get(peer, self.group)
@@ -259,9 +309,10 @@ class P2P:
 
     def flush(self) -> None:
         """Order the current stream after every send issued so far, release them."""
+        timeout = self.timeout if self._host_waits else None
         for w in self._pending_sends:
-            w.wait()  # type: ignore[attr-defined]
+            _wait(w, timeout, 'pending send')
         self._pending_sends = []
         for w in self._pending_meta:
-            w.wait()  # type: ignore[attr-defined]
+            _wait(w, self.timeout, 'pending metadata send')
         self._pending_meta = []

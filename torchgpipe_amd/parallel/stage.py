@@ -27,6 +27,7 @@ Every cell is a function ``flat_inputs → flat_outputs`` where ``flat_inputs``
 output tensors + skips stashed for other ranks, so checkpointing
 (``Checkpointing``) treats cross-rank skips like any other input/output.
 """
+import datetime
 from collections import OrderedDict
 from typing import Any, Callable, Dict, Hashable, List, Optional, Sequence, Tuple, Union
 
@@ -39,7 +40,7 @@ from torchgpipe_amd.batchnorm import DeferredBatchNorm, set_micro_batches
 from torchgpipe_amd.checkpoint import Checkpointing
 from torchgpipe_amd.gpipe import check_balance, partition_layers, verify_module
 from torchgpipe_amd.microbatch import Batch
-from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P
+from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P, _wait
 from torchgpipe_amd.skip.layout import SkipLayout, inspect_skip_layout
 from torchgpipe_amd.skip.namespace import Namespace
 from torchgpipe_amd.skip.skippable import Skippable, verify_skippables
@@ -147,6 +148,12 @@ class PipelineStage:
             off for gloo).
         materialize: called on this rank's partition before it is moved to
             ``device`` (e.g. to initialise layers built on the ``meta`` device).
+        timeout: seconds any host-blocking wait of this stage (shape metadata,
+            control messages, gloo tensors) may take before raising
+            :class:`~torchgpipe_amd.parallel.p2p.PipelineTimeout`; also the
+            timeout of the groups this stage creates.  ``None`` = the default
+            group's timeout.  RCCL transfers are bounded by the RCCL process
+            group's own watchdog timeout (``init_process_group(timeout=...)``).
     """
 
     def __init__(self, module: nn.Sequential, balance: Sequence[int], *,
@@ -156,7 +163,8 @@ class PipelineStage:
                  ctrl_group: Optional[dist.ProcessGroup] = None,
                  deferred_batch_norm: bool = False, pack: bool = True,
                  links: Optional[bool] = None,
-                 materialize: Optional[Callable[[nn.Module], None]] = None) -> None:
+                 materialize: Optional[Callable[[nn.Module], None]] = None,
+                 timeout: Optional[float] = None) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
         if checkpoint not in ('always', 'except_last', 'never'):
@@ -182,6 +190,9 @@ class PipelineStage:
         self.chunks = chunks
         self.checkpoint = checkpoint
         self.training = True
+        self.timeout = timeout
+        group_kwargs: Dict[str, Any] = ({} if timeout is None else
+                                        {'timeout': datetime.timedelta(seconds=timeout)})
 
         if device is None:
             device = torch.device('cpu')
@@ -221,10 +232,11 @@ class PipelineStage:
             if dist.get_backend(group) == 'gloo':
                 ctrl_group = group
             else:
-                ctrl_group = dist.new_group(ranks=self.ranks, backend='gloo')
+                ctrl_group = dist.new_group(ranks=self.ranks, backend='gloo', **group_kwargs)
         self.ctrl_group = ctrl_group
         self.p2p = P2P(device, group=group, ctrl_group=ctrl_group, pack=pack,
-                       link_groups=self._make_links(links) if distributed else None)
+                       link_groups=self._make_links(links, group_kwargs) if distributed else None,
+                       timeout=timeout)
 
         self._cells: List[_Cell] = []
         self._sig: Optional[Signature] = None
@@ -263,13 +275,15 @@ class PipelineStage:
             if self.rank == a:
                 works.append(dist.isend(buf, peer, group=self.p2p._link(peer)))
             else:
-                dist.irecv(buf, peer, group=self.p2p._link(peer)).wait()
+                _wait(dist.irecv(buf, peer, group=self.p2p._link(peer)),
+                      self.p2p.timeout if staged else None, f'link handshake with rank {peer}')
         for w in works:
-            w.wait()
+            _wait(w, self.p2p.timeout if staged else None, 'link handshake')
         if where.type == 'cuda':
             torch.cuda.synchronize(where)
 
-    def _make_links(self, enabled: Optional[bool]) -> Dict[int, dist.ProcessGroup]:
+    def _make_links(self, enabled: Optional[bool], group_kwargs: Dict[str, Any]
+                    ) -> Dict[int, dist.ProcessGroup]:
         """Create one 2-rank process group per pipeline link this model uses.
 
         ``new_group`` is collective over WORLD, so every rank creates every
@@ -289,7 +303,7 @@ class PipelineStage:
             return {}
         links: Dict[int, dist.ProcessGroup] = {}
         for a, b in self._link_pairs():
-            pg = dist.new_group(ranks=[self.ranks[a], self.ranks[b]])
+            pg = dist.new_group(ranks=[self.ranks[a], self.ranks[b]], **group_kwargs)
             if self.rank == a:
                 links[self.ranks[b]] = pg
             elif self.rank == b:
