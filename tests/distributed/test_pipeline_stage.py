@@ -250,7 +250,7 @@ def _dead_peer_worker(rank, world):
 def test_dead_peer_raises_pipeline_timeout(tmp_path):
     results = run(_dead_peer_worker, 3, tmp_path, barrier=False)
     assert results[1]['raised'] == 'PipelineTimeout', results[1]
-    assert results[1]['elapsed'] < 4.5, results[1]
+    assert results[1]["elapsed"] < 10.0, results[1]
     assert 'rank 0' in results[1]['msg']
 
 
@@ -273,5 +273,5 @@ def test_misordered_exchange_raises_pipeline_timeout(tmp_path):
     results = run(_misordered_worker, 2, tmp_path, barrier=False)
     for r in results:
         assert r['raised'] == 'PipelineTimeout', r
-        assert r['elapsed'] < 4.5, r
+        assert r["elapsed"] < 10.0, r
         assert "'act'" in r['msg']

@@ -1,0 +1,287 @@
+// BatchNorm (training) kernels around the implicit-GEMM convolutions of conv_gemm.hip.
+//
+// The forward's statistics come from the convolution epilogue as per-(column block,
+// channel) (mean, M2) partials; bn_finalize merges them with Chan's parallel formula in
+// fp64 (no E[x^2] - E[x]^2 cancellation, whatever the mean), applies the running-stat
+// EMA (unbiased variance, like nn.BatchNorm) and writes mean / invstd for bn_apply and
+// the backward.  bn_apply normalises and optionally adds the other branch of an
+// AmoebaNet node (left + right) in the same pass.  The backward is two passes: per
+// channel sums of dy and dy*(z-mean), then dz and the affine gradients.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace tgpipe {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Chan's parallel merge of (count, mean, M2) triples.
+__device__ __forceinline__ void chan_merge(double& na, double& ma, double& m2a, double nb,
+                                           double mb, double m2b) {
+  const double n = na + nb;
+  if (n <= 0.0) return;
+  const double d = mb - ma;
+  ma += d * nb / n;
+  m2a += m2b + d * d * na * nb / n;
+  na = n;
+}
+
+// 32 lanes per channel merge strided subsets of the column-block partials, then a
+// 5-level shuffle tree merges the lanes: ~blocks/32 + 5 dependent fp64 steps instead
+// of `blocks` (AmoebaNet's 56^2 planes at 20 images: 980 blocks).
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    const float* __restrict__ pm, const float* __restrict__ pm2, int blocks, int width,
+    int64_t total, int64_t c, float eps, double momentum, float* __restrict__ mean,
+    float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv,
+    int64_t* __restrict__ tracked) {
+  const int lane = threadIdx.x & 31;
+  const int64_t ch = static_cast<int64_t>(blockIdx.x) * 8 + (threadIdx.x >> 5);
+  if (tracked != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *tracked += 1;
+  double na = 0.0, ma = 0.0, m2a = 0.0;
+  if (ch < c) {
+    for (int b = lane; b < blocks; b += 32) {
+      const int64_t left = total - static_cast<int64_t>(b) * width;
+      chan_merge(na, ma, m2a, static_cast<double>(left < width ? left : width), pm[b * c + ch],
+                 pm2[b * c + ch]);
+    }
+  }
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) {
+    const double nb = __shfl_xor(na, off, 32);
+    const double mb = __shfl_xor(ma, off, 32);
+    const double m2b = __shfl_xor(m2a, off, 32);
+    chan_merge(na, ma, m2a, nb, mb, m2b);
+  }
+  if (ch >= c || lane != 0) return;
+  const double var = na > 0.0 ? m2a / na : 0.0;
+  mean[ch] = static_cast<float>(ma);
+  invstd[ch] = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  if (rm != nullptr) {
+    const double unbiased = na > 1.0 ? m2a / (na - 1.0) : var;
+    rm[ch] = static_cast<float>((1.0 - momentum) * rm[ch] + momentum * ma);
+    rv[ch] = static_cast<float>((1.0 - momentum) * rv[ch] + momentum * unbiased);
+  }
+}
+
+template <bool kVec, bool kAdd>
+__global__ __launch_bounds__(256) void bn_apply_kernel(
+    const float* __restrict__ z, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ add,
+    float* __restrict__ y, int64_t total, int64_t c, int64_t s) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  if constexpr (kVec) {
+    // s % 4 == 0: a quad never straddles two channels
+    for (int64_t q = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; q < total / 4;
+         q += stride) {
+      const int64_t ch = (4 * q / s) % c;
+      const float k = invstd[ch] * (gamma ? gamma[ch] : 1.f);
+      const float b = (beta ? beta[ch] : 0.f) - mean[ch] * k;
+      floatx4 v = reinterpret_cast<const floatx4*>(z)[q];
+      v = v * k + b;
+      if constexpr (kAdd) v += reinterpret_cast<const floatx4*>(add)[q];
+      reinterpret_cast<floatx4*>(y)[q] = v;
+    }
+  } else {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
+         i += stride) {
+      const int64_t ch = (i / s) % c;
+      const float k = invstd[ch] * (gamma ? gamma[ch] : 1.f);
+      float v = (z[i] - mean[ch]) * k + (beta ? beta[ch] : 0.f);
+      if constexpr (kAdd) v += add[i];
+      y[i] = v;
+    }
+  }
+}
+
+// One workgroup per (channel, image range): sums of dy and dy * (z - mean).
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const float* __restrict__ dy, const float* __restrict__ z, const float* __restrict__ mean,
+    float* __restrict__ sums, int64_t n, int64_t c, int64_t s, int64_t n_per) {
+  const int64_t ch = blockIdx.x;
+  const int64_t n0 = blockIdx.y * n_per, n1 = min(n, n0 + n_per);
+  const float mu = mean[ch];
+  float sd = 0.f, sdz = 0.f;
+  for (int64_t img = n0; img < n1; ++img) {
+    const int64_t base = (img * c + ch) * s;
+    if ((s & 3) == 0) {
+      for (int64_t q = threadIdx.x; q < s / 4; q += 256) {
+        const floatx4 g = reinterpret_cast<const floatx4*>(dy + base)[q];
+        const floatx4 v = reinterpret_cast<const floatx4*>(z + base)[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sd += g[e];
+          sdz += g[e] * (v[e] - mu);
+        }
+      }
+    } else {
+      for (int64_t i = threadIdx.x; i < s; i += 256) {
+        const float g = dy[base + i];
+        sd += g;
+        sdz += g * (z[base + i] - mu);
+      }
+    }
+  }
+  __shared__ float red[2][4];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    sd += __shfl_xor(sd, off);
+    sdz += __shfl_xor(sdz, off);
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wave] = sd;
+    red[1][wave] = sdz;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(sums + ch, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(sums + c + ch, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
+    const float* __restrict__ dy, const float* __restrict__ z, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ sums, float* __restrict__ dz, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, int64_t total, int64_t c, int64_t s, float inv_m) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  const int64_t first = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (first < c) {
+    if (dgamma) dgamma[first] = sums[c + first] * invstd[first];
+    if (dbeta) dbeta[first] = sums[first];
+  }
+  if constexpr (kVec) {
+    for (int64_t q = first; q < total / 4; q += stride) {
+      const int64_t ch = (4 * q / s) % c;
+      const float is = invstd[ch];
+      const float k1 = (gamma ? gamma[ch] : 1.f) * is;
+      const float k2 = sums[ch] * inv_m;
+      const float k3 = is * is * sums[c + ch] * inv_m;
+      const float mu = mean[ch];
+      const floatx4 g = reinterpret_cast<const floatx4*>(dy)[q];
+      const floatx4 v = reinterpret_cast<const floatx4*>(z)[q];
+      floatx4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = k1 * (g[e] - k2 - (v[e] - mu) * k3);
+      reinterpret_cast<floatx4*>(dz)[q] = o;
+    }
+  } else {
+    for (int64_t i = first; i < total; i += stride) {
+      const int64_t ch = (i / s) % c;
+      const float is = invstd[ch];
+      const float k1 = (gamma ? gamma[ch] : 1.f) * is;
+      dz[i] = k1 * (dy[i] - sums[ch] * inv_m - (z[i] - mean[ch]) * is * is * sums[c + ch] * inv_m);
+    }
+  }
+}
+
+// One workgroup per (channel, image): mean and centred M2 of the plane (two passes; the
+// plane is L2-resident for the second).  Used when the convolution split its reduction.
+__global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ z,
+                                                       float* __restrict__ pm,
+                                                       float* __restrict__ pm2, int64_t c,
+                                                       int64_t s) {
+  const int64_t ch = blockIdx.x, img = blockIdx.y;
+  const float* plane = z + (img * c + ch) * s;
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < s; i += 256) acc += plane[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / static_cast<float>(s);
+  __syncthreads();
+  acc = 0.f;
+  for (int64_t i = threadIdx.x; i < s; i += 256) {
+    const float d = plane[i] - mean;
+    acc += d * d;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    pm[img * c + ch] = mean;
+    pm2[img * c + ch] = red[0] + red[1] + red[2] + red[3];
+  }
+}
+
+unsigned grid_for(int64_t work) {
+  const int64_t blocks = (work + 255) / 256;
+  return static_cast<unsigned>(blocks < 8192 ? (blocks > 0 ? blocks : 1) : 8192);
+}
+
+}  // namespace
+
+void launch_bn_finalize(const float* part_mean, const float* part_m2, int blocks, int width,
+                        int64_t total, int64_t c, float eps, double momentum, float* mean,
+                        float* invstd, float* running_mean, float* running_var, int64_t* tracked,
+                        hipStream_t stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(static_cast<unsigned>((c + 7) / 8)),
+                     dim3(256), 0, stream, part_mean, part_m2, blocks, width, total, c, eps,
+                     momentum, mean, invstd, running_mean, running_var, tracked);
+}
+
+void launch_bn_stats(const float* z, float* part_mean, float* part_m2, int64_t n, int64_t c,
+                     int64_t s, hipStream_t stream) {
+  if (n == 0 || c == 0) return;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(static_cast<unsigned>(c), static_cast<unsigned>(n)),
+                     dim3(256), 0, stream, z, part_mean, part_m2, c, s);
+}
+
+void launch_bn_apply(const float* z, const float* mean, const float* invstd, const float* gamma,
+                     const float* beta, const float* add, float* y, int64_t n, int64_t c,
+                     int64_t s, hipStream_t stream) {
+  const int64_t total = n * c * s;
+  if (total == 0) return;
+  const bool vec = (s & 3) == 0;
+  const unsigned grid = grid_for(vec ? total / 4 : total);
+  if (vec) {
+    if (add)
+      hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(grid), dim3(256), 0, stream, z, mean,
+                         invstd, gamma, beta, add, y, total, c, s);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(grid), dim3(256), 0, stream, z,
+                         mean, invstd, gamma, beta, add, y, total, c, s);
+  } else {
+    if (add)
+      hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(grid), dim3(256), 0, stream, z,
+                         mean, invstd, gamma, beta, add, y, total, c, s);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(grid), dim3(256), 0, stream, z,
+                         mean, invstd, gamma, beta, add, y, total, c, s);
+  }
+}
+
+void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
+                        const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
+                        int64_t n, int64_t c, int64_t s, hipStream_t stream) {
+  const int64_t total = n * c * s;
+  if (total == 0) return;
+  // enough (channel, image range) workgroups to cover the chip ~4x
+  int64_t splits = (1024 + c - 1) / c;
+  if (splits > n) splits = n;
+  if (splits < 1) splits = 1;
+  const int64_t n_per = (n + splits - 1) / splits;
+  splits = (n + n_per - 1) / n_per;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(static_cast<unsigned>(c),
+                                                static_cast<unsigned>(splits)),
+                     dim3(256), 0, stream, dy, z, mean, sums, n, c, s, n_per);
+  const bool vec = (s & 3) == 0;
+  int64_t work = vec ? total / 4 : total;
+  if (work < c) work = c;
+  const unsigned grid = grid_for(work);
+  const float inv_m = 1.f / static_cast<float>(n * s);
+  if (vec)
+    hipLaunchKernelGGL((bn_bwd_dz_kernel<true>), dim3(grid), dim3(256), 0, stream, dy, z, mean,
+                       invstd, gamma, sums, dz, dgamma, dbeta, total, c, s, inv_m);
+  else
+    hipLaunchKernelGGL((bn_bwd_dz_kernel<false>), dim3(grid), dim3(256), 0, stream, dy, z, mean,
+                       invstd, gamma, sums, dz, dgamma, dbeta, total, c, s, inv_m);
+}
+
+}  // namespace tgpipe

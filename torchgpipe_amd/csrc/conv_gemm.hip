@@ -1,0 +1,714 @@
+// Implicit-GEMM convolution on the fp32 MFMA pipes of CDNA4 (gfx950) for the
+// AmoebaNet-D cell operations: 1x1 (stride 1 / 2, input offset for FactorizedReduce)
+// and 1xk / kx1 convolutions, NCHW fp32, fused with the ReLU that precedes every
+// convolution of the model and with the statistics of the BatchNorm that follows it.
+//
+//   forward      Z[n][co][p]    = sum_{ci,t} W[co][ci][t] * relu(X[n][ci][tap(p,t)])
+//                M = Co, N = images x output pixels, K = Ci x taps
+//                epilogue: Z tile -> LDS -> coalesced stores + per-(channel, column block)
+//                (mean, M2) partials for the BatchNorm (merged with Chan's formula later)
+//   backward-data dX[n][ci][q]  = relu'(X) * sum_{co,t} W[co][ci][t] * dZ[n][co][tap^-1(q,t)]
+//                M = Ci, N = images x input pixels, K = Co x taps  (A = W transposed)
+//                strided 1x1 ("scatter"): N = output pixels, each result scattered to
+//                its input pixel (the stride holes are zero; 4x less work than a
+//                dense pass that reads zeros for them)
+//   weight-grad  dW[co][ci][t]  = sum_{n,p} dZ[n][co][p] * relu(X[n][ci][tap(p,t)])
+//                M = Co, N = Ci x taps, K = images x output pixels
+//
+// Workgroups (Cfg): 128 x 128 blocks of 8 waves (2 x 4, each 64 x 32 = two
+// v_mfma_f32_32x32x2_f32 tiles) or 64 x 64 blocks of 4 waves (one tile each), BK = 32
+// reduction steps per double-buffered LDS stage: one barrier and 32 / 16 MFMAs per wave
+// per stage, with the next stage's global loads in flight meanwhile (a two-stage-ahead
+// variant with two register sets measured 3 % slower: profiles/convbn_bench.json notes).
+// Grids that would not fill the 256 CUs split the reduction (grid.y) and accumulate
+// with hardware fp32 atomics into a zeroed output; the forward then leaves the
+// BatchNorm statistics to a separate pass (bn_stats, batchnorm.hip).
+//
+// LDS images:
+//   K-major operand (k contiguous in HBM: weights, dZ in weight-grad, X in weight-grad)
+//     [BK/4][rows][4] with the 4 k of a quad stored (0, 2, 1, 3): lane half h of a
+//     32x32x2 MFMA pair (k-steps 2g, 2g+1) reads its two operands as one ds_read_b64.
+//   N-major operand (pixels contiguous: X in forward, dZ in backward-data)
+//     [BK][cols + 32]: the two lane halves read rows k and k+1, 32 banks apart.
+// Out-of-range taps (padding, stride holes, tails) are raw buffer loads at an offset
+// past the buffer: the hardware returns 0, so padding needs no select.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace tgpipe {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kBK = 32;
+constexpr uint32_t kOOB = 0x7ffffff0u;  // buffer offset past every tensor (< 2 GiB)
+
+enum Mode : int { kFwd = 0, kBwdData = 1, kWgrad = 2 };
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), static_cast<short>(0),
+                                           static_cast<int>(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+__device__ __forceinline__ floatx4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return floatx4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                 __uint_as_float(v[3])};
+}
+
+__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+
+// Geometry of one convolution (all byte offsets fit in 31 bits: checked on the host).
+struct Geo {
+  int n, ci, h, w;       // input
+  int co, ho, wo;        // output (co = channels of this convolution)
+  int co_total, co_off;  // channel count / offset of its output inside Z (concat outputs)
+  int kh, kw, taps;      // kernel (one of kh, kw is 1), taps = kh * kw
+  int sh, sw, ph, pw;    // stride, padding
+  int oh, ow;            // extra input offset (FactorizedReduce's shifted branch: 1)
+  int relu;              // ReLU on the input (forward / weight-grad) / its mask (bwd-data)
+  int scatter;           // bwd-data over output pixels, results scattered (strided 1x1)
+};
+
+// Tile configurations.  CFG 0: 64 x 64 block, 4 waves (2 x 2) of one 32 x 32 MFMA tile;
+// CFG 1: 128 x 128 block, 8 waves (2 x 4) of 64 x 32 (two tiles) -- two waves per SIMD
+// from one workgroup, so one wave's MFMAs cover the other's LDS reads and barrier.
+template <int CFG>
+struct Cfg {
+  static constexpr int WVM = 2;
+  static constexpr int WVN = CFG == 0 ? 2 : 4;
+  static constexpr int TM = CFG == 0 ? 1 : 2;   // 32 x 32 MFMA tiles per wave (rows)
+  static constexpr int TN = 1;                  // (columns)
+  static constexpr int kThreads = 64 * WVM * WVN;
+  static constexpr int BM = WVM * 32 * TM;
+  static constexpr int BN = WVN * 32 * TN;
+  static constexpr int kAImg = kBK * BM;          // K-major image
+  static constexpr int kBImgK = kBK * BN;         // K-major image
+  static constexpr int kBStrideN = BN + 32;       // N-major row stride
+  static constexpr int kBImgN = kBK * kBStrideN;  // N-major image
+  static constexpr int kCStride = BN + 4;         // epilogue C tile row stride
+  static constexpr int kOpFloats(bool k_major) {
+    return 2 * kAImg + 2 * (k_major ? kBImgK : kBImgN);
+  }
+  // operand images (double-buffered), reused by the epilogue's C tile (forward /
+  // bwd-data); 128 x 128: 72 KiB -> two workgroups per CU
+  static constexpr int kLdsFloats(int mode) {
+    return mode == 2 ? kOpFloats(true)
+                     : (kOpFloats(false) > BM * kCStride ? kOpFloats(false) : BM * kCStride);
+  }
+  static constexpr int kAQuads = kBK * BM / 4 / kThreads;   // per thread per stage
+  static constexpr int kBQuadsN = kBK * BN / 4 / kThreads;
+  static constexpr int kBQuadsK = kBK * BN / 4 / kThreads;
+};
+
+// ---- operand staging -----------------------------------------------------------------------
+// K-major operand: quad index i of thread t -> row r = (t >> 3) + (THREADS / 8) * i,
+// k quad (t & 7).
+template <int ROWS, int Q, int THREADS>
+__device__ __forceinline__ void store_kmajor(float* img, const floatx4 (&v)[Q], int tid) {
+  const int q = tid & 7;
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const int row = (tid >> 3) + (THREADS / 8) * i;
+    *reinterpret_cast<floatx4*>(img + (q * ROWS + row) * 4) =
+        floatx4{v[i][0], v[i][2], v[i][1], v[i][3]};
+  }
+}
+
+// N-major operand: quad index i of thread t -> row k = t / (BN/4) + (THREADS / (BN/4)) * i,
+// column quad t % (BN/4).
+template <int BN, int Q, int THREADS>
+__device__ __forceinline__ void store_nmajor(float* img, const floatx4 (&v)[Q], int tid) {
+  constexpr int QPR = BN / 4;
+  constexpr int RPP = THREADS / QPR;
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const int k = tid / QPR + RPP * i;
+    *reinterpret_cast<floatx4*>(img + k * (BN + 32) + (tid % QPR) * 4) = v[i];
+  }
+}
+
+// ---- the GEMM core ------------------------------------------------------------------------
+
+template <int CFG, bool kBKMajor>
+__device__ __forceinline__ void mfma_stage(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG>::TN],
+                                           const float* aimg, const float* bimg, int lane, int wm,
+                                           int wn) {
+  using C = Cfg<CFG>;
+  constexpr int WM = C::TM, WN = C::TN;
+  const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int g = 0; g < kBK / 4; ++g) {
+    floatx2 a[WM], b[WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+      a[i] = *reinterpret_cast<const floatx2*>(
+          aimg + (g * C::BM + wm * 32 * WM + i * 32 + l32) * 4 + 2 * h);
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      if constexpr (kBKMajor) {
+        b[j] = *reinterpret_cast<const floatx2*>(
+            bimg + (g * C::BN + wn * 32 * WN + j * 32 + l32) * 4 + 2 * h);
+      } else {
+        const int col = wn * 32 * WN + j * 32 + l32;
+        b[j] = floatx2{bimg[(4 * g + h) * C::kBStrideN + col],
+                       bimg[(4 * g + 2 + h) * C::kBStrideN + col]};
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+  }
+}
+
+// Per-column constants of an N-major operand column (fixed for the whole K loop).
+struct Col {
+  int base;  // element offset of the column's image / channel-0 plane (+ pixel if plain)
+  int y, x;  // pixel coordinates (tap-independent part of the source position)
+  bool ok;
+};
+
+// kPlain: 1x1 / stride 1 / no padding / no offset: column pixel == source pixel.
+template <int MODE, bool kPlain>
+__device__ __forceinline__ Col make_col(const Geo& g, int j, int N) {
+  Col c;
+  c.ok = j < N;
+  const int jj = c.ok ? j : 0;
+  const bool out_space = MODE == kFwd || g.scatter;  // columns are output pixels
+  const int hw = out_space ? g.ho * g.wo : g.h * g.w;
+  const int wdt = out_space ? g.wo : g.w;
+  const int n = jj / hw, p = jj - n * hw;
+  if constexpr (MODE == kFwd) {
+    if (kPlain) {
+      c.base = n * g.ci * hw + p;
+      c.y = c.x = 0;
+    } else {
+      const int y = p / wdt;
+      c.base = n * g.ci * g.h * g.w;
+      c.y = y * g.sh - g.ph + g.oh;
+      c.x = (p - y * wdt) * g.sw - g.pw + g.ow;
+    }
+  } else {  // bwd-data: dZ source
+    if (kPlain || g.scatter) {
+      c.base = (n * g.co_total + g.co_off) * g.ho * g.wo + p;
+      c.y = c.x = 0;
+      if (g.scatter) {  // destination input pixel, for the epilogue
+        const int y = p / wdt;
+        c.y = y * g.sh - g.ph + g.oh;
+        c.x = (p - y * wdt) * g.sw - g.pw + g.ow;
+      }
+    } else {
+      const int y = p / wdt;
+      c.base = (n * g.co_total + g.co_off) * g.ho * g.wo;
+      c.y = y + g.ph - g.oh;
+      c.x = (p - y * wdt) + g.pw - g.ow;
+    }
+  }
+  return c;
+}
+
+template <int MODE, int CFG, bool kPlain>
+__global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
+    const float* __restrict__ a_src, const float* __restrict__ b_src,
+    const float* __restrict__ x_mask, float* __restrict__ out, float* __restrict__ part_mean,
+    float* __restrict__ part_m2, Geo g, int M, int N, int K, int k_chunk, int atomic,
+    int accumulate, int64_t a_bytes, int64_t b_bytes) {
+  using C = Cfg<CFG>;
+  constexpr int WM = C::TM, WN = C::TN, kThreads = C::kThreads;
+  constexpr bool kBK_major = MODE == kWgrad;
+  constexpr int kBImg = kBK_major ? C::kBImgK : C::kBImgN;
+  __shared__ __attribute__((aligned(16))) float lds[C::kLdsFloats(MODE)];
+  auto aimg = [&](int b) { return lds + b * C::kAImg; };
+  auto bimg = [&](int b) { return lds + 2 * C::kAImg + b * kBImg; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % C::WVM, wn = wave / C::WVM;
+
+  // XCD-aware block order: the 8 XCDs take consecutive blocks round-robin; remap so
+  // each XCD owns a contiguous run of (m fastest) blocks, i.e. the m-blocks sharing a
+  // column block (one B tile) run on one XCD's L2.
+  const int mb_count = (M + C::BM - 1) / C::BM;
+  int bid = blockIdx.x;
+  const int nblk = gridDim.x;
+  if ((nblk & 7) == 0) bid = (bid & 7) * (nblk >> 3) + (bid >> 3);
+  const int mblk = bid % mb_count, nb_i = bid / mb_count;
+  const int m0 = mblk * C::BM, n0 = nb_i * C::BN;
+  const int k_begin = blockIdx.y * k_chunk;
+  const int k_end = min(K, k_begin + k_chunk);
+
+  const __amdgpu_buffer_rsrc_t ar = rsrc(a_src, a_bytes);
+  const __amdgpu_buffer_rsrc_t br = rsrc(b_src, b_bytes);
+  const int hw_out = g.ho * g.wo, hw_in = g.h * g.w;
+  const bool quads = kPlain && (hw_out & 3) == 0;
+
+  constexpr int kRB = kBK_major ? C::kBQuadsK : C::kBQuadsN;
+  floatx4 ra[C::kAQuads], rb[kRB];
+
+  // N-major B columns of this thread (forward / bwd-data)
+  constexpr int QPR = C::BN / 4;
+  Col col[4];
+  if constexpr (!kBK_major) {
+    const int jq = n0 + (tid % QPR) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) col[e] = make_col<MODE, kPlain>(g, jq + e, N);
+  }
+
+  // A: K-major rows (tid >> 3) + (threads / 8) i, k quad (tid & 7)
+  auto load_a = [&](int k0, floatx4 (&ra)[C::kAQuads]) {
+    const int k = k0 + 4 * (tid & 7);
+#pragma unroll
+    for (int i = 0; i < C::kAQuads; ++i) {
+      const int row = m0 + (tid >> 3) + (kThreads / 8) * i;
+      if constexpr (MODE == kFwd) {
+        // W[co][ci*T + t], row-major
+        if (row < M && k + 3 < k_end && (K & 3) == 0) {
+          ra[i] = bload4(ar, static_cast<uint32_t>((row * K + k) * 4));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            ra[i][e] = bload(ar, row < M && k + e < k_end
+                                     ? static_cast<uint32_t>((row * K + k + e) * 4) : kOOB);
+        }
+      } else if constexpr (MODE == kBwdData) {
+        // A[ci][co*T + t] = W[co][ci][t]: gathered from the untransposed weight (L2)
+        const int T = g.taps;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t off = kOOB;
+          if (row < M && k + e < k_end) {
+            const int co = T == 1 ? k + e : (k + e) / T;
+            const int t = k + e - co * T;
+            off = static_cast<uint32_t>(((co * g.ci + row) * T + t) * 4);
+          }
+          ra[i][e] = bload(ar, off);
+        }
+      } else {
+        // dZ rows: A[co][k = (n, p)]
+        if (quads && row < M && k + 3 < k_end) {
+          const int n = k / hw_out, p = k - n * hw_out;
+          ra[i] = bload4(ar, static_cast<uint32_t>(
+                                 ((n * g.co_total + g.co_off + row) * hw_out + p) * 4));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            uint32_t off = kOOB;
+            if (row < M && k + e < k_end) {
+              const int n = (k + e) / hw_out, p = k + e - n * hw_out;
+              off = static_cast<uint32_t>(((n * g.co_total + g.co_off + row) * hw_out + p) * 4);
+            }
+            ra[i][e] = bload(ar, off);
+          }
+        }
+      }
+    }
+  };
+
+  auto load_b = [&](int k0, floatx4 (&rb)[kRB]) {
+    if constexpr (MODE == kFwd) {
+      // relu(X) taps: B[k = (ci, t)][j = output pixel]
+#pragma unroll
+      for (int i = 0; i < C::kBQuadsN; ++i) {
+        const int k = k0 + tid / QPR + (kThreads / QPR) * i;
+        const bool kin = k < k_end;
+        floatx4 v;
+        if constexpr (kPlain) {
+          const int coff = k * hw_in;
+          if (quads && col[3].ok && kin) {
+            v = bload4(br, static_cast<uint32_t>((col[0].base + coff) * 4));
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              v[e] = bload(br, col[e].ok && kin
+                                   ? static_cast<uint32_t>((col[e].base + coff) * 4) : kOOB);
+          }
+        } else {
+          const int ci = k / g.taps, t = k - ci * g.taps;
+          const int th = g.kh == 1 ? 0 : t, tw = g.kh == 1 ? t : 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int yi = col[e].y + th, xi = col[e].x + tw;
+            const bool ok = col[e].ok && kin && yi >= 0 && yi < g.h && xi >= 0 && xi < g.w;
+            v[e] = bload(br, ok ? static_cast<uint32_t>(
+                                      (col[e].base + (ci * g.h + yi) * g.w + xi) * 4) : kOOB);
+          }
+        }
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = relu(v[e]);
+        }
+        rb[i] = v;
+      }
+    } else if constexpr (MODE == kBwdData) {
+      // dZ taps: B[k = (co, t)][j = pixel]
+#pragma unroll
+      for (int i = 0; i < C::kBQuadsN; ++i) {
+        const int k = k0 + tid / QPR + (kThreads / QPR) * i;
+        const bool kin = k < k_end;
+        floatx4 v;
+        if (kPlain || g.scatter) {
+          const int coff = k * hw_out;
+          if (((hw_out & 3) == 0) && col[3].ok && kin) {
+            v = bload4(br, static_cast<uint32_t>((col[0].base + coff) * 4));
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              v[e] = bload(br, col[e].ok && kin
+                                   ? static_cast<uint32_t>((col[e].base + coff) * 4) : kOOB);
+          }
+        } else {
+          // stride 1: output pixel = input pixel + pad - tap - offset
+          const int co = k / g.taps, t = k - co * g.taps;
+          const int th = g.kh == 1 ? 0 : t, tw = g.kh == 1 ? t : 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int y = col[e].y - th, x = col[e].x - tw;
+            const bool ok = col[e].ok && kin && y >= 0 && y < g.ho && x >= 0 && x < g.wo;
+            v[e] = bload(br, ok ? static_cast<uint32_t>(
+                                      (col[e].base + co * hw_out + y * g.wo + x) * 4) : kOOB);
+          }
+        }
+        rb[i] = v;
+      }
+    } else {
+      // relu(X) taps: B[k = output pixel (n, p)][j = (ci, t)]
+      const int k = k0 + 4 * (tid & 7);
+#pragma unroll
+      for (int i = 0; i < C::kBQuadsK; ++i) {
+        const int j = n0 + (tid >> 3) + (kThreads / 8) * i;
+        const int ci = j / g.taps, t = j - ci * g.taps;
+        floatx4 v;
+        if (quads && j < N && k + 3 < k_end) {
+          const int n = k / hw_out, p = k - n * hw_out;
+          v = bload4(br, static_cast<uint32_t>(((n * g.ci + ci) * hw_in + p) * 4));
+        } else {
+          const int th = g.kh == 1 ? 0 : t, tw = g.kh == 1 ? t : 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            uint32_t off = kOOB;
+            if (j < N && k + e < k_end) {
+              const int n = (k + e) / hw_out, p = k + e - n * hw_out;
+              const int y = p / g.wo, x = p - y * g.wo;
+              const int yi = y * g.sh - g.ph + th + g.oh, xi = x * g.sw - g.pw + tw + g.ow;
+              if (yi >= 0 && yi < g.h && xi >= 0 && xi < g.w)
+                off = static_cast<uint32_t>((((n * g.ci + ci) * g.h + yi) * g.w + xi) * 4);
+            }
+            v[e] = bload(br, off);
+          }
+        }
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = relu(v[e]);
+        }
+        rb[i] = v;
+      }
+    }
+  };
+
+  auto store_stage = [&](int buf, const floatx4 (&ra)[C::kAQuads], const floatx4 (&rb)[kRB]) {
+    store_kmajor<C::BM, C::kAQuads, kThreads>(aimg(buf), ra, tid);
+    if constexpr (kBK_major)
+      store_kmajor<C::BN, C::kBQuadsK, kThreads>(bimg(buf), rb, tid);
+    else
+      store_nmajor<C::BN, C::kBQuadsN, kThreads>(bimg(buf), rb, tid);
+  };
+
+  floatx16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int stages = (k_end - k_begin + kBK - 1) / kBK;
+  if (stages > 0) {
+    load_a(k_begin, ra);
+    load_b(k_begin, rb);
+    store_stage(0, ra, rb);
+    __syncthreads();
+    for (int s = 0; s < stages; ++s) {
+      const int buf = s & 1;
+      const bool more = s + 1 < stages;
+      if (more) {
+        load_a(k_begin + (s + 1) * kBK, ra);
+        load_b(k_begin + (s + 1) * kBK, rb);
+      }
+      mfma_stage<CFG, kBK_major>(acc, aimg(buf), bimg(buf), lane, wm, wn);
+      if (more) store_stage(buf ^ 1, ra, rb);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogues ----
+  const int h = lane >> 5, l32 = lane & 31;
+  if constexpr (MODE == kWgrad) {
+    // dW[co][ci*T + t]: split-K partial sums by fp32 atomics (dW zeroed by the host)
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const int cj = n0 + wn * 32 * WN + j * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (row < M && cj < N) {
+            float* dst = out + static_cast<int64_t>(row) * N + cj;
+            if (atomic)
+              atomicAdd(dst, acc[i][j][r]);
+            else
+              *dst = acc[i][j][r];
+          }
+        }
+      }
+    return;
+  }
+
+  // C tile through LDS (reusing the operand images): coalesced row stores.
+  float* ct = lds;
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int cc = wn * 32 * WN + j * 32 + l32;
+        ct[row * C::kCStride + cc] = acc[i][j][r];
+      }
+  __syncthreads();
+
+  constexpr int kQuads = C::BN / 4;
+  const bool scatter = MODE == kBwdData && g.scatter;
+  const int hw = (MODE == kFwd || scatter) ? hw_out : hw_in;
+  const int ch_total = MODE == kFwd ? g.co_total : g.ci;
+  const int ch_off = MODE == kFwd ? g.co_off : 0;
+  const __amdgpu_buffer_rsrc_t mr = rsrc(x_mask, x_mask ? static_cast<int64_t>(g.n) * g.ci *
+                                                              hw_in * 4 : 0);
+  for (int idx = tid; idx < C::BM * kQuads; idx += kThreads) {
+    const int row = idx / kQuads, q = idx - row * kQuads;
+    const int m = m0 + row, j = n0 + 4 * q;
+    if (m >= M || j >= N) continue;
+    floatx4 v = *reinterpret_cast<const floatx4*>(ct + row * C::kCStride + 4 * q);
+    if (scatter) {
+      // strided 1x1 backward-data: output pixel (y, x) -> input (y*sh+oh, x*sw+ow)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int je = j + e;
+        if (je >= N) break;
+        const int n = je / hw_out, p = je - n * hw_out;
+        const int y = p / g.wo, x = p - y * g.wo;
+        const int yi = y * g.sh - g.ph + g.oh, xi = x * g.sw - g.pw + g.ow;
+        if (yi < 0 || yi >= g.h || xi < 0 || xi >= g.w) continue;
+        const int64_t off = ((static_cast<int64_t>(n) * g.ci + m) * g.h + yi) * g.w + xi;
+        float val = v[e];
+        if (g.relu && !(bload(mr, static_cast<uint32_t>(off * 4)) > 0.f)) val = 0.f;
+        if (atomic)
+          atomicAdd(out + off, val);
+        else
+          out[off] = accumulate ? out[off] + val : val;
+      }
+      continue;
+    }
+    const int n = j / hw, p = j - n * hw;
+    const int64_t base = (static_cast<int64_t>(n) * ch_total + ch_off + m) * hw + p;
+    if ((hw & 3) == 0 && j + 3 < N) {
+      if constexpr (MODE == kBwdData) {
+        if (g.relu) {
+          const floatx4 xv = bload4(mr, static_cast<uint32_t>(base * 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = xv[e] > 0.f ? v[e] : 0.f;
+        }
+      }
+      if (atomic) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(out + base + e, v[e]);
+      } else {
+        if (MODE == kBwdData && accumulate) v += *reinterpret_cast<const floatx4*>(out + base);
+        *reinterpret_cast<floatx4*>(out + base) = v;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int je = j + e;
+        if (je >= N) break;
+        const int ne = je / hw, pe = je - ne * hw;
+        const int64_t off = (static_cast<int64_t>(ne) * ch_total + ch_off + m) * hw + pe;
+        float val = v[e];
+        if constexpr (MODE == kBwdData) {
+          if (g.relu && !(bload(mr, static_cast<uint32_t>(off * 4)) > 0.f)) val = 0.f;
+        }
+        if (atomic)
+          atomicAdd(out + off, val);
+        else
+          out[off] = (MODE == kBwdData && accumulate) ? out[off] + val : val;
+      }
+    }
+  }
+
+  if constexpr (MODE == kFwd) {
+    if (part_mean == nullptr) return;
+    // BatchNorm statistics of this block's columns: two threads per row, two passes
+    // over the LDS tile (mean, then centred second moment), Chan-merged per row later.
+    const int cols = min(C::BN, N - n0);
+    for (int row = tid >> 1; row < C::BM; row += kThreads / 2) {
+      const int half = tid & 1;
+      const int c0 = half * (C::BN / 2), c1 = min(cols, c0 + C::BN / 2);
+      float s = 0.f;
+      for (int c = c0; c < c1; ++c) s += ct[row * C::kCStride + c];
+      const float s_all = s + __shfl_xor(s, 1);
+      const float mean = cols > 0 ? s_all / static_cast<float>(cols) : 0.f;
+      float m2 = 0.f;
+      for (int c = c0; c < c1; ++c) {
+        const float d = ct[row * C::kCStride + c] - mean;
+        m2 += d * d;
+      }
+      m2 += __shfl_xor(m2, 1);
+      const int m = m0 + row;
+      if (half == 0 && m < M) {
+        part_mean[static_cast<int64_t>(nb_i) * g.co_total + g.co_off + m] = mean;
+        part_m2[static_cast<int64_t>(nb_i) * g.co_total + g.co_off + m] = m2;
+      }
+    }
+  }
+}
+
+template <int MODE, int CFG>
+void launch_cfg(const float* a, const float* b, const float* xm, float* out, float* pmean,
+                float* pm2, const Geo& g, int M, int N, int K, int splits, bool atomic,
+                bool accumulate, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
+  using C = Cfg<CFG>;
+  const int mb = (M + C::BM - 1) / C::BM, nb = (N + C::BN - 1) / C::BN;
+  int k_chunk = (K + splits - 1) / splits;
+  k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
+  const int zs = (K + k_chunk - 1) / k_chunk;
+  const bool plain = g.taps == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 &&
+                     g.oh == 0 && g.ow == 0;
+  const dim3 grid(mb * nb, zs), block(C::kThreads);
+  if (plain)
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, true>), grid, block, 0, stream, a, b, xm,
+                       out, pmean, pm2, g, M, N, K, k_chunk, atomic ? 1 : 0, accumulate ? 1 : 0,
+                       a_bytes, b_bytes);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, false>), grid, block, 0, stream, a, b, xm,
+                       out, pmean, pm2, g, M, N, K, k_chunk, atomic ? 1 : 0, accumulate ? 1 : 0,
+                       a_bytes, b_bytes);
+}
+
+Geo make_geo(const ConvGemmGeo& cg) {
+  Geo g{cg.n, cg.ci, cg.h, cg.w, cg.co, cg.ho, cg.wo, cg.co_total, cg.co_off, cg.kh, cg.kw,
+        cg.kh * cg.kw, cg.sh, cg.sw, cg.ph, cg.pw, cg.oh, cg.ow, cg.relu ? 1 : 0, 0};
+  return g;
+}
+
+void gemm_dims(int mode, const Geo& g, int& M, int& N, int& K) {
+  if (mode == kFwd) {
+    M = g.co; N = g.n * g.ho * g.wo; K = g.ci * g.taps;
+  } else if (mode == kBwdData) {
+    M = g.ci; N = g.n * (g.scatter ? g.ho * g.wo : g.h * g.w); K = g.co * g.taps;
+  } else {
+    M = g.co; N = g.ci * g.taps; K = g.n * g.ho * g.wo;
+  }
+}
+
+bool scatter_bwd(const ConvGemmGeo& cg) {
+  return cg.kh == 1 && cg.kw == 1 && (cg.sh > 1 || cg.sw > 1);
+}
+
+}  // namespace
+
+int env_int(const char* name, int fallback) {
+  const char* v = std::getenv(name);
+  return v != nullptr && *v != 0 ? std::atoi(v) : fallback;
+}
+
+ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
+  Geo g = make_geo(cg);
+  g.scatter = mode == kBwdData && scatter_bwd(cg);
+  int M, N, K;
+  gemm_dims(mode, g, M, N, K);
+  ConvGemmPlan plan;
+  // Workgroups per launch to aim for: the 128 x 128 kernel runs 2 per CU (LDS), the
+  // 64 x 64 one 4; fewer leave SIMDs with a single wave that cannot hide its own
+  // global-load latency, so small grids split the reduction (>= 4 stages per split).
+  static const int fill_big = env_int("TGPIPE_CG_FILL_BIG", 200);
+  static const int fill_small = env_int("TGPIPE_CG_FILL_SMALL", 200);
+  static const int target_small = env_int("TGPIPE_CG_TARGET_SMALL", 400);
+  static const int target_wgrad = env_int("TGPIPE_CG_TARGET_WGRAD", 512);
+  const int64_t big = static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128);
+  const int64_t small = static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
+  const int64_t max_split = std::max<int64_t>(1, K / (4 * kBK));
+  if (mode == kWgrad) {
+    // few output tiles, long reduction: split until ~512 workgroups
+    plan.big = big >= 64;
+    const int64_t tiles = plan.big ? big : small;
+    plan.splits = static_cast<int>(
+        std::min<int64_t>((target_wgrad + tiles - 1) / tiles, max_split));
+  } else {
+    plan.big = big >= fill_big;
+    const int64_t tiles = plan.big ? big : small;
+    const int64_t fill = plan.big ? fill_big : fill_small;
+    plan.splits = tiles >= fill ? 1
+                  : static_cast<int>(std::min<int64_t>((target_small + tiles - 1) / tiles,
+                                                       max_split));
+  }
+  if (plan.splits < 1) plan.splits = 1;
+  plan.col_width = plan.big ? 128 : 64;
+  plan.col_blocks = static_cast<int>((N + plan.col_width - 1) / plan.col_width);
+  plan.scatter = g.scatter;
+  return plan;
+}
+
+void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_mask, float* out,
+                      float* part_mean, float* part_m2, const ConvGemmGeo& cg,
+                      const ConvGemmPlan& plan, bool accumulate, int64_t a_bytes,
+                      int64_t b_bytes, hipStream_t stream) {
+  Geo g = make_geo(cg);
+  g.scatter = plan.scatter ? 1 : 0;
+  int M, N, K;
+  gemm_dims(mode, g, M, N, K);
+  if (M == 0 || N == 0) return;
+  // split reductions accumulate with atomics into an output the host zeroed; the
+  // weight gradient always does (dW is zeroed)
+  const bool atomic = plan.splits > 1 || mode == kWgrad;
+  float* pm = plan.splits > 1 ? nullptr : part_mean;
+  float* pm2 = plan.splits > 1 ? nullptr : part_m2;
+  if (mode == kFwd) {
+    if (plan.big)
+      launch_cfg<kFwd, 1>(a, b, x_mask, out, pm, pm2, g, M, N, K, plan.splits, atomic,
+                             accumulate, a_bytes, b_bytes, stream);
+    else
+      launch_cfg<kFwd, 0>(a, b, x_mask, out, pm, pm2, g, M, N, K, plan.splits, atomic,
+                             accumulate, a_bytes, b_bytes, stream);
+  } else if (mode == kBwdData) {
+    if (plan.big)
+      launch_cfg<kBwdData, 1>(a, b, x_mask, out, nullptr, nullptr, g, M, N, K, plan.splits,
+                                 atomic, accumulate, a_bytes, b_bytes, stream);
+    else
+      launch_cfg<kBwdData, 0>(a, b, x_mask, out, nullptr, nullptr, g, M, N, K, plan.splits,
+                                 atomic, accumulate, a_bytes, b_bytes, stream);
+  } else {
+    if (plan.big)
+      launch_cfg<kWgrad, 1>(a, b, nullptr, out, nullptr, nullptr, g, M, N, K, plan.splits,
+                               atomic, accumulate, a_bytes, b_bytes, stream);
+    else
+      launch_cfg<kWgrad, 0>(a, b, nullptr, out, nullptr, nullptr, g, M, N, K, plan.splits,
+                               atomic, accumulate, a_bytes, b_bytes, stream);
+  }
+}
+
+}  // namespace tgpipe

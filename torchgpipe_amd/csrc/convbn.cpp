@@ -1,0 +1,305 @@
+// ATen bindings of the fused ReLU -> Conv -> BatchNorm(train) operation of AmoebaNet-D
+// cells (conv_gemm.hip, batchnorm.hip).  One call runs the whole forward or backward of
+// the operation, so the host issues one op per cell operation instead of ~10 ATen ops.
+//
+// A "part" is one convolution writing a channel slice of the concatenated output Z
+// (FactorizedReduce = two parts reading the same input, the second shifted by one
+// pixel); geometry per part: {kh, kw, sh, sw, ph, pw, oh, ow}.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+namespace tgpipe {
+namespace {
+
+constexpr int64_t kMaxBytes = 0x7ffffff0;  // buffer-resource offsets (conv_gemm.hip)
+
+hipStream_t cur_stream(const at::Tensor& t) {
+  return at::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_f32(const at::Tensor& t, const char* name, const at::Tensor& like) {
+  TORCH_CHECK(t.is_cuda() && t.device() == like.device(), name, " must be on ", like.device());
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.numel() * 4 <= kMaxBytes, name, " is too large (< 2 GiB per tensor)");
+}
+
+const float* opt_ptr(const c10::optional<at::Tensor>& t, const char* name, const at::Tensor& like,
+                     int64_t numel) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_f32(*t, name, like);
+  TORCH_CHECK(t->numel() == numel, name, " must have ", numel, " elements");
+  return t->data_ptr<float>();
+}
+
+struct Parts {
+  std::vector<ConvGemmGeo> geo;
+  int64_t co_total = 0, ho = 0, wo = 0;
+};
+
+Parts make_parts(const at::Tensor& x, at::TensorList weights, at::IntArrayRef geo, bool relu) {
+  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+  TORCH_CHECK(!weights.empty() && geo.size() == weights.size() * 8,
+              "need 8 geometry values {kh, kw, sh, sw, ph, pw, oh, ow} per weight");
+  Parts p;
+  const int64_t n = x.size(0), ci = x.size(1), h = x.size(2), w = x.size(3);
+  for (size_t i = 0; i < weights.size(); ++i) {
+    const auto& wt = weights[i];
+    check_f32(wt, "weight", x);
+    const int64_t* g = geo.data() + 8 * i;
+    const int64_t kh = g[0], kw = g[1], sh = g[2], sw = g[3], ph = g[4], pw = g[5];
+    TORCH_CHECK(kh == 1 || kw == 1, "one kernel dimension must be 1 (1x1, 1xk, kx1)");
+    TORCH_CHECK(wt.dim() == 4 && wt.size(1) == ci && wt.size(2) == kh && wt.size(3) == kw,
+                "weight must be [Co][Ci][kh][kw] matching x and the geometry");
+    TORCH_CHECK(sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && g[6] >= 0 && g[7] >= 0,
+                "bad stride / padding / offset");
+    TORCH_CHECK(kh * kw == 1 || (sh == 1 && sw == 1), "1xk / kx1 kernels need stride 1");
+    const int64_t ho = (h + 2 * ph - kh) / sh + 1, wo = (w + 2 * pw - kw) / sw + 1;
+    TORCH_CHECK(ho > 0 && wo > 0, "empty output");
+    if (i == 0) {
+      p.ho = ho;
+      p.wo = wo;
+    }
+    TORCH_CHECK(ho == p.ho && wo == p.wo, "all parts must produce the same output plane");
+    ConvGemmGeo c;
+    c.n = static_cast<int>(n);
+    c.ci = static_cast<int>(ci);
+    c.h = static_cast<int>(h);
+    c.w = static_cast<int>(w);
+    c.co = static_cast<int>(wt.size(0));
+    c.ho = static_cast<int>(ho);
+    c.wo = static_cast<int>(wo);
+    c.co_off = static_cast<int>(p.co_total);
+    c.kh = static_cast<int>(kh);
+    c.kw = static_cast<int>(kw);
+    c.sh = static_cast<int>(sh);
+    c.sw = static_cast<int>(sw);
+    c.ph = static_cast<int>(ph);
+    c.pw = static_cast<int>(pw);
+    c.oh = static_cast<int>(g[6]);
+    c.ow = static_cast<int>(g[7]);
+    c.relu = relu;
+    p.geo.push_back(c);
+    p.co_total += wt.size(0);
+  }
+  for (auto& c : p.geo) c.co_total = static_cast<int>(p.co_total);
+  TORCH_CHECK(n * p.co_total * p.ho * p.wo * 4 <= kMaxBytes, "output too large");
+  return p;
+}
+
+// Forward (training): returns {y, z, mean, invstd} with z the convolution output and
+// mean / invstd its batch statistics (saved for the backward).
+std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList weights,
+                                       at::IntArrayRef geo, bool relu,
+                                       const c10::optional<at::Tensor>& gamma,
+                                       const c10::optional<at::Tensor>& beta,
+                                       const c10::optional<at::Tensor>& running_mean,
+                                       const c10::optional<at::Tensor>& running_var,
+                                       const c10::optional<at::Tensor>& num_batches_tracked,
+                                       double momentum, double eps,
+                                       const c10::optional<at::Tensor>& add) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Parts p = make_parts(x, weights, geo, relu);
+  const int64_t n = x.size(0), c = p.co_total, s = p.ho * p.wo, cols = n * s;
+  const auto stream = cur_stream(x);
+  std::vector<ConvGemmPlan> plans;
+  bool split = false;
+  for (const auto& g : p.geo) {
+    plans.push_back(conv_gemm_plan(0, g));
+    split = split || plans.back().splits > 1;
+  }
+  // statistics partials: from the GEMM epilogue (all parts share one column tiling), or
+  // per (image, channel) from a separate pass when a reduction is split
+  for (const auto& pl : plans)
+    split = split || pl.col_width != plans[0].col_width;
+  const int width = split ? static_cast<int>(s) : plans[0].col_width;
+  const int blocks = split ? static_cast<int>(n) : plans[0].col_blocks;
+  auto z = split ? at::zeros({n, c, p.ho, p.wo}, x.options())
+                 : at::empty({n, c, p.ho, p.wo}, x.options());
+  auto part = at::empty({2, blocks, c}, x.options());
+  for (size_t i = 0; i < p.geo.size(); ++i) {
+    const auto wt = weights[i];
+    const ConvGemmPlan& pl = plans[i];
+    launch_conv_gemm(0, wt.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
+                     split ? nullptr : part[0].data_ptr<float>(),
+                     split ? nullptr : part[1].data_ptr<float>(), p.geo[i], pl, false,
+                     wt.numel() * 4, x.numel() * 4, stream);
+  }
+  if (split)
+    launch_bn_stats(z.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n,
+                    c, s, stream);
+  auto mean = at::empty({c}, x.options());
+  auto invstd = at::empty({c}, x.options());
+  const float* rm = opt_ptr(running_mean, "running_mean", x, c);
+  const float* rv = opt_ptr(running_var, "running_var", x, c);
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean and running_var go together");
+  int64_t* tracked = nullptr;
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->device() == x.device() &&
+                    num_batches_tracked->scalar_type() == at::kLong &&
+                    num_batches_tracked->numel() == 1,
+                "num_batches_tracked must be a 1-element int64 tensor on the input's device");
+    tracked = num_batches_tracked->data_ptr<int64_t>();
+  }
+  launch_bn_finalize(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, cols, c,
+                     static_cast<float>(eps), momentum, mean.data_ptr<float>(),
+                     invstd.data_ptr<float>(), const_cast<float*>(rm), const_cast<float*>(rv),
+                     tracked, stream);
+  const float* ga = opt_ptr(gamma, "gamma", x, c);
+  const float* be = opt_ptr(beta, "beta", x, c);
+  const float* ad = nullptr;
+  at::Tensor add_c;
+  if (add.has_value() && add->defined()) {
+    add_c = add->contiguous();
+    check_f32(add_c, "add", x);
+    TORCH_CHECK(add_c.sizes() == z.sizes(), "add must have the output's shape");
+    ad = add_c.data_ptr<float>();
+  }
+  auto y = at::empty_like(z);
+  launch_bn_apply(z.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), ga, be,
+                  ad, y.data_ptr<float>(), n, c, s, stream);
+  return {y, z, mean, invstd};
+}
+
+// Backward: returns {dx (undefined unless need_dx), dgamma, dbeta, dw_0, dw_1, ...}.
+std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
+                                        const at::Tensor& z, const at::Tensor& mean,
+                                        const at::Tensor& invstd,
+                                        const c10::optional<at::Tensor>& gamma,
+                                        at::TensorList weights, at::IntArrayRef geo, bool relu,
+                                        bool need_dx) {
+  auto x = x_in.contiguous();
+  auto dy = dy_in.contiguous();
+  check_f32(x, "x", x);
+  check_f32(dy, "dy", x);
+  check_f32(z, "z", x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Parts p = make_parts(x, weights, geo, relu);
+  const int64_t n = x.size(0), c = p.co_total, s = p.ho * p.wo;
+  TORCH_CHECK(dy.sizes() == z.sizes() && z.size(1) == c && z.size(2) == p.ho,
+              "dy / z do not match the operation's output");
+  check_f32(mean, "mean", x);
+  check_f32(invstd, "invstd", x);
+  TORCH_CHECK(mean.numel() == c && invstd.numel() == c, "statistics must have C elements");
+  const auto stream = cur_stream(x);
+  const float* ga = opt_ptr(gamma, "gamma", x, c);
+  auto sums = at::zeros({2, c}, x.options());
+  auto dz = at::empty_like(z);
+  auto dgamma = at::empty({c}, x.options());
+  auto dbeta = at::empty({c}, x.options());
+  launch_bn_backward(dy.data_ptr<float>(), z.data_ptr<float>(), mean.data_ptr<float>(),
+                     invstd.data_ptr<float>(), ga, sums.data_ptr<float>(), dz.data_ptr<float>(),
+                     dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), n, c, s, stream);
+  std::vector<at::Tensor> out;
+  at::Tensor dx;
+  if (need_dx) {
+    std::vector<ConvGemmPlan> plans;
+    bool zero = false;
+    for (const auto& g : p.geo) {
+      plans.push_back(conv_gemm_plan(1, g));
+      zero = zero || plans.back().splits > 1 || plans.back().scatter;
+    }
+    dx = zero ? at::zeros_like(x) : at::empty_like(x);
+    for (size_t i = 0; i < p.geo.size(); ++i) {
+      const auto& wt = weights[i];
+      launch_conv_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+                       dx.data_ptr<float>(), nullptr, nullptr, p.geo[i], plans[i],
+                       i > 0 || zero, wt.numel() * 4, dz.numel() * 4, stream);
+    }
+  }
+  out.push_back(dx);
+  out.push_back(dgamma);
+  out.push_back(dbeta);
+  for (size_t i = 0; i < p.geo.size(); ++i) {
+    auto dw = at::zeros_like(weights[i]);
+    launch_conv_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
+                     nullptr, nullptr, p.geo[i], conv_gemm_plan(2, p.geo[i]), true,
+                     dz.numel() * 4, x.numel() * 4, stream);
+    out.push_back(dw);
+  }
+  return out;
+}
+
+// Plain convolution (no BatchNorm) through the same kernels: forward / backward-data /
+// weight-gradient, e.g. U-Net's final 1x1 segmentation convolution.
+at::Tensor conv_gemm_forward(const at::Tensor& x_in, const at::Tensor& weight,
+                             at::IntArrayRef geo, bool relu) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Parts p = make_parts(x, {weight}, geo, relu);
+  const ConvGemmPlan plan = conv_gemm_plan(0, p.geo[0]);
+  auto z = plan.splits > 1 ? at::zeros({x.size(0), p.co_total, p.ho, p.wo}, x.options())
+                           : at::empty({x.size(0), p.co_total, p.ho, p.wo}, x.options());
+  launch_conv_gemm(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
+                   nullptr, nullptr, p.geo[0], plan, false, weight.numel() * 4, x.numel() * 4,
+                   cur_stream(x));
+  return z;
+}
+
+at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_in,
+                                   const at::Tensor& weight, at::IntArrayRef geo, bool relu) {
+  auto x = x_in.contiguous();
+  auto dz = dz_in.contiguous();
+  check_f32(x, "x", x);
+  check_f32(dz, "dz", x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Parts p = make_parts(x, {weight}, geo, relu);
+  TORCH_CHECK(dz.size(1) == p.co_total && dz.size(2) == p.ho && dz.size(3) == p.wo,
+              "dz does not match the convolution's output");
+  const ConvGemmPlan plan = conv_gemm_plan(1, p.geo[0]);
+  const bool zero = plan.splits > 1 || plan.scatter;
+  auto dx = zero ? at::zeros_like(x) : at::empty_like(x);
+  launch_conv_gemm(1, weight.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+                   dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], plan, false,
+                   weight.numel() * 4, dz.numel() * 4, cur_stream(x));
+  return dx;
+}
+
+at::Tensor conv_gemm_backward_weight(const at::Tensor& dz_in, const at::Tensor& x_in,
+                                     const at::Tensor& weight, at::IntArrayRef geo, bool relu) {
+  auto x = x_in.contiguous();
+  auto dz = dz_in.contiguous();
+  check_f32(x, "x", x);
+  check_f32(dz, "dz", x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Parts p = make_parts(x, {weight}, geo, relu);
+  TORCH_CHECK(dz.size(1) == p.co_total && dz.size(2) == p.ho && dz.size(3) == p.wo,
+              "dz does not match the convolution's output");
+  auto dw = at::zeros_like(weight);
+  launch_conv_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
+                   nullptr, nullptr, p.geo[0], conv_gemm_plan(2, p.geo[0]), true, dz.numel() * 4,
+                   x.numel() * 4, cur_stream(x));
+  return dw;
+}
+
+}  // namespace
+}  // namespace tgpipe
+
+TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
+  m.def("convbn_forward(Tensor x, Tensor[] weights, int[] geo, bool relu, Tensor? gamma, "
+        "Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
+        "Tensor(c!)? num_batches_tracked, float momentum, float eps, Tensor? add) -> Tensor[]");
+  m.def("convbn_backward(Tensor dy, Tensor x, Tensor z, Tensor mean, Tensor invstd, "
+        "Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx) -> Tensor[]");
+  m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
+  m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu) "
+        "-> Tensor");
+  m.def("conv_gemm_backward_weight(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu) "
+        "-> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
+  m.impl("convbn_forward", &tgpipe::convbn_forward);
+  m.impl("convbn_backward", &tgpipe::convbn_backward);
+  m.impl("conv_gemm_forward", &tgpipe::conv_gemm_forward);
+  m.impl("conv_gemm_backward_data", &tgpipe::conv_gemm_backward_data);
+  m.impl("conv_gemm_backward_weight", &tgpipe::conv_gemm_backward_weight);
+}

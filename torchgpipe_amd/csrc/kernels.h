@@ -113,4 +113,61 @@ void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, in
                        int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
                        hipStream_t stream);
 
+// ---- AmoebaNet cell operations (conv_gemm.hip, batchnorm.hip) -----------------------------
+
+// Implicit-GEMM convolution with one of kh, kw equal to 1 (1x1, 1xk, kx1), NCHW fp32.
+struct ConvGemmGeo {
+  int n, ci, h, w;       // input
+  int co, ho, wo;        // output of this convolution
+  int co_total, co_off;  // its channel slice inside the (concatenated) output Z
+  int kh, kw, sh, sw, ph, pw;
+  int oh, ow;            // extra input offset (FactorizedReduce's shifted branch)
+  bool relu;             // ReLU on the input (its mask in backward-data)
+};
+// mode 0: forward  Z[:, co_off:co_off+co] = conv(relu(X)); a = W[co][ci*kh*kw], b = X;
+//         part_mean / part_m2 ([col_blocks][co_total]): per column block mean and centred
+//         second moment of each output channel (BatchNorm statistics) -- only when the
+//         plan does not split the reduction (splits > 1: Z must be zeroed, statistics by
+//         launch_bn_stats).
+// mode 1: backward-data  dX (+)= relu'(X) * conv^T(dZ); a = W (untransposed), b = dZ,
+//         x_mask = X (relu mask); `accumulate` adds to dX (several convolutions of one X).
+//         dX must be zeroed when the plan splits or scatters.
+// mode 2: weight gradient  dW[co][ci*kh*kw] += dZ * relu(X); a = dZ, b = X; dW zeroed.
+// Supported: 1x1 with any stride / offset, 1xk / kx1 with stride 1.
+struct ConvGemmPlan {
+  bool big = true;       // 128 x 128 tiles (else 64 x 64)
+  int splits = 1;        // reduction splits (grid.y), > 1: fp32 atomics into zeroed output
+  int col_width = 128;   // forward: columns per statistics block
+  int col_blocks = 0;    // forward: statistics blocks
+  bool scatter = false;  // backward-data of a strided 1x1 over output pixels
+};
+ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& g);
+void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_mask, float* out,
+                      float* part_mean, float* part_m2, const ConvGemmGeo& g,
+                      const ConvGemmPlan& plan, bool accumulate, int64_t a_bytes,
+                      int64_t b_bytes, hipStream_t stream);
+
+// (mean, M2) partials of z[n][c][s] per (image, channel): part_*[n][c] (width s).
+void launch_bn_stats(const float* z, float* part_mean, float* part_m2, int64_t n, int64_t c,
+                     int64_t s, hipStream_t stream);
+
+// BatchNorm (training) around the convolutions.  Statistics partials of `blocks` column
+// blocks of `width` columns (`total` columns per channel) are merged with Chan's formula
+// in fp64 into mean / invstd; the running statistics get the EMA with factor `momentum`
+// (unbiased variance) when running_mean is non-null, and `tracked` (BatchNorm's
+// num_batches_tracked, may be null) is incremented in the same launch.
+void launch_bn_finalize(const float* part_mean, const float* part_m2, int blocks, int width,
+                        int64_t total, int64_t c, float eps, double momentum, float* mean,
+                        float* invstd, float* running_mean, float* running_var, int64_t* tracked,
+                        hipStream_t stream);
+// y[n][c][p] = (z - mean) * invstd * gamma + beta (+ add[n][c][p]), planes of s pixels.
+void launch_bn_apply(const float* z, const float* mean, const float* invstd, const float* gamma,
+                     const float* beta, const float* add, float* y, int64_t n, int64_t c,
+                     int64_t s, hipStream_t stream);
+// Backward: sums[2][C] (zeroed) += (sum dy, sum dy*(z-mean)); then
+// dz = gamma*invstd*(dy - sum_dy/M - (z-mean)*invstd^2*sum_dyz/M), dgamma, dbeta.
+void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
+                        const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
+                        int64_t n, int64_t c, int64_t s, hipStream_t stream);
+
 }  // namespace tgpipe

@@ -11,12 +11,22 @@ tables (``benchmarks/amoebanetd-speed/main.py:35-96``) apply unchanged.
 Kept quirks of the reference for benchmark fidelity: the normal-cell concat is
 TensorFlow's ``[0, 3, 4, 6]``, and ``max_pool_3x3`` is an average pool
 (``operations.py:57-59`` in the reference).
+
+MI355X path: every ReLU → Conv(1×1 / 1×7 / 7×1) → BatchNorm triplet is an
+``ops.convbn`` fused op (implicit-GEMM fp32 MFMA kernel with the ReLU on its
+operand load and the BatchNorm statistics in its epilogue), FactorizedReduce is
+one fused op over both shifted branches, and the ``left + right`` sum of each
+cell node is folded into the right branch's normalisation pass.  The modules
+keep the reference's children, so parameters and state-dict keys are the same
+as the plain model (``fused=False``), which also serves as the numerics oracle.
 """
 from collections import OrderedDict
-from typing import Callable, Iterator, List, Tuple, Union
+from typing import Callable, Iterator, List, Optional, Tuple, Union
 
 import torch
 from torch import Tensor, nn
+
+from torchgpipe_amd.ops.convbn import FusedChain, ReLUConvBN, fusable, relu_conv_bn
 
 __all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS']
 
@@ -30,14 +40,22 @@ class Operation(nn.Module):
     def __repr__(self) -> str:
         return f'Operation[{self.name}]'
 
-    def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
-        return self.module(x)
+    def forward(self, x: Tensor, add: Optional[Tensor] = None) -> Tensor:  # type: ignore[override]
+        """``module(x)``, plus ``add`` (folded into a fused op's last pass when it can)."""
+        if add is not None and isinstance(self.module, (FusedChain, FactorizedReduce)):
+            return self.module(x, add)
+        out = self.module(x)
+        return out if add is None else out + add
 
 
-def relu_conv_bn(cin: int, cout: int, kernel=1, stride=1, padding=0) -> nn.Sequential:  # type: ignore[no-untyped-def]
-    return nn.Sequential(nn.ReLU(inplace=False),
-                         nn.Conv2d(cin, cout, kernel, stride, padding, bias=False),
-                         nn.BatchNorm2d(cout))
+def conv_bn_chain(*modules: nn.Module) -> nn.Sequential:
+    return FusedChain(*modules)
+
+
+def _relu_conv_bn(cin: int, cout: int, kernel=1, stride=1, padding=0) -> nn.Sequential:  # type: ignore[no-untyped-def]
+    return ReLUConvBN(nn.ReLU(inplace=False),
+                      nn.Conv2d(cin, cout, kernel, stride, padding, bias=False),
+                      nn.BatchNorm2d(cout))
 
 
 class FactorizedReduce(nn.Module):
@@ -51,10 +69,15 @@ class FactorizedReduce(nn.Module):
         self.conv2 = nn.Conv2d(cin, cout // 2, kernel_size=1, stride=2, bias=False)
         self.bn = nn.BatchNorm2d(cout)
 
-    def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
+    def forward(self, x: Tensor, add: Optional[Tensor] = None) -> Tensor:  # type: ignore[override]
+        if fusable(x, [self.conv1, self.conv2], self.bn):
+            # both strided branches in one op: the second reads x shifted by one pixel
+            # (the zero pad of the reference falls out of the bounds check)
+            return relu_conv_bn(x, [(self.conv1, 0), (self.conv2, 1)], self.bn, add=add)
         x = self.relu(x)
         shifted = self.pad(x[:, :, 1:, 1:])
-        return self.bn(torch.cat([self.conv1(x), self.conv2(shifted)], dim=1))
+        out = self.bn(torch.cat([self.conv1(x), self.conv2(shifted)], dim=1))
+        return out if add is None else out + add
 
 
 def op_none(c: int, stride: int) -> Operation:
@@ -78,9 +101,10 @@ def op_max_pool_2x2(c: int, stride: int) -> Operation:
 
 def _bottleneck(c: int, middle: List[nn.Module]) -> nn.Sequential:
     q = c // 4
-    return nn.Sequential(nn.ReLU(inplace=False), nn.Conv2d(c, q, 1, bias=False), nn.BatchNorm2d(q),
-                         *middle,
-                         nn.ReLU(inplace=False), nn.Conv2d(q, c, 1, bias=False), nn.BatchNorm2d(c))
+    return conv_bn_chain(nn.ReLU(inplace=False), nn.Conv2d(c, q, 1, bias=False),
+                         nn.BatchNorm2d(q), *middle,
+                         nn.ReLU(inplace=False), nn.Conv2d(q, c, 1, bias=False),
+                         nn.BatchNorm2d(c))
 
 
 def op_conv_1x7_7x1(c: int, stride: int) -> Operation:
@@ -97,9 +121,7 @@ def op_conv_1x7_7x1(c: int, stride: int) -> Operation:
 
 
 def op_conv_1x1(c: int, stride: int) -> Operation:
-    return Operation('conv_1x1', nn.Sequential(nn.ReLU(inplace=False),
-                                               nn.Conv2d(c, c, 1, stride=stride, bias=False),
-                                               nn.BatchNorm2d(c)))
+    return Operation('conv_1x1', _relu_conv_bn(c, c, 1, stride))
 
 
 def op_conv_3x3(c: int, stride: int) -> Operation:
@@ -159,12 +181,12 @@ class Cell(nn.Module):
     def __init__(self, c_prev_prev: int, c_prev: int, c: int, reduction: bool,
                  reduction_prev: bool) -> None:
         super().__init__()
-        self.reduce1 = relu_conv_bn(c_prev, c)
+        self.reduce1 = _relu_conv_bn(c_prev, c)
         self.reduce2: nn.Module = nn.Identity()
         if reduction_prev:
             self.reduce2 = FactorizedReduce(c_prev_prev, c)
         elif c_prev_prev != c:
-            self.reduce2 = relu_conv_bn(c_prev_prev, c)
+            self.reduce2 = _relu_conv_bn(c_prev_prev, c)
 
         genotype = REDUCTION_OPERATIONS if reduction else NORMAL_OPERATIONS
         self.concat = REDUCTION_CONCAT if reduction else NORMAL_CONCAT
@@ -183,8 +205,7 @@ class Cell(nn.Module):
         ops = list(self.operations)
         for k in range(0, len(ops), 2):
             left = ops[k](nodes[self.indices[k]])
-            right = ops[k + 1](nodes[self.indices[k + 1]])
-            nodes.append(left + right)
+            nodes.append(ops[k + 1](nodes[self.indices[k + 1]], add=left))
         return torch.cat([nodes[i] for i in self.concat], dim=1), skip
 
 

@@ -1,0 +1,169 @@
+"""Fused ReLU → Conv → BatchNorm for AmoebaNet-D cells on the CDNA4 matrix cores.
+
+Every convolution of AmoebaNet-D (reference ``benchmarks/models/amoebanet/
+operations.py:9-114``) is preceded by a ReLU and followed by a BatchNorm, and
+except for the stem and the stride-2 3×3 of the reduction cells they are 1×1,
+1×7 or 7×1.  :func:`relu_conv_bn` runs such a triplet as one native op
+(``csrc/conv_gemm.hip``, ``csrc/batchnorm.hip``, ``csrc/convbn.cpp``):
+
+* forward: an implicit-GEMM ``v_mfma_f32_32x32x2_f32`` kernel reads ``relu(x)``
+  straight from the input (no ReLU output tensor), writes the convolution output
+  ``z`` and, from its epilogue, per-block (mean, M2) BatchNorm partials; a
+  finalize kernel merges them (Chan, fp64), updates the running statistics and
+  ``num_batches_tracked``; one elementwise pass normalises and may add the other
+  branch of the AmoebaNet node (``left + right``);
+* backward: BatchNorm reduction + ``dz`` pass, then the backward-data GEMM with
+  the ReLU mask in its epilogue and the split-K weight-gradient GEMM.
+
+:class:`ReLUConvBN` / :class:`FusedChain` are ``nn.Sequential`` subclasses with
+the reference's children (``ReLU``, ``Conv2d``, ``BatchNorm2d`` …), so the
+state-dict keys are unchanged; they fall back to the eager modules on CPU, in
+eval mode, for non-fp32 tensors or unsupported convolutions.
+"""
+import contextlib
+import os
+from typing import Iterator, List, Optional, Sequence, Tuple
+
+import torch
+from torch import Tensor, nn
+import torch.nn.functional as F
+
+from torchgpipe_amd.ops import _ext
+
+__all__ = ['relu_conv_bn', 'ReLUConvBN', 'FusedChain', 'conv_supported', 'fused_triplets',
+           'fusable', 'disabled']
+
+# TGPIPE_FUSED_CONVBN=0 runs the eager ReLU / Conv2d / BatchNorm2d modules instead.
+_ENABLED = os.environ.get('TGPIPE_FUSED_CONVBN', '1') != '0'
+
+
+@contextlib.contextmanager
+def disabled() -> Iterator[None]:
+    """Run the eager modules inside this block (numerics oracle, A/B timing)."""
+    global _ENABLED
+    prev, _ENABLED = _ENABLED, False
+    try:
+        yield
+    finally:
+        _ENABLED = prev
+
+
+Geo = Tuple[int, int, int, int, int, int, int, int]  # kh, kw, sh, sw, ph, pw, oh, ow
+
+
+def conv_supported(conv: nn.Conv2d) -> bool:
+    """1×1 / 1×k / k×1, no bias, no groups / dilation, zero padding."""
+    kh, kw = conv.kernel_size
+    return ((kh == 1 or kw == 1) and conv.bias is None and conv.groups == 1
+            and tuple(conv.dilation) == (1, 1) and conv.padding_mode == 'zeros'
+            and isinstance(conv.padding, tuple))
+
+
+def _geo(conv: nn.Conv2d, offset: int = 0) -> List[int]:
+    kh, kw = conv.kernel_size
+    sh, sw = conv.stride
+    ph, pw = conv.padding  # type: ignore[misc]
+    return [kh, kw, sh, sw, ph, pw, offset, offset]
+
+
+def _bn_ok(bn: nn.Module, x: Tensor) -> bool:
+    return (isinstance(bn, nn.BatchNorm2d) and bn.training and x.is_cuda
+            and x.dtype == torch.float32 and x.dim() == 4
+            and (bn.momentum is not None or not bn.track_running_stats))
+
+
+class _ConvBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: Tensor, add: Optional[Tensor], gamma: Optional[Tensor],  # type: ignore[override]
+                beta: Optional[Tensor], bn: nn.BatchNorm2d, geo: List[int], relu: bool,
+                *weights: Tensor) -> Tensor:
+        ops = _ext.require(x)
+        track = bn.track_running_stats and bn.running_mean is not None
+        y, z, mean, invstd = ops.convbn_forward(
+            x, list(weights), geo, relu, gamma, beta,
+            bn.running_mean if track else None, bn.running_var if track else None,
+            bn.num_batches_tracked if track else None,
+            float(bn.momentum) if bn.momentum is not None else 0.0, float(bn.eps), add)
+        ctx.save_for_backward(x, z, mean, invstd, gamma, *weights)
+        ctx.geo = geo
+        ctx.relu = relu
+        ctx.has_add = add is not None
+        ctx.n_weights = len(weights)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy: Tensor):  # type: ignore[override]
+        x, z, mean, invstd, gamma, *weights = ctx.saved_tensors
+        need_dx = ctx.needs_input_grad[0]
+        dx, dgamma, dbeta, *dws = _ext.require(dy).convbn_backward(
+            dy, x, z, mean, invstd, gamma, weights, ctx.geo, ctx.relu, need_dx)
+        return (dx if need_dx else None, dy if ctx.has_add else None,
+                dgamma if ctx.needs_input_grad[2] else None,
+                dbeta if ctx.needs_input_grad[3] else None, None, None, None, *dws)
+
+
+def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.BatchNorm2d,
+                 relu: bool = True, add: Optional[Tensor] = None) -> Tensor:
+    """``bn(cat([conv(relu(x) shifted by offset) for conv, offset in convs]))`` (+ ``add``).
+
+    ``convs`` are ``(conv, offset)`` pairs whose outputs are concatenated on channels
+    (one pair for ReLU-Conv-BN, two for FactorizedReduce: offsets 0 and 1).  Runs the
+    fused HIP op when :func:`fusable`; callers check that first.
+    """
+    geo: List[int] = []
+    for conv, offset in convs:
+        geo += _geo(conv, offset)
+    weights = [conv.weight for conv, _ in convs]
+    return _ConvBN.apply(x, add, bn.weight, bn.bias, bn, geo, relu, *weights)
+
+
+def fusable(x: Tensor, convs: Sequence[nn.Conv2d], bn: nn.Module) -> bool:
+    return (_ENABLED and _bn_ok(bn, x) and all(conv_supported(c) for c in convs)
+            and _ext.available()
+            and all(c.weight.dtype == torch.float32 and c.weight.is_cuda for c in convs))
+
+
+def fused_triplets(seq: nn.Sequential) -> Optional[List[Tuple[bool, nn.Conv2d, nn.BatchNorm2d]]]:
+    """Split ``seq`` into (relu?, conv, bn) triplets, or ``None`` if it is not such a chain."""
+    mods = list(seq.children())
+    out: List[Tuple[bool, nn.Conv2d, nn.BatchNorm2d]] = []
+    i = 0
+    while i < len(mods):
+        relu = isinstance(mods[i], nn.ReLU)
+        j = i + 1 if relu else i
+        if j + 1 >= len(mods) or not isinstance(mods[j], nn.Conv2d) or \
+                not isinstance(mods[j + 1], nn.BatchNorm2d):
+            return None
+        out.append((relu, mods[j], mods[j + 1]))
+        i = j + 2
+    return out
+
+
+class FusedChain(nn.Sequential):
+    """A chain of (ReLU, Conv2d, BatchNorm2d) triplets run as fused ops.
+
+    Children are the plain modules (the reference's state-dict keys); any triplet
+    whose convolution the GEMM kernels do not cover (e.g. the stride-2 3×3 of a
+    reduction cell's bottleneck) runs eagerly.  ``add`` is folded into the last
+    triplet's normalisation pass.
+    """
+
+    def forward(self, x: Tensor, add: Optional[Tensor] = None) -> Tensor:  # type: ignore[override]
+        triplets = fused_triplets(self)
+        if triplets is None:
+            out = super().forward(x)
+            return out if add is None else out + add
+        last = len(triplets) - 1
+        for k, (relu, conv, bn) in enumerate(triplets):
+            extra = add if k == last else None
+            if fusable(x, [conv], bn):
+                x = relu_conv_bn(x, [(conv, 0)], bn, relu=relu, add=extra)
+            else:
+                x = bn(conv(F.relu(x) if relu else x))
+                if extra is not None:
+                    x = x + extra
+        return x
+
+
+class ReLUConvBN(FusedChain):
+    """``nn.Sequential(ReLU, Conv2d, BatchNorm2d)`` running as one fused op."""
