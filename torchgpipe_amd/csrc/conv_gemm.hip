@@ -20,9 +20,9 @@
 // reduction steps per double-buffered LDS stage: one barrier and 32 / 16 MFMAs per wave
 // per stage, with the next stage's global loads in flight meanwhile (a two-stage-ahead
 // variant with two register sets measured 3 % slower: profiles/convbn_bench.json notes).
-// Grids that would not fill the 256 CUs split the reduction (grid.y) and accumulate
-// with hardware fp32 atomics into a zeroed output; the forward then leaves the
-// BatchNorm statistics to a separate pass (bn_stats, batchnorm.hip).
+// Grids that would not fill the 256 CUs split the reduction (grid.y): each split stores
+// its partial tile into a workspace slice and split_reduce sums them (no atomics); the
+// forward then leaves the BatchNorm statistics to a separate pass (bn_stats).
 //
 // LDS images:
 //   K-major operand (k contiguous in HBM: weights, dZ in weight-grad, X in weight-grad)
@@ -37,6 +37,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #include "kernels.h"
 
@@ -97,7 +98,9 @@ struct Cfg {
   static constexpr int kBImgK = kBK * BN;         // K-major image
   static constexpr int kBStrideN = BN + 32;       // N-major row stride
   static constexpr int kBImgN = kBK * kBStrideN;  // N-major image
-  static constexpr int kCStride = BN + 4;         // epilogue C tile row stride
+  // epilogue C tile row stride: rows 4 apart (the two halves of an MFMA result
+  // register) land 32 banks apart
+  static constexpr int kCStride = BN + 8;
   static constexpr int kOpFloats(bool k_major) {
     return 2 * kAImg + 2 * (k_major ? kBImgK : kBImgN);
   }
@@ -114,14 +117,18 @@ struct Cfg {
 
 // ---- operand staging -----------------------------------------------------------------------
 // K-major operand: quad index i of thread t -> row r = (t >> 3) + (THREADS / 8) * i,
-// k quad (t & 7).
+// k quad q = t & 7, stored at slot [q][r ^ 2q]: the 16 lanes of a ds_write_b128 pass
+// (2 rows x 8 quads) hit 16 distinct 16-byte bank groups, and the 32 consecutive rows an
+// MFMA fragment read covers stay a permutation of one aligned 32-row block.
+__device__ __forceinline__ int kswz(int row, int q) { return row ^ (2 * q); }
+
 template <int ROWS, int Q, int THREADS>
 __device__ __forceinline__ void store_kmajor(float* img, const floatx4 (&v)[Q], int tid) {
   const int q = tid & 7;
 #pragma unroll
   for (int i = 0; i < Q; ++i) {
     const int row = (tid >> 3) + (THREADS / 8) * i;
-    *reinterpret_cast<floatx4*>(img + (q * ROWS + row) * 4) =
+    *reinterpret_cast<floatx4*>(img + (q * ROWS + kswz(row, q)) * 4) =
         floatx4{v[i][0], v[i][2], v[i][1], v[i][3]};
   }
 }
@@ -154,12 +161,12 @@ __device__ __forceinline__ void mfma_stage(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG
 #pragma unroll
     for (int i = 0; i < WM; ++i)
       a[i] = *reinterpret_cast<const floatx2*>(
-          aimg + (g * C::BM + wm * 32 * WM + i * 32 + l32) * 4 + 2 * h);
+          aimg + (g * C::BM + kswz(wm * 32 * WM + i * 32 + l32, g)) * 4 + 2 * h);
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
       if constexpr (kBKMajor) {
         b[j] = *reinterpret_cast<const floatx2*>(
-            bimg + (g * C::BN + wn * 32 * WN + j * 32 + l32) * 4 + 2 * h);
+            bimg + (g * C::BN + kswz(wn * 32 * WN + j * 32 + l32, g)) * 4 + 2 * h);
       } else {
         const int col = wn * 32 * WN + j * 32 + l32;
         b[j] = floatx2{bimg[(4 * g + h) * C::kBStrideN + col],
@@ -226,7 +233,7 @@ template <int MODE, int CFG, bool kPlain>
 __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
     const float* __restrict__ a_src, const float* __restrict__ b_src,
     const float* __restrict__ x_mask, float* __restrict__ out, float* __restrict__ part_mean,
-    float* __restrict__ part_m2, Geo g, int M, int N, int K, int k_chunk, int atomic,
+    float* __restrict__ part_m2, Geo g, int M, int N, int K, int k_chunk, int64_t split_stride,
     int accumulate, int64_t a_bytes, int64_t b_bytes) {
   using C = Cfg<CFG>;
   constexpr int WM = C::TM, WN = C::TN, kThreads = C::kThreads;
@@ -455,9 +462,12 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
   }
 
   // ---- epilogues ----
+  // split reductions: each split writes its own slice of a workspace (reduced by
+  // split_reduce_kernel), plain stores, no atomics
+  out += blockIdx.y * split_stride;
   const int h = lane >> 5, l32 = lane & 31;
   if constexpr (MODE == kWgrad) {
-    // dW[co][ci*T + t]: split-K partial sums by fp32 atomics (dW zeroed by the host)
+    // dW[co][ci*T + t] (or this split's workspace slice)
 #pragma unroll
     for (int i = 0; i < WM; ++i)
 #pragma unroll
@@ -466,13 +476,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (row < M && cj < N) {
-            float* dst = out + static_cast<int64_t>(row) * N + cj;
-            if (atomic)
-              atomicAdd(dst, acc[i][j][r]);
-            else
-              *dst = acc[i][j][r];
-          }
+          if (row < M && cj < N) out[static_cast<int64_t>(row) * N + cj] = acc[i][j][r];
         }
       }
     return;
@@ -517,10 +521,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
         const int64_t off = ((static_cast<int64_t>(n) * g.ci + m) * g.h + yi) * g.w + xi;
         float val = v[e];
         if (g.relu && !(bload(mr, static_cast<uint32_t>(off * 4)) > 0.f)) val = 0.f;
-        if (atomic)
-          atomicAdd(out + off, val);
-        else
-          out[off] = accumulate ? out[off] + val : val;
+        out[off] = accumulate ? out[off] + val : val;
       }
       continue;
     }
@@ -534,13 +535,8 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
           for (int e = 0; e < 4; ++e) v[e] = xv[e] > 0.f ? v[e] : 0.f;
         }
       }
-      if (atomic) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(out + base + e, v[e]);
-      } else {
-        if (MODE == kBwdData && accumulate) v += *reinterpret_cast<const floatx4*>(out + base);
-        *reinterpret_cast<floatx4*>(out + base) = v;
-      }
+      if (MODE == kBwdData && accumulate) v += *reinterpret_cast<const floatx4*>(out + base);
+      *reinterpret_cast<floatx4*>(out + base) = v;
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -552,34 +548,33 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
         if constexpr (MODE == kBwdData) {
           if (g.relu && !(bload(mr, static_cast<uint32_t>(off * 4)) > 0.f)) val = 0.f;
         }
-        if (atomic)
-          atomicAdd(out + off, val);
-        else
-          out[off] = (MODE == kBwdData && accumulate) ? out[off] + val : val;
+        out[off] = (MODE == kBwdData && accumulate) ? out[off] + val : val;
       }
     }
   }
 
   if constexpr (MODE == kFwd) {
     if (part_mean == nullptr) return;
-    // BatchNorm statistics of this block's columns: two threads per row, two passes
-    // over the LDS tile (mean, then centred second moment), Chan-merged per row later.
+    // BatchNorm statistics of this block's columns: one wave per row at a time, lanes
+    // across columns (conflict-free LDS reads), shuffle-reduced mean then centred M2.
     const int cols = min(C::BN, N - n0);
-    for (int row = tid >> 1; row < C::BM; row += kThreads / 2) {
-      const int half = tid & 1;
-      const int c0 = half * (C::BN / 2), c1 = min(cols, c0 + C::BN / 2);
+    constexpr int kWaves = kThreads / 64;
+    for (int row = wave; row < C::BM; row += kWaves) {
+      const float* r = ct + row * C::kCStride;
       float s = 0.f;
-      for (int c = c0; c < c1; ++c) s += ct[row * C::kCStride + c];
-      const float s_all = s + __shfl_xor(s, 1);
-      const float mean = cols > 0 ? s_all / static_cast<float>(cols) : 0.f;
+      for (int c = lane; c < cols; c += 64) s += r[c];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+      const float mean = s / static_cast<float>(cols);
       float m2 = 0.f;
-      for (int c = c0; c < c1; ++c) {
-        const float d = ct[row * C::kCStride + c] - mean;
+      for (int c = lane; c < cols; c += 64) {
+        const float d = r[c] - mean;
         m2 += d * d;
       }
-      m2 += __shfl_xor(m2, 1);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m2 += __shfl_xor(m2, off);
       const int m = m0 + row;
-      if (half == 0 && m < M) {
+      if (lane == 0 && m < M) {
         part_mean[static_cast<int64_t>(nb_i) * g.co_total + g.co_off + m] = mean;
         part_m2[static_cast<int64_t>(nb_i) * g.co_total + g.co_off + m] = m2;
       }
@@ -589,7 +584,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
 
 template <int MODE, int CFG>
 void launch_cfg(const float* a, const float* b, const float* xm, float* out, float* pmean,
-                float* pm2, const Geo& g, int M, int N, int K, int splits, bool atomic,
+                float* pm2, const Geo& g, int M, int N, int K, int splits, int64_t split_stride,
                 bool accumulate, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
   using C = Cfg<CFG>;
   const int mb = (M + C::BM - 1) / C::BM, nb = (N + C::BN - 1) / C::BN;
@@ -601,12 +596,68 @@ void launch_cfg(const float* a, const float* b, const float* xm, float* out, flo
   const dim3 grid(mb * nb, zs), block(C::kThreads);
   if (plain)
     hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, true>), grid, block, 0, stream, a, b, xm,
-                       out, pmean, pm2, g, M, N, K, k_chunk, atomic ? 1 : 0, accumulate ? 1 : 0,
+                       out, pmean, pm2, g, M, N, K, k_chunk, split_stride, accumulate ? 1 : 0,
                        a_bytes, b_bytes);
   else
     hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, false>), grid, block, 0, stream, a, b, xm,
-                       out, pmean, pm2, g, M, N, K, k_chunk, atomic ? 1 : 0, accumulate ? 1 : 0,
+                       out, pmean, pm2, g, M, N, K, k_chunk, split_stride, accumulate ? 1 : 0,
                        a_bytes, b_bytes);
+}
+
+// Sum of the split partials: ws[s][plane][c][hw] -> out[plane][c_off + c][hw] (c_total
+// channels), times the ReLU mask (x_mask, indexed like out) when given, plus the
+// previous contents of out when accumulating.
+template <bool kVec>
+__global__ __launch_bounds__(256) void split_reduce_kernel(
+    const float* __restrict__ ws, int splits, int64_t stride, float* __restrict__ out,
+    const float* __restrict__ mask, int accumulate, int64_t total, int64_t c, int64_t hw,
+    int64_t c_total, int64_t c_off) {
+  const int64_t step = static_cast<int64_t>(gridDim.x) * 256;
+  if constexpr (kVec) {
+    for (int64_t q = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; q < total / 4;
+         q += step) {
+      const int64_t i = 4 * q;
+      const int64_t pl = i / (c * hw), r = i - pl * c * hw;
+      const int64_t o = (pl * c_total + c_off) * hw + r;
+      floatx4 v = reinterpret_cast<const floatx4*>(ws)[q];
+      for (int s = 1; s < splits; ++s) v += reinterpret_cast<const floatx4*>(ws + s * stride)[q];
+      if (mask) {
+        const floatx4 m = *reinterpret_cast<const floatx4*>(mask + o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
+      }
+      if (accumulate) v += *reinterpret_cast<const floatx4*>(out + o);
+      *reinterpret_cast<floatx4*>(out + o) = v;
+    }
+  } else {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total; i += step) {
+      const int64_t pl = i / (c * hw), r = i - pl * c * hw;
+      const int64_t o = (pl * c_total + c_off) * hw + r;
+      float v = ws[i];
+      for (int s = 1; s < splits; ++s) v += ws[s * stride + i];
+      if (mask && !(mask[o] > 0.f)) v = 0.f;
+      if (accumulate) v += out[o];
+      out[o] = v;
+    }
+  }
+}
+
+void launch_split_reduce(const float* ws, int splits, int64_t stride, float* out,
+                         const float* mask, bool accumulate, int64_t planes, int64_t c,
+                         int64_t hw, int64_t c_total, int64_t c_off, hipStream_t stream) {
+  const int64_t total = planes * c * hw;
+  if (total == 0) return;
+  const bool vec = (hw & 3) == 0 && (stride & 3) == 0;
+  int64_t blocks = ((vec ? total / 4 : total) + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (vec)
+    hipLaunchKernelGGL(split_reduce_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(256),
+                       0, stream, ws, splits, stride, out, mask, accumulate ? 1 : 0, total, c,
+                       hw, c_total, c_off);
+  else
+    hipLaunchKernelGGL(split_reduce_kernel<false>, dim3(static_cast<unsigned>(blocks)),
+                       dim3(256), 0, stream, ws, splits, stride, out, mask, accumulate ? 1 : 0,
+                       total, c, hw, c_total, c_off);
 }
 
 Geo make_geo(const ConvGemmGeo& cg) {
@@ -659,56 +710,133 @@ ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
     plan.splits = static_cast<int>(
         std::min<int64_t>((target_wgrad + tiles - 1) / tiles, max_split));
   } else {
-    plan.big = big >= fill_big;
-    const int64_t tiles = plan.big ? big : small;
-    const int64_t fill = plan.big ? fill_big : fill_small;
-    plan.splits = tiles >= fill ? 1
-                  : static_cast<int>(std::min<int64_t>((target_small + tiles - 1) / tiles,
-                                                       max_split));
+    static const int bigsplit_k = env_int("TGPIPE_CG_BIGSPLIT_MINK", 1 << 30);
+    static const int target_big = env_int("TGPIPE_CG_TARGET_BIG", 256);
+    if (big < fill_big && K >= bigsplit_k) {
+      // long reduction over a small output: 8-wave 128 x 128 tiles, split reduction
+      plan.big = true;
+      plan.splits = static_cast<int>(std::min<int64_t>((target_big + big - 1) / big, max_split));
+    } else {
+      plan.big = big >= fill_big;
+      const int64_t tiles = plan.big ? big : small;
+      const int64_t fill = plan.big ? fill_big : fill_small;
+      plan.splits = tiles >= fill ? 1
+                    : static_cast<int>(std::min<int64_t>((target_small + tiles - 1) / tiles,
+                                                         max_split));
+    }
   }
-  if (plan.splits < 1) plan.splits = 1;
+  if (plan.splits < 1 || g.scatter) plan.splits = 1;
+  // the launch rounds each split to whole stages: report the number it really runs
+  int k_chunk = (K + plan.splits - 1) / plan.splits;
+  k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
+  plan.splits = std::max(1, (K + k_chunk - 1) / k_chunk);
   plan.col_width = plan.big ? 128 : 64;
   plan.col_blocks = static_cast<int>((N + plan.col_width - 1) / plan.col_width);
   plan.scatter = g.scatter;
   return plan;
 }
 
+std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) {
+  Geo g = make_geo(cg);
+  g.scatter = mode == kBwdData && scatter_bwd(cg);
+  int M, N, K;
+  gemm_dims(mode, g, M, N, K);
+  std::vector<ConvGemmPlan> out;
+  const int max_split = std::max(1, K / (4 * kBK));
+  for (int big = 0; big < 2; ++big) {
+    const int64_t tiles = big ? static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128)
+                              : static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
+    int last = 0;
+    for (int s : {1, 2, 3, 4, 6, 8, 12, 16, 24, 32}) {
+      if (s > max_split || (s > 1 && g.scatter) || tiles * s > 8192) break;
+      int k_chunk = (K + s - 1) / s;
+      k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
+      const int real = std::max(1, (K + k_chunk - 1) / k_chunk);
+      if (real == last) continue;
+      last = real;
+      ConvGemmPlan p;
+      p.big = big != 0;
+      p.splits = real;
+      p.col_width = big ? 128 : 64;
+      p.col_blocks = static_cast<int>((N + p.col_width - 1) / p.col_width);
+      p.scatter = g.scatter;
+      out.push_back(p);
+    }
+  }
+  return out;
+}
+
+int64_t conv_gemm_workspace(int mode, const ConvGemmGeo& cg, const ConvGemmPlan& plan) {
+  if (plan.splits <= 1) return 0;
+  Geo g = make_geo(cg);
+  int M, N, K;
+  gemm_dims(mode, g, M, N, K);
+  // one output-shaped slice per split (forward: this convolution's channels only)
+  return static_cast<int64_t>(plan.splits) * M * N;
+}
+
 void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_mask, float* out,
                       float* part_mean, float* part_m2, const ConvGemmGeo& cg,
-                      const ConvGemmPlan& plan, bool accumulate, int64_t a_bytes,
+                      const ConvGemmPlan& plan, bool accumulate, float* ws, int64_t a_bytes,
                       int64_t b_bytes, hipStream_t stream) {
   Geo g = make_geo(cg);
   g.scatter = plan.scatter ? 1 : 0;
   int M, N, K;
   gemm_dims(mode, g, M, N, K);
   if (M == 0 || N == 0) return;
-  // split reductions accumulate with atomics into an output the host zeroed; the
-  // weight gradient always does (dW is zeroed)
-  const bool atomic = plan.splits > 1 || mode == kWgrad;
-  float* pm = plan.splits > 1 ? nullptr : part_mean;
-  float* pm2 = plan.splits > 1 ? nullptr : part_m2;
+  const bool split = plan.splits > 1;
+  const int64_t stride = split ? static_cast<int64_t>(M) * N : 0;
+  float* dst = out;
+  Geo gk = g;
+  if (split) {
+    // the GEMM writes raw partial sums into ws; split_reduce applies the channel slice,
+    // the ReLU mask and the accumulation
+    dst = ws;
+    if (mode == kFwd) {
+      gk.co_total = g.co;
+      gk.co_off = 0;
+    } else if (mode == kBwdData) {
+      gk.relu = 0;
+    }
+  }
+  float* pm = split ? nullptr : part_mean;
+  float* pm2 = split ? nullptr : part_m2;
+  const bool acc = accumulate && !split;
   if (mode == kFwd) {
     if (plan.big)
-      launch_cfg<kFwd, 1>(a, b, x_mask, out, pm, pm2, g, M, N, K, plan.splits, atomic,
-                             accumulate, a_bytes, b_bytes, stream);
+      launch_cfg<kFwd, 1>(a, b, x_mask, dst, pm, pm2, gk, M, N, K, plan.splits, stride, acc,
+                          a_bytes, b_bytes, stream);
     else
-      launch_cfg<kFwd, 0>(a, b, x_mask, out, pm, pm2, g, M, N, K, plan.splits, atomic,
-                             accumulate, a_bytes, b_bytes, stream);
+      launch_cfg<kFwd, 0>(a, b, x_mask, dst, pm, pm2, gk, M, N, K, plan.splits, stride, acc,
+                          a_bytes, b_bytes, stream);
   } else if (mode == kBwdData) {
     if (plan.big)
-      launch_cfg<kBwdData, 1>(a, b, x_mask, out, nullptr, nullptr, g, M, N, K, plan.splits,
-                                 atomic, accumulate, a_bytes, b_bytes, stream);
+      launch_cfg<kBwdData, 1>(a, b, x_mask, dst, nullptr, nullptr, gk, M, N, K, plan.splits,
+                              stride, acc, a_bytes, b_bytes, stream);
     else
-      launch_cfg<kBwdData, 0>(a, b, x_mask, out, nullptr, nullptr, g, M, N, K, plan.splits,
-                                 atomic, accumulate, a_bytes, b_bytes, stream);
+      launch_cfg<kBwdData, 0>(a, b, x_mask, dst, nullptr, nullptr, gk, M, N, K, plan.splits,
+                              stride, acc, a_bytes, b_bytes, stream);
   } else {
     if (plan.big)
-      launch_cfg<kWgrad, 1>(a, b, nullptr, out, nullptr, nullptr, g, M, N, K, plan.splits,
-                               atomic, accumulate, a_bytes, b_bytes, stream);
+      launch_cfg<kWgrad, 1>(a, b, nullptr, dst, nullptr, nullptr, gk, M, N, K, plan.splits,
+                            stride, acc, a_bytes, b_bytes, stream);
     else
-      launch_cfg<kWgrad, 0>(a, b, nullptr, out, nullptr, nullptr, g, M, N, K, plan.splits,
-                               atomic, accumulate, a_bytes, b_bytes, stream);
+      launch_cfg<kWgrad, 0>(a, b, nullptr, dst, nullptr, nullptr, gk, M, N, K, plan.splits,
+                            stride, acc, a_bytes, b_bytes, stream);
   }
+  if (!split) return;
+  // out[dst(i)] = (accumulate ? out : 0) + mask * sum_s ws[s][i]
+  int64_t planes, c, hw, c_total = 0, c_off = 0;
+  if (mode == kFwd) {
+    planes = g.n; c = g.co; hw = static_cast<int64_t>(g.ho) * g.wo;
+    c_total = g.co_total; c_off = g.co_off;
+  } else if (mode == kBwdData) {
+    planes = 1; c = static_cast<int64_t>(M) * N; hw = 1; c_total = c;
+  } else {
+    planes = 1; c = static_cast<int64_t>(M) * N; hw = 1; c_total = c;
+  }
+  launch_split_reduce(ws, plan.splits, stride, out, mode == kBwdData && g.relu ? x_mask : nullptr,
+                      accumulate, planes, c, hw, c_total, c_off, stream);
 }
 
 }  // namespace tgpipe

@@ -9,6 +9,10 @@
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "kernels.h"
@@ -20,6 +24,77 @@ constexpr int64_t kMaxBytes = 0x7ffffff0;  // buffer-resource offsets (conv_gemm
 
 hipStream_t cur_stream(const at::Tensor& t) {
   return at::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void launch_one(int mode, const float* a, const float* b, const float* mask, float* out,
+                float* pm, float* pm2, const ConvGemmGeo& g, const ConvGemmPlan& plan,
+                bool accumulate, int64_t a_bytes, int64_t b_bytes, const at::Tensor& like) {
+  const int64_t ws_size = conv_gemm_workspace(mode, g, plan);
+  at::Tensor ws;
+  if (ws_size > 0) ws = at::empty({ws_size}, like.options());
+  launch_conv_gemm(mode, a, b, mask, out, pm, pm2, g, plan, accumulate,
+                   ws_size > 0 ? ws.data_ptr<float>() : nullptr, a_bytes, b_bytes,
+                   cur_stream(like));
+}
+
+// Measured launch plans per (mode, device, geometry), like MIOpen's find step: the first
+// launch of a shape times every candidate (tile size x reduction splits) on the current
+// stream and keeps the fastest.  TGPIPE_CG_TUNE=0 uses the static heuristic instead;
+// accumulating launches and stream captures never tune (they cannot re-run freely).
+using PlanKey = std::tuple<int, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                           int, int>;
+std::mutex plan_mutex;
+std::map<PlanKey, ConvGemmPlan> plan_cache;
+
+ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* mask, float* out,
+                        float* pm, float* pm2, const ConvGemmGeo& g, bool accumulate,
+                        int64_t a_bytes, int64_t b_bytes, const at::Tensor& like) {
+  static const bool tune = [] {
+    const char* v = std::getenv("TGPIPE_CG_TUNE");
+    return v == nullptr || std::string(v) != "0";
+  }();
+  const ConvGemmPlan heuristic = conv_gemm_plan(mode, g);
+  if (!tune || accumulate) return heuristic;
+  const hipStream_t stream = cur_stream(like);
+  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &capture) != hipSuccess ||
+      capture != hipStreamCaptureStatusNone)
+    return heuristic;
+  const PlanKey key{mode, static_cast<int>(like.device().index()), g.n, g.ci, g.h, g.w, g.co,
+                    g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.oh, g.ow, g.co_total};
+  std::lock_guard<std::mutex> lock(plan_mutex);
+  auto hit = plan_cache.find(key);
+  if (hit != plan_cache.end()) return hit->second;
+  hipEvent_t t0, t1;
+  hipEventCreate(&t0);
+  hipEventCreate(&t1);
+  ConvGemmPlan best = heuristic;
+  float best_ms = -1.f;
+  for (const auto& cand : conv_gemm_candidates(mode, g)) {
+    float ms = 0.f;
+    for (int rep = 0; rep < 2; ++rep) {  // first run: warm-up (code object, caches)
+      hipEventRecord(t0, stream);
+      launch_one(mode, a, b, mask, out, pm, pm2, g, cand, false, a_bytes, b_bytes, like);
+      hipEventRecord(t1, stream);
+      hipEventSynchronize(t1);
+      hipEventElapsedTime(&ms, t0, t1);
+    }
+    if (best_ms < 0.f || ms < best_ms) {
+      best_ms = ms;
+      best = cand;
+    }
+  }
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  plan_cache[key] = best;
+  return best;
+}
+
+// One implicit-GEMM launch with its split-reduction workspace.
+void run_gemm(int mode, const float* a, const float* b, const float* mask, float* out,
+              float* pm, float* pm2, const ConvGemmGeo& g, const ConvGemmPlan& plan,
+              bool accumulate, int64_t a_bytes, int64_t b_bytes, const at::Tensor& like) {
+  launch_one(mode, a, b, mask, out, pm, pm2, g, plan, accumulate, a_bytes, b_bytes, like);
 }
 
 void check_f32(const at::Tensor& t, const char* name, const at::Tensor& like) {
@@ -109,10 +184,14 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
   Parts p = make_parts(x, weights, geo, relu);
   const int64_t n = x.size(0), c = p.co_total, s = p.ho * p.wo, cols = n * s;
   const auto stream = cur_stream(x);
+  auto z = at::empty({n, c, p.ho, p.wo}, x.options());
   std::vector<ConvGemmPlan> plans;
   bool split = false;
-  for (const auto& g : p.geo) {
-    plans.push_back(conv_gemm_plan(0, g));
+  for (size_t i = 0; i < p.geo.size(); ++i) {
+    // (tuning candidates write z without statistics; the real launches follow)
+    plans.push_back(tuned_plan(0, weights[i].data_ptr<float>(), x.data_ptr<float>(), nullptr,
+                               z.data_ptr<float>(), nullptr, nullptr, p.geo[i], false,
+                               weights[i].numel() * 4, x.numel() * 4, x));
     split = split || plans.back().splits > 1;
   }
   // statistics partials: from the GEMM epilogue (all parts share one column tiling), or
@@ -121,16 +200,14 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     split = split || pl.col_width != plans[0].col_width;
   const int width = split ? static_cast<int>(s) : plans[0].col_width;
   const int blocks = split ? static_cast<int>(n) : plans[0].col_blocks;
-  auto z = split ? at::zeros({n, c, p.ho, p.wo}, x.options())
-                 : at::empty({n, c, p.ho, p.wo}, x.options());
   auto part = at::empty({2, blocks, c}, x.options());
   for (size_t i = 0; i < p.geo.size(); ++i) {
     const auto wt = weights[i];
     const ConvGemmPlan& pl = plans[i];
-    launch_conv_gemm(0, wt.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
-                     split ? nullptr : part[0].data_ptr<float>(),
-                     split ? nullptr : part[1].data_ptr<float>(), p.geo[i], pl, false,
-                     wt.numel() * 4, x.numel() * 4, stream);
+    run_gemm(0, wt.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
+             split ? nullptr : part[0].data_ptr<float>(),
+             split ? nullptr : part[1].data_ptr<float>(), p.geo[i], pl, false, wt.numel() * 4,
+             x.numel() * 4, x);
   }
   if (split)
     launch_bn_stats(z.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n,
@@ -202,26 +279,30 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   if (need_dx) {
     std::vector<ConvGemmPlan> plans;
     bool zero = false;
-    for (const auto& g : p.geo) {
-      plans.push_back(conv_gemm_plan(1, g));
-      zero = zero || plans.back().splits > 1 || plans.back().scatter;
-    }
-    dx = zero ? at::zeros_like(x) : at::empty_like(x);
+    for (const auto& g : p.geo) zero = zero || conv_gemm_plan(1, g).scatter;
+    dx = zero ? at::zeros_like(x) : at::empty_like(x);  // stride holes receive nothing
+    for (size_t i = 0; i < p.geo.size(); ++i)
+      plans.push_back(tuned_plan(1, weights[i].data_ptr<float>(), dz.data_ptr<float>(),
+                                 x.data_ptr<float>(), dx.data_ptr<float>(), nullptr, nullptr,
+                                 p.geo[i], i > 0 || zero, weights[i].numel() * 4,
+                                 dz.numel() * 4, x));
     for (size_t i = 0; i < p.geo.size(); ++i) {
       const auto& wt = weights[i];
-      launch_conv_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-                       dx.data_ptr<float>(), nullptr, nullptr, p.geo[i], plans[i],
-                       i > 0 || zero, wt.numel() * 4, dz.numel() * 4, stream);
+      run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+               dx.data_ptr<float>(), nullptr, nullptr, p.geo[i], plans[i], i > 0 || zero,
+               wt.numel() * 4, dz.numel() * 4, x);
     }
   }
   out.push_back(dx);
   out.push_back(dgamma);
   out.push_back(dbeta);
   for (size_t i = 0; i < p.geo.size(); ++i) {
-    auto dw = at::zeros_like(weights[i]);
-    launch_conv_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
-                     nullptr, nullptr, p.geo[i], conv_gemm_plan(2, p.geo[i]), true,
-                     dz.numel() * 4, x.numel() * 4, stream);
+    auto dw = at::empty_like(weights[i]);
+    const ConvGemmPlan plan =
+        tuned_plan(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
+                   nullptr, nullptr, p.geo[i], false, dz.numel() * 4, x.numel() * 4, x);
+    run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(), nullptr,
+             nullptr, p.geo[i], plan, false, dz.numel() * 4, x.numel() * 4, x);
     out.push_back(dw);
   }
   return out;
@@ -235,12 +316,12 @@ at::Tensor conv_gemm_forward(const at::Tensor& x_in, const at::Tensor& weight,
   check_f32(x, "x", x);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Parts p = make_parts(x, {weight}, geo, relu);
-  const ConvGemmPlan plan = conv_gemm_plan(0, p.geo[0]);
-  auto z = plan.splits > 1 ? at::zeros({x.size(0), p.co_total, p.ho, p.wo}, x.options())
-                           : at::empty({x.size(0), p.co_total, p.ho, p.wo}, x.options());
-  launch_conv_gemm(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
-                   nullptr, nullptr, p.geo[0], plan, false, weight.numel() * 4, x.numel() * 4,
-                   cur_stream(x));
+  auto z = at::empty({x.size(0), p.co_total, p.ho, p.wo}, x.options());
+  const ConvGemmPlan plan =
+      tuned_plan(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
+                 nullptr, nullptr, p.geo[0], false, weight.numel() * 4, x.numel() * 4, x);
+  run_gemm(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
+           nullptr, nullptr, p.geo[0], plan, false, weight.numel() * 4, x.numel() * 4, x);
   return z;
 }
 
@@ -254,12 +335,15 @@ at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_
   Parts p = make_parts(x, {weight}, geo, relu);
   TORCH_CHECK(dz.size(1) == p.co_total && dz.size(2) == p.ho && dz.size(3) == p.wo,
               "dz does not match the convolution's output");
-  const ConvGemmPlan plan = conv_gemm_plan(1, p.geo[0]);
-  const bool zero = plan.splits > 1 || plan.scatter;
-  auto dx = zero ? at::zeros_like(x) : at::empty_like(x);
-  launch_conv_gemm(1, weight.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-                   dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], plan, false,
-                   weight.numel() * 4, dz.numel() * 4, cur_stream(x));
+  const bool scatter = conv_gemm_plan(1, p.geo[0]).scatter;
+  auto dx = scatter ? at::zeros_like(x) : at::empty_like(x);
+  const ConvGemmPlan plan =
+      tuned_plan(1, weight.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+                 dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], scatter, weight.numel() * 4,
+                 dz.numel() * 4, x);
+  run_gemm(1, weight.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+           dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], plan, plan.scatter,
+           weight.numel() * 4, dz.numel() * 4, x);
   return dx;
 }
 
@@ -273,10 +357,12 @@ at::Tensor conv_gemm_backward_weight(const at::Tensor& dz_in, const at::Tensor& 
   Parts p = make_parts(x, {weight}, geo, relu);
   TORCH_CHECK(dz.size(1) == p.co_total && dz.size(2) == p.ho && dz.size(3) == p.wo,
               "dz does not match the convolution's output");
-  auto dw = at::zeros_like(weight);
-  launch_conv_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
-                   nullptr, nullptr, p.geo[0], conv_gemm_plan(2, p.geo[0]), true, dz.numel() * 4,
-                   x.numel() * 4, cur_stream(x));
+  auto dw = at::empty_like(weight);
+  const ConvGemmPlan plan =
+      tuned_plan(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
+                 nullptr, nullptr, p.geo[0], false, dz.numel() * 4, x.numel() * 4, x);
+  run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(), nullptr,
+           nullptr, p.geo[0], plan, false, dz.numel() * 4, x.numel() * 4, x);
   return dw;
 }
 

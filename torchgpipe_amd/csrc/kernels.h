@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace tgpipe {
 
 // K1: per-channel sum / sum of squares of x[N, C, S] accumulated into sum[C], sumsq[C].
@@ -127,24 +129,27 @@ struct ConvGemmGeo {
 // mode 0: forward  Z[:, co_off:co_off+co] = conv(relu(X)); a = W[co][ci*kh*kw], b = X;
 //         part_mean / part_m2 ([col_blocks][co_total]): per column block mean and centred
 //         second moment of each output channel (BatchNorm statistics) -- only when the
-//         plan does not split the reduction (splits > 1: Z must be zeroed, statistics by
-//         launch_bn_stats).
+//         plan does not split the reduction (splits > 1: statistics by launch_bn_stats).
 // mode 1: backward-data  dX (+)= relu'(X) * conv^T(dZ); a = W (untransposed), b = dZ,
 //         x_mask = X (relu mask); `accumulate` adds to dX (several convolutions of one X).
-//         dX must be zeroed when the plan splits or scatters.
-// mode 2: weight gradient  dW[co][ci*kh*kw] += dZ * relu(X); a = dZ, b = X; dW zeroed.
+//         dX must be zeroed when the plan scatters (stride holes).
+// mode 2: weight gradient  dW[co][ci*kh*kw] = dZ * relu(X); a = dZ, b = X.
+// splits > 1 needs a workspace of conv_gemm_workspace() floats.
 // Supported: 1x1 with any stride / offset, 1xk / kx1 with stride 1.
 struct ConvGemmPlan {
   bool big = true;       // 128 x 128 tiles (else 64 x 64)
-  int splits = 1;        // reduction splits (grid.y), > 1: fp32 atomics into zeroed output
+  int splits = 1;        // reduction splits (grid.y), > 1: workspace slices + split_reduce
   int col_width = 128;   // forward: columns per statistics block
   int col_blocks = 0;    // forward: statistics blocks
   bool scatter = false;  // backward-data of a strided 1x1 over output pixels
 };
 ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& g);
+// Every launch shape worth timing (tile size x reduction splits) for the autotuner.
+std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& g);
+int64_t conv_gemm_workspace(int mode, const ConvGemmGeo& g, const ConvGemmPlan& plan);
 void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_mask, float* out,
                       float* part_mean, float* part_m2, const ConvGemmGeo& g,
-                      const ConvGemmPlan& plan, bool accumulate, int64_t a_bytes,
+                      const ConvGemmPlan& plan, bool accumulate, float* ws, int64_t a_bytes,
                       int64_t b_bytes, hipStream_t stream);
 
 // (mean, M2) partials of z[n][c][s] per (image, channel): part_*[n][c] (width s).
