@@ -40,6 +40,7 @@ CASES = [
     (4, 256, 7, 7, 256, 1, 7, 1, 3, 0),      # small grid: split reduction (atomics)
     (4, 1024, 7, 7, 256, 1, 1, 1, 0, 0),     # split reduction, 1x1
     (4, 96, 14, 14, 64, 1, 1, 2, 0, 1),      # strided scatter backward, even plane
+    (2, 3, 32, 32, 16, 3, 3, 1, 1, 0),       # U-Net's 3-channel input convolution (2-D taps)
 ]
 
 
@@ -196,3 +197,20 @@ def test_amoebanet_fused_matches_fp64_eager():
         assert err_fused <= 2 * err_plain + 1e-5, (name, err_fused, err_plain)
     print(f'worst relative gradient error: fused {worst_fused:.2e}, eager {worst_plain:.2e}')
     assert worst_fused < 0.1
+
+
+def test_gemm_conv2d_module_matches_conv2d():
+    from torchgpipe_amd.ops.convbn import GemmConv2d
+    torch.manual_seed(5)
+    conv = GemmConv2d(32, 1, 1, bias=False).cuda()
+    ref = nn.Conv2d(32, 1, 1, bias=False).cuda().double()
+    ref.load_state_dict(conv.state_dict())
+    x = torch.randn(3, 32, 24, 24, device='cuda', requires_grad=True)
+    x64 = x.detach().double().requires_grad_(True)
+    y, y64 = conv(x), ref(x64)
+    assert rel_err(y, y64) < 2e-6
+    g = torch.randn_like(y)
+    y.backward(g)
+    y64.backward(g.double())
+    assert rel_err(x.grad, x64.grad) < 2e-6
+    assert rel_err(conv.weight.grad, ref.weight.grad) < 5e-6

@@ -2,6 +2,7 @@
 // AmoebaNet-D cell operations: 1x1 (stride 1 / 2, input offset for FactorizedReduce)
 // and 1xk / kx1 convolutions, NCHW fp32, fused with the ReLU that precedes every
 // convolution of the model and with the statistics of the BatchNorm that follows it.
+// Any kh x kw kernel works at stride 1 (U-Net's 3-channel input convolution uses it).
 //
 //   forward      Z[n][co][p]    = sum_{ci,t} W[co][ci][t] * relu(X[n][ci][tap(p,t)])
 //                M = Co, N = images x output pixels, K = Ci x taps
@@ -75,7 +76,7 @@ struct Geo {
   int n, ci, h, w;       // input
   int co, ho, wo;        // output (co = channels of this convolution)
   int co_total, co_off;  // channel count / offset of its output inside Z (concat outputs)
-  int kh, kw, taps;      // kernel (one of kh, kw is 1), taps = kh * kw
+  int kh, kw, taps;      // kernel, taps = kh * kw (tap t = (t / kw, t % kw))
   int sh, sw, ph, pw;    // stride, padding
   int oh, ow;            // extra input offset (FactorizedReduce's shifted branch: 1)
   int relu;              // ReLU on the input (forward / weight-grad) / its mask (bwd-data)
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
           }
         } else {
           const int ci = k / g.taps, t = k - ci * g.taps;
-          const int th = g.kh == 1 ? 0 : t, tw = g.kh == 1 ? t : 0;
+          const int th = t / g.kw, tw = t - th * g.kw;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int yi = col[e].y + th, xi = col[e].x + tw;
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
         } else {
           // stride 1: output pixel = input pixel + pad - tap - offset
           const int co = k / g.taps, t = k - co * g.taps;
-          const int th = g.kh == 1 ? 0 : t, tw = g.kh == 1 ? t : 0;
+          const int th = t / g.kw, tw = t - th * g.kw;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int y = col[e].y - th, x = col[e].x - tw;
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
           const int n = k / hw_out, p = k - n * hw_out;
           v = bload4(br, static_cast<uint32_t>(((n * g.ci + ci) * hw_in + p) * 4));
         } else {
-          const int th = g.kh == 1 ? 0 : t, tw = g.kh == 1 ? t : 0;
+          const int th = t / g.kw, tw = t - th * g.kw;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             uint32_t off = kOOB;
@@ -747,7 +748,7 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
     const int64_t tiles = big ? static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128)
                               : static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
     int last = 0;
-    for (int s : {1, 2, 3, 4, 6, 8, 12, 16, 24, 32}) {
+    for (int s : {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256, 512, 1024}) {
       if (s > max_split || (s > 1 && g.scatter) || tiles * s > 8192) break;
       int k_chunk = (K + s - 1) / s;
       k_chunk = (k_chunk + kBK - 1) / kBK * kBK;

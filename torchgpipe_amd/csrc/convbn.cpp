@@ -128,12 +128,11 @@ Parts make_parts(const at::Tensor& x, at::TensorList weights, at::IntArrayRef ge
     check_f32(wt, "weight", x);
     const int64_t* g = geo.data() + 8 * i;
     const int64_t kh = g[0], kw = g[1], sh = g[2], sw = g[3], ph = g[4], pw = g[5];
-    TORCH_CHECK(kh == 1 || kw == 1, "one kernel dimension must be 1 (1x1, 1xk, kx1)");
     TORCH_CHECK(wt.dim() == 4 && wt.size(1) == ci && wt.size(2) == kh && wt.size(3) == kw,
                 "weight must be [Co][Ci][kh][kw] matching x and the geometry");
     TORCH_CHECK(sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && g[6] >= 0 && g[7] >= 0,
                 "bad stride / padding / offset");
-    TORCH_CHECK(kh * kw == 1 || (sh == 1 && sw == 1), "1xk / kx1 kernels need stride 1");
+    TORCH_CHECK(kh * kw == 1 || (sh == 1 && sw == 1), "kernels larger than 1x1 need stride 1");
     const int64_t ho = (h + 2 * ph - kh) / sh + 1, wo = (w + 2 * pw - kw) / sw + 1;
     TORCH_CHECK(ho > 0 && wo > 0, "empty output");
     if (i == 0) {

@@ -117,7 +117,8 @@ void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, in
 
 // ---- AmoebaNet cell operations (conv_gemm.hip, batchnorm.hip) -----------------------------
 
-// Implicit-GEMM convolution with one of kh, kw equal to 1 (1x1, 1xk, kx1), NCHW fp32.
+// Implicit-GEMM convolution, NCHW fp32: 1x1 with any stride / offset, any kh x kw at
+// stride 1 (AmoebaNet's 1x1 / 1x7 / 7x1, U-Net's 3-channel input and 1x1 output convs).
 struct ConvGemmGeo {
   int n, ci, h, w;       // input
   int co, ho, wo;        // output of this convolution
@@ -135,7 +136,6 @@ struct ConvGemmGeo {
 //         dX must be zeroed when the plan scatters (stride holes).
 // mode 2: weight gradient  dW[co][ci*kh*kw] = dZ * relu(X); a = dZ, b = X.
 // splits > 1 needs a workspace of conv_gemm_workspace() floats.
-// Supported: 1x1 with any stride / offset, 1xk / kx1 with stride 1.
 struct ConvGemmPlan {
   bool big = true;       // 128 x 128 tiles (else 64 x 64)
   int splits = 1;        // reduction splits (grid.y), > 1: workspace slices + split_reduce

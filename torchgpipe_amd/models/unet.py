@@ -12,9 +12,11 @@ parameters, so the reference balance tables (e.g. p8 =
 ``fused=True`` (default) keeps the 241-layer structure but makes the
 ``dropout`` layer a :class:`~torchgpipe_amd.ops.fused.DropNormAct` HIP kernel
 (Dropout2d + InstanceNorm2d + LeakyReLU in one pass), the ``norm`` /
-``relu`` layers identities, and the 3×3 convolutions
-:class:`~torchgpipe_amd.ops.conv.WinogradConv2d` (Winograd F(2,3) on the f32
-matrix cores; same parameters as ``nn.Conv2d``).  Because every layer stays in place, any balance
+``relu`` layers identities, the 3×3 convolutions
+:class:`~torchgpipe_amd.ops.conv.WinogradConv2d` (Winograd F(4,3)/F(2,3) on the f32
+matrix cores; same parameters as ``nn.Conv2d``), and the 3-channel input and 1×1
+output convolutions the implicit-GEMM kernel (``ops.convbn.GemmConv2d``), so no
+MIOpen kernel is compiled on the first step.  Because every layer stays in place, any balance
 that splits a cell between partitions still computes the same function, and
 the state-dict is identical (those layers have no parameters).
 """
@@ -27,6 +29,7 @@ import torch.nn.functional as F
 
 from torchgpipe_amd.models.flatten import flatten_sequential
 from torchgpipe_amd.ops.conv import WinogradConv2d
+from torchgpipe_amd.ops.convbn import GemmConv2d
 from torchgpipe_amd.ops.fused import DropNormAct
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
@@ -112,7 +115,8 @@ def unet(depth: int = 5, num_convs: int = 5, base_channels: int = 64, input_chan
             ('decode', cell(dec(i))),
         ])) for i in reversed(range(depth))])
 
-    segment = nn.Conv2d(dec(0)['out'], output_channels, kernel_size=1, bias=False)
+    segment = (GemmConv2d if fused else nn.Conv2d)(dec(0)['out'], output_channels,
+                                                   kernel_size=1, bias=False)
 
     model = nn.Sequential(OrderedDict([
         ('encoder', encoder),

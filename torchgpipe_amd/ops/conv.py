@@ -229,6 +229,11 @@ class WinogradConv2d(nn.Conv2d):
                                                           self.padding, self.dilation,
                                                           self.groups):
             return _WinogradConv.apply(input, self.weight, self.bias, self._wino)
+        # few-channel convolutions (U-Net's 3-channel input) on the implicit-GEMM kernel:
+        # no MIOpen kernel to compile on the first step
+        from torchgpipe_amd.ops.convbn import gemm_conv2d, gemm_conv_eligible
+        if WINOGRAD_ENABLED and gemm_conv_eligible(input, self):
+            return gemm_conv2d(input, self)
         return super().forward(input)
 
     def __getstate__(self):  # type: ignore[no-untyped-def]

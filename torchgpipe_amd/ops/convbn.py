@@ -31,7 +31,7 @@ import torch.nn.functional as F
 from torchgpipe_amd.ops import _ext
 
 __all__ = ['relu_conv_bn', 'ReLUConvBN', 'FusedChain', 'conv_supported', 'fused_triplets',
-           'fusable', 'disabled']
+           'fusable', 'disabled', 'GemmConv2d', 'gemm_conv2d', 'gemm_conv_eligible']
 
 # TGPIPE_FUSED_CONVBN=0 runs the eager ReLU / Conv2d / BatchNorm2d modules instead.
 _ENABLED = os.environ.get('TGPIPE_FUSED_CONVBN', '1') != '0'
@@ -167,3 +167,49 @@ class FusedChain(nn.Sequential):
 
 class ReLUConvBN(FusedChain):
     """``nn.Sequential(ReLU, Conv2d, BatchNorm2d)`` running as one fused op."""
+
+
+# -- plain convolutions on the same implicit-GEMM kernels --------------------------------
+
+def gemm_conv_eligible(x: Tensor, conv: nn.Conv2d) -> bool:
+    """Convolutions the implicit-GEMM kernels take without BatchNorm: any kernel at
+    stride 1 or a strided 1x1, no bias / groups / dilation, fp32 on the GPU."""
+    kh, kw = conv.kernel_size
+    return (_ENABLED and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and conv.weight.dtype == torch.float32 and conv.bias is None and conv.groups == 1
+            and tuple(conv.dilation) == (1, 1) and conv.padding_mode == 'zeros'
+            and isinstance(conv.padding, tuple)
+            and (kh * kw == 1 or tuple(conv.stride) == (1, 1)) and _ext.available())
+
+
+class _GemmConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: Tensor, weight: Tensor, geo: List[int]) -> Tensor:  # type: ignore[override]
+        ctx.save_for_backward(x, weight)
+        ctx.geo = geo
+        return _ext.require(x).conv_gemm_forward(x, weight, geo, False)
+
+    @staticmethod
+    def backward(ctx, dz: Tensor):  # type: ignore[override]
+        x, weight = ctx.saved_tensors
+        ops = _ext.require(dz)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.conv_gemm_backward_data(dz, x, weight, ctx.geo, False)
+        if ctx.needs_input_grad[1]:
+            dw = ops.conv_gemm_backward_weight(dz, x, weight, ctx.geo, False)
+        return dx, dw, None
+
+
+def gemm_conv2d(x: Tensor, conv: nn.Conv2d) -> Tensor:
+    """``conv(x)`` on the implicit-GEMM MFMA kernels (caller checks eligibility)."""
+    return _GemmConv.apply(x, conv.weight, _geo(conv))
+
+
+class GemmConv2d(nn.Conv2d):
+    """``nn.Conv2d`` whose GPU fp32 path is the implicit-GEMM MFMA kernel (no MIOpen)."""
+
+    def forward(self, input: Tensor) -> Tensor:
+        if gemm_conv_eligible(input, self):
+            return gemm_conv2d(input, self)
+        return super().forward(input)
