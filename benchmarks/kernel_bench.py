@@ -87,6 +87,29 @@ def main() -> None:
                      'torch_ms': round(t_t, 4), 'hip_TBps': round(nbytes / t_k / 1e9, 2)})
         print(json.dumps(rows[-1]), flush=True)
 
+    # K1+K3: native DeferredBatchNorm train forward (statistics + fp64 tracking + normalise)
+    # vs tracking kernel + MIOpen BatchNorm (the round-1 path).  Bytes: 2 reads + 1 write.
+    ops = torch.ops.tgpipe
+    for n, c, hw in [(40, 256, 56), (40, 1024, 14), (64, 64, 112)]:
+        x = torch.randn(n, c, hw, hw, device=dev)
+        w = torch.ones(c, device=dev)
+        b = torch.zeros(c, device=dev)
+        acc = torch.zeros(3, c, device=dev, dtype=torch.float64)
+        s = torch.zeros(c, device=dev)
+        q = torch.zeros(c, device=dev)
+        nbytes = 3 * x.numel() * 4
+
+        def old_path():
+            dbn.track(x, s, q)
+            F.batch_norm(x, None, None, w, b, True, 0.0, 1e-5)
+
+        t_k = timeit(lambda: ops.bn_train_forward(x, w, b, acc, 1e-5))
+        t_t = timeit(old_path)
+        rows.append({'op': 'dbn_bn_train_forward', 'shape': [n, c, hw, hw],
+                     'hip_ms': round(t_k, 4), 'track_plus_miopen_ms': round(t_t, 4),
+                     'hip_TBps': round(nbytes / t_k / 1e9, 2)})
+        print(json.dumps(rows[-1]), flush=True)
+
     # K4: elementwise Philox dropout.
     x = torch.randn(64 * 1024 * 1024, device=dev)
     t_k = timeit(lambda: dropout_ops._Dropout.apply(x, 0.1, 7, 0))

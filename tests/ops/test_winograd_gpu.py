@@ -180,3 +180,33 @@ def test_forward_variants_and_splits(variant, shape, splits):
     want = _ref(x, wt, b)
     torch.testing.assert_close(y.double(), want, rtol=1e-4,
                                atol=2e-5 * (want.abs().max().item() + 1))
+
+
+def test_weight_update_through_data_is_seen_by_the_next_pipeline_step():
+    """``p.data.copy_`` does not bump ``_version``; the per-step cache key does."""
+    from torchgpipe_amd import GPipe
+    from torchgpipe_amd.ops.conv import WinogradConv2d
+    torch.manual_seed(0)
+    conv = WinogradConv2d(16, 16, 3, padding=1, bias=False).cuda()
+    model = GPipe(torch.nn.Sequential(conv), [1], devices=[0], chunks=2)
+    x = torch.randn(4, 16, 12, 12, device='cuda')
+    with torch.no_grad():
+        model(x)  # fills the cache
+        conv.weight.data.copy_(torch.randn_like(conv.weight))
+        got = model(x)
+    want = F.conv2d(x.double(), conv.weight.double(), padding=1)
+    assert ((got.double() - want).norm() / want.norm()).item() < 1e-5
+
+
+def test_cache_budget_zero_keeps_no_transforms(monkeypatch):
+    from torchgpipe_amd.ops import conv as convmod
+    monkeypatch.setattr(convmod, '_BUDGET', 0)
+    torch.manual_seed(1)
+    layer = convmod.WinogradConv2d(16, 16, 3, padding=1, bias=False).cuda()
+    x = torch.randn(2, 16, 12, 12, device='cuda', requires_grad=True)
+    before = convmod.cache_bytes()
+    y = layer(x)
+    y.sum().backward()
+    assert convmod.cache_bytes() == before
+    want = F.conv2d(x.double(), layer.weight.double(), padding=1)
+    assert ((y.double() - want).norm() / want.norm()).item() < 1e-5

@@ -140,3 +140,42 @@ def test_gpipe_training_gradients_match_one_device(devices, checkpoint, kind):
     want, want_loss = parity.reference(kind, torch.device('cuda', 0), chunks)
     got = [p.grad.detach().cpu() for p in gpipe.parameters()]
     parity.assert_parity([{'grads': got, 'loss': loss.item()}], want, want_loss, rel=1e-4)
+
+
+def test_deferred_batch_norm_large_mean_keeps_running_var():
+    """Verdict r1 #5: mean 1e3, std 1e-1 inputs -> running_var of an fp64 nn.BatchNorm2d to
+    1e-4 relative (fp64 Chan accumulators; fp32 sums of x and x^2 cancel here)."""
+    torch.manual_seed(3)
+    bn = nn.BatchNorm2d(8, momentum=1.0).double().cuda()
+    gpipe = GPipe(nn.Sequential(nn.BatchNorm2d(8, momentum=1.0)), balance=[1], devices=[0],
+                  chunks=4, deferred_batch_norm=True)
+    x = 1e3 + 0.1 * torch.randn(32, 8, 20, 20, device='cuda')
+    gpipe(x)
+    bn(x.double())
+    dbn = gpipe[0]
+    rel = ((dbn.running_var.double() - bn.running_var).abs() / bn.running_var).max().item()
+    assert rel < 1e-4, rel
+    torch.testing.assert_close(dbn.running_mean.double(), bn.running_mean, rtol=1e-6, atol=1e-6)
+
+
+def test_deferred_batch_norm_native_forward_backward_match_fp64():
+    from torchgpipe_amd.batchnorm import DeferredBatchNorm
+    torch.manual_seed(4)
+    dbn = DeferredBatchNorm(16, chunks=1).cuda()
+    with torch.no_grad():
+        dbn.weight.uniform_(0.5, 1.5)
+        dbn.bias.uniform_(-1, 1)
+    ref = nn.BatchNorm2d(16).cuda().double()
+    ref.load_state_dict({k: v for k, v in dbn.state_dict().items()
+                         if k not in ('sum', 'sum_squares')})
+    x = (torch.randn(6, 16, 9, 9, device='cuda') * 3 + 2).requires_grad_(True)
+    x64 = x.detach().double().requires_grad_(True)
+    y, y64 = dbn(x), ref(x64)
+    torch.testing.assert_close(y.double(), y64, rtol=1e-5, atol=1e-5)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y64.backward(g.double())
+    torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dbn.weight.grad.double(), ref.weight.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dbn.bias.grad.double(), ref.bias.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dbn.running_var.double(), ref.running_var, rtol=1e-5, atol=1e-6)

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
     const float* __restrict__ pm, const float* __restrict__ pm2, int blocks, int width,
     int64_t total, int64_t c, float eps, double momentum, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv,
-    int64_t* __restrict__ tracked) {
+    int64_t* __restrict__ tracked, double* __restrict__ acc) {
   const int lane = threadIdx.x & 31;
   const int64_t ch = static_cast<int64_t>(blockIdx.x) * 8 + (threadIdx.x >> 5);
   if (tracked != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *tracked += 1;
@@ -58,6 +58,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
   const double var = na > 0.0 ? m2a / na : 0.0;
   mean[ch] = static_cast<float>(ma);
   invstd[ch] = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  if (acc != nullptr) {
+    // DeferredBatchNorm: fold this micro-batch into the mini-batch accumulators
+    // (count, mean, M2) -- committed once per mini-batch by dbn_commit64
+    double n0 = acc[ch], m0 = acc[c + ch], q0 = acc[2 * c + ch];
+    chan_merge(n0, m0, q0, na, ma, m2a);
+    acc[ch] = n0;
+    acc[c + ch] = m0;
+    acc[2 * c + ch] = q0;
+  }
   if (rm != nullptr) {
     const double unbiased = na > 1.0 ? m2a / (na - 1.0) : var;
     rm[ch] = static_cast<float>((1.0 - momentum) * rm[ch] + momentum * ma);
@@ -178,36 +187,71 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
   }
 }
 
-// One workgroup per (channel, image): mean and centred M2 of the plane (two passes; the
-// plane is L2-resident for the second).  Used when the convolution split its reduction.
+// One wave per (image, channel) plane, four planes per workgroup: mean and centred M2
+// of the plane (two passes, the second from L1/L2), 16-byte loads when s % 4 == 0.
+// Wave-sized work keeps small planes (7^2..14^2) from leaving 3/4 of a workgroup idle.
+template <bool kVec>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ z,
                                                        float* __restrict__ pm,
-                                                       float* __restrict__ pm2, int64_t c,
-                                                       int64_t s) {
-  const int64_t ch = blockIdx.x, img = blockIdx.y;
+                                                       float* __restrict__ pm2, int64_t n,
+                                                       int64_t c, int64_t s) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ch = blockIdx.x, img = static_cast<int64_t>(blockIdx.y) * 4 + (threadIdx.x >> 6);
+  if (img >= n) return;
   const float* plane = z + (img * c + ch) * s;
-  __shared__ float red[4];
   float acc = 0.f;
-  for (int64_t i = threadIdx.x; i < s; i += 256) acc += plane[i];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  const float mean = (red[0] + red[1] + red[2] + red[3]) / static_cast<float>(s);
-  __syncthreads();
-  acc = 0.f;
-  for (int64_t i = threadIdx.x; i < s; i += 256) {
-    const float d = plane[i] - mean;
-    acc += d * d;
+  if constexpr (kVec) {
+    for (int64_t q = lane; q < s / 4; q += 64) {
+      const floatx4 v = reinterpret_cast<const floatx4*>(plane)[q];
+      acc += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+  } else {
+    for (int64_t i = lane; i < s; i += 64) acc += plane[i];
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
+  const float mean = acc / static_cast<float>(s);
+  float m2 = 0.f;
+  if constexpr (kVec) {
+    for (int64_t q = lane; q < s / 4; q += 64) {
+      const floatx4 v = reinterpret_cast<const floatx4*>(plane)[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[e] - mean;
+        m2 += d * d;
+      }
+    }
+  } else {
+    for (int64_t i = lane; i < s; i += 64) {
+      const float d = plane[i] - mean;
+      m2 += d * d;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m2 += __shfl_xor(m2, off);
+  if (lane == 0) {
     pm[img * c + ch] = mean;
-    pm2[img * c + ch] = red[0] + red[1] + red[2] + red[3];
+    pm2[img * c + ch] = m2;
   }
+}
+
+// DeferredBatchNorm commit: running-stat EMA from the fp64 (count, mean, M2)
+// accumulators (unbiased variance), then the accumulators are zeroed.
+__global__ __launch_bounds__(256) void dbn_commit64_kernel(double* __restrict__ acc,
+                                                           float* __restrict__ rm,
+                                                           float* __restrict__ rv, int64_t c,
+                                                           double momentum) {
+  const int64_t ch = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (ch >= c) return;
+  const double n = acc[ch], mean = acc[c + ch], m2 = acc[2 * c + ch];
+  if (n > 0.0) {
+    const double var = n > 1.0 ? m2 / (n - 1.0) : 0.0;
+    rm[ch] = static_cast<float>((1.0 - momentum) * rm[ch] + momentum * mean);
+    rv[ch] = static_cast<float>((1.0 - momentum) * rv[ch] + momentum * var);
+  }
+  acc[ch] = 0.0;
+  acc[c + ch] = 0.0;
+  acc[2 * c + ch] = 0.0;
 }
 
 unsigned grid_for(int64_t work) {
@@ -220,17 +264,29 @@ unsigned grid_for(int64_t work) {
 void launch_bn_finalize(const float* part_mean, const float* part_m2, int blocks, int width,
                         int64_t total, int64_t c, float eps, double momentum, float* mean,
                         float* invstd, float* running_mean, float* running_var, int64_t* tracked,
-                        hipStream_t stream) {
+                        double* acc, hipStream_t stream) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(static_cast<unsigned>((c + 7) / 8)),
                      dim3(256), 0, stream, part_mean, part_m2, blocks, width, total, c, eps,
-                     momentum, mean, invstd, running_mean, running_var, tracked);
+                     momentum, mean, invstd, running_mean, running_var, tracked, acc);
+}
+
+void launch_dbn_commit64(double* acc, float* running_mean, float* running_var, int64_t c,
+                         double momentum, hipStream_t stream) {
+  if (c == 0) return;
+  hipLaunchKernelGGL(dbn_commit64_kernel, dim3(static_cast<unsigned>((c + 255) / 256)), dim3(256),
+                     0, stream, acc, running_mean, running_var, c, momentum);
 }
 
 void launch_bn_stats(const float* z, float* part_mean, float* part_m2, int64_t n, int64_t c,
                      int64_t s, hipStream_t stream) {
   if (n == 0 || c == 0) return;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(static_cast<unsigned>(c), static_cast<unsigned>(n)),
-                     dim3(256), 0, stream, z, part_mean, part_m2, c, s);
+  const dim3 grid(static_cast<unsigned>(c), static_cast<unsigned>((n + 3) / 4));
+  if ((s & 3) == 0)
+    hipLaunchKernelGGL(bn_stats_kernel<true>, grid, dim3(256), 0, stream, z, part_mean, part_m2,
+                       n, c, s);
+  else
+    hipLaunchKernelGGL(bn_stats_kernel<false>, grid, dim3(256), 0, stream, z, part_mean, part_m2,
+                       n, c, s);
 }
 
 void launch_bn_apply(const float* z, const float* mean, const float* invstd, const float* gamma,

@@ -227,7 +227,7 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
   launch_bn_finalize(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, cols, c,
                      static_cast<float>(eps), momentum, mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), const_cast<float*>(rm), const_cast<float*>(rv),
-                     tracked, stream);
+                     tracked, nullptr, stream);
   const float* ga = opt_ptr(gamma, "gamma", x, c);
   const float* be = opt_ptr(beta, "beta", x, c);
   const float* ad = nullptr;
@@ -365,10 +365,88 @@ at::Tensor conv_gemm_backward_weight(const at::Tensor& dz_in, const at::Tensor& 
   return dw;
 }
 
+// BatchNorm (training) of x[N][C][*] with micro-batch statistics, for DeferredBatchNorm:
+// statistics partials per (image, channel), Chan/fp64 finalize (folded into the fp64
+// accumulators `acc` [3][C] when given), one normalising pass.  Returns {y, mean, invstd}.
+std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
+                                         const c10::optional<at::Tensor>& gamma,
+                                         const c10::optional<at::Tensor>& beta,
+                                         const c10::optional<at::Tensor>& acc, double eps) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  TORCH_CHECK(x.dim() >= 2, "x must be [N][C][*]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t n = x.size(0), c = x.size(1), s = n * c == 0 ? 0 : x.numel() / (n * c);
+  const auto stream = cur_stream(x);
+  auto part = at::empty({2, n, c}, x.options());
+  auto mean = at::empty({c}, x.options());
+  auto invstd = at::empty({c}, x.options());
+  auto y = at::empty_like(x);
+  if (x.numel() == 0) return {y, mean.zero_(), invstd.fill_(1.f)};
+  double* accp = nullptr;
+  if (acc.has_value() && acc->defined()) {
+    TORCH_CHECK(acc->device() == x.device() && acc->scalar_type() == at::kDouble &&
+                    acc->is_contiguous() && acc->numel() == 3 * c,
+                "acc must be a contiguous float64 [3][C] tensor on the input's device");
+    accp = acc->data_ptr<double>();
+  }
+  launch_bn_stats(x.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n, c,
+                  s, stream);
+  launch_bn_finalize(part[0].data_ptr<float>(), part[1].data_ptr<float>(), static_cast<int>(n),
+                     static_cast<int>(s), n * s, c, static_cast<float>(eps), 0.0,
+                     mean.data_ptr<float>(), invstd.data_ptr<float>(), nullptr, nullptr, nullptr,
+                     accp, stream);
+  launch_bn_apply(x.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                  opt_ptr(gamma, "gamma", x, c), opt_ptr(beta, "beta", x, c), nullptr,
+                  y.data_ptr<float>(), n, c, s, stream);
+  return {y, mean, invstd};
+}
+
+// Backward of bn_train_forward: {dx, dgamma, dbeta}.
+std::vector<at::Tensor> bn_train_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
+                                          const at::Tensor& mean, const at::Tensor& invstd,
+                                          const c10::optional<at::Tensor>& gamma) {
+  auto x = x_in.contiguous();
+  auto dy = dy_in.contiguous();
+  check_f32(x, "x", x);
+  check_f32(dy, "dy", x);
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy must have x's shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t n = x.size(0), c = x.size(1), s = n * c == 0 ? 0 : x.numel() / (n * c);
+  auto sums = at::zeros({2, c}, x.options());
+  auto dx = at::empty_like(x);
+  auto dgamma = at::empty({c}, x.options());
+  auto dbeta = at::empty({c}, x.options());
+  launch_bn_backward(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(),
+                     invstd.data_ptr<float>(), opt_ptr(gamma, "gamma", x, c),
+                     sums.data_ptr<float>(), dx.data_ptr<float>(), dgamma.data_ptr<float>(),
+                     dbeta.data_ptr<float>(), n, c, s, cur_stream(x));
+  return {dx, dgamma, dbeta};
+}
+
+void dbn_commit64(at::Tensor& acc, at::Tensor& running_mean, at::Tensor& running_var,
+                  double momentum) {
+  TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kDouble && acc.is_contiguous(),
+              "acc must be a contiguous float64 GPU tensor");
+  const int64_t c = running_mean.numel();
+  check_f32(running_mean, "running_mean", running_mean);
+  check_f32(running_var, "running_var", running_mean);
+  TORCH_CHECK(acc.numel() == 3 * c && running_var.numel() == c, "acc must be [3][C]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(acc.device());
+  launch_dbn_commit64(acc.data_ptr<double>(), running_mean.data_ptr<float>(),
+                      running_var.data_ptr<float>(), c, momentum, cur_stream(running_mean));
+}
+
 }  // namespace
 }  // namespace tgpipe
 
 TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
+  m.def("bn_train_forward(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? acc, float eps) "
+        "-> Tensor[]");
+  m.def("bn_train_backward(Tensor dy, Tensor x, Tensor mean, Tensor invstd, Tensor? gamma) "
+        "-> Tensor[]");
+  m.def("dbn_commit64(Tensor(a!) acc, Tensor(b!) running_mean, Tensor(c!) running_var, "
+        "float momentum) -> ()");
   m.def("convbn_forward(Tensor x, Tensor[] weights, int[] geo, bool relu, Tensor? gamma, "
         "Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "Tensor(c!)? num_batches_tracked, float momentum, float eps, Tensor? add) -> Tensor[]");
@@ -387,4 +465,7 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("conv_gemm_forward", &tgpipe::conv_gemm_forward);
   m.impl("conv_gemm_backward_data", &tgpipe::conv_gemm_backward_data);
   m.impl("conv_gemm_backward_weight", &tgpipe::conv_gemm_backward_weight);
+  m.impl("bn_train_forward", &tgpipe::bn_train_forward);
+  m.impl("bn_train_backward", &tgpipe::bn_train_backward);
+  m.impl("dbn_commit64", &tgpipe::dbn_commit64);
 }

@@ -160,11 +160,15 @@ void launch_bn_stats(const float* z, float* part_mean, float* part_m2, int64_t n
 // blocks of `width` columns (`total` columns per channel) are merged with Chan's formula
 // in fp64 into mean / invstd; the running statistics get the EMA with factor `momentum`
 // (unbiased variance) when running_mean is non-null, and `tracked` (BatchNorm's
-// num_batches_tracked, may be null) is incremented in the same launch.
+// num_batches_tracked, may be null) is incremented in the same launch.  `acc` (may be
+// null): DeferredBatchNorm's fp64 [3][C] (count, mean, M2) accumulators, Chan-merged.
 void launch_bn_finalize(const float* part_mean, const float* part_m2, int blocks, int width,
                         int64_t total, int64_t c, float eps, double momentum, float* mean,
                         float* invstd, float* running_mean, float* running_var, int64_t* tracked,
-                        hipStream_t stream);
+                        double* acc, hipStream_t stream);
+// DeferredBatchNorm commit from the fp64 accumulators; zeroes them.
+void launch_dbn_commit64(double* acc, float* running_mean, float* running_var, int64_t c,
+                         double momentum, hipStream_t stream);
 // y[n][c][p] = (z - mean) * invstd * gamma + beta (+ add[n][c][p]), planes of s pixels.
 void launch_bn_apply(const float* z, const float* mean, const float* invstd, const float* gamma,
                      const float* beta, const float* add, float* y, int64_t n, int64_t c,

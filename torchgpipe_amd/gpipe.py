@@ -30,6 +30,7 @@ from torchgpipe_amd.pipeline import Pipeline
 from torchgpipe_amd.skip.layout import inspect_skip_layout
 from torchgpipe_amd.skip.skippable import verify_skippables
 from torchgpipe_amd.stream import AbstractStream, StreamPool
+from torchgpipe_amd.ops.conv import new_step as wino_new_step
 from torchgpipe_amd.utils.meta import is_meta, materialize
 from torchgpipe_amd.worker import WorkerPool
 
@@ -263,6 +264,7 @@ class GPipe(nn.Module):
         if not self._peers_ready:
             enable_peer_access(self.devices)
             self._peers_ready = True
+        wino_new_step()  # weights may have changed since the last step (even via .data)
         batches = microbatch.scatter(input, self.chunks)
         if self._has_dbn:
             set_micro_batches(self, len(batches))

@@ -9,9 +9,20 @@ wrw (see ``_wgrad_f4`` and ``_wgrad_on_mfma``).
 Other configurations, CPU tensors and non-fp32 dtypes use ``F.conv2d``.
 
 The Winograd-domain weights ``U = G g Gᵀ`` (and the rotated/transposed ``U'``
-of backward-data) are cached per parameter version: a pipeline step runs the
-same weights over every micro-batch (forward, recompute, backward), so the
-transform runs once per optimizer step instead of once per call.
+of backward-data) are cached per parameter version *and pipeline step*: a step
+runs the same weights over every micro-batch (forward, recompute, backward), so
+the transform runs once per optimizer step instead of once per call.
+
+* Staleness: the key includes a step counter that ``GPipe.forward`` /
+  ``PipelineStage.forward`` advance (:func:`new_step`), so weights changed
+  between steps through ``param.data`` (which does not bump ``_version``), EMA
+  swaps or manual surgery are always re-transformed; :func:`clear_winograd_caches`
+  drops a module's caches explicitly.
+* Memory: every cached byte counts against one process-wide budget
+  (``TGPIPE_WINOGRAD_CACHE_MB``, default 5 % of the device's memory).  A
+  transform that would exceed it is used for the call and then dropped, so giant
+  models (U-Net(48, 576)'s 18432-channel layers) keep the memory footprint of
+  the uncached path.
 """
 import os
 from typing import Dict, Optional, Tuple
@@ -22,34 +33,86 @@ import torch.nn.functional as F
 
 from torchgpipe_amd.ops import _ext
 
-__all__ = ['WinogradConv2d', 'winograd_conv2d', 'wino_eligible']
+__all__ = ['WinogradConv2d', 'winograd_conv2d', 'wino_eligible', 'new_step',
+           'clear_winograd_caches', 'cache_bytes']
+
+_STEP = 0
+_CACHE_BYTES = 0
+_BUDGET: Optional[int] = None
+
+
+def new_step() -> None:
+    """Start a new pipeline step: every cached weight transform is re-validated."""
+    global _STEP
+    _STEP += 1
+
+
+def cache_bytes() -> int:
+    """Bytes currently held by Winograd weight-transform caches (this process)."""
+    return _CACHE_BYTES
+
+
+def _budget(device: torch.device) -> int:
+    global _BUDGET
+    if _BUDGET is None:
+        mb = os.environ.get('TGPIPE_WINOGRAD_CACHE_MB')
+        if mb is not None:
+            _BUDGET = int(float(mb) * (1 << 20))
+        else:
+            _BUDGET = torch.cuda.get_device_properties(device).total_memory // 20
+    return _BUDGET
 
 
 class _TransformCache:
-    """Winograd-domain weights keyed by (storage, version, device) of the parameter.
+    """Winograd-domain weights keyed by (storage, version, device, step) of the parameter.
 
     Entries per (flip, f4): F(2x2) ``U[Rp][Op][16]`` and F(4x4) ``U4[Rp/4][Op/16][4][16][36]``.
     """
 
-    __slots__ = ('_entries',)
+    __slots__ = ('_entries', '__weakref__')
 
     def __init__(self) -> None:
-        self._entries: Dict[Tuple[bool, bool], Tuple[Tuple[int, int, torch.device], Tensor]] = {}
+        self._entries: Dict[Tuple[bool, bool], Tuple[Tuple[int, int, torch.device, int],
+                                                     Tensor]] = {}
 
     def get(self, weight: Tensor, flip: bool, f4: bool = False) -> Tensor:
-        key = (weight.data_ptr(), weight._version, weight.device)
+        global _CACHE_BYTES
+        key = (weight.data_ptr(), weight._version, weight.device, _STEP)
         hit = self._entries.get((flip, f4))
         if hit is not None and hit[0] == key:
             return hit[1]
+        if hit is not None:  # stale: release before transforming again
+            _CACHE_BYTES -= hit[1].numel() * hit[1].element_size()
+            del self._entries[(flip, f4)]
         ops = _ext.require(weight)
         with torch.no_grad():
             w = weight.detach().contiguous()
             u = ops.wino4_weight(w, flip) if f4 else ops.wino_weight(w, flip)
-        self._entries[(flip, f4)] = (key, u)
+        size = u.numel() * u.element_size()
+        if _CACHE_BYTES + size <= _budget(weight.device):
+            self._entries[(flip, f4)] = (key, u)
+            _CACHE_BYTES += size
         return u
 
     def clear(self) -> None:
+        global _CACHE_BYTES
+        for _, u in self._entries.values():
+            _CACHE_BYTES -= u.numel() * u.element_size()
         self._entries.clear()
+
+    def __del__(self) -> None:
+        try:
+            self.clear()
+        except Exception:  # interpreter shutdown
+            pass
+
+
+def clear_winograd_caches(module: torch.nn.Module) -> None:
+    """Drop the cached weight transforms of every WinogradConv2d in ``module``."""
+    for m in module.modules():
+        cache = getattr(m, '_wino', None)
+        if isinstance(cache, _TransformCache):
+            cache.clear()
 
 
 # Winograd F(4x4,3x3) (csrc/winograd_f4.hip) on planes of at least this size; F(2x2) on

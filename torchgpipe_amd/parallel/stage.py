@@ -40,6 +40,7 @@ from torchgpipe_amd.batchnorm import DeferredBatchNorm, set_micro_batches
 from torchgpipe_amd.checkpoint import Checkpointing
 from torchgpipe_amd.gpipe import check_balance, partition_layers, verify_module
 from torchgpipe_amd.microbatch import Batch
+from torchgpipe_amd.ops.conv import new_step as wino_new_step
 from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P, _wait
 from torchgpipe_amd.skip.layout import SkipLayout, inspect_skip_layout
 from torchgpipe_amd.skip.namespace import Namespace
@@ -405,6 +406,7 @@ class PipelineStage:
         """
         if input is not None:
             microbatch.check(input)
+        wino_new_step()  # weights may have changed since the last step (even via .data)
         sig = self._agree_signature(input, signature)
         if sig != self._sig:
             self._sig = sig
