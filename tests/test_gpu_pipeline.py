@@ -179,3 +179,42 @@ def test_deferred_batch_norm_native_forward_backward_match_fp64():
     torch.testing.assert_close(dbn.weight.grad.double(), ref.weight.grad, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dbn.bias.grad.double(), ref.bias.grad, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dbn.running_var.double(), ref.running_var, rtol=1e-5, atol=1e-6)
+
+
+def test_tuple_boundary_is_one_packed_peer_copy():
+    """K5/K6: a 2-tensor hop between GPUs is packed into one transfer (views arrive)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip('needs 2 GPUs')
+    from torchgpipe_amd import copy as copymod
+    from tests.distributed import parity
+    model = parity.build('amoebanet')
+    gpipe = GPipe(model, [3, len(model) - 3], devices=[0, 1], chunks=2, checkpoint='never')
+    x, t = parity.data('amoebanet', torch.device('cuda', 0))
+    before = copymod.packed_hops
+    out = gpipe(x)
+    assert copymod.packed_hops - before == 2  # one packed hop per micro-batch
+    F.cross_entropy(out, t.to(out.device)).backward()
+    assert copymod.packed_hops - before == 4  # and one per micro-batch for the gradients
+
+
+def test_gather_writes_preallocated_output_during_pipeline():
+    """K11: the last partition's outputs land in one preallocated buffer (no torch.cat);
+    backward hands each micro-batch a view of the gradient."""
+    model = small_unet()
+    ref = copy.deepcopy(model).cuda()
+    gpipe = GPipe(model, [10, len(model) - 10], devices=[0, 0], chunks=4,
+                  checkpoint='except_last')
+    for m in list(gpipe.modules()) + list(ref.modules()):
+        if hasattr(m, 'p'):
+            m.p = 0.0
+    x = torch.rand(8, 3, 32, 32, device='cuda')
+    out = gpipe(x)
+    assert type(out.grad_fn).__name__ == '_GatherIntoBackward'
+    want = ref(x)
+    torch.testing.assert_close(out, want, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(out)
+    out.backward(g)
+    want.backward(g)
+    for p, q in zip(gpipe.parameters(), ref.parameters()):
+        err = ((p.grad - q.grad).norm() / q.grad.norm()).item()
+        assert err < 1e-4, (p.shape, err)

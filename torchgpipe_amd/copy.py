@@ -11,6 +11,13 @@ overlaps with compute on both sides.  The allocator is told about the
 cross-stream lifetimes with ``record_stream`` on both ends.  Backward copies
 the gradients in the reverse direction on the same stream pair.
 
+A multi-tensor hop between two GPUs (AmoebaNet's ``(x, skip)`` boundaries,
+their gradients, several skips bound for one partition) is *packed*: the HIP
+segment-copy kernel (``copy_segments``) gathers the tensors into one byte
+buffer on the source GPU, one peer copy moves it over xGMI, and the
+destination tensors are zero-copy views into the received buffer -- one DMA
+per hop instead of one per tensor.
+
 ``Wait`` is a value identity that inserts a stream→stream dependency
 (HIP event record + wait): forward makes ``next`` wait for ``prev``;
 backward makes ``prev`` wait for ``next``.
@@ -23,9 +30,38 @@ from torch import Tensor
 from torchgpipe_amd.stream import (AbstractStream, current_stream, get_device, record_stream,
                                    use_stream, wait_stream)
 
-__all__: List[str] = []
-
 Tensors = Tuple[Tensor, ...]
+
+# counters of packed hops (tests / diagnostics)
+packed_hops = 0
+
+
+def _packable(tensors: Tensors, device: torch.device) -> bool:
+    if len(tensors) < 2 or device.type != 'cuda':
+        return False
+    src = tensors[0].device
+    return (src.type == 'cuda' and src != device
+            and all(t.device == src and not t.is_sparse for t in tensors))
+
+
+def _packed_transfer(tensors: Tensors, device: torch.device) -> List[Tensor]:
+    """Pack on the source GPU, one peer copy, views on the destination (current streams)."""
+    global packed_hops
+    from torchgpipe_amd.ops import misc
+    nbytes = misc.packed_nbytes(tensors)
+    buf = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=tensors[0].device)
+    misc.pack([t.detach() for t in tensors], buf)
+    moved = buf.to(device, non_blocking=True)
+    out: List[Tensor] = []
+    pos = 0
+    for t in tensors:
+        size = t.numel() * t.element_size()
+        out.append(moved[pos:pos + size].view(t.dtype).view(t.shape))
+        pos = (pos + size + 15) // 16 * 16
+    packed_hops += 1
+    return out
+
+__all__: List[str] = []
 
 
 def _transfer(tensors: Tensors,
@@ -35,6 +71,13 @@ def _transfer(tensors: Tensors,
               consumer_stream: AbstractStream) -> List[Tensor]:
     out: List[Tensor] = []
     with use_stream(src_stream), use_stream(dst_stream):
+        if _packable(tensors, device):
+            out = _packed_transfer(tensors, device)
+            for x in tensors:
+                record_stream(x, src_stream)
+            for y in out:
+                record_stream(y, consumer_stream)
+            return out
         for x in tensors:
             # Peer (GPU→GPU) copies are stream-ordered; anything touching the
             # host must stay blocking because CPU "streams" carry no ordering.

@@ -86,9 +86,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
          q += stride) {
       const int64_t ch = (4 * q / s) % c;
       const float k = invstd[ch] * (gamma ? gamma[ch] : 1.f);
-      const float b = (beta ? beta[ch] : 0.f) - mean[ch] * k;
-      floatx4 v = reinterpret_cast<const floatx4*>(z)[q];
-      v = v * k + b;
+      const float b = beta ? beta[ch] : 0.f;
+      const float mu = mean[ch];
+      // (z - mean) * k, not z * k - mean * k: no cancellation when |mean| >> std
+      floatx4 v = (reinterpret_cast<const floatx4*>(z)[q] - mu) * k + b;
       if constexpr (kAdd) v += reinterpret_cast<const floatx4*>(add)[q];
       reinterpret_cast<floatx4*>(y)[q] = v;
     }

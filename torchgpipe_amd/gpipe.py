@@ -269,11 +269,16 @@ class GPipe(nn.Module):
         if self._has_dbn:
             set_micro_batches(self, len(batches))
         copy_streams = self._ensure_copy_streams()
+        # K11: outputs land in preallocated buffers on the last device's copy streams
+        # while later micro-batches still compute (no torch.cat after the pipeline)
+        gatherer = microbatch.Gatherer([b[0].shape[0] if b[0].dim() else 1 for b in batches],
+                                       copy_streams[-1])
         pipeline = Pipeline(batches, list(self.partitions), self.devices, copy_streams,
                             self._skip_layout, self.checkpoint_stop(),
-                            queues=self._workers.queues(self.devices))
+                            queues=self._workers.queues(self.devices),
+                            on_output=gatherer.put)
         pipeline.run()
-        return microbatch.gather(batches)
+        return gatherer.result(batches)
 
     def __getstate__(self) -> Any:
         state = self.__dict__.copy()

@@ -9,7 +9,7 @@ tensors of a micro-batch without re-wrapping.
 number of micro-batches may be smaller than ``chunks`` (N=6, chunks=4 → 3).
 """
 import typing
-from typing import Callable, Iterator, List, Tuple, Union, cast
+from typing import Callable, Iterator, List, Optional, Sequence, Tuple, Union, cast
 
 import torch
 from torch import Tensor
@@ -126,3 +126,96 @@ def gather(outputs: List[Batch]) -> TensorOrTensors:
         return torch.cat(tuple(b.tensor for b in outputs))
     columns = zip(*(b.tensors for b in outputs))
     return tuple(torch.cat(col) for col in columns)
+
+
+class _GatherInto(torch.autograd.Function):
+    """Autograd view of buffers that already hold every micro-batch's output.
+
+    Forward returns the buffers (filled by :class:`Gatherer` while the pipeline ran);
+    backward hands each micro-batch output its slice of the gradient -- views, no copy
+    (the reference's ``torch.cat`` backward also slices).
+    """
+
+    @staticmethod
+    def forward(ctx, bounds: List[Tuple[int, int]], nbuf: int,  # type: ignore[override]
+                *tensors: Tensor) -> Tensors:
+        ctx.bounds = bounds
+        ctx.nbuf = nbuf
+        return tuple(b.detach() for b in tensors[:nbuf])
+
+    @staticmethod
+    def backward(ctx, *grads: Tensor):  # type: ignore[override]
+        out: List[Optional[Tensor]] = [None, None] + [None] * ctx.nbuf
+        for lo, hi in ctx.bounds:
+            for g in grads:
+                out.append(None if g is None else g[lo:hi])
+        return tuple(out)
+
+
+class Gatherer:
+    """K11 zero-copy gather: micro-batch outputs land in preallocated mini-batch buffers.
+
+    ``put(i, batch)`` runs when micro-batch ``i`` leaves the last partition: its tensors
+    are copied into their slice of the output buffers on a side stream (overlapping the
+    remaining micro-batches' compute) instead of one ``torch.cat`` after the pipeline;
+    :meth:`result` fences the side streams and returns the buffers through
+    :class:`_GatherInto`.  Falls back to :func:`gather` when an output's first
+    dimension is not its micro-batch size, or on CPU.
+    """
+
+    def __init__(self, sizes: Sequence[int], streams: Optional[Sequence[object]] = None) -> None:
+        self.sizes = list(sizes)
+        self.bounds: List[Tuple[int, int]] = []
+        pos = 0
+        for n in self.sizes:
+            self.bounds.append((pos, pos + n))
+            pos += n
+        self.total = pos
+        self.streams = streams
+        self.buffers: Optional[List[Tensor]] = None
+        self.atomic = True
+        self.ok = True
+        self.used: List[object] = []
+
+    def put(self, i: int, batch: Batch) -> None:
+        from torchgpipe_amd.stream import current_stream, record_stream, use_stream, wait_stream
+        if not self.ok:
+            return
+        tensors = list(batch)
+        if self.buffers is None:
+            self.atomic = batch.atomic
+            if any(not isinstance(t, Tensor) or not t.is_cuda or t.dim() == 0
+                   for t in tensors):
+                self.ok = False
+                return
+            self.buffers = [torch.empty((self.total, *t.shape[1:]), dtype=t.dtype,
+                                        device=t.device) for t in tensors]
+        lo, hi = self.bounds[i]
+        if len(tensors) != len(self.buffers) or any(not isinstance(t, Tensor) for t in tensors) \
+                or any(
+                t.shape[0] != hi - lo or t.shape[1:] != b.shape[1:] or t.dtype != b.dtype
+                or t.device != b.device for t, b in zip(tensors, self.buffers)):
+            self.ok = False
+            return
+        compute = current_stream(tensors[0].device)
+        side = self.streams[i] if self.streams is not None else compute
+        wait_stream(side, compute)  # type: ignore[arg-type]
+        with use_stream(side):  # type: ignore[arg-type]
+            for t, b in zip(tensors, self.buffers):
+                b[lo:hi].copy_(t.detach(), non_blocking=True)
+                record_stream(t, side)  # type: ignore[arg-type]
+        self.used.append(side)
+
+    def result(self, outputs: List[Batch]) -> TensorOrTensors:
+        from torchgpipe_amd.stream import current_stream, wait_stream
+        if not self.ok or self.buffers is None:
+            return gather(outputs)
+        compute = current_stream(self.buffers[0].device)
+        seen = set()
+        for side in self.used:
+            if id(side) not in seen:
+                seen.add(id(side))
+                wait_stream(compute, side)  # type: ignore[arg-type]
+        flat = [t for b in outputs for t in b]
+        out = _GatherInto.apply(self.bounds, len(self.buffers), *self.buffers, *flat)
+        return out[0] if self.atomic else tuple(out)

@@ -261,12 +261,19 @@ MIN_CHANNELS = 8
 # TGPIPE_WINOGRAD=0: every convolution on MIOpen (F.conv2d), no weight-transform caches.
 WINOGRAD_ENABLED = os.environ.get('TGPIPE_WINOGRAD', '1') != '0'
 
+# A layer whose F(2x2) weight transform (16 floats per channel pair, 1.78x the weight)
+# would pass this stays on MIOpen: giant models (U-Net(48,576)'s 18432^2 bottleneck
+# convolutions, 21.7 GB per transform) must not need a transient copy of that size.
+MAX_TRANSFORM_BYTES = int(float(os.environ.get('TGPIPE_WINOGRAD_MAX_TRANSFORM_MB', '2048'))
+                          * (1 << 20))
+
 
 def wino_eligible(x: Tensor, weight: Tensor, stride=(1, 1), padding=(1, 1), dilation=(1, 1),
                   groups: int = 1) -> bool:
     """Whether the HIP Winograd kernel computes this convolution."""
     return (WINOGRAD_ENABLED and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
             and weight.shape[1] >= MIN_CHANNELS
+            and weight.shape[0] * weight.shape[1] * 16 * 4 <= MAX_TRANSFORM_BYTES
             and weight.dtype == torch.float32 and tuple(weight.shape[2:]) == (3, 3)
             and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
             and tuple(dilation) == (1, 1) and groups == 1)
@@ -295,7 +302,8 @@ class WinogradConv2d(nn.Conv2d):
         # few-channel convolutions (U-Net's 3-channel input) on the implicit-GEMM kernel:
         # no MIOpen kernel to compile on the first step
         from torchgpipe_amd.ops.convbn import gemm_conv2d, gemm_conv_eligible
-        if WINOGRAD_ENABLED and gemm_conv_eligible(input, self):
+        if WINOGRAD_ENABLED and self.weight.shape[1] < MIN_CHANNELS and \
+                gemm_conv_eligible(input, self):
             return gemm_conv2d(input, self)
         return super().forward(input)
 

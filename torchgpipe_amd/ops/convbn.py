@@ -118,7 +118,11 @@ def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.Batch
 
 
 def fusable(x: Tensor, convs: Sequence[nn.Conv2d], bn: nn.Module) -> bool:
+    limit = (1 << 31) - 64  # 32-bit buffer offsets of the kernels
+    co = sum(c.out_channels for c in convs)
     return (_ENABLED and _bn_ok(bn, x) and all(conv_supported(c) for c in convs)
+            and x.numel() * 4 < limit and x.numel() // max(1, x.shape[1]) * co * 4 < limit
+            and all(c.weight.numel() * 4 < limit for c in convs)
             and _ext.available()
             and all(c.weight.dtype == torch.float32 and c.weight.is_cuda for c in convs))
 
@@ -175,7 +179,11 @@ def gemm_conv_eligible(x: Tensor, conv: nn.Conv2d) -> bool:
     """Convolutions the implicit-GEMM kernels take without BatchNorm: any kernel at
     stride 1 or a strided 1x1, no bias / groups / dilation, fp32 on the GPU."""
     kh, kw = conv.kernel_size
+    limit = (1 << 31) - 64  # 32-bit buffer offsets of the kernels
+    out_numel = x.numel() // max(1, x.shape[1]) * conv.out_channels if x.dim() == 4 else 0
     return (_ENABLED and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and x.numel() * 4 < limit and conv.weight.numel() * 4 < limit
+            and out_numel * 4 < limit
             and conv.weight.dtype == torch.float32 and conv.bias is None and conv.groups == 1
             and tuple(conv.dilation) == (1, 1) and conv.padding_mode == 'zeros'
             and isinstance(conv.padding, tuple)

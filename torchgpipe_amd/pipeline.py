@@ -84,6 +84,7 @@ class Pipeline:
                  skip_layout: Optional[SkipLayout] = None,
                  checkpoint_stop: int = 0,
                  queues: Optional[Tuple[List[InQueue], List[OutQueue]]] = None,
+                 on_output: Optional[Callable[[int, Batch], None]] = None,
                  ) -> None:
         self.batches = batches
         self.partitions = partitions
@@ -98,6 +99,8 @@ class Pipeline:
         self.skip_layout = skip_layout
         self.checkpoint_stop = checkpoint_stop
         self._queues = queues
+        # called with (i, batch) as micro-batch i leaves the last partition (K11 gather)
+        self.on_output = on_output
 
     def run(self) -> None:
         m = len(self.batches)
@@ -160,6 +163,8 @@ class Pipeline:
                 wait(batch, streams[j], copy_streams[j][i])
             with use_device(devices[j]):
                 task.finalize(batch)
+                if j == n - 1 and self.on_output is not None:
+                    self.on_output(i, batch)
             batches[i] = batch
 
         if exc_info is not None:
