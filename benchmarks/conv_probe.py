@@ -16,7 +16,8 @@ from torchgpipe_amd.ops import _ext  # noqa: E402
 def main() -> None:
     p = argparse.ArgumentParser()
     p.add_argument('--shape', type=int, nargs=4, default=[40, 128, 128, 96], help='N C K H')
-    p.add_argument('--op', choices=['fwd', 'wgrad', 'fwd4', 'wgrad4', 'fwd4nf', 'wgrad4nf'], default='fwd')
+    p.add_argument('--op', choices=['fwd', 'wgrad', 'fwd4', 'wgrad4', 'fwd4nf', 'wgrad4nf'],
+                   default='fwd')
     p.add_argument('--iters', type=int, default=20)
     a = p.parse_args()
     n, c, k, h = a.shape

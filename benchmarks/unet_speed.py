@@ -1,7 +1,8 @@
 """U-Net(5,64) speed benchmark (reference: benchmarks/unet-speed/main.py:23-68).
 
     python benchmarks/unet_speed.py pipeline-8 --devices 0,1,2,3,4,5,6,7
-    python -m torch.distributed.run --nproc-per-node 8 benchmarks/unet_speed.py pipeline-8 --mode stage
+    python -m torch.distributed.run --nproc-per-node 8 benchmarks/unet_speed.py pipeline-8 \\
+        --mode stage
 """
 import torch
 import torch.nn.functional as F

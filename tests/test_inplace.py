@@ -4,7 +4,8 @@ from torch import nn
 
 from torchgpipe_amd import GPipe
 
-LEAF_INPLACE = 'a leaf Variable that requires grad (is being|has been) used in an in-place operation.'
+LEAF_INPLACE = ('a leaf Variable that requires grad (is being|has been) used in an in-place '
+                'operation.')
 
 
 def test_inplace_on_requires_grad():

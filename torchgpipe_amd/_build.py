@@ -26,7 +26,8 @@ TARGET = os.path.join(HERE, '_C.so')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
 ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 
-KERNEL_SOURCES = ['kernels.hip', 'winograd.hip', 'winograd_f4.hip', 'conv_gemm.hip', 'batchnorm.hip']
+KERNEL_SOURCES = ['kernels.hip', 'winograd.hip', 'winograd_f4.hip', 'conv_gemm.hip',
+                  'batchnorm.hip']
 HOST_SOURCES = ['bindings.cpp', 'convbn.cpp']
 HEADERS = ['kernels.h', 'philox.h']
 

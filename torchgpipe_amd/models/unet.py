@@ -30,6 +30,7 @@ import torch.nn.functional as F
 from torchgpipe_amd.models.flatten import flatten_sequential
 from torchgpipe_amd.ops.conv import WinogradConv2d
 from torchgpipe_amd.ops.convbn import GemmConv2d
+from torchgpipe_amd.ops.dropout import Dropout2d
 from torchgpipe_amd.ops.fused import DropNormAct
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
@@ -64,7 +65,7 @@ def conv_block(in_channels: int, out_channels: int, fused: bool) -> nn.Sequentia
         layers['norm'] = nn.Identity()
         layers['relu'] = nn.Identity()
     else:
-        layers['dropout'] = nn.Dropout2d(p=0.1)
+        layers['dropout'] = Dropout2d(p=0.1)  # Philox, replayed from the checkpoint tape
         layers['norm'] = nn.InstanceNorm2d(out_channels)
         layers['relu'] = nn.LeakyReLU(negative_slope=1e-2)
     return nn.Sequential(layers)

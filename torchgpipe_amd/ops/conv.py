@@ -25,7 +25,7 @@ the transform runs once per optimizer step instead of once per call.
   the uncached path.
 """
 import os
-from typing import Dict, Optional, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -268,7 +268,8 @@ MAX_TRANSFORM_BYTES = int(float(os.environ.get('TGPIPE_WINOGRAD_MAX_TRANSFORM_MB
                           * (1 << 20))
 
 
-def wino_eligible(x: Tensor, weight: Tensor, stride=(1, 1), padding=(1, 1), dilation=(1, 1),
+def wino_eligible(x: Tensor, weight: Tensor, stride: Sequence[int] = (1, 1),
+                  padding: Sequence[int] = (1, 1), dilation: Sequence[int] = (1, 1),
                   groups: int = 1) -> bool:
     """Whether the HIP Winograd kernel computes this convolution."""
     return (WINOGRAD_ENABLED and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32

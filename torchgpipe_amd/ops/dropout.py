@@ -1,8 +1,12 @@
-"""Elementwise inverted dropout with explicit Philox ``(seed, offset)`` (K4).
+"""Inverted dropout with explicit Philox ``(seed, offset)`` (K4).
 
-Unlike ``nn.Dropout`` it stores no mask: backward regenerates it from the
-saved ``(seed, offset)``, and checkpoint recomputation replays the same pair
-from the cell's RNG tape instead of restoring global generator state.
+:class:`Dropout` (elementwise) and :class:`Dropout2d` (whole channels) are
+drop-in replacements for ``nn.Dropout`` / ``nn.Dropout2d`` used by the model
+zoo.  Their randomness comes from :func:`~torchgpipe_amd.utils.rng.philox_pair`,
+so checkpoint recomputation replays the cell's recorded ``(seed, offset)``
+pairs from its RNG tape instead of restoring global generator state from an
+autograd thread (the reference's ``fork_rng``, ``torchgpipe/checkpoint.py:191-231``).
+The elementwise kernel stores no mask: backward regenerates it from the pair.
 """
 from typing import Tuple
 
@@ -14,7 +18,7 @@ from torchgpipe_amd.ops.fused import _signed64
 from torchgpipe_amd.ops.philox import uniform
 from torchgpipe_amd.utils.rng import philox_pair
 
-__all__ = ['dropout', 'Dropout']
+__all__ = ['dropout', 'Dropout', 'dropout2d', 'Dropout2d']
 
 
 def _reference(x: Tensor, p: float, seed: int, offset: int) -> Tensor:
@@ -58,3 +62,47 @@ class Dropout(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
         return dropout(x, self.p, self.training)
+
+
+class _Dropout2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: Tensor, scale: Tensor) -> Tensor:  # type: ignore[override]
+        ctx.save_for_backward(scale)
+        return x * scale
+
+    @staticmethod
+    def backward(ctx, dy: Tensor) -> Tuple:  # type: ignore[override]
+        (scale,) = ctx.saved_tensors
+        return dy * scale, None
+
+
+def dropout2d(x: Tensor, p: float = 0.5, training: bool = True) -> Tensor:
+    """Channel dropout: each (image, channel) plane is kept with probability ``1 - p``."""
+    if not training or p == 0.0:
+        return x
+    if p >= 1.0:
+        return x * 0.0
+    planes = x.shape[0] * x.shape[1]
+    seed, offset = philox_pair(x.device, planes)
+    if x.is_cuda:
+        u = _ext.require(x).philox_uniform(planes, _signed64(seed), _signed64(offset), x.device)
+    else:
+        u = uniform(planes, seed, offset)
+    keep = (u >= p).to(x.dtype).view(x.shape[0], x.shape[1], *([1] * (x.dim() - 2)))
+    return _Dropout2d.apply(x, keep.to(x.device) / (1.0 - p))
+
+
+class Dropout2d(nn.Module):
+    """``nn.Dropout2d`` on tape-replayable Philox draws."""
+
+    def __init__(self, p: float = 0.5) -> None:
+        super().__init__()
+        if not 0.0 <= p <= 1.0:
+            raise ValueError(f'dropout probability has to be between 0 and 1, but got {p}')
+        self.p = p
+
+    def extra_repr(self) -> str:
+        return f'p={self.p}'
+
+    def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
+        return dropout2d(x, self.p, self.training)

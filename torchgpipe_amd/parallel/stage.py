@@ -439,7 +439,7 @@ class PipelineStage:
             else:
                 act_msg = self.p2p.recv(prev, self._key('act', i, prev, me))  # type: ignore[arg-type]
                 in_atomic = True
-            skip_msgs = [(self.p2p.recv(self.ranks[src], self._key('skip', i, self.ranks[src], me)))
+            skip_msgs = [self.p2p.recv(self.ranks[src], self._key('skip', i, self.ranks[src], me))
                          for src in sorted({s for s, _ in self.in_skips})]
             if act_msg is not None:
                 acts = act_msg.wait()
@@ -500,8 +500,9 @@ class PipelineStage:
                 grad_msg = self.p2p.recv(nxt, self._key('gact', i, nxt, me))
             skip_grad_msgs = []
             for dst in sorted({d for d, _ in self.out_skips}):
+                peer = self.ranks[dst]
                 skip_grad_msgs.append(
-                    (dst, self.p2p.recv(self.ranks[dst], self._key('gskip', i, self.ranks[dst], me))))
+                    (dst, self.p2p.recv(peer, self._key('gskip', i, peer, me))))
             # 2. ... then recompute while they are in flight
             if cell.chk is not None:
                 with trace.range(f'recompute mb{i} stage{self.rank}'):
@@ -545,7 +546,8 @@ class PipelineStage:
             for (src, _), t in zip(self.in_skips, skip_in):
                 by_src.setdefault(src, []).append(self._grad_of(t))
             for src in sorted(by_src):
-                self.p2p.send(by_src[src], self.ranks[src], self._key('gskip', i, me, self.ranks[src]))
+                peer = self.ranks[src]
+                self.p2p.send(by_src[src], peer, self._key('gskip', i, me, peer))
             cell.inputs = []
             cell.outputs = []
             cell.chk = None
