@@ -62,3 +62,32 @@ def test_sharded_save_load_with_rebalance(tmp_path):
     merged = {**loaded[0], **loaded[1]}
     for k, v in want.state_dict().items():
         torch.testing.assert_close(merged[k], v)
+
+
+def _load_spy(rank, world, directory):
+    import json
+    from unittest import mock
+    from torchgpipe_amd.parallel import PipelineStage
+    stage = PipelineStage(model(), [4, 1], chunks=1)
+    with open(f'{directory}/index.json') as f:
+        layers = json.load(f)['layers']
+    real_load = torch.load
+    opened = []
+
+    def spy(path, *args, **kwargs):
+        opened.append(path.rsplit('/', 1)[1])
+        return real_load(path, *args, **kwargs)
+
+    with mock.patch.object(torch, 'load', spy):
+        state_io.load_sharded(stage, directory)
+    return {'opened': opened, 'layers': layers}
+
+
+def test_load_sharded_reads_only_owning_shards(tmp_path):
+    """with balance [4, 1] rank 1 owns layer 4, stored only in shard rank1.pt."""
+    d = str(tmp_path / 'ckpt')
+    run(_save, 2, tmp_path / 'a', d)
+    got = run(_load_spy, 2, tmp_path / 'b', d)
+    assert got[0]['layers'] == [['0', '1'], ['2', '3', '4']]
+    assert got[0]['opened'] == ['rank0.pt', 'rank1.pt']
+    assert got[1]['opened'] == ['rank1.pt']

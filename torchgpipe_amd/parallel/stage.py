@@ -201,6 +201,8 @@ class PipelineStage:
 
         groups = partition_layers(module, balance)
         parts = [nn.Sequential(g) for g in groups]
+        # every partition's layer names (checkpoint index: which shard holds which layers)
+        self.layer_names = [[name for name, _ in part.named_children()] for part in parts]
         self.layout = inspect_skip_layout(parts)
         partition = parts[self.rank]
         if deferred_batch_norm:

@@ -87,7 +87,9 @@ def save_sharded(stage, directory: str, extra: Optional[dict] = None) -> str:  #
     torch.save({k: v.detach().cpu() for k, v in stage_state_dict(stage).items()}, path)
     if stage.rank == 0:
         index = {'format': 'torchgpipe_amd/partitioned-v1', 'balance': list(stage.balance),
-                 'world': stage.n, 'extra': extra or {}}
+                 'world': stage.n, 'extra': extra or {},
+                 # which layers each shard holds: loaders read only the shards they need
+                 'layers': getattr(stage, 'layer_names', None)}
         with open(os.path.join(directory, 'index.json'), 'w') as f:
             json.dump(index, f, indent=1)
     return path
@@ -96,17 +98,23 @@ def save_sharded(stage, directory: str, extra: Optional[dict] = None) -> str:  #
 def load_sharded(stage, directory: str, strict: bool = True) -> None:  # type: ignore[no-untyped-def]
     """Load this stage from a sharded checkpoint, even if saved with another balance.
 
-    Only the shards that contain this stage's layers are read, with
-    ``weights_only=True`` and ``map_location`` set to the stage's device.
+    Only the shards that hold one of this stage's layers are read (the index records
+    every shard's layer names), with ``weights_only=True`` onto the host; only this
+    stage's tensors then move to its device, so no rank stages foreign shards through
+    its GPU.  Indexes without layer names (older checkpoints) read every shard.
     """
     with open(os.path.join(directory, 'index.json')) as f:
         index = json.load(f)
     mine = set(_layer_names(stage.partition))
+    layers = index.get('layers')
+    ranks = (range(index['world']) if not layers
+             else [r for r, names in enumerate(layers) if mine & set(names)])
     merged: Dict[str, Tensor] = {}
-    for r in range(index['world']):
-        shard = torch.load(os.path.join(directory, f'rank{r}.pt'), map_location=stage.device,
+    for r in ranks:
+        shard = torch.load(os.path.join(directory, f'rank{r}.pt'), map_location='cpu',
                            weights_only=True)
         for key, value in to_sequential_state(shard).items():
             if key.split('.', 1)[0] in mine:
-                merged[key] = value
+                merged[key] = value.to(stage.device)
+        del shard
     stage.partition.load_state_dict(merged, strict=strict)
