@@ -216,3 +216,68 @@ def test_gemm_conv2d_module_matches_conv2d():
     y64.backward(g.double())
     assert rel_err(x.grad, x64.grad) < 2e-6
     assert rel_err(conv.weight.grad, ref.weight.grad) < 5e-6
+
+
+@pytest.mark.parametrize('stride', [1, 2])
+@pytest.mark.parametrize('hw', [(7, 7), (12, 9), (1, 1), (2, 3)])
+@pytest.mark.parametrize('with_add', [False, True])
+def test_avgpool3_matches_fp64(stride, hw, with_add):
+    from torchgpipe_amd.ops.pool import AvgPool3x3
+    _ext.require()
+    torch.manual_seed(0)
+    x = torch.randn(3, 5, *hw, device='cuda', requires_grad=True)
+    ho, wo = (hw[0] - 1) // stride + 1, (hw[1] - 1) // stride + 1
+    add = torch.randn(3, 5, ho, wo, device='cuda', requires_grad=True) if with_add else None
+    pool = AvgPool3x3(stride)
+    y = pool(x, add)
+    x64 = x.detach().double().requires_grad_()
+    ref = F.avg_pool2d(x64, 3, stride, 1, count_include_pad=False)
+    if with_add:
+        add64 = add.detach().double().requires_grad_()
+        ref = ref + add64
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.double(), ref, rtol=1e-6, atol=1e-6)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ref.backward(dy.double())
+    torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-6, atol=1e-6)
+    if with_add:
+        torch.testing.assert_close(add.grad.double(), add64.grad)
+
+
+def test_fused_gradient_accumulation_matches_autograd(monkeypatch):
+    """Micro-batch loop: weight / BN-affine gradients accumulated by the kernels in place
+    (ops/gradacc.py) equal autograd's accumulation; autograd.grad still returns them."""
+    from torchgpipe_amd.ops import gradacc
+    from torchgpipe_amd.ops.convbn import GemmConv2d, ReLUConvBN
+    _ext.require()
+    torch.manual_seed(0)
+
+    def build():
+        torch.manual_seed(1)
+        return nn.Sequential(
+            ReLUConvBN(nn.ReLU(), nn.Conv2d(16, 32, (1, 7), padding=(0, 3), bias=False),
+                       nn.BatchNorm2d(32)),
+            GemmConv2d(32, 8, 1, bias=False)).cuda()
+
+    xs = [torch.randn(4, 16, 9, 9, device='cuda') for _ in range(3)]
+    fused = build()
+    for x in xs:
+        fused(x).square().sum().backward()
+    monkeypatch.setattr(gradacc, '_ENABLED', False)
+    plain = build()
+    for x in xs:
+        plain(x).square().sum().backward()
+    for (name, a), b in zip(fused.named_parameters(), plain.parameters()):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-5, msg=name)
+    monkeypatch.setattr(gradacc, '_ENABLED', True)
+    params = list(fused.parameters())
+    before = [p.grad.clone() for p in params]
+    got = torch.autograd.grad(fused(xs[0]).square().sum(), params)
+    for p, b in zip(params, before):
+        torch.testing.assert_close(p.grad, b)  # untouched by autograd.grad
+    plain.zero_grad(set_to_none=True)
+    monkeypatch.setattr(gradacc, '_ENABLED', False)
+    plain(xs[0]).square().sum().backward()
+    for g, p in zip(got, plain.parameters()):
+        torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-5)

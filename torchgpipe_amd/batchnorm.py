@@ -56,14 +56,15 @@ class _BNTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: Tensor, weight: Optional[Tensor], bias: Optional[Tensor],  # type: ignore[override]
                 acc: Optional[Tensor], eps: float) -> Tensor:
-        y, mean, invstd = _ext.require(x).bn_train_forward(x, weight, bias, acc, eps)
-        ctx.save_for_backward(x, mean, invstd, weight)
+        y, mean, invstd, sums = _ext.require(x).bn_train_forward(x, weight, bias, acc, eps)
+        ctx.save_for_backward(x, mean, invstd, sums, weight)
         return y
 
     @staticmethod
     def backward(ctx, dy: Tensor):  # type: ignore[override]
-        x, mean, invstd, weight = ctx.saved_tensors
-        dx, dgamma, dbeta = _ext.require(dy).bn_train_backward(dy, x, mean, invstd, weight)
+        x, mean, invstd, sums, weight = ctx.saved_tensors
+        dx, dgamma, dbeta = _ext.require(dy).bn_train_backward(dy, x, mean, invstd, sums,
+                                                                weight)
         return (dx, dgamma if ctx.needs_input_grad[1] else None,
                 dbeta if ctx.needs_input_grad[2] else None, None, None)
 

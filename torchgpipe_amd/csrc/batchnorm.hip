@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
     const float* __restrict__ pm, const float* __restrict__ pm2, int blocks, int width,
     int64_t total, int64_t c, float eps, double momentum, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv,
-    int64_t* __restrict__ tracked, double* __restrict__ acc) {
+    int64_t* __restrict__ tracked, double* __restrict__ acc, float* __restrict__ zero2c) {
   const int lane = threadIdx.x & 31;
   const int64_t ch = static_cast<int64_t>(blockIdx.x) * 8 + (threadIdx.x >> 5);
   if (tracked != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *tracked += 1;
@@ -55,6 +55,10 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
     chan_merge(na, ma, m2a, nb, mb, m2b);
   }
   if (ch >= c || lane != 0) return;
+  if (zero2c != nullptr) {  // the backward's [2][C] reduction buffer, zeroed here for free
+    zero2c[ch] = 0.f;
+    zero2c[c + ch] = 0.f;
+  }
   const double var = na > 0.0 ? m2a / na : 0.0;
   mean[ch] = static_cast<float>(ma);
   invstd[ch] = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
@@ -156,12 +160,14 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
     const float* __restrict__ dy, const float* __restrict__ z, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ sums, float* __restrict__ dz, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, int64_t total, int64_t c, int64_t s, float inv_m) {
+    float* __restrict__ dbeta, int acc_gamma, int acc_beta, int64_t total, int64_t c, int64_t s,
+    float inv_m) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
   const int64_t first = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (first < c) {
-    if (dgamma) dgamma[first] = sums[c + first] * invstd[first];
-    if (dbeta) dbeta[first] = sums[first];
+  if (first < c) {  // parameter gradients, accumulated into .grad across micro-batches
+    if (dgamma)
+      dgamma[first] = (acc_gamma ? dgamma[first] : 0.f) + sums[c + first] * invstd[first];
+    if (dbeta) dbeta[first] = (acc_beta ? dbeta[first] : 0.f) + sums[first];
   }
   if constexpr (kVec) {
     for (int64_t q = first; q < total / 4; q += stride) {
@@ -265,10 +271,10 @@ unsigned grid_for(int64_t work) {
 void launch_bn_finalize(const float* part_mean, const float* part_m2, int blocks, int width,
                         int64_t total, int64_t c, float eps, double momentum, float* mean,
                         float* invstd, float* running_mean, float* running_var, int64_t* tracked,
-                        double* acc, hipStream_t stream) {
+                        double* acc, float* zero2c, hipStream_t stream) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(static_cast<unsigned>((c + 7) / 8)),
                      dim3(256), 0, stream, part_mean, part_m2, blocks, width, total, c, eps,
-                     momentum, mean, invstd, running_mean, running_var, tracked, acc);
+                     momentum, mean, invstd, running_mean, running_var, tracked, acc, zero2c);
 }
 
 void launch_dbn_commit64(double* acc, float* running_mean, float* running_var, int64_t c,
@@ -316,7 +322,8 @@ void launch_bn_apply(const float* z, const float* mean, const float* invstd, con
 
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
-                        int64_t n, int64_t c, int64_t s, hipStream_t stream) {
+                        bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
+                        hipStream_t stream) {
   const int64_t total = n * c * s;
   if (total == 0) return;
   // enough (channel, image range) workgroups to cover the chip ~4x
@@ -335,10 +342,12 @@ void launch_bn_backward(const float* dy, const float* z, const float* mean, cons
   const float inv_m = 1.f / static_cast<float>(n * s);
   if (vec)
     hipLaunchKernelGGL((bn_bwd_dz_kernel<true>), dim3(grid), dim3(256), 0, stream, dy, z, mean,
-                       invstd, gamma, sums, dz, dgamma, dbeta, total, c, s, inv_m);
+                       invstd, gamma, sums, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
+                       acc_beta ? 1 : 0, total, c, s, inv_m);
   else
     hipLaunchKernelGGL((bn_bwd_dz_kernel<false>), dim3(grid), dim3(256), 0, stream, dy, z, mean,
-                       invstd, gamma, sums, dz, dgamma, dbeta, total, c, s, inv_m);
+                       invstd, gamma, sums, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
+                       acc_beta ? 1 : 0, total, c, s, inv_m);
 }
 
 }  // namespace tgpipe

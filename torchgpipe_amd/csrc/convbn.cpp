@@ -40,7 +40,8 @@ void launch_one(int mode, const float* a, const float* b, const float* mask, flo
 // Measured launch plans per (mode, device, geometry), like MIOpen's find step: the first
 // launch of a shape times every candidate (tile size x reduction splits) on the current
 // stream and keeps the fastest.  TGPIPE_CG_TUNE=0 uses the static heuristic instead;
-// accumulating launches and stream captures never tune (they cannot re-run freely).
+// stream captures never tune; an accumulating launch times its candidates on a scratch
+// output (`out_numel` floats) so the real output is untouched.
 using PlanKey = std::tuple<int, int, int, int, int, int, int, int, int, int, int, int, int, int,
                            int, int>;
 std::mutex plan_mutex;
@@ -48,13 +49,14 @@ std::map<PlanKey, ConvGemmPlan> plan_cache;
 
 ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* mask, float* out,
                         float* pm, float* pm2, const ConvGemmGeo& g, bool accumulate,
-                        int64_t a_bytes, int64_t b_bytes, const at::Tensor& like) {
+                        int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
+                        int64_t out_numel) {
   static const bool tune = [] {
     const char* v = std::getenv("TGPIPE_CG_TUNE");
     return v == nullptr || std::string(v) != "0";
   }();
   const ConvGemmPlan heuristic = conv_gemm_plan(mode, g);
-  if (!tune || accumulate) return heuristic;
+  if (!tune) return heuristic;
   const hipStream_t stream = cur_stream(like);
   hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &capture) != hipSuccess ||
@@ -65,6 +67,12 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
   std::lock_guard<std::mutex> lock(plan_mutex);
   auto hit = plan_cache.find(key);
   if (hit != plan_cache.end()) return hit->second;
+  at::Tensor scratch;
+  if (accumulate) {
+    scratch = at::empty({out_numel}, like.options());
+    out = scratch.data_ptr<float>();
+    pm = pm2 = nullptr;
+  }
   hipEvent_t t0, t1;
   hipEventCreate(&t0);
   hipEventCreate(&t1);
@@ -190,7 +198,7 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     // (tuning candidates write z without statistics; the real launches follow)
     plans.push_back(tuned_plan(0, weights[i].data_ptr<float>(), x.data_ptr<float>(), nullptr,
                                z.data_ptr<float>(), nullptr, nullptr, p.geo[i], false,
-                               weights[i].numel() * 4, x.numel() * 4, x));
+                               weights[i].numel() * 4, x.numel() * 4, x, z.numel()));
     split = split || plans.back().splits > 1;
   }
   // statistics partials: from the GEMM epilogue (all parts share one column tiling), or
@@ -224,10 +232,11 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
                 "num_batches_tracked must be a 1-element int64 tensor on the input's device");
     tracked = num_batches_tracked->data_ptr<int64_t>();
   }
+  auto sums = at::empty({2, c}, x.options());  // zeroed by the finalize, for the backward
   launch_bn_finalize(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, cols, c,
                      static_cast<float>(eps), momentum, mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), const_cast<float*>(rm), const_cast<float*>(rv),
-                     tracked, nullptr, stream);
+                     tracked, nullptr, sums.data_ptr<float>(), stream);
   const float* ga = opt_ptr(gamma, "gamma", x, c);
   const float* be = opt_ptr(beta, "beta", x, c);
   const float* ad = nullptr;
@@ -241,16 +250,20 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
   auto y = at::empty_like(z);
   launch_bn_apply(z.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), ga, be,
                   ad, y.data_ptr<float>(), n, c, s, stream);
-  return {y, z, mean, invstd};
+  return {y, z, mean, invstd, sums};
 }
 
 // Backward: returns {dx (undefined unless need_dx), dgamma, dbeta, dw_0, dw_1, ...}.
+// `sums` is the forward's zeroed [2][C] buffer (consumed).  `accum` is empty or holds one
+// optional entry per parameter gradient {dgamma, dbeta, dw_0, ...}: a given tensor (the
+// parameter's .grad across micro-batches) is accumulated into in place and returned.
 std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
                                         const at::Tensor& z, const at::Tensor& mean,
-                                        const at::Tensor& invstd,
+                                        const at::Tensor& invstd, at::Tensor& sums,
                                         const c10::optional<at::Tensor>& gamma,
                                         at::TensorList weights, at::IntArrayRef geo, bool relu,
-                                        bool need_dx) {
+                                        bool need_dx,
+                                        const c10::List<c10::optional<at::Tensor>>& accum) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   check_f32(x, "x", x);
@@ -266,13 +279,27 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   TORCH_CHECK(mean.numel() == c && invstd.numel() == c, "statistics must have C elements");
   const auto stream = cur_stream(x);
   const float* ga = opt_ptr(gamma, "gamma", x, c);
-  auto sums = at::zeros({2, c}, x.options());
+  check_f32(sums, "sums", x);
+  TORCH_CHECK(sums.numel() == 2 * c, "sums must be the forward's [2][C] buffer");
+  const size_t n_grads = 2 + p.geo.size();
+  TORCH_CHECK(accum.empty() || accum.size() == n_grads,
+              "accum must be empty or hold {dgamma, dbeta, dw...}");
+  std::vector<at::Tensor> into(n_grads);
+  for (size_t i = 0; i < accum.size(); ++i) {
+    const c10::optional<at::Tensor> t = accum.get(i);
+    if (!t.has_value() || !t->defined()) continue;
+    check_f32(*t, "accumulated gradient", x);
+    TORCH_CHECK(t->numel() == (i < 2 ? c : weights[i - 2].numel()),
+                "accumulated gradient has the wrong size");
+    into[i] = *t;
+  }
   auto dz = at::empty_like(z);
-  auto dgamma = at::empty({c}, x.options());
-  auto dbeta = at::empty({c}, x.options());
+  auto dgamma = into[0].defined() ? into[0] : at::empty({c}, x.options());
+  auto dbeta = into[1].defined() ? into[1] : at::empty({c}, x.options());
   launch_bn_backward(dy.data_ptr<float>(), z.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), ga, sums.data_ptr<float>(), dz.data_ptr<float>(),
-                     dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), n, c, s, stream);
+                     dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), into[0].defined(),
+                     into[1].defined(), n, c, s, stream);
   std::vector<at::Tensor> out;
   at::Tensor dx;
   if (need_dx) {
@@ -284,7 +311,7 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
       plans.push_back(tuned_plan(1, weights[i].data_ptr<float>(), dz.data_ptr<float>(),
                                  x.data_ptr<float>(), dx.data_ptr<float>(), nullptr, nullptr,
                                  p.geo[i], i > 0 || zero, weights[i].numel() * 4,
-                                 dz.numel() * 4, x));
+                                 dz.numel() * 4, x, x.numel()));
     for (size_t i = 0; i < p.geo.size(); ++i) {
       const auto& wt = weights[i];
       run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
@@ -296,12 +323,13 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   out.push_back(dgamma);
   out.push_back(dbeta);
   for (size_t i = 0; i < p.geo.size(); ++i) {
-    auto dw = at::empty_like(weights[i]);
+    const bool acc = into[2 + i].defined();
+    auto dw = acc ? into[2 + i] : at::empty_like(weights[i]);
     const ConvGemmPlan plan =
         tuned_plan(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
-                   nullptr, nullptr, p.geo[i], false, dz.numel() * 4, x.numel() * 4, x);
+                   nullptr, nullptr, p.geo[i], acc, dz.numel() * 4, x.numel() * 4, x, dw.numel());
     run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(), nullptr,
-             nullptr, p.geo[i], plan, false, dz.numel() * 4, x.numel() * 4, x);
+             nullptr, p.geo[i], plan, acc, dz.numel() * 4, x.numel() * 4, x);
     out.push_back(dw);
   }
   return out;
@@ -318,7 +346,8 @@ at::Tensor conv_gemm_forward(const at::Tensor& x_in, const at::Tensor& weight,
   auto z = at::empty({x.size(0), p.co_total, p.ho, p.wo}, x.options());
   const ConvGemmPlan plan =
       tuned_plan(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
-                 nullptr, nullptr, p.geo[0], false, weight.numel() * 4, x.numel() * 4, x);
+                 nullptr, nullptr, p.geo[0], false, weight.numel() * 4, x.numel() * 4, x,
+                 z.numel());
   run_gemm(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
            nullptr, nullptr, p.geo[0], plan, false, weight.numel() * 4, x.numel() * 4, x);
   return z;
@@ -339,15 +368,17 @@ at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_
   const ConvGemmPlan plan =
       tuned_plan(1, weight.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
                  dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], scatter, weight.numel() * 4,
-                 dz.numel() * 4, x);
+                 dz.numel() * 4, x, x.numel());
   run_gemm(1, weight.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
            dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], plan, plan.scatter,
            weight.numel() * 4, dz.numel() * 4, x);
   return dx;
 }
 
+// `accum` (optional): accumulate into this tensor (the weight's .grad) and return it.
 at::Tensor conv_gemm_backward_weight(const at::Tensor& dz_in, const at::Tensor& x_in,
-                                     const at::Tensor& weight, at::IntArrayRef geo, bool relu) {
+                                     const at::Tensor& weight, at::IntArrayRef geo, bool relu,
+                                     const c10::optional<at::Tensor>& accum) {
   auto x = x_in.contiguous();
   auto dz = dz_in.contiguous();
   check_f32(x, "x", x);
@@ -356,12 +387,17 @@ at::Tensor conv_gemm_backward_weight(const at::Tensor& dz_in, const at::Tensor& 
   Parts p = make_parts(x, {weight}, geo, relu);
   TORCH_CHECK(dz.size(1) == p.co_total && dz.size(2) == p.ho && dz.size(3) == p.wo,
               "dz does not match the convolution's output");
-  auto dw = at::empty_like(weight);
+  const bool acc = accum.has_value() && accum->defined();
+  if (acc) {
+    check_f32(*accum, "accum", x);
+    TORCH_CHECK(accum->numel() == weight.numel(), "accum must have the weight's size");
+  }
+  auto dw = acc ? *accum : at::empty_like(weight);
   const ConvGemmPlan plan =
       tuned_plan(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
-                 nullptr, nullptr, p.geo[0], false, dz.numel() * 4, x.numel() * 4, x);
+                 nullptr, nullptr, p.geo[0], acc, dz.numel() * 4, x.numel() * 4, x, dw.numel());
   run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(), nullptr,
-           nullptr, p.geo[0], plan, false, dz.numel() * 4, x.numel() * 4, x);
+           nullptr, p.geo[0], plan, acc, dz.numel() * 4, x.numel() * 4, x);
   return dw;
 }
 
@@ -382,7 +418,7 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
   auto mean = at::empty({c}, x.options());
   auto invstd = at::empty({c}, x.options());
   auto y = at::empty_like(x);
-  if (x.numel() == 0) return {y, mean.zero_(), invstd.fill_(1.f)};
+  if (x.numel() == 0) return {y, mean.zero_(), invstd.fill_(1.f), at::zeros({2, c}, x.options())};
   double* accp = nullptr;
   if (acc.has_value() && acc->defined()) {
     TORCH_CHECK(acc->device() == x.device() && acc->scalar_type() == at::kDouble &&
@@ -392,19 +428,21 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
   }
   launch_bn_stats(x.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n, c,
                   s, stream);
+  auto sums = at::empty({2, c}, x.options());  // zeroed by the finalize, for the backward
   launch_bn_finalize(part[0].data_ptr<float>(), part[1].data_ptr<float>(), static_cast<int>(n),
                      static_cast<int>(s), n * s, c, static_cast<float>(eps), 0.0,
                      mean.data_ptr<float>(), invstd.data_ptr<float>(), nullptr, nullptr, nullptr,
-                     accp, stream);
+                     accp, sums.data_ptr<float>(), stream);
   launch_bn_apply(x.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                   opt_ptr(gamma, "gamma", x, c), opt_ptr(beta, "beta", x, c), nullptr,
                   y.data_ptr<float>(), n, c, s, stream);
-  return {y, mean, invstd};
+  return {y, mean, invstd, sums};
 }
 
 // Backward of bn_train_forward: {dx, dgamma, dbeta}.
 std::vector<at::Tensor> bn_train_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
                                           const at::Tensor& mean, const at::Tensor& invstd,
+                                          at::Tensor& sums,
                                           const c10::optional<at::Tensor>& gamma) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
@@ -413,14 +451,15 @@ std::vector<at::Tensor> bn_train_backward(const at::Tensor& dy_in, const at::Ten
   TORCH_CHECK(dy.sizes() == x.sizes(), "dy must have x's shape");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t n = x.size(0), c = x.size(1), s = n * c == 0 ? 0 : x.numel() / (n * c);
-  auto sums = at::zeros({2, c}, x.options());
+  check_f32(sums, "sums", x);
+  TORCH_CHECK(sums.numel() == 2 * c, "sums must be the forward's [2][C] buffer");
   auto dx = at::empty_like(x);
   auto dgamma = at::empty({c}, x.options());
   auto dbeta = at::empty({c}, x.options());
   launch_bn_backward(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), opt_ptr(gamma, "gamma", x, c),
                      sums.data_ptr<float>(), dx.data_ptr<float>(), dgamma.data_ptr<float>(),
-                     dbeta.data_ptr<float>(), n, c, s, cur_stream(x));
+                     dbeta.data_ptr<float>(), false, false, n, c, s, cur_stream(x));
   return {dx, dgamma, dbeta};
 }
 
@@ -437,26 +476,69 @@ void dbn_commit64(at::Tensor& acc, at::Tensor& running_mean, at::Tensor& running
                       running_var.data_ptr<float>(), c, momentum, cur_stream(running_mean));
 }
 
+// AmoebaNet's 3x3 average pools (pool.hip): y = pool(x) (+ add).
+at::Tensor avgpool3_forward(const at::Tensor& x_in, int64_t stride,
+                            const c10::optional<at::Tensor>& add) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  TORCH_CHECK(x.dim() == 4 && (stride == 1 || stride == 2), "x must be NCHW, stride 1 or 2");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t h = x.size(2), w = x.size(3);
+  auto y = at::empty({x.size(0), x.size(1), (h - 1) / stride + 1, (w - 1) / stride + 1},
+                     x.options());
+  const float* ad = nullptr;
+  at::Tensor add_c;
+  if (add.has_value() && add->defined()) {
+    add_c = add->contiguous();
+    check_f32(add_c, "add", x);
+    TORCH_CHECK(add_c.sizes() == y.sizes(), "add must have the pooled shape");
+    ad = add_c.data_ptr<float>();
+  }
+  if (y.numel() > 0)
+    launch_avgpool3_forward(x.data_ptr<float>(), ad, y.data_ptr<float>(), x.size(0) * x.size(1),
+                            static_cast<int>(h), static_cast<int>(w), static_cast<int>(stride),
+                            cur_stream(x));
+  return y;
+}
+
+at::Tensor avgpool3_backward(const at::Tensor& dy_in, int64_t h, int64_t w, int64_t stride) {
+  auto dy = dy_in.contiguous();
+  check_f32(dy, "dy", dy);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(2) == (h - 1) / stride + 1 &&
+                  dy.size(3) == (w - 1) / stride + 1,
+              "dy does not match the pooled shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  auto dx = at::empty({dy.size(0), dy.size(1), h, w}, dy.options());
+  if (dx.numel() > 0)
+    launch_avgpool3_backward(dy.data_ptr<float>(), dx.data_ptr<float>(), dy.size(0) * dy.size(1),
+                             static_cast<int>(h), static_cast<int>(w), static_cast<int>(stride),
+                             cur_stream(dy));
+  return dx;
+}
+
 }  // namespace
 }  // namespace tgpipe
 
 TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
+  m.def("avgpool3_forward(Tensor x, int stride, Tensor? add) -> Tensor");
+  m.def("avgpool3_backward(Tensor dy, int h, int w, int stride) -> Tensor");
   m.def("bn_train_forward(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? acc, float eps) "
         "-> Tensor[]");
-  m.def("bn_train_backward(Tensor dy, Tensor x, Tensor mean, Tensor invstd, Tensor? gamma) "
-        "-> Tensor[]");
+  m.def("bn_train_backward(Tensor dy, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) sums, "
+        "Tensor? gamma) -> Tensor[]");
   m.def("dbn_commit64(Tensor(a!) acc, Tensor(b!) running_mean, Tensor(c!) running_var, "
         "float momentum) -> ()");
   m.def("convbn_forward(Tensor x, Tensor[] weights, int[] geo, bool relu, Tensor? gamma, "
         "Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "Tensor(c!)? num_batches_tracked, float momentum, float eps, Tensor? add) -> Tensor[]");
   m.def("convbn_backward(Tensor dy, Tensor x, Tensor z, Tensor mean, Tensor invstd, "
-        "Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx) -> Tensor[]");
+        "Tensor(a!) sums, Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx, "
+        "Tensor?[] accum) -> Tensor[]");
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
   m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu) "
         "-> Tensor");
-  m.def("conv_gemm_backward_weight(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu) "
-        "-> Tensor");
+  m.def("conv_gemm_backward_weight(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "
+        "Tensor? accum=None) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
@@ -468,4 +550,6 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("bn_train_forward", &tgpipe::bn_train_forward);
   m.impl("bn_train_backward", &tgpipe::bn_train_backward);
   m.impl("dbn_commit64", &tgpipe::dbn_commit64);
+  m.impl("avgpool3_forward", &tgpipe::avgpool3_forward);
+  m.impl("avgpool3_backward", &tgpipe::avgpool3_backward);
 }

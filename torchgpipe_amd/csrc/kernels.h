@@ -162,10 +162,11 @@ void launch_bn_stats(const float* z, float* part_mean, float* part_m2, int64_t n
 // (unbiased variance) when running_mean is non-null, and `tracked` (BatchNorm's
 // num_batches_tracked, may be null) is incremented in the same launch.  `acc` (may be
 // null): DeferredBatchNorm's fp64 [3][C] (count, mean, M2) accumulators, Chan-merged.
+// `zero2c` (may be null): a [2][C] buffer zeroed by the same launch (the backward's sums).
 void launch_bn_finalize(const float* part_mean, const float* part_m2, int blocks, int width,
                         int64_t total, int64_t c, float eps, double momentum, float* mean,
                         float* invstd, float* running_mean, float* running_var, int64_t* tracked,
-                        double* acc, hipStream_t stream);
+                        double* acc, float* zero2c, hipStream_t stream);
 // DeferredBatchNorm commit from the fp64 accumulators; zeroes them.
 void launch_dbn_commit64(double* acc, float* running_mean, float* running_var, int64_t c,
                          double momentum, hipStream_t stream);
@@ -173,10 +174,19 @@ void launch_dbn_commit64(double* acc, float* running_mean, float* running_var, i
 void launch_bn_apply(const float* z, const float* mean, const float* invstd, const float* gamma,
                      const float* beta, const float* add, float* y, int64_t n, int64_t c,
                      int64_t s, hipStream_t stream);
-// Backward: sums[2][C] (zeroed) += (sum dy, sum dy*(z-mean)); then
+// Backward: sums[2][C] (zeroed, e.g. by the forward's finalize) += (sum dy,
+// sum dy*(z-mean)); then
 // dz = gamma*invstd*(dy - sum_dy/M - (z-mean)*invstd^2*sum_dyz/M), dgamma, dbeta.
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
-                        int64_t n, int64_t c, int64_t s, hipStream_t stream);
+                        bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
+                        hipStream_t stream);
+
+// 3x3 average pool, padding 1, count_include_pad = False, stride 1 / 2 (pool.hip):
+// y = pool(x) (+ add) over `planes` = N*C planes of h x w; backward gathers dx.
+void launch_avgpool3_forward(const float* x, const float* add, float* y, int64_t planes, int h,
+                             int w, int stride, hipStream_t stream);
+void launch_avgpool3_backward(const float* dy, float* dx, int64_t planes, int h, int w,
+                              int stride, hipStream_t stream);
 
 }  // namespace tgpipe

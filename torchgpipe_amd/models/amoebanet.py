@@ -27,6 +27,7 @@ import torch
 from torch import Tensor, nn
 
 from torchgpipe_amd.ops.convbn import FusedChain, ReLUConvBN, fusable, relu_conv_bn
+from torchgpipe_amd.ops.pool import AvgPool3x3
 
 __all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS']
 
@@ -40,9 +41,14 @@ class Operation(nn.Module):
     def __repr__(self) -> str:
         return f'Operation[{self.name}]'
 
+    @property
+    def takes_add(self) -> bool:
+        """Whether ``add`` folds into the module's own last pass (no separate add)."""
+        return isinstance(self.module, (FusedChain, FactorizedReduce, AvgPool3x3))
+
     def forward(self, x: Tensor, add: Optional[Tensor] = None) -> Tensor:  # type: ignore[override]
         """``module(x)``, plus ``add`` (folded into a fused op's last pass when it can)."""
-        if add is not None and isinstance(self.module, (FusedChain, FactorizedReduce)):
+        if add is not None and self.takes_add:
             return self.module(x, add)
         out = self.module(x)
         return out if add is None else out + add
@@ -85,14 +91,12 @@ def op_none(c: int, stride: int) -> Operation:
 
 
 def op_avg_pool_3x3(c: int, stride: int) -> Operation:
-    return Operation('avg_pool_3x3',
-                     nn.AvgPool2d(3, stride=stride, padding=1, count_include_pad=False))
+    return Operation('avg_pool_3x3', AvgPool3x3(stride))
 
 
 def op_max_pool_3x3(c: int, stride: int) -> Operation:
     # Reference quirk: implemented as an average pool.
-    return Operation('max_pool_3x3',
-                     nn.AvgPool2d(3, stride=stride, padding=1, count_include_pad=False))
+    return Operation('max_pool_3x3', AvgPool3x3(stride))
 
 
 def op_max_pool_2x2(c: int, stride: int) -> Operation:
@@ -204,8 +208,11 @@ class Cell(nn.Module):
         nodes = [self.reduce1(s1), self.reduce2(s2)]
         ops = list(self.operations)
         for k in range(0, len(ops), 2):
-            left = ops[k](nodes[self.indices[k]])
-            nodes.append(ops[k + 1](nodes[self.indices[k + 1]], add=left))
+            # node = left + right: run the operation that cannot fold a sum first and
+            # hand its output to the other one's last pass
+            a, b = (k, k + 1) if ops[k + 1].takes_add or not ops[k].takes_add else (k + 1, k)
+            first = ops[a](nodes[self.indices[a]])
+            nodes.append(ops[b](nodes[self.indices[b]], add=first))
         return torch.cat([nodes[i] for i in self.concat], dim=1), skip
 
 

@@ -28,7 +28,7 @@ import torch
 from torch import Tensor, nn
 import torch.nn.functional as F
 
-from torchgpipe_amd.ops import _ext
+from torchgpipe_amd.ops import _ext, gradacc
 
 __all__ = ['relu_conv_bn', 'ReLUConvBN', 'FusedChain', 'conv_supported', 'fused_triplets',
            'fusable', 'disabled', 'GemmConv2d', 'gemm_conv2d', 'gemm_conv_eligible']
@@ -79,12 +79,13 @@ class _ConvBN(torch.autograd.Function):
                 *weights: Tensor) -> Tensor:
         ops = _ext.require(x)
         track = bn.track_running_stats and bn.running_mean is not None
-        y, z, mean, invstd = ops.convbn_forward(
+        y, z, mean, invstd, sums = ops.convbn_forward(
             x, list(weights), geo, relu, gamma, beta,
             bn.running_mean if track else None, bn.running_var if track else None,
             bn.num_batches_tracked if track else None,
             float(bn.momentum) if bn.momentum is not None else 0.0, float(bn.eps), add)
-        ctx.save_for_backward(x, z, mean, invstd, gamma, *weights)
+        ctx.save_for_backward(x, z, mean, invstd, sums, gamma, *weights)
+        ctx.params = (gamma, beta) + weights  # gradient-accumulation fusion (ops/gradacc.py)
         ctx.geo = geo
         ctx.relu = relu
         ctx.has_add = add is not None
@@ -93,10 +94,20 @@ class _ConvBN(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy: Tensor):  # type: ignore[override]
-        x, z, mean, invstd, gamma, *weights = ctx.saved_tensors
+        x, z, mean, invstd, sums, gamma, *weights = ctx.saved_tensors
         need_dx = ctx.needs_input_grad[0]
+        fused = [gradacc.target(p) for p in ctx.params]
         dx, dgamma, dbeta, *dws = _ext.require(dy).convbn_backward(
-            dy, x, z, mean, invstd, gamma, weights, ctx.geo, ctx.relu, need_dx)
+            dy, x, z, mean, invstd, sums, gamma, weights, ctx.geo, ctx.relu, need_dx,
+            [into for _, into in fused])
+        grads = [dgamma, dbeta] + dws
+        for k, ((fuse, into), p) in enumerate(zip(fused, ctx.params)):
+            if fuse:  # written into p.grad by the kernels
+                if into is None:
+                    gradacc.commit(p, grads[k])
+                grads[k] = None
+        del ctx.params
+        dgamma, dbeta, *dws = grads
         return (dx if need_dx else None, dy if ctx.has_add else None,
                 dgamma if ctx.needs_input_grad[2] else None,
                 dbeta if ctx.needs_input_grad[3] else None, None, None, None, *dws)
@@ -194,6 +205,7 @@ class _GemmConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: Tensor, weight: Tensor, geo: List[int]) -> Tensor:  # type: ignore[override]
         ctx.save_for_backward(x, weight)
+        ctx.param = weight
         ctx.geo = geo
         return _ext.require(x).conv_gemm_forward(x, weight, geo, False)
 
@@ -205,7 +217,13 @@ class _GemmConv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = ops.conv_gemm_backward_data(dz, x, weight, ctx.geo, False)
         if ctx.needs_input_grad[1]:
-            dw = ops.conv_gemm_backward_weight(dz, x, weight, ctx.geo, False)
+            fuse, into = gradacc.target(ctx.param)
+            dw = ops.conv_gemm_backward_weight(dz, x, weight, ctx.geo, False, into)
+            if fuse:  # accumulated into / stored as weight.grad (ops/gradacc.py)
+                if into is None:
+                    gradacc.commit(ctx.param, dw)
+                dw = None
+        del ctx.param
         return dx, dw, None
 
 
