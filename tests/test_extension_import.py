@@ -25,3 +25,23 @@ def test_extension_imports_and_registers_ops():
                          text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.strip().endswith('True')
+
+
+def test_shipped_plan_table_loads():
+    """The shipped MI355X plan table parses and every entry is a valid launch shape."""
+    table = os.path.join(ROOT, 'torchgpipe_amd', 'tuned', 'conv_gemm_mi355x.txt')
+    if not os.path.exists(table) or not any(
+            f.startswith('_C') and f.endswith('.so')
+            for f in os.listdir(os.path.join(ROOT, 'torchgpipe_amd'))):
+        pytest.skip('extension or plan table missing')
+    with open(table) as f:
+        lines = [ln for ln in f.read().splitlines() if ln.strip()]
+    code = ('import os; os.environ["TGPIPE_CG_DB"] = "0"; import torch, torchgpipe_amd._C; '
+            'from torchgpipe_amd.ops import _ext; '
+            f'print(_ext.load_plans({table!r}), '
+            'torch.ops.tgpipe.conv_gemm_plans_export().count(chr(10)))')
+    out = subprocess.run([sys.executable, '-c', code], cwd=ROOT, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    taken, exported = map(int, out.stdout.split()[-2:])
+    assert taken == len(lines) == exported

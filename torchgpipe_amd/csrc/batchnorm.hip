@@ -78,6 +78,101 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
   }
 }
 
+// Finalize + apply in one launch.  Workgroup (channel, image range): its 256 threads
+// merge the channel's partials (thread-strided Chan merges, a 64-lane shuffle tree, then
+// the 4 waves through LDS -- the same fixed order in every workgroup of the channel, so
+// all of them hold bit-identical statistics), workgroup (channel, 0) publishes mean /
+// invstd / running statistics, and every workgroup normalises its own images.  Saves the
+// separate finalize launch per BatchNorm (AmoebaNet: ~17 k launches per training step).
+template <bool kVec, bool kAdd>
+__global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
+    const float* __restrict__ pm, const float* __restrict__ pm2, int blocks, int width,
+    int cols, int n, int c, int s, int n_per, float eps, double momentum,
+    float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rm,
+    float* __restrict__ rv, int64_t* __restrict__ tracked, double* __restrict__ acc,
+    float* __restrict__ zero2c, const float* __restrict__ z, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ add, float* __restrict__ y) {
+  const int ch = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double na = 0.0, ma = 0.0, m2a = 0.0;
+  for (int b = tid; b < blocks; b += 256) {
+    const int left = cols - b * width;
+    chan_merge(na, ma, m2a, static_cast<double>(left < width ? left : width), pm[b * c + ch],
+               pm2[b * c + ch]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double nb = __shfl_xor(na, off);
+    const double mb = __shfl_xor(ma, off);
+    const double m2b = __shfl_xor(m2a, off);
+    chan_merge(na, ma, m2a, nb, mb, m2b);
+  }
+  __shared__ double red[3][4];
+  __shared__ float kb[3];
+  if (lane == 0) {
+    red[0][wave] = na;
+    red[1][wave] = ma;
+    red[2][wave] = m2a;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    na = red[0][0];
+    ma = red[1][0];
+    m2a = red[2][0];
+    for (int k = 1; k < 4; ++k) chan_merge(na, ma, m2a, red[0][k], red[1][k], red[2][k]);
+    const double var = na > 0.0 ? m2a / na : 0.0;
+    const float mu = static_cast<float>(ma);
+    const float is = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+    kb[0] = mu;
+    kb[1] = is * (gamma ? gamma[ch] : 1.f);
+    kb[2] = beta ? beta[ch] : 0.f;
+    if (blockIdx.y == 0) {
+      if (tracked != nullptr && ch == 0) *tracked += 1;
+      if (zero2c != nullptr) {  // the backward's [2][C] reduction buffer
+        zero2c[ch] = 0.f;
+        zero2c[c + ch] = 0.f;
+      }
+      mean[ch] = mu;
+      invstd[ch] = is;
+      if (acc != nullptr) {  // DeferredBatchNorm mini-batch accumulators (dbn_commit64)
+        double n0 = acc[ch], m0 = acc[c + ch], q0 = acc[2 * c + ch];
+        chan_merge(n0, m0, q0, na, ma, m2a);
+        acc[ch] = n0;
+        acc[c + ch] = m0;
+        acc[2 * c + ch] = q0;
+      }
+      if (rm != nullptr) {
+        const double unbiased = na > 1.0 ? m2a / (na - 1.0) : var;
+        rm[ch] = static_cast<float>((1.0 - momentum) * rm[ch] + momentum * ma);
+        rv[ch] = static_cast<float>((1.0 - momentum) * rv[ch] + momentum * unbiased);
+      }
+    }
+  }
+  __syncthreads();
+  const float mu = kb[0], k = kb[1], bb = kb[2];
+  const int n0 = blockIdx.y * n_per, n1 = min(n, n0 + n_per);
+  if constexpr (kVec) {
+    const int sq = s >> 2, quads = (n1 - n0) * sq;
+    for (int q = tid; q < quads; q += 256) {
+      const int img = n0 + q / sq;
+      const int64_t off = (static_cast<int64_t>(img) * c + ch) * sq + (q - (img - n0) * sq);
+      // (z - mean) * k, not z * k - mean * k: no cancellation when |mean| >> std
+      floatx4 v = (reinterpret_cast<const floatx4*>(z)[off] - mu) * k + bb;
+      if constexpr (kAdd) v += reinterpret_cast<const floatx4*>(add)[off];
+      reinterpret_cast<floatx4*>(y)[off] = v;
+    }
+  } else {
+    const int elems = (n1 - n0) * s;
+    for (int e = tid; e < elems; e += 256) {
+      const int img = n0 + e / s;
+      const int64_t off = (static_cast<int64_t>(img) * c + ch) * s + (e - (img - n0) * s);
+      float v = (z[off] - mu) * k + bb;
+      if constexpr (kAdd) v += add[off];
+      y[off] = v;
+    }
+  }
+}
+
 template <bool kVec, bool kAdd>
 __global__ __launch_bounds__(256) void bn_apply_kernel(
     const float* __restrict__ z, const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -275,6 +370,34 @@ void launch_bn_finalize(const float* part_mean, const float* part_m2, int blocks
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(static_cast<unsigned>((c + 7) / 8)),
                      dim3(256), 0, stream, part_mean, part_m2, blocks, width, total, c, eps,
                      momentum, mean, invstd, running_mean, running_var, tracked, acc, zero2c);
+}
+
+void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int blocks,
+                              int width, int64_t n, int64_t c, int64_t s, float eps,
+                              double momentum, float* mean, float* invstd, float* running_mean,
+                              float* running_var, int64_t* tracked, double* acc, float* zero2c,
+                              const float* z, const float* gamma, const float* beta,
+                              const float* add, float* y, hipStream_t stream) {
+  if (c == 0) return;
+  // enough (channel, image range) workgroups to cover the chip ~4x
+  int64_t splits = (1024 + c - 1) / c;
+  if (splits > n) splits = n;
+  if (splits < 1) splits = 1;
+  const int64_t n_per = (n + splits - 1) / splits;
+  splits = n == 0 ? 1 : (n + n_per - 1) / n_per;
+  const dim3 grid(static_cast<unsigned>(c), static_cast<unsigned>(splits));
+  const int cols = static_cast<int>(n * s);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, part_mean, part_m2, blocks, width, cols,
+                       static_cast<int>(n), static_cast<int>(c), static_cast<int>(s),
+                       static_cast<int>(n_per), eps, momentum, mean, invstd, running_mean,
+                       running_var, tracked, acc, zero2c, z, gamma, beta, add, y);
+  };
+  const bool vec = (s & 3) == 0;
+  if (vec && add) go(bn_finalize_apply_kernel<true, true>);
+  else if (vec) go(bn_finalize_apply_kernel<true, false>);
+  else if (add) go(bn_finalize_apply_kernel<false, true>);
+  else go(bn_finalize_apply_kernel<false, false>);
 }
 
 void launch_dbn_commit64(double* acc, float* running_mean, float* running_var, int64_t c,

@@ -749,7 +749,7 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
                               : static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
     int last = 0;
     for (int s : {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256, 512, 1024}) {
-      if (s > max_split || (s > 1 && g.scatter) || tiles * s > 8192) break;
+      if (s > 1 && (s > max_split || g.scatter || tiles * s > 8192)) break;
       int k_chunk = (K + s - 1) / s;
       k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
       const int real = std::max(1, (K + k_chunk - 1) / k_chunk);

@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <sstream>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -42,8 +44,11 @@ void launch_one(int mode, const float* a, const float* b, const float* mask, flo
 // stream and keeps the fastest.  TGPIPE_CG_TUNE=0 uses the static heuristic instead;
 // stream captures never tune; an accumulating launch times its candidates on a scratch
 // output (`out_numel` floats) so the real output is untouched.
+// Keyed by geometry only: every GPU of a process is the same gfx950 part.  The table can
+// be exported / imported as text (conv_gemm_plans_export/import): the package ships the
+// plans measured on an MI355X for its benchmark models, so a fresh process skips the find.
 using PlanKey = std::tuple<int, int, int, int, int, int, int, int, int, int, int, int, int, int,
-                           int, int>;
+                           int>;
 std::mutex plan_mutex;
 std::map<PlanKey, ConvGemmPlan> plan_cache;
 
@@ -62,8 +67,8 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
   if (hipStreamIsCapturing(stream, &capture) != hipSuccess ||
       capture != hipStreamCaptureStatusNone)
     return heuristic;
-  const PlanKey key{mode, static_cast<int>(like.device().index()), g.n, g.ci, g.h, g.w, g.co,
-                    g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.oh, g.ow, g.co_total};
+  const PlanKey key{mode, g.n, g.ci, g.h, g.w, g.co, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.oh,
+                    g.ow, g.co_total};
   std::lock_guard<std::mutex> lock(plan_mutex);
   auto hit = plan_cache.find(key);
   if (hit != plan_cache.end()) return hit->second;
@@ -96,6 +101,71 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
   hipEventDestroy(t1);
   plan_cache[key] = best;
   return best;
+}
+
+// One line per plan: "mode n ci h w co kh kw sh sw ph pw oh ow co_total big splits".
+std::string conv_gemm_plans_export() {
+  std::lock_guard<std::mutex> lock(plan_mutex);
+  std::ostringstream out;
+  for (const auto& kv : plan_cache) {
+    const auto& k = kv.first;
+    out << std::get<0>(k) << ' ' << std::get<1>(k) << ' ' << std::get<2>(k) << ' '
+        << std::get<3>(k) << ' ' << std::get<4>(k) << ' ' << std::get<5>(k) << ' '
+        << std::get<6>(k) << ' ' << std::get<7>(k) << ' ' << std::get<8>(k) << ' '
+        << std::get<9>(k) << ' ' << std::get<10>(k) << ' ' << std::get<11>(k) << ' '
+        << std::get<12>(k) << ' ' << std::get<13>(k) << ' ' << std::get<14>(k) << ' '
+        << (kv.second.big ? 1 : 0) << ' ' << kv.second.splits << '\n';
+  }
+  return out.str();
+}
+
+// Adds the plans of `text` that are still valid launch shapes for this build (a plan must
+// equal one of conv_gemm_candidates for its geometry); plans already measured win.
+// Returns the number of plans taken.
+int64_t conv_gemm_plans_import(const std::string& text) {
+  std::istringstream in(text);
+  std::string line;
+  int64_t taken = 0;
+  std::lock_guard<std::mutex> lock(plan_mutex);
+  while (std::getline(in, line)) {
+    std::istringstream ls(line);
+    int v[17];
+    int got = 0;
+    while (got < 17 && (ls >> v[got])) ++got;
+    if (got != 17 || v[0] < 0 || v[0] > 2) continue;
+    ConvGemmGeo g;
+    g.n = v[1];
+    g.ci = v[2];
+    g.h = v[3];
+    g.w = v[4];
+    g.co = v[5];
+    g.kh = v[6];
+    g.kw = v[7];
+    g.sh = v[8];
+    g.sw = v[9];
+    g.ph = v[10];
+    g.pw = v[11];
+    g.oh = v[12];
+    g.ow = v[13];
+    g.co_total = v[14];
+    if (g.n <= 0 || g.ci <= 0 || g.h <= 0 || g.w <= 0 || g.co <= 0 || g.kh <= 0 || g.kw <= 0 ||
+        g.sh <= 0 || g.sw <= 0 || g.ph < 0 || g.pw < 0 || g.co_total < g.co)
+      continue;
+    g.ho = (g.h + 2 * g.ph - g.kh) / g.sh + 1;
+    g.wo = (g.w + 2 * g.pw - g.kw) / g.sw + 1;
+    if (g.ho <= 0 || g.wo <= 0) continue;
+    const PlanKey key{v[0], g.n, g.ci, g.h, g.w, g.co, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.oh,
+                      g.ow, g.co_total};
+    if (plan_cache.count(key)) continue;
+    for (const auto& cand : conv_gemm_candidates(v[0], g)) {
+      if (cand.big == (v[15] != 0) && cand.splits == v[16]) {
+        plan_cache[key] = cand;
+        ++taken;
+        break;
+      }
+    }
+  }
+  return taken;
 }
 
 // One implicit-GEMM launch with its split-reduction workspace.
@@ -233,10 +303,6 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     tracked = num_batches_tracked->data_ptr<int64_t>();
   }
   auto sums = at::empty({2, c}, x.options());  // zeroed by the finalize, for the backward
-  launch_bn_finalize(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, cols, c,
-                     static_cast<float>(eps), momentum, mean.data_ptr<float>(),
-                     invstd.data_ptr<float>(), const_cast<float*>(rm), const_cast<float*>(rv),
-                     tracked, nullptr, sums.data_ptr<float>(), stream);
   const float* ga = opt_ptr(gamma, "gamma", x, c);
   const float* be = opt_ptr(beta, "beta", x, c);
   const float* ad = nullptr;
@@ -248,8 +314,11 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     ad = add_c.data_ptr<float>();
   }
   auto y = at::empty_like(z);
-  launch_bn_apply(z.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), ga, be,
-                  ad, y.data_ptr<float>(), n, c, s, stream);
+  launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, n,
+                           c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
+                           invstd.data_ptr<float>(), const_cast<float*>(rm),
+                           const_cast<float*>(rv), tracked, nullptr, sums.data_ptr<float>(),
+                           z.data_ptr<float>(), ga, be, ad, y.data_ptr<float>(), stream);
   return {y, z, mean, invstd, sums};
 }
 
@@ -429,13 +498,13 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
   launch_bn_stats(x.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n, c,
                   s, stream);
   auto sums = at::empty({2, c}, x.options());  // zeroed by the finalize, for the backward
-  launch_bn_finalize(part[0].data_ptr<float>(), part[1].data_ptr<float>(), static_cast<int>(n),
-                     static_cast<int>(s), n * s, c, static_cast<float>(eps), 0.0,
-                     mean.data_ptr<float>(), invstd.data_ptr<float>(), nullptr, nullptr, nullptr,
-                     accp, sums.data_ptr<float>(), stream);
-  launch_bn_apply(x.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                  opt_ptr(gamma, "gamma", x, c), opt_ptr(beta, "beta", x, c), nullptr,
-                  y.data_ptr<float>(), n, c, s, stream);
+  launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(),
+                           static_cast<int>(n), static_cast<int>(s), n, c, s,
+                           static_cast<float>(eps), 0.0, mean.data_ptr<float>(),
+                           invstd.data_ptr<float>(), nullptr, nullptr, nullptr, accp,
+                           sums.data_ptr<float>(), x.data_ptr<float>(),
+                           opt_ptr(gamma, "gamma", x, c), opt_ptr(beta, "beta", x, c), nullptr,
+                           y.data_ptr<float>(), stream);
   return {y, mean, invstd, sums};
 }
 
@@ -535,6 +604,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
         "Tensor(a!) sums, Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx, "
         "Tensor?[] accum) -> Tensor[]");
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
+  m.def("conv_gemm_plans_export() -> str", &tgpipe::conv_gemm_plans_export);
+  m.def("conv_gemm_plans_import(str text) -> int", &tgpipe::conv_gemm_plans_import);
   m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu) "
         "-> Tensor");
   m.def("conv_gemm_backward_weight(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "

@@ -177,6 +177,14 @@ void launch_bn_apply(const float* z, const float* mean, const float* invstd, con
 // Backward: sums[2][C] (zeroed, e.g. by the forward's finalize) += (sum dy,
 // sum dy*(z-mean)); then
 // dz = gamma*invstd*(dy - sum_dy/M - (z-mean)*invstd^2*sum_dyz/M), dgamma, dbeta.
+// BatchNorm finalize (as launch_bn_finalize) fused with the normalising pass (as
+// launch_bn_apply): one launch of (channel, image range) workgroups.
+void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int blocks,
+                              int width, int64_t n, int64_t c, int64_t s, float eps,
+                              double momentum, float* mean, float* invstd, float* running_mean,
+                              float* running_var, int64_t* tracked, double* acc, float* zero2c,
+                              const float* z, const float* gamma, const float* beta,
+                              const float* add, float* y, hipStream_t stream);
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
                         bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,

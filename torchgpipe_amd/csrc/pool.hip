@@ -16,44 +16,52 @@
 namespace tgpipe {
 namespace {
 
+// 32-bit index math throughout (the host caps tensors at 2 GiB): 64-bit division by the
+// plane size would cost more than the nine loads.
 __global__ __launch_bounds__(256) void avgpool3_fwd_kernel(const float* __restrict__ x,
                                                            const float* __restrict__ add,
-                                                           float* __restrict__ y, int64_t planes,
+                                                           float* __restrict__ y, int total,
                                                            int h, int w, int ho, int wo,
                                                            int stride) {
-  const int64_t total = planes * ho * wo;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * 256) {
-    const int64_t pl = i / (ho * wo);
-    const int r = static_cast<int>(i - pl * ho * wo);
+  const int plane_out = ho * wo;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pl = i / plane_out;
+    const int r = i - pl * plane_out;
     const int oy = r / wo, ox = r - oy * wo;
     const int cy = oy * stride, cx = ox * stride;
-    const int y0 = max(cy - 1, 0), y1 = min(cy + 1, h - 1);
-    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, w - 1);
-    const float* p = x + pl * h * w;
+    const float* p = x + static_cast<int64_t>(pl) * h * w;
     float s = 0.f;
-    for (int yy = y0; yy <= y1; ++yy)
-      for (int xx = x0; xx <= x1; ++xx) s += p[yy * w + xx];
-    float v = s / static_cast<float>((y1 - y0 + 1) * (x1 - x0 + 1));
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int yy = cy + dy;
+      if (yy < 0 || yy >= h) continue;
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int xx = cx + dx;
+        if (xx >= 0 && xx < w) s += p[yy * w + xx];
+      }
+    }
+    const int ny = min(cy + 1, h - 1) - max(cy - 1, 0) + 1;
+    const int nx = min(cx + 1, w - 1) - max(cx - 1, 0) + 1;
+    float v = s / static_cast<float>(ny * nx);
     if (add != nullptr) v += add[i];
     y[i] = v;
   }
 }
 
 __global__ __launch_bounds__(256) void avgpool3_bwd_kernel(const float* __restrict__ dy,
-                                                           float* __restrict__ dx, int64_t planes,
+                                                           float* __restrict__ dx, int total,
                                                            int h, int w, int ho, int wo,
                                                            int stride) {
-  const int64_t total = planes * h * w;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * 256) {
-    const int64_t pl = i / (h * w);
-    const int r = static_cast<int>(i - pl * h * w);
+  const int plane_in = h * w;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pl = i / plane_in;
+    const int r = i - pl * plane_in;
     const int iy = r / w, ix = r - iy * w;
     // outputs whose window [c-1, c+1] (c = o * stride) contains the input pixel
     const int oy0 = max((iy - 1 + stride - 1) / stride, 0), oy1 = min((iy + 1) / stride, ho - 1);
     const int ox0 = max((ix - 1 + stride - 1) / stride, 0), ox1 = min((ix + 1) / stride, wo - 1);
-    const float* g = dy + pl * ho * wo;
+    const float* g = dy + static_cast<int64_t>(pl) * ho * wo;
     float s = 0.f;
     for (int oy = oy0; oy <= oy1; ++oy) {
       const int cy = oy * stride;
@@ -78,15 +86,17 @@ unsigned blocks_for(int64_t work) {
 void launch_avgpool3_forward(const float* x, const float* add, float* y, int64_t planes, int h,
                              int w, int stride, hipStream_t stream) {
   const int ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
-  hipLaunchKernelGGL(avgpool3_fwd_kernel, dim3(blocks_for(planes * ho * wo)), dim3(256), 0,
-                     stream, x, add, y, planes, h, w, ho, wo, stride);
+  const int64_t total = planes * ho * wo;  // < 2^31 (2 GiB tensors)
+  hipLaunchKernelGGL(avgpool3_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, x, add,
+                     y, static_cast<int>(total), h, w, ho, wo, stride);
 }
 
 void launch_avgpool3_backward(const float* dy, float* dx, int64_t planes, int h, int w,
                               int stride, hipStream_t stream) {
   const int ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
-  hipLaunchKernelGGL(avgpool3_bwd_kernel, dim3(blocks_for(planes * h * w)), dim3(256), 0, stream,
-                     dy, dx, planes, h, w, ho, wo, stride);
+  const int64_t total = planes * h * w;
+  hipLaunchKernelGGL(avgpool3_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, dy, dx,
+                     static_cast<int>(total), h, w, ho, wo, stride);
 }
 
 }  // namespace tgpipe

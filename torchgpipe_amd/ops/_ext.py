@@ -11,7 +11,12 @@ from typing import Any, Optional
 
 import torch
 
-__all__ = ['available', 'ops', 'require', 'load_error']
+__all__ = ['available', 'ops', 'require', 'load_error', 'load_plans', 'save_plans']
+
+# Implicit-GEMM launch plans measured on an MI355X for the benchmark models (written by
+# benchmarks/tune_plans.py).  TGPIPE_CG_DB=<file> loads another table, =0 none.
+SHIPPED_PLANS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             'tuned', 'conv_gemm_mi355x.txt')
 
 _loaded = False
 _error: Optional[BaseException] = None
@@ -24,6 +29,9 @@ def _load() -> None:
     try:
         importlib.import_module('torchgpipe_amd._C')
         _loaded = True
+        db = os.environ.get('TGPIPE_CG_DB', SHIPPED_PLANS)
+        if db != '0' and os.path.exists(db):
+            load_plans(db)
     except Exception as exc:  # pragma: no cover - depends on the build
         _error = exc
         if os.environ.get('TGPIPE_AUTOBUILD', '0') == '1':
@@ -57,3 +65,21 @@ def require(*tensors: torch.Tensor) -> Any:
 
 def ops() -> Any:
     return require()
+
+
+def load_plans(path: str) -> int:
+    """Seed the convolution autotuner with a saved plan table; returns plans taken.
+
+    Entries that are not valid launch shapes of this build are ignored, and shapes already
+    measured in this process keep their plan.
+    """
+    with open(path) as f:
+        return int(torch.ops.tgpipe.conv_gemm_plans_import(f.read()))
+
+
+def save_plans(path: str) -> int:
+    """Write every plan measured (or loaded) in this process; returns the line count."""
+    text = require().conv_gemm_plans_export()
+    with open(path, 'w') as f:
+        f.write(text)
+    return text.count('\n')
