@@ -57,10 +57,18 @@ def _geo(kh, kw, stride, pad, offset):
     return [kh, kw, stride, stride, ph, pw, offset, offset]
 
 
+@pytest.fixture(params=[-1, 0, 1, 2], ids=['tuned', 'cfg0', 'cfg1', 'cfg2'])
+def tile_cfg(request):
+    """Every tile configuration of the implicit-GEMM kernel, then the tuned plans."""
+    ops().conv_gemm_force_cfg(request.param)
+    yield request.param
+    ops().conv_gemm_force_cfg(-1)
+
+
 @pytest.mark.parametrize('relu', [True, False])
 @pytest.mark.parametrize('case', CASES, ids=[f'{c[5]}x{c[6]}s{c[7]}o{c[9]}_{c[0]}x{c[1]}x{c[2]}'
                                             for c in CASES])
-def test_conv_gemm_matches_fp64(case, relu):
+def test_conv_gemm_matches_fp64(case, relu, tile_cfg):
     n, ci, h, w, co, kh, kw, stride, pad, offset = case
     torch.manual_seed(0)
     x = torch.randn(n, ci, h, w, device='cuda')
@@ -96,7 +104,7 @@ def _block(kind, ci, co):
 @pytest.mark.parametrize('with_add', [False, True])
 @pytest.mark.parametrize('channels', [(32, 48, 14), (512, 256, 7)], ids=['epilogue-stats',
                                                                        'split-stats'])
-def test_fused_relu_conv_bn_matches_fp64_training_step(kind, with_add, channels):
+def test_fused_relu_conv_bn_matches_fp64_training_step(kind, with_add, channels, tile_cfg):
     torch.manual_seed(1)
     ci, co, hw = channels
     block = _block(kind, ci, co).cuda()

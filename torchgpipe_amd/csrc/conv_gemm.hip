@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "kernels.h"
@@ -85,13 +86,15 @@ struct Geo {
 
 // Tile configurations.  CFG 0: 64 x 64 block, 4 waves (2 x 2) of one 32 x 32 MFMA tile;
 // CFG 1: 128 x 128 block, 8 waves (2 x 4) of 64 x 32 (two tiles) -- two waves per SIMD
-// from one workgroup, so one wave's MFMAs cover the other's LDS reads and barrier.
+// from one workgroup, so one wave's MFMAs cover the other's LDS reads and barrier;
+// CFG 2: 128 x 128 block, 4 waves (2 x 2) of 64 x 64 (2 x 2 tiles): each A / B fragment
+// read from LDS feeds two MFMAs, half the LDS traffic per MFMA of CFG 1.
 template <int CFG>
 struct Cfg {
   static constexpr int WVM = 2;
-  static constexpr int WVN = CFG == 0 ? 2 : 4;
+  static constexpr int WVN = CFG == 1 ? 4 : 2;
   static constexpr int TM = CFG == 0 ? 1 : 2;   // 32 x 32 MFMA tiles per wave (rows)
-  static constexpr int TN = 1;                  // (columns)
+  static constexpr int TN = CFG == 2 ? 2 : 1;   // (columns)
   static constexpr int kThreads = 64 * WVM * WVN;
   static constexpr int BM = WVM * 32 * TM;
   static constexpr int BN = WVN * 32 * TN;
@@ -706,8 +709,8 @@ ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
   const int64_t max_split = std::max<int64_t>(1, K / (4 * kBK));
   if (mode == kWgrad) {
     // few output tiles, long reduction: split until ~512 workgroups
-    plan.big = big >= 64;
-    const int64_t tiles = plan.big ? big : small;
+    plan.cfg = big >= 64 ? 1 : 0;
+    const int64_t tiles = plan.cfg ? big : small;
     plan.splits = static_cast<int>(
         std::min<int64_t>((target_wgrad + tiles - 1) / tiles, max_split));
   } else {
@@ -715,12 +718,12 @@ ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
     static const int target_big = env_int("TGPIPE_CG_TARGET_BIG", 256);
     if (big < fill_big && K >= bigsplit_k) {
       // long reduction over a small output: 8-wave 128 x 128 tiles, split reduction
-      plan.big = true;
+      plan.cfg = 1;
       plan.splits = static_cast<int>(std::min<int64_t>((target_big + big - 1) / big, max_split));
     } else {
-      plan.big = big >= fill_big;
-      const int64_t tiles = plan.big ? big : small;
-      const int64_t fill = plan.big ? fill_big : fill_small;
+      plan.cfg = big >= fill_big ? 1 : 0;
+      const int64_t tiles = plan.cfg ? big : small;
+      const int64_t fill = plan.cfg ? fill_big : fill_small;
       plan.splits = tiles >= fill ? 1
                     : static_cast<int>(std::min<int64_t>((target_small + tiles - 1) / tiles,
                                                          max_split));
@@ -731,7 +734,7 @@ ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
   int k_chunk = (K + plan.splits - 1) / plan.splits;
   k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
   plan.splits = std::max(1, (K + k_chunk - 1) / k_chunk);
-  plan.col_width = plan.big ? 128 : 64;
+  plan.col_width = plan.cfg ? 128 : 64;
   plan.col_blocks = static_cast<int>((N + plan.col_width - 1) / plan.col_width);
   plan.scatter = g.scatter;
   return plan;
@@ -744,8 +747,8 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
   gemm_dims(mode, g, M, N, K);
   std::vector<ConvGemmPlan> out;
   const int max_split = std::max(1, K / (4 * kBK));
-  for (int big = 0; big < 2; ++big) {
-    const int64_t tiles = big ? static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128)
+  for (int cfg = 0; cfg < 3; ++cfg) {
+    const int64_t tiles = cfg ? static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128)
                               : static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
     int last = 0;
     for (int s : {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256, 512, 1024}) {
@@ -756,9 +759,9 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
       if (real == last) continue;
       last = real;
       ConvGemmPlan p;
-      p.big = big != 0;
+      p.cfg = cfg;
       p.splits = real;
-      p.col_width = big ? 128 : 64;
+      p.col_width = cfg ? 128 : 64;
       p.col_blocks = static_cast<int>((N + p.col_width - 1) / p.col_width);
       p.scatter = g.scatter;
       out.push_back(p);
@@ -803,27 +806,29 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
   float* pm = split ? nullptr : part_mean;
   float* pm2 = split ? nullptr : part_m2;
   const bool acc = accumulate && !split;
+  auto go = [&](auto mode_c, auto cfg_c, float* p1, float* p2, const float* mask) {
+    launch_cfg<decltype(mode_c)::value, decltype(cfg_c)::value>(
+        a, b, mask, dst, p1, p2, gk, M, N, K, plan.splits, stride, acc, a_bytes, b_bytes,
+        stream);
+  };
+  using F = std::integral_constant<int, kFwd>;
+  using D = std::integral_constant<int, kBwdData>;
+  using W = std::integral_constant<int, kWgrad>;
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using C2 = std::integral_constant<int, 2>;
   if (mode == kFwd) {
-    if (plan.big)
-      launch_cfg<kFwd, 1>(a, b, x_mask, dst, pm, pm2, gk, M, N, K, plan.splits, stride, acc,
-                          a_bytes, b_bytes, stream);
-    else
-      launch_cfg<kFwd, 0>(a, b, x_mask, dst, pm, pm2, gk, M, N, K, plan.splits, stride, acc,
-                          a_bytes, b_bytes, stream);
+    if (plan.cfg == 2) go(F{}, C2{}, pm, pm2, x_mask);
+    else if (plan.cfg == 1) go(F{}, C1{}, pm, pm2, x_mask);
+    else go(F{}, C0{}, pm, pm2, x_mask);
   } else if (mode == kBwdData) {
-    if (plan.big)
-      launch_cfg<kBwdData, 1>(a, b, x_mask, dst, nullptr, nullptr, gk, M, N, K, plan.splits,
-                              stride, acc, a_bytes, b_bytes, stream);
-    else
-      launch_cfg<kBwdData, 0>(a, b, x_mask, dst, nullptr, nullptr, gk, M, N, K, plan.splits,
-                              stride, acc, a_bytes, b_bytes, stream);
+    if (plan.cfg == 2) go(D{}, C2{}, nullptr, nullptr, x_mask);
+    else if (plan.cfg == 1) go(D{}, C1{}, nullptr, nullptr, x_mask);
+    else go(D{}, C0{}, nullptr, nullptr, x_mask);
   } else {
-    if (plan.big)
-      launch_cfg<kWgrad, 1>(a, b, nullptr, dst, nullptr, nullptr, gk, M, N, K, plan.splits,
-                            stride, acc, a_bytes, b_bytes, stream);
-    else
-      launch_cfg<kWgrad, 0>(a, b, nullptr, dst, nullptr, nullptr, gk, M, N, K, plan.splits,
-                            stride, acc, a_bytes, b_bytes, stream);
+    if (plan.cfg == 2) go(W{}, C2{}, nullptr, nullptr, nullptr);
+    else if (plan.cfg == 1) go(W{}, C1{}, nullptr, nullptr, nullptr);
+    else go(W{}, C0{}, nullptr, nullptr, nullptr);
   }
   if (!split) return;
   // out[dst(i)] = (accumulate ? out : 0) + mask * sum_s ws[s][i]

@@ -9,6 +9,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -51,6 +52,10 @@ using PlanKey = std::tuple<int, int, int, int, int, int, int, int, int, int, int
                            int>;
 std::mutex plan_mutex;
 std::map<PlanKey, ConvGemmPlan> plan_cache;
+std::atomic<int> forced_cfg{-1};
+
+// Test hook: run every implicit-GEMM launch with tile config `cfg` (unsplit), -1 = tuned.
+void conv_gemm_force_cfg(int64_t cfg) { forced_cfg.store(static_cast<int>(cfg)); }
 
 ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* mask, float* out,
                         float* pm, float* pm2, const ConvGemmGeo& g, bool accumulate,
@@ -61,6 +66,12 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
     return v == nullptr || std::string(v) != "0";
   }();
   const ConvGemmPlan heuristic = conv_gemm_plan(mode, g);
+  const int forced = forced_cfg.load();
+  if (forced >= 0) {  // test hook: the first (unsplit) candidate of that tile config
+    for (const auto& cand : conv_gemm_candidates(mode, g))
+      if (cand.cfg == forced) return cand;
+    return heuristic;
+  }
   if (!tune) return heuristic;
   const hipStream_t stream = cur_stream(like);
   hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
@@ -103,7 +114,7 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
   return best;
 }
 
-// One line per plan: "mode n ci h w co kh kw sh sw ph pw oh ow co_total big splits".
+// One line per plan: "mode n ci h w co kh kw sh sw ph pw oh ow co_total cfg splits".
 std::string conv_gemm_plans_export() {
   std::lock_guard<std::mutex> lock(plan_mutex);
   std::ostringstream out;
@@ -114,7 +125,7 @@ std::string conv_gemm_plans_export() {
         << std::get<6>(k) << ' ' << std::get<7>(k) << ' ' << std::get<8>(k) << ' '
         << std::get<9>(k) << ' ' << std::get<10>(k) << ' ' << std::get<11>(k) << ' '
         << std::get<12>(k) << ' ' << std::get<13>(k) << ' ' << std::get<14>(k) << ' '
-        << (kv.second.big ? 1 : 0) << ' ' << kv.second.splits << '\n';
+        << kv.second.cfg << ' ' << kv.second.splits << '\n';
   }
   return out.str();
 }
@@ -158,7 +169,7 @@ int64_t conv_gemm_plans_import(const std::string& text) {
                       g.ow, g.co_total};
     if (plan_cache.count(key)) continue;
     for (const auto& cand : conv_gemm_candidates(v[0], g)) {
-      if (cand.big == (v[15] != 0) && cand.splits == v[16]) {
+      if (cand.cfg == v[15] && cand.splits == v[16]) {
         plan_cache[key] = cand;
         ++taken;
         break;
@@ -605,6 +616,7 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
         "Tensor?[] accum) -> Tensor[]");
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
   m.def("conv_gemm_plans_export() -> str", &tgpipe::conv_gemm_plans_export);
+  m.def("conv_gemm_force_cfg(int cfg) -> ()", &tgpipe::conv_gemm_force_cfg);
   m.def("conv_gemm_plans_import(str text) -> int", &tgpipe::conv_gemm_plans_import);
   m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu) "
         "-> Tensor");

@@ -137,7 +137,8 @@ struct ConvGemmGeo {
 // mode 2: weight gradient  dW[co][ci*kh*kw] = dZ * relu(X); a = dZ, b = X.
 // splits > 1 needs a workspace of conv_gemm_workspace() floats.
 struct ConvGemmPlan {
-  bool big = true;       // 128 x 128 tiles (else 64 x 64)
+  int cfg = 1;           // tiles: 0 = 64 x 64 (4 waves), 1 = 128 x 128 (8 waves),
+                         // 2 = 128 x 128 (4 waves of 2 x 2 MFMA tiles)
   int splits = 1;        // reduction splits (grid.y), > 1: workspace slices + split_reduce
   int col_width = 128;   // forward: columns per statistics block
   int col_blocks = 0;    // forward: statistics blocks
