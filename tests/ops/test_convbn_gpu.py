@@ -57,7 +57,7 @@ def _geo(kh, kw, stride, pad, offset):
     return [kh, kw, stride, stride, ph, pw, offset, offset]
 
 
-@pytest.fixture(params=[-1, 0, 1, 2], ids=['tuned', 'cfg0', 'cfg1', 'cfg2'])
+@pytest.fixture(params=[-1, 0, 1, 2, 3, 4, 5], ids=['tuned'] + [f'cfg{i}' for i in range(6)])
 def tile_cfg(request):
     """Every tile configuration of the implicit-GEMM kernel, then the tuned plans."""
     ops().conv_gemm_force_cfg(request.param)

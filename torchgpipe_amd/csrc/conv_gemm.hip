@@ -89,16 +89,21 @@ struct Geo {
 // from one workgroup, so one wave's MFMAs cover the other's LDS reads and barrier;
 // CFG 2: 128 x 128 block, 4 waves (2 x 2) of 64 x 64 (2 x 2 tiles): each A / B fragment
 // read from LDS feeds two MFMAs, half the LDS traffic per MFMA of CFG 1.
+// CFG 3 / 4 / 5: CFG 0 / 1 / 2 with SUB = 4 / 2 / 2 BK-deep sub-stages per barrier and
+// per prefetch: a small grid (one workgroup per CU) then keeps SUB x more loads in flight
+// per wave -- each stage's MFMAs cover one global-load latency instead of a fraction.
 template <int CFG>
 struct Cfg {
+  static constexpr int TILE = CFG % 3;
+  static constexpr int SUB = CFG < 3 ? 1 : (CFG == 3 ? 4 : 2);
   static constexpr int WVM = 2;
-  static constexpr int WVN = CFG == 1 ? 4 : 2;
-  static constexpr int TM = CFG == 0 ? 1 : 2;   // 32 x 32 MFMA tiles per wave (rows)
-  static constexpr int TN = CFG == 2 ? 2 : 1;   // (columns)
+  static constexpr int WVN = TILE == 1 ? 4 : 2;
+  static constexpr int TM = TILE == 0 ? 1 : 2;   // 32 x 32 MFMA tiles per wave (rows)
+  static constexpr int TN = TILE == 2 ? 2 : 1;   // (columns)
   static constexpr int kThreads = 64 * WVM * WVN;
   static constexpr int BM = WVM * 32 * TM;
   static constexpr int BN = WVN * 32 * TN;
-  static constexpr int kAImg = kBK * BM;          // K-major image
+  static constexpr int kAImg = kBK * BM;          // K-major image (one sub-stage)
   static constexpr int kBImgK = kBK * BN;         // K-major image
   static constexpr int kBStrideN = BN + 32;       // N-major row stride
   static constexpr int kBImgN = kBK * kBStrideN;  // N-major image
@@ -106,7 +111,7 @@ struct Cfg {
   // register) land 32 banks apart
   static constexpr int kCStride = BN + 8;
   static constexpr int kOpFloats(bool k_major) {
-    return 2 * kAImg + 2 * (k_major ? kBImgK : kBImgN);
+    return 2 * SUB * (kAImg + (k_major ? kBImgK : kBImgN));
   }
   // operand images (double-buffered), reused by the epilogue's C tile (forward /
   // bwd-data); 128 x 128: 72 KiB -> two workgroups per CU
@@ -243,9 +248,11 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
   constexpr int WM = C::TM, WN = C::TN, kThreads = C::kThreads;
   constexpr bool kBK_major = MODE == kWgrad;
   constexpr int kBImg = kBK_major ? C::kBImgK : C::kBImgN;
+  constexpr int SUB = C::SUB;
   __shared__ __attribute__((aligned(16))) float lds[C::kLdsFloats(MODE)];
-  auto aimg = [&](int b) { return lds + b * C::kAImg; };
-  auto bimg = [&](int b) { return lds + 2 * C::kAImg + b * kBImg; };
+  // buffer b, sub-stage u
+  auto aimg = [&](int b, int u) { return lds + (b * SUB + u) * C::kAImg; };
+  auto bimg = [&](int b, int u) { return lds + 2 * SUB * C::kAImg + (b * SUB + u) * kBImg; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % C::WVM, wn = wave / C::WVM;
@@ -268,7 +275,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
   const bool quads = kPlain && (hw_out & 3) == 0;
 
   constexpr int kRB = kBK_major ? C::kBQuadsK : C::kBQuadsN;
-  floatx4 ra[C::kAQuads], rb[kRB];
+  floatx4 ra[SUB][C::kAQuads], rb[SUB][kRB];
 
   // N-major B columns of this thread (forward / bwd-data)
   constexpr int QPR = C::BN / 4;
@@ -430,12 +437,22 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
     }
   };
 
-  auto store_stage = [&](int buf, const floatx4 (&ra)[C::kAQuads], const floatx4 (&rb)[kRB]) {
-    store_kmajor<C::BM, C::kAQuads, kThreads>(aimg(buf), ra, tid);
-    if constexpr (kBK_major)
-      store_kmajor<C::BN, C::kBQuadsK, kThreads>(bimg(buf), rb, tid);
-    else
-      store_nmajor<C::BN, C::kBQuadsN, kThreads>(bimg(buf), rb, tid);
+  auto load_stage = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) {
+      load_a(k0 + u * kBK, ra[u]);
+      load_b(k0 + u * kBK, rb[u]);
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) {
+      store_kmajor<C::BM, C::kAQuads, kThreads>(aimg(buf, u), ra[u], tid);
+      if constexpr (kBK_major)
+        store_kmajor<C::BN, C::kBQuadsK, kThreads>(bimg(buf, u), rb[u], tid);
+      else
+        store_nmajor<C::BN, C::kBQuadsN, kThreads>(bimg(buf, u), rb[u], tid);
+    }
   };
 
   floatx16 acc[WM][WN];
@@ -446,21 +463,20 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int stages = (k_end - k_begin + kBK - 1) / kBK;
+  constexpr int kStageK = kBK * SUB;
+  const int stages = (k_end - k_begin + kStageK - 1) / kStageK;
   if (stages > 0) {
-    load_a(k_begin, ra);
-    load_b(k_begin, rb);
-    store_stage(0, ra, rb);
+    load_stage(k_begin);
+    store_stage(0);
     __syncthreads();
     for (int s = 0; s < stages; ++s) {
       const int buf = s & 1;
       const bool more = s + 1 < stages;
-      if (more) {
-        load_a(k_begin + (s + 1) * kBK, ra);
-        load_b(k_begin + (s + 1) * kBK, rb);
-      }
-      mfma_stage<CFG, kBK_major>(acc, aimg(buf), bimg(buf), lane, wm, wn);
-      if (more) store_stage(buf ^ 1, ra, rb);
+      if (more) load_stage(k_begin + (s + 1) * kStageK);
+#pragma unroll
+      for (int u = 0; u < SUB; ++u)
+        mfma_stage<CFG, kBK_major>(acc, aimg(buf, u), bimg(buf, u), lane, wm, wn);
+      if (more) store_stage(buf ^ 1);
       __syncthreads();
     }
   }
@@ -593,7 +609,7 @@ void launch_cfg(const float* a, const float* b, const float* xm, float* out, flo
   using C = Cfg<CFG>;
   const int mb = (M + C::BM - 1) / C::BM, nb = (N + C::BN - 1) / C::BN;
   int k_chunk = (K + splits - 1) / splits;
-  k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
+  k_chunk = (k_chunk + kBK - 1) / kBK * kBK;  // (the plan's split count: whole BK steps)
   const int zs = (K + k_chunk - 1) / k_chunk;
   const bool plain = g.taps == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 &&
                      g.oh == 0 && g.ow == 0;
@@ -610,40 +626,50 @@ void launch_cfg(const float* a, const float* b, const float* xm, float* out, flo
 
 // Sum of the split partials: ws[s][plane][c][hw] -> out[plane][c_off + c][hw] (c_total
 // channels), times the ReLU mask (x_mask, indexed like out) when given, plus the
-// previous contents of out when accumulating.
+// previous contents of out when accumulating.  A workgroup covers 64 quads (or 64
+// elements) with its 4 waves each summing every 4th split through 4 independent
+// accumulators (16 loads in flight per lane), then the waves combine through LDS: the
+// weight gradient's 30-60-way splits no longer walk a serial chain of dependent loads
+// per element (measured 12 us for 62 x 64 KiB partials with one lane per element).
 template <bool kVec>
 __global__ __launch_bounds__(256) void split_reduce_kernel(
     const float* __restrict__ ws, int splits, int64_t stride, float* __restrict__ out,
     const float* __restrict__ mask, int accumulate, int64_t total, int64_t c, int64_t hw,
     int64_t c_total, int64_t c_off) {
-  const int64_t step = static_cast<int64_t>(gridDim.x) * 256;
-  if constexpr (kVec) {
-    for (int64_t q = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; q < total / 4;
-         q += step) {
-      const int64_t i = 4 * q;
-      const int64_t pl = i / (c * hw), r = i - pl * c * hw;
-      const int64_t o = (pl * c_total + c_off) * hw + r;
-      floatx4 v = reinterpret_cast<const floatx4*>(ws)[q];
-      for (int s = 1; s < splits; ++s) v += reinterpret_cast<const floatx4*>(ws + s * stride)[q];
-      if (mask) {
-        const floatx4 m = *reinterpret_cast<const floatx4*>(mask + o);
+  constexpr int kE = kVec ? 4 : 1;
+  typedef float V __attribute__((ext_vector_type(kE)));
+  __shared__ V part[3][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t items = total / kE;
+  const int64_t q = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  const bool ok = q < items;
+  const V* src = reinterpret_cast<const V*>(ws) + (ok ? q : 0);
+  const int64_t vstride = stride / kE;
+  V acc[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
-      }
-      if (accumulate) v += *reinterpret_cast<const floatx4*>(out + o);
-      *reinterpret_cast<floatx4*>(out + o) = v;
-    }
-  } else {
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total; i += step) {
-      const int64_t pl = i / (c * hw), r = i - pl * c * hw;
-      const int64_t o = (pl * c_total + c_off) * hw + r;
-      float v = ws[i];
-      for (int s = 1; s < splits; ++s) v += ws[s * stride + i];
-      if (mask && !(mask[o] > 0.f)) v = 0.f;
-      if (accumulate) v += out[o];
-      out[o] = v;
-    }
+  for (int u = 0; u < 4; ++u) acc[u] = V(0.f);
+  int sp = grp;
+  for (; sp + 12 < splits; sp += 16) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] += src[(sp + 4 * u) * vstride];
   }
+  for (; sp < splits; sp += 4) acc[0] += src[sp * vstride];
+  V v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  if (grp > 0) part[grp - 1][lane] = v;
+  __syncthreads();
+  if (grp != 0 || !ok) return;
+  v += part[0][lane] + part[1][lane] + part[2][lane];
+  const int64_t i = q * kE;
+  const int64_t pl = i / (c * hw), r = i - pl * c * hw;
+  const int64_t o = (pl * c_total + c_off) * hw + r;
+  V* dst = reinterpret_cast<V*>(out + o);
+  if (mask) {
+    const V m = *reinterpret_cast<const V*>(mask + o);
+#pragma unroll
+    for (int e = 0; e < kE; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
+  }
+  if (accumulate) v += *dst;
+  *dst = v;
 }
 
 void launch_split_reduce(const float* ws, int splits, int64_t stride, float* out,
@@ -652,16 +678,15 @@ void launch_split_reduce(const float* ws, int splits, int64_t stride, float* out
   const int64_t total = planes * c * hw;
   if (total == 0) return;
   const bool vec = (hw & 3) == 0 && (stride & 3) == 0;
-  int64_t blocks = ((vec ? total / 4 : total) + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  const int64_t items = vec ? total / 4 : total;
+  const unsigned blocks = static_cast<unsigned>((items + 63) / 64);
   if (vec)
-    hipLaunchKernelGGL(split_reduce_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(256),
-                       0, stream, ws, splits, stride, out, mask, accumulate ? 1 : 0, total, c,
-                       hw, c_total, c_off);
+    hipLaunchKernelGGL(split_reduce_kernel<true>, dim3(blocks), dim3(256), 0, stream, ws, splits,
+                       stride, out, mask, accumulate ? 1 : 0, total, c, hw, c_total, c_off);
   else
-    hipLaunchKernelGGL(split_reduce_kernel<false>, dim3(static_cast<unsigned>(blocks)),
-                       dim3(256), 0, stream, ws, splits, stride, out, mask, accumulate ? 1 : 0,
-                       total, c, hw, c_total, c_off);
+    hipLaunchKernelGGL(split_reduce_kernel<false>, dim3(blocks), dim3(256), 0, stream, ws,
+                       splits, stride, out, mask, accumulate ? 1 : 0, total, c, hw, c_total,
+                       c_off);
 }
 
 Geo make_geo(const ConvGemmGeo& cg) {
@@ -734,7 +759,7 @@ ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
   int k_chunk = (K + plan.splits - 1) / plan.splits;
   k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
   plan.splits = std::max(1, (K + k_chunk - 1) / k_chunk);
-  plan.col_width = plan.cfg ? 128 : 64;
+  plan.col_width = plan.cfg % 3 ? 128 : 64;
   plan.col_blocks = static_cast<int>((N + plan.col_width - 1) / plan.col_width);
   plan.scatter = g.scatter;
   return plan;
@@ -747,9 +772,9 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
   gemm_dims(mode, g, M, N, K);
   std::vector<ConvGemmPlan> out;
   const int max_split = std::max(1, K / (4 * kBK));
-  for (int cfg = 0; cfg < 3; ++cfg) {
-    const int64_t tiles = cfg ? static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128)
-                              : static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
+  for (int cfg = 0; cfg < 6; ++cfg) {
+    const int64_t tiles = cfg % 3 ? static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128)
+                                  : static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
     int last = 0;
     for (int s : {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256, 512, 1024}) {
       if (s > 1 && (s > max_split || g.scatter || tiles * s > 8192)) break;
@@ -761,7 +786,7 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
       ConvGemmPlan p;
       p.cfg = cfg;
       p.splits = real;
-      p.col_width = cfg ? 128 : 64;
+      p.col_width = cfg % 3 ? 128 : 64;
       p.col_blocks = static_cast<int>((N + p.col_width - 1) / p.col_width);
       p.scatter = g.scatter;
       out.push_back(p);
@@ -817,19 +842,25 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
   using C2 = std::integral_constant<int, 2>;
-  if (mode == kFwd) {
-    if (plan.cfg == 2) go(F{}, C2{}, pm, pm2, x_mask);
-    else if (plan.cfg == 1) go(F{}, C1{}, pm, pm2, x_mask);
-    else go(F{}, C0{}, pm, pm2, x_mask);
-  } else if (mode == kBwdData) {
-    if (plan.cfg == 2) go(D{}, C2{}, nullptr, nullptr, x_mask);
-    else if (plan.cfg == 1) go(D{}, C1{}, nullptr, nullptr, x_mask);
-    else go(D{}, C0{}, nullptr, nullptr, x_mask);
-  } else {
-    if (plan.cfg == 2) go(W{}, C2{}, nullptr, nullptr, nullptr);
-    else if (plan.cfg == 1) go(W{}, C1{}, nullptr, nullptr, nullptr);
-    else go(W{}, C0{}, nullptr, nullptr, nullptr);
-  }
+  using C3 = std::integral_constant<int, 3>;
+  using C4 = std::integral_constant<int, 4>;
+  using C5 = std::integral_constant<int, 5>;
+  auto by_cfg = [&](auto mode_c, float* p1, float* p2, const float* mask) {
+    switch (plan.cfg) {
+      case 1: go(mode_c, C1{}, p1, p2, mask); break;
+      case 2: go(mode_c, C2{}, p1, p2, mask); break;
+      case 3: go(mode_c, C3{}, p1, p2, mask); break;
+      case 4: go(mode_c, C4{}, p1, p2, mask); break;
+      case 5: go(mode_c, C5{}, p1, p2, mask); break;
+      default: go(mode_c, C0{}, p1, p2, mask); break;
+    }
+  };
+  if (mode == kFwd)
+    by_cfg(F{}, pm, pm2, x_mask);
+  else if (mode == kBwdData)
+    by_cfg(D{}, nullptr, nullptr, x_mask);
+  else
+    by_cfg(W{}, nullptr, nullptr, nullptr);
   if (!split) return;
   // out[dst(i)] = (accumulate ? out : 0) + mask * sum_s ws[s][i]
   int64_t planes, c, hw, c_total = 0, c_off = 0;

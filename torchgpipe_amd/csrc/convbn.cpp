@@ -53,9 +53,14 @@ using PlanKey = std::tuple<int, int, int, int, int, int, int, int, int, int, int
 std::mutex plan_mutex;
 std::map<PlanKey, ConvGemmPlan> plan_cache;
 std::atomic<int> forced_cfg{-1};
+std::atomic<int> forced_splits{1};
 
-// Test hook: run every implicit-GEMM launch with tile config `cfg` (unsplit), -1 = tuned.
-void conv_gemm_force_cfg(int64_t cfg) { forced_cfg.store(static_cast<int>(cfg)); }
+// Test / profiling hook: run every implicit-GEMM launch with tile config `cfg` and (at
+// most) `splits` reduction splits; cfg -1 = tuned plans.
+void conv_gemm_force_cfg(int64_t cfg, int64_t splits) {
+  forced_cfg.store(static_cast<int>(cfg));
+  forced_splits.store(static_cast<int>(splits));
+}
 
 ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* mask, float* out,
                         float* pm, float* pm2, const ConvGemmGeo& g, bool accumulate,
@@ -67,10 +72,16 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
   }();
   const ConvGemmPlan heuristic = conv_gemm_plan(mode, g);
   const int forced = forced_cfg.load();
-  if (forced >= 0) {  // test hook: the first (unsplit) candidate of that tile config
+  if (forced >= 0) {  // test hook: that tile config's candidate with the most splits <= N
+    ConvGemmPlan pick = heuristic;
+    bool found = false;
     for (const auto& cand : conv_gemm_candidates(mode, g))
-      if (cand.cfg == forced) return cand;
-    return heuristic;
+      if (cand.cfg == forced && cand.splits <= std::max(1, forced_splits.load()) &&
+          (!found || cand.splits > pick.splits)) {
+        pick = cand;
+        found = true;
+      }
+    return pick;
   }
   if (!tune) return heuristic;
   const hipStream_t stream = cur_stream(like);
@@ -415,6 +426,58 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   return out;
 }
 
+// Benchmark hook (benchmarks/convgemm_sweep.py): device time of every candidate plan of one
+// convolution's GEMM `mode` (0 fwd, 1 bwd-data, 2 wgrad), `reps` back-to-back launches each
+// (kernel + split reduction) between two events.  Returns [cfg, splits, microseconds]*.
+std::vector<double> conv_gemm_sweep(int64_t mode, const at::Tensor& x_in,
+                                    const at::Tensor& weight, at::IntArrayRef geo, int64_t reps) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  TORCH_CHECK(mode >= 0 && mode <= 2 && reps > 0, "mode 0-2, reps > 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Parts p = make_parts(x, {weight}, geo, false);
+  const ConvGemmGeo& g = p.geo[0];
+  auto z = at::randn({x.size(0), p.co_total, p.ho, p.wo}, x.options());
+  auto dx = at::empty_like(x);
+  auto dw = at::empty_like(weight);
+  const float *a, *b;
+  float* out;
+  int64_t a_bytes, b_bytes;
+  if (mode == 0) {
+    a = weight.data_ptr<float>(); b = x.data_ptr<float>(); out = z.data_ptr<float>();
+    a_bytes = weight.numel() * 4; b_bytes = x.numel() * 4;
+  } else if (mode == 1) {
+    a = weight.data_ptr<float>(); b = z.data_ptr<float>(); out = dx.data_ptr<float>();
+    a_bytes = weight.numel() * 4; b_bytes = z.numel() * 4;
+  } else {
+    a = z.data_ptr<float>(); b = x.data_ptr<float>(); out = dw.data_ptr<float>();
+    a_bytes = z.numel() * 4; b_bytes = x.numel() * 4;
+  }
+  const hipStream_t stream = cur_stream(x);
+  hipEvent_t t0, t1;
+  hipEventCreate(&t0);
+  hipEventCreate(&t1);
+  std::vector<double> res;
+  for (const auto& cand : conv_gemm_candidates(static_cast<int>(mode), g)) {
+    launch_one(static_cast<int>(mode), a, b, nullptr, out, nullptr, nullptr, g, cand,
+               cand.scatter, a_bytes, b_bytes, x);  // warm-up
+    hipEventRecord(t0, stream);
+    for (int64_t r = 0; r < reps; ++r)
+      launch_one(static_cast<int>(mode), a, b, nullptr, out, nullptr, nullptr, g, cand,
+                 cand.scatter, a_bytes, b_bytes, x);
+    hipEventRecord(t1, stream);
+    hipEventSynchronize(t1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, t0, t1);
+    res.push_back(cand.cfg);
+    res.push_back(cand.splits);
+    res.push_back(1000.0 * ms / static_cast<double>(reps));
+  }
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  return res;
+}
+
 // Plain convolution (no BatchNorm) through the same kernels: forward / backward-data /
 // weight-gradient, e.g. U-Net's final 1x1 segmentation convolution.
 at::Tensor conv_gemm_forward(const at::Tensor& x_in, const at::Tensor& weight,
@@ -616,7 +679,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
         "Tensor?[] accum) -> Tensor[]");
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
   m.def("conv_gemm_plans_export() -> str", &tgpipe::conv_gemm_plans_export);
-  m.def("conv_gemm_force_cfg(int cfg) -> ()", &tgpipe::conv_gemm_force_cfg);
+  m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
+  m.def("conv_gemm_sweep(int mode, Tensor x, Tensor weight, int[] geo, int reps) -> float[]");
   m.def("conv_gemm_plans_import(str text) -> int", &tgpipe::conv_gemm_plans_import);
   m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu) "
         "-> Tensor");
@@ -628,6 +692,7 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("convbn_forward", &tgpipe::convbn_forward);
   m.impl("convbn_backward", &tgpipe::convbn_backward);
   m.impl("conv_gemm_forward", &tgpipe::conv_gemm_forward);
+  m.impl("conv_gemm_sweep", &tgpipe::conv_gemm_sweep);
   m.impl("conv_gemm_backward_data", &tgpipe::conv_gemm_backward_data);
   m.impl("conv_gemm_backward_weight", &tgpipe::conv_gemm_backward_weight);
   m.impl("bn_train_forward", &tgpipe::bn_train_forward);
