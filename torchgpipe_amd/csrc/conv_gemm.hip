@@ -365,11 +365,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
                                       (col[e].base + (ci * g.h + yi) * g.w + xi) * 4) : kOOB);
           }
         }
-        if (g.relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = relu(v[e]);
-        }
-        rb[i] = v;
+        rb[i] = v;  // (ReLU at store time: using the value here would wait for the load)
       }
     } else if constexpr (MODE == kBwdData) {
       // dZ taps: B[k = (co, t)][j = pixel]
@@ -428,11 +424,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
             v[e] = bload(br, off);
           }
         }
-        if (g.relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = relu(v[e]);
-        }
-        rb[i] = v;
+        rb[i] = v;  // (ReLU at store time)
       }
     }
   };
@@ -444,7 +436,20 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
       load_b(k0 + u * kBK, rb[u]);
     }
   };
+  // The forward / weight-gradient ReLU of X is applied here, after the stage's MFMAs:
+  // applied in load_b it made every prefetch wait for its own loads (vmcnt(0) right
+  // after issue), leaving the global-load latency exposed once per stage.
   auto store_stage = [&](int buf) {
+    if constexpr (MODE != kBwdData) {
+      if (g.relu) {
+#pragma unroll
+        for (int u = 0; u < SUB; ++u)
+#pragma unroll
+          for (int i = 0; i < kRB; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rb[u][i][e] = relu(rb[u][i][e]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       store_kmajor<C::BM, C::kAQuads, kThreads>(aimg(buf, u), ra[u], tid);
