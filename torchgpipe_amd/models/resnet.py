@@ -14,7 +14,7 @@ from torch import Tensor, nn
 from torchgpipe_amd.models.flatten import flatten_sequential
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
-__all__ = ['resnet101', 'build_resnet']
+__all__ = ['resnet50', 'resnet101', 'build_resnet']
 
 
 @skippable(stash=['identity'])
@@ -97,3 +97,8 @@ def build_resnet(layers: List[int], num_classes: int = 1000, inplace: bool = Fal
 
 def resnet101(**kwargs: Any) -> nn.Sequential:
     return build_resnet([3, 4, 23, 3], **kwargs)
+
+
+def resnet50(**kwargs: Any) -> nn.Sequential:
+    """ResNet-50 (the reference's distributed accuracy benchmark also offers it)."""
+    return build_resnet([3, 4, 6, 3], **kwargs)
