@@ -218,3 +218,26 @@ def test_gather_writes_preallocated_output_during_pipeline():
     for p, q in zip(gpipe.parameters(), ref.parameters()):
         err = ((p.grad - q.grad).norm() / q.grad.norm()).item()
         assert err < 1e-4, (p.shape, err)
+
+
+@pytest.mark.parametrize('pool', [1, 4, None], ids=['ring1', 'ring4', 'per-microbatch'])
+@pytest.mark.parametrize('devices', [[0, 0], [0, 1]], ids=['1gpu', '2gpu'])
+def test_copy_stream_ring_size_is_transparent(devices, pool):
+    """micro-batches i and i+4 share a copy stream in the default 4-stream ring.
+    The ring size only changes stream sharing, never results: a training step with one
+    shared stream, the default ring and one stream per micro-batch (the reference's
+    layout) gives the unpartitioned model's gradients."""
+    from tests.distributed import parity
+    if max(devices) >= torch.cuda.device_count():
+        pytest.skip(f'needs {max(devices) + 1} GPUs')
+    chunks = 6  # one sample per micro-batch: micro-batches 0/4 and 1/5 share ring4 streams
+    gpipe = GPipe(parity.build('unet'), parity.balance('unet', 2), devices=devices,
+                  chunks=chunks, checkpoint='except_last',
+                  copy_streams_per_device=pool or chunks)
+    x, t = parity.data('unet', torch.device('cuda', devices[0]))
+    out = gpipe(x)
+    loss = parity.loss_fn('unet')(out, t.to(out.device))
+    loss.backward()
+    want, want_loss = parity.reference('unet', torch.device('cuda', 0), chunks)
+    got = [p.grad.detach().cpu() for p in gpipe.parameters()]
+    parity.assert_parity([{'grads': got, 'loss': loss.item()}], want, want_loss, rel=1e-4)

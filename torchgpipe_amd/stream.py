@@ -123,6 +123,15 @@ class StreamPool:
     small ring of streams; correctness only needs that the stream used to copy
     micro-batch ``i`` into partition ``j`` is the same one that its ``Wait``
     synchronises with, which the modulo mapping guarantees.
+
+    Why a ring of 4 by default: a HIP process gets ``GPU_MAX_HW_QUEUES`` (4) hardware
+    queues per device, so streams beyond that are multiplexed onto the same queues
+    anyway, and in the fill-drain schedule at most ~2 micro-batches per device are in
+    flight on the copy path at once.  Micro-batches ``i`` and ``i + 4`` then share a stream,
+    which only adds ordering between copies that the clock schedule already orders.
+    ``GPipe(copy_streams_per_device=chunks)`` restores the reference's one stream per
+    micro-batch; ``tests/test_gpu_pipeline.py::test_copy_stream_ring_size_is_transparent``
+    checks that rings of 1, 4 and ``chunks`` give identical training gradients.
     """
 
     def __init__(self, size: int = 4) -> None:
