@@ -227,7 +227,7 @@ def test_gemm_conv2d_module_matches_conv2d():
 
 
 @pytest.mark.parametrize('stride', [1, 2])
-@pytest.mark.parametrize('hw', [(7, 7), (12, 9), (1, 1), (2, 3)])
+@pytest.mark.parametrize('hw', [(7, 7), (12, 9), (1, 1), (2, 3), (120, 121)])
 @pytest.mark.parametrize('with_add', [False, True])
 def test_avgpool3_matches_fp64(stride, hw, with_add):
     from torchgpipe_amd.ops.pool import AvgPool3x3
