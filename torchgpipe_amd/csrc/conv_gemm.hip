@@ -82,6 +82,7 @@ struct Geo {
   int oh, ow;            // extra input offset (FactorizedReduce's shifted branch: 1)
   int relu;              // ReLU on the input (forward / weight-grad) / its mask (bwd-data)
   int scatter;           // bwd-data over output pixels, results scattered (strided 1x1)
+  int a_t;               // bwd-data: A is the transposed weight [ci][co*T] (row-major)
 };
 
 // Tile configurations.  CFG 0: 64 x 64 block, 4 waves (2 x 2) of one 32 x 32 MFMA tile;
@@ -303,6 +304,17 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
                                      ? static_cast<uint32_t>((row * K + k + e) * 4) : kOOB);
         }
       } else if constexpr (MODE == kBwdData) {
+        if (g.a_t) {  // transposed weight [ci][co*T]: K-contiguous rows, like the forward
+          if (row < M && k + 3 < k_end && (K & 3) == 0) {
+            ra[i] = bload4(ar, static_cast<uint32_t>((row * K + k) * 4));
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              ra[i][e] = bload(ar, row < M && k + e < k_end
+                                       ? static_cast<uint32_t>((row * K + k + e) * 4) : kOOB);
+          }
+          continue;
+        }
         // A[ci][co*T + t] = W[co][ci][t]: gathered from the untransposed weight (L2)
         const int T = g.taps;
 #pragma unroll
@@ -682,7 +694,10 @@ void launch_split_reduce(const float* ws, int splits, int64_t stride, float* out
                          int64_t hw, int64_t c_total, int64_t c_off, hipStream_t stream) {
   const int64_t total = planes * c * hw;
   if (total == 0) return;
-  const bool vec = (hw & 3) == 0 && (stride & 3) == 0;
+  // quads never straddle a channel plane when hw % 4 == 0, and a single dense output
+  // (backward-data / weight-gradient partials: planes 1, hw 1) is one flat array
+  const bool flat = planes == 1 && c_off == 0 && c_total == c;
+  const bool vec = ((hw & 3) == 0 || (flat && (total & 3) == 0)) && (stride & 3) == 0;
   const int64_t items = vec ? total / 4 : total;
   const unsigned blocks = static_cast<unsigned>((items + 63) / 64);
   if (vec)
@@ -696,7 +711,8 @@ void launch_split_reduce(const float* ws, int splits, int64_t stride, float* out
 
 Geo make_geo(const ConvGemmGeo& cg) {
   Geo g{cg.n, cg.ci, cg.h, cg.w, cg.co, cg.ho, cg.wo, cg.co_total, cg.co_off, cg.kh, cg.kw,
-        cg.kh * cg.kw, cg.sh, cg.sw, cg.ph, cg.pw, cg.oh, cg.ow, cg.relu ? 1 : 0, 0};
+        cg.kh * cg.kw, cg.sh, cg.sw, cg.ph, cg.pw, cg.oh, cg.ow, cg.relu ? 1 : 0, 0,
+        cg.a_t ? 1 : 0};
   return g;
 }
 

@@ -354,7 +354,8 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                                         const c10::optional<at::Tensor>& gamma,
                                         at::TensorList weights, at::IntArrayRef geo, bool relu,
                                         bool need_dx,
-                                        const c10::List<c10::optional<at::Tensor>>& accum) {
+                                        const c10::List<c10::optional<at::Tensor>>& accum,
+                                        at::TensorList weights_t) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   check_f32(x, "x", x);
@@ -398,13 +399,32 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
     bool zero = false;
     for (const auto& g : p.geo) zero = zero || conv_gemm_plan(1, g).scatter;
     dx = zero ? at::zeros_like(x) : at::empty_like(x);  // stride holes receive nothing
+    // the backward-data A operand is W^T: one small transpose per weight, then the
+    // GEMM streams K-contiguous rows instead of gathering a column per element
+    // (`weights_t`: the caller's per-step cached transposes, ops/conv.py _TransformCache)
+    std::vector<at::Tensor> wts;
+    TORCH_CHECK(weights_t.empty() || weights_t.size() == p.geo.size(),
+                "weights_t must be empty or hold one transposed weight per weight");
+    for (size_t i = 0; i < p.geo.size(); ++i) {
+      if (weights_t.empty()) {
+        wts.push_back(weights[i].transpose(0, 1).contiguous());
+      } else {
+        check_f32(weights_t[i], "weights_t", x);
+        TORCH_CHECK(weights_t[i].dim() == 4 && weights_t[i].size(0) == weights[i].size(1) &&
+                        weights_t[i].size(1) == weights[i].size(0) &&
+                        weights_t[i].numel() == weights[i].numel(),
+                    "weights_t[i] must be weights[i] transposed to [ci][co][kh][kw]");
+        wts.push_back(weights_t[i]);
+      }
+      p.geo[i].a_t = true;
+    }
     for (size_t i = 0; i < p.geo.size(); ++i)
-      plans.push_back(tuned_plan(1, weights[i].data_ptr<float>(), dz.data_ptr<float>(),
+      plans.push_back(tuned_plan(1, wts[i].data_ptr<float>(), dz.data_ptr<float>(),
                                  x.data_ptr<float>(), dx.data_ptr<float>(), nullptr, nullptr,
-                                 p.geo[i], i > 0 || zero, weights[i].numel() * 4,
+                                 p.geo[i], i > 0 || zero, wts[i].numel() * 4,
                                  dz.numel() * 4, x, x.numel()));
     for (size_t i = 0; i < p.geo.size(); ++i) {
-      const auto& wt = weights[i];
+      const auto& wt = wts[i];
       run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
                dx.data_ptr<float>(), nullptr, nullptr, p.geo[i], plans[i], i > 0 || zero,
                wt.numel() * 4, dz.numel() * 4, x);
@@ -436,7 +456,8 @@ std::vector<double> conv_gemm_sweep(int64_t mode, const at::Tensor& x_in,
   TORCH_CHECK(mode >= 0 && mode <= 2 && reps > 0, "mode 0-2, reps > 0");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Parts p = make_parts(x, {weight}, geo, false);
-  const ConvGemmGeo& g = p.geo[0];
+  ConvGemmGeo& g = p.geo[0];
+  const at::Tensor wt_t = weight.transpose(0, 1).contiguous();
   auto z = at::randn({x.size(0), p.co_total, p.ho, p.wo}, x.options());
   auto dx = at::empty_like(x);
   auto dw = at::empty_like(weight);
@@ -447,8 +468,9 @@ std::vector<double> conv_gemm_sweep(int64_t mode, const at::Tensor& x_in,
     a = weight.data_ptr<float>(); b = x.data_ptr<float>(); out = z.data_ptr<float>();
     a_bytes = weight.numel() * 4; b_bytes = x.numel() * 4;
   } else if (mode == 1) {
-    a = weight.data_ptr<float>(); b = z.data_ptr<float>(); out = dx.data_ptr<float>();
+    a = wt_t.data_ptr<float>(); b = z.data_ptr<float>(); out = dx.data_ptr<float>();
     a_bytes = weight.numel() * 4; b_bytes = z.numel() * 4;
+    g.a_t = true;
   } else {
     a = z.data_ptr<float>(); b = x.data_ptr<float>(); out = dw.data_ptr<float>();
     a_bytes = z.numel() * 4; b_bytes = x.numel() * 4;
@@ -497,7 +519,8 @@ at::Tensor conv_gemm_forward(const at::Tensor& x_in, const at::Tensor& weight,
 }
 
 at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_in,
-                                   const at::Tensor& weight, at::IntArrayRef geo, bool relu) {
+                                   const at::Tensor& weight, at::IntArrayRef geo, bool relu,
+                                   const c10::optional<at::Tensor>& weight_t) {
   auto x = x_in.contiguous();
   auto dz = dz_in.contiguous();
   check_f32(x, "x", x);
@@ -508,13 +531,24 @@ at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_
               "dz does not match the convolution's output");
   const bool scatter = conv_gemm_plan(1, p.geo[0]).scatter;
   auto dx = scatter ? at::zeros_like(x) : at::empty_like(x);
+  at::Tensor wt;  // A = W^T (see convbn_backward)
+  if (weight_t.has_value() && weight_t->defined()) {
+    check_f32(*weight_t, "weight_t", x);
+    TORCH_CHECK(weight_t->dim() == 4 && weight_t->size(0) == weight.size(1) &&
+                    weight_t->size(1) == weight.size(0) && weight_t->numel() == weight.numel(),
+                "weight_t must be the weight transposed to [ci][co][kh][kw]");
+    wt = *weight_t;
+  } else {
+    wt = weight.transpose(0, 1).contiguous();
+  }
+  p.geo[0].a_t = true;
   const ConvGemmPlan plan =
-      tuned_plan(1, weight.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-                 dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], scatter, weight.numel() * 4,
+      tuned_plan(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+                 dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], scatter, wt.numel() * 4,
                  dz.numel() * 4, x, x.numel());
-  run_gemm(1, weight.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+  run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
            dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], plan, plan.scatter,
-           weight.numel() * 4, dz.numel() * 4, x);
+           wt.numel() * 4, dz.numel() * 4, x);
   return dx;
 }
 
@@ -676,14 +710,14 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
         "Tensor(c!)? num_batches_tracked, float momentum, float eps, Tensor? add) -> Tensor[]");
   m.def("convbn_backward(Tensor dy, Tensor x, Tensor z, Tensor mean, Tensor invstd, "
         "Tensor(a!) sums, Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx, "
-        "Tensor?[] accum) -> Tensor[]");
+        "Tensor?[] accum, Tensor[] weights_t) -> Tensor[]");
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
   m.def("conv_gemm_plans_export() -> str", &tgpipe::conv_gemm_plans_export);
   m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
   m.def("conv_gemm_sweep(int mode, Tensor x, Tensor weight, int[] geo, int reps) -> float[]");
   m.def("conv_gemm_plans_import(str text) -> int", &tgpipe::conv_gemm_plans_import);
-  m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu) "
-        "-> Tensor");
+  m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "
+        "Tensor? weight_t=None) -> Tensor");
   m.def("conv_gemm_backward_weight(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "
         "Tensor? accum=None) -> Tensor");
 }

@@ -126,6 +126,7 @@ struct ConvGemmGeo {
   int kh, kw, sh, sw, ph, pw;
   int oh, ow;            // extra input offset (FactorizedReduce's shifted branch)
   bool relu;             // ReLU on the input (its mask in backward-data)
+  bool a_t = false;      // backward-data: `a` is W transposed, [ci][co*kh*kw] row-major
 };
 // mode 0: forward  Z[:, co_off:co_off+co] = conv(relu(X)); a = W[co][ci*kh*kw], b = X;
 //         part_mean / part_m2 ([col_blocks][co_total]): per column block mean and centred

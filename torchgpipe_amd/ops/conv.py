@@ -72,8 +72,7 @@ class _TransformCache:
     __slots__ = ('_entries', '__weakref__')
 
     def __init__(self) -> None:
-        self._entries: Dict[Tuple[bool, bool], Tuple[Tuple[int, int, torch.device, int],
-                                                     Tensor]] = {}
+        self._entries: Dict[Tuple, Tuple[Tuple[int, int, torch.device, int], Tensor]] = {}
 
     def get(self, weight: Tensor, flip: bool, f4: bool = False) -> Tensor:
         global _CACHE_BYTES
@@ -94,6 +93,26 @@ class _TransformCache:
             _CACHE_BYTES += size
         return u
 
+    def get_transposed(self, weight: Tensor) -> Tensor:
+        """``weight`` as ``[ci][co][kh][kw]`` (contiguous): the backward-data GEMM operand
+        of the implicit-GEMM convolutions, transposed once per step instead of per call."""
+        global _CACHE_BYTES
+        key = (weight.data_ptr(), weight._version, weight.device, _STEP)
+        slot = (True, True, 'T')
+        hit = self._entries.get(slot)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        if hit is not None:
+            _CACHE_BYTES -= hit[1].numel() * hit[1].element_size()
+            del self._entries[slot]
+        with torch.no_grad():
+            t = weight.detach().transpose(0, 1).contiguous()
+        size = t.numel() * t.element_size()
+        if _CACHE_BYTES + size <= _budget(weight.device):
+            self._entries[slot] = (key, t)
+            _CACHE_BYTES += size
+        return t
+
     def clear(self) -> None:
         global _CACHE_BYTES
         for _, u in self._entries.values():
@@ -108,11 +127,13 @@ class _TransformCache:
 
 
 def clear_winograd_caches(module: torch.nn.Module) -> None:
-    """Drop the cached weight transforms of every WinogradConv2d in ``module``."""
+    """Drop the cached weight transforms of every WinogradConv2d (and the transposed
+    weights of the implicit-GEMM convolutions) in ``module``."""
     for m in module.modules():
-        cache = getattr(m, '_wino', None)
-        if isinstance(cache, _TransformCache):
-            cache.clear()
+        for attr in ('_wino', '_wt_cache'):
+            cache = getattr(m, attr, None)
+            if isinstance(cache, _TransformCache):
+                cache.clear()
 
 
 # Winograd F(4x4,3x3) (csrc/winograd_f4.hip) on planes of at least this size; F(2x2) on

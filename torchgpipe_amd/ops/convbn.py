@@ -29,6 +29,7 @@ from torch import Tensor, nn
 import torch.nn.functional as F
 
 from torchgpipe_amd.ops import _ext, gradacc
+from torchgpipe_amd.ops.conv import _TransformCache
 
 __all__ = ['relu_conv_bn', 'ReLUConvBN', 'FusedChain', 'conv_supported', 'fused_triplets',
            'fusable', 'disabled', 'GemmConv2d', 'gemm_conv2d', 'gemm_conv_eligible']
@@ -76,7 +77,7 @@ class _ConvBN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: Tensor, add: Optional[Tensor], gamma: Optional[Tensor],  # type: ignore[override]
                 beta: Optional[Tensor], bn: nn.BatchNorm2d, geo: List[int], relu: bool,
-                *weights: Tensor) -> Tensor:
+                caches: List[_TransformCache], *weights: Tensor) -> Tensor:
         ops = _ext.require(x)
         track = bn.track_running_stats and bn.running_mean is not None
         y, z, mean, invstd, sums = ops.convbn_forward(
@@ -86,6 +87,7 @@ class _ConvBN(torch.autograd.Function):
             float(bn.momentum) if bn.momentum is not None else 0.0, float(bn.eps), add)
         ctx.save_for_backward(x, z, mean, invstd, sums, gamma, *weights)
         ctx.params = (gamma, beta) + weights  # gradient-accumulation fusion (ops/gradacc.py)
+        ctx.caches = caches
         ctx.geo = geo
         ctx.relu = relu
         ctx.has_add = add is not None
@@ -97,20 +99,22 @@ class _ConvBN(torch.autograd.Function):
         x, z, mean, invstd, sums, gamma, *weights = ctx.saved_tensors
         need_dx = ctx.needs_input_grad[0]
         fused = [gradacc.target(p) for p in ctx.params]
+        # the backward-data GEMM reads W^T: transposed once per step, not per micro-batch
+        wts = [c.get_transposed(w) for c, w in zip(ctx.caches, weights)] if need_dx else []
         dx, dgamma, dbeta, *dws = _ext.require(dy).convbn_backward(
             dy, x, z, mean, invstd, sums, gamma, weights, ctx.geo, ctx.relu, need_dx,
-            [into for _, into in fused])
+            [into for _, into in fused], wts)
         grads = [dgamma, dbeta] + dws
         for k, ((fuse, into), p) in enumerate(zip(fused, ctx.params)):
             if fuse:  # written into p.grad by the kernels
                 if into is None:
                     gradacc.commit(p, grads[k])
                 grads[k] = None
-        del ctx.params
+        del ctx.params, ctx.caches
         dgamma, dbeta, *dws = grads
         return (dx if need_dx else None, dy if ctx.has_add else None,
                 dgamma if ctx.needs_input_grad[2] else None,
-                dbeta if ctx.needs_input_grad[3] else None, None, None, None, *dws)
+                dbeta if ctx.needs_input_grad[3] else None, None, None, None, None, *dws)
 
 
 def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.BatchNorm2d,
@@ -125,7 +129,17 @@ def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.Batch
     for conv, offset in convs:
         geo += _geo(conv, offset)
     weights = [conv.weight for conv, _ in convs]
-    return _ConvBN.apply(x, add, bn.weight, bn.bias, bn, geo, relu, *weights)
+    return _ConvBN.apply(x, add, bn.weight, bn.bias, bn, geo, relu,
+                         [_weight_cache(conv) for conv, _ in convs], *weights)
+
+
+def _weight_cache(conv: nn.Module) -> _TransformCache:
+    """The module's step-scoped cache of derived weights (here: the transposed weight)."""
+    cache = conv.__dict__.get('_wt_cache')
+    if cache is None:
+        cache = _TransformCache()
+        conv.__dict__['_wt_cache'] = cache
+    return cache
 
 
 def fusable(x: Tensor, convs: Sequence[nn.Conv2d], bn: nn.Module) -> bool:
@@ -203,9 +217,11 @@ def gemm_conv_eligible(x: Tensor, conv: nn.Conv2d) -> bool:
 
 class _GemmConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x: Tensor, weight: Tensor, geo: List[int]) -> Tensor:  # type: ignore[override]
+    def forward(ctx, x: Tensor, weight: Tensor, geo: List[int],  # type: ignore[override]
+                cache: _TransformCache) -> Tensor:
         ctx.save_for_backward(x, weight)
         ctx.param = weight
+        ctx.cache = cache
         ctx.geo = geo
         return _ext.require(x).conv_gemm_forward(x, weight, geo, False)
 
@@ -215,7 +231,8 @@ class _GemmConv(torch.autograd.Function):
         ops = _ext.require(dz)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = ops.conv_gemm_backward_data(dz, x, weight, ctx.geo, False)
+            dx = ops.conv_gemm_backward_data(dz, x, weight, ctx.geo, False,
+                                             ctx.cache.get_transposed(weight))
         if ctx.needs_input_grad[1]:
             fuse, into = gradacc.target(ctx.param)
             dw = ops.conv_gemm_backward_weight(dz, x, weight, ctx.geo, False, into)
@@ -223,13 +240,13 @@ class _GemmConv(torch.autograd.Function):
                 if into is None:
                     gradacc.commit(ctx.param, dw)
                 dw = None
-        del ctx.param
-        return dx, dw, None
+        del ctx.param, ctx.cache
+        return dx, dw, None, None
 
 
 def gemm_conv2d(x: Tensor, conv: nn.Conv2d) -> Tensor:
     """``conv(x)`` on the implicit-GEMM MFMA kernels (caller checks eligibility)."""
-    return _GemmConv.apply(x, conv.weight, _geo(conv))
+    return _GemmConv.apply(x, conv.weight, _geo(conv), _weight_cache(conv))
 
 
 class GemmConv2d(nn.Conv2d):
