@@ -289,3 +289,26 @@ def test_fused_gradient_accumulation_matches_autograd(monkeypatch):
     plain(xs[0]).square().sum().backward()
     for g, p in zip(got, plain.parameters()):
         torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-5)
+
+
+def test_backward_reads_channel_sliced_gradients_in_place():
+    """A cell output is a concatenation: its gradient reaches the fused ops as channel
+    slices, which the BN backward and the pool backward read without a copy."""
+    from torchgpipe_amd.ops.convbn import ReLUConvBN
+    from torchgpipe_amd.ops.pool import AvgPool3x3
+    _ext.require()
+    torch.manual_seed(0)
+    x = torch.randn(4, 16, 14, 14, device='cuda', requires_grad=True)
+    op = ReLUConvBN(nn.ReLU(), nn.Conv2d(16, 24, 1, bias=False), nn.BatchNorm2d(24)).cuda()
+    pool = AvgPool3x3(1)
+    outs = [op(x), pool(x)]
+    big = torch.randn(4, 24 + 16 + 8, 14, 14, device='cuda')
+    grads = [big[:, 8:32], big[:, 32:48]]
+    assert not grads[0].is_contiguous()
+    torch.autograd.backward(outs, grads)
+    got = x.grad.clone()
+    x.grad = None
+    op2 = copy.deepcopy(op)
+    outs = [op2(x), pool(x)]
+    torch.autograd.backward(outs, [g.contiguous() for g in grads])
+    torch.testing.assert_close(got, x.grad, rtol=1e-6, atol=1e-6)

@@ -241,3 +241,23 @@ def test_copy_stream_ring_size_is_transparent(devices, pool):
     want, want_loss = parity.reference('unet', torch.device('cuda', 0), chunks)
     got = [p.grad.detach().cpu() for p in gpipe.parameters()]
     parity.assert_parity([{'grads': got, 'loss': loss.item()}], want, want_loss, rel=1e-4)
+
+
+def test_process_exits_cleanly_after_gpipe_training():
+    """Persistent device worker threads must not abort the interpreter at exit."""
+    import subprocess
+    import sys
+    code = ('import torch, torch.nn.functional as F\n'
+            'from torchgpipe_amd import GPipe\n'
+            'from tests.distributed import parity\n'
+            'g = GPipe(parity.build("amoebanet"), parity.balance("amoebanet", 2), '
+            'devices=[0, 0], chunks=3, checkpoint="except_last")\n'
+            'x, t = parity.data("amoebanet", torch.device("cuda", 0))\n'
+            'F.cross_entropy(g(x), t).backward()\n'
+            'torch.cuda.synchronize()\n'
+            'print("done")\n')
+    root = __import__('os').path.dirname(__import__('os').path.dirname(__file__))
+    out = subprocess.run([sys.executable, '-c', code], cwd=root, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert out.stdout.strip().endswith('done')

@@ -205,18 +205,21 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
 }
 
 // One workgroup per (channel, image range): sums of dy and dy * (z - mean).
+// dy may be a channel slice of a wider tensor (the gradient of a concatenated cell
+// output): image `img` of dy starts at dy + img * dy_img (z and dz are dense).
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const float* __restrict__ dy, const float* __restrict__ z, const float* __restrict__ mean,
-    float* __restrict__ sums, int64_t n, int64_t c, int64_t s, int64_t n_per) {
+    float* __restrict__ sums, int64_t n, int64_t c, int64_t s, int64_t n_per, int64_t dy_img) {
   const int64_t ch = blockIdx.x;
   const int64_t n0 = blockIdx.y * n_per, n1 = min(n, n0 + n_per);
   const float mu = mean[ch];
   float sd = 0.f, sdz = 0.f;
   for (int64_t img = n0; img < n1; ++img) {
     const int64_t base = (img * c + ch) * s;
+    const float* dyp = dy + img * dy_img + ch * s;
     if ((s & 3) == 0) {
       for (int64_t q = threadIdx.x; q < s / 4; q += 256) {
-        const floatx4 g = reinterpret_cast<const floatx4*>(dy + base)[q];
+        const floatx4 g = reinterpret_cast<const floatx4*>(dyp)[q];
         const floatx4 v = reinterpret_cast<const floatx4*>(z + base)[q];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
       }
     } else {
       for (int64_t i = threadIdx.x; i < s; i += 256) {
-        const float g = dy[base + i];
+        const float g = dyp[i];
         sd += g;
         sdz += g * (z[base + i] - mu);
       }
@@ -256,7 +259,8 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ sums, float* __restrict__ dz, float* __restrict__ dgamma,
     float* __restrict__ dbeta, int acc_gamma, int acc_beta, int64_t total, int64_t c, int64_t s,
-    float inv_m) {
+    float inv_m, int64_t dy_img) {
+  const int64_t cs = c * s;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
   const int64_t first = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (first < c) {  // parameter gradients, accumulated into .grad across micro-batches
@@ -272,7 +276,8 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
       const float k2 = sums[ch] * inv_m;
       const float k3 = is * is * sums[c + ch] * inv_m;
       const float mu = mean[ch];
-      const floatx4 g = reinterpret_cast<const floatx4*>(dy)[q];
+      const int64_t img = 4 * q / cs;
+      const floatx4 g = *reinterpret_cast<const floatx4*>(dy + img * dy_img + (4 * q - img * cs));
       const floatx4 v = reinterpret_cast<const floatx4*>(z)[q];
       floatx4 o;
 #pragma unroll
@@ -284,7 +289,9 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
       const int64_t ch = (i / s) % c;
       const float is = invstd[ch];
       const float k1 = (gamma ? gamma[ch] : 1.f) * is;
-      dz[i] = k1 * (dy[i] - sums[ch] * inv_m - (z[i] - mean[ch]) * is * is * sums[c + ch] * inv_m);
+      const int64_t img = i / cs;
+      const float g = dy[img * dy_img + (i - img * cs)];
+      dz[i] = k1 * (g - sums[ch] * inv_m - (z[i] - mean[ch]) * is * is * sums[c + ch] * inv_m);
     }
   }
 }
@@ -446,7 +453,8 @@ void launch_bn_apply(const float* z, const float* mean, const float* invstd, con
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
                         bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
-                        hipStream_t stream) {
+                        int64_t dy_img, hipStream_t stream) {
+  if (dy_img <= 0) dy_img = c * s;
   const int64_t total = n * c * s;
   if (total == 0) return;
   // enough (channel, image range) workgroups to cover the chip ~4x
@@ -457,7 +465,7 @@ void launch_bn_backward(const float* dy, const float* z, const float* mean, cons
   splits = (n + n_per - 1) / n_per;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(static_cast<unsigned>(c),
                                                 static_cast<unsigned>(splits)),
-                     dim3(256), 0, stream, dy, z, mean, sums, n, c, s, n_per);
+                     dim3(256), 0, stream, dy, z, mean, sums, n, c, s, n_per, dy_img);
   const bool vec = (s & 3) == 0;
   int64_t work = vec ? total / 4 : total;
   if (work < c) work = c;
@@ -466,11 +474,11 @@ void launch_bn_backward(const float* dy, const float* z, const float* mean, cons
   if (vec)
     hipLaunchKernelGGL((bn_bwd_dz_kernel<true>), dim3(grid), dim3(256), 0, stream, dy, z, mean,
                        invstd, gamma, sums, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
-                       acc_beta ? 1 : 0, total, c, s, inv_m);
+                       acc_beta ? 1 : 0, total, c, s, inv_m, dy_img);
   else
     hipLaunchKernelGGL((bn_bwd_dz_kernel<false>), dim3(grid), dim3(256), 0, stream, dy, z, mean,
                        invstd, gamma, sums, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
-                       acc_beta ? 1 : 0, total, c, s, inv_m);
+                       acc_beta ? 1 : 0, total, c, s, inv_m, dy_img);
 }
 
 }  // namespace tgpipe

@@ -197,6 +197,18 @@ void run_gemm(int mode, const float* a, const float* b, const float* mask, float
   launch_one(mode, a, b, mask, out, pm, pm2, g, plan, accumulate, a_bytes, b_bytes, like);
 }
 
+// A channel slice of a dense NCHW tensor (e.g. the gradient of one input of a
+// concatenation): dense within each image, any image stride.  Returns that stride, or 0.
+int64_t image_stride_if_channel_slice(const at::Tensor& t) {
+  if (t.dim() != 4 || t.scalar_type() != at::kFloat || !t.is_cuda()) return 0;
+  const int64_t c = t.size(1), h = t.size(2), w = t.size(3);
+  if (t.stride(3) != 1 || t.stride(2) != w || t.stride(1) != h * w) return 0;
+  if (t.size(0) > 1 && t.stride(0) < c * h * w) return 0;
+  if ((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) != 0) return 0;  // float4 loads
+  if ((t.stride(0) & 3) != 0) return 0;
+  return t.size(0) > 1 ? t.stride(0) : c * h * w;
+}
+
 void check_f32(const at::Tensor& t, const char* name, const at::Tensor& like) {
   TORCH_CHECK(t.is_cuda() && t.device() == like.device(), name, " must be on ", like.device());
   TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
@@ -357,9 +369,15 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                                         const c10::List<c10::optional<at::Tensor>>& accum,
                                         at::TensorList weights_t) {
   auto x = x_in.contiguous();
-  auto dy = dy_in.contiguous();
+  // dy is read in place when it is a channel slice (a concatenated cell output's gradient)
+  int64_t dy_img = image_stride_if_channel_slice(dy_in);
+  auto dy = dy_img > 0 ? dy_in : dy_in.contiguous();
+  if (dy_img == 0) {
+    check_f32(dy, "dy", x);
+  } else {
+    TORCH_CHECK(dy.device() == x.device(), "dy must be on ", x.device());
+  }
   check_f32(x, "x", x);
-  check_f32(dy, "dy", x);
   check_f32(z, "z", x);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Parts p = make_parts(x, weights, geo, relu);
@@ -391,7 +409,7 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   launch_bn_backward(dy.data_ptr<float>(), z.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), ga, sums.data_ptr<float>(), dz.data_ptr<float>(),
                      dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), into[0].defined(),
-                     into[1].defined(), n, c, s, stream);
+                     into[1].defined(), n, c, s, dy_img, stream);
   std::vector<at::Tensor> out;
   at::Tensor dx;
   if (need_dx) {
@@ -636,7 +654,7 @@ std::vector<at::Tensor> bn_train_backward(const at::Tensor& dy_in, const at::Ten
   launch_bn_backward(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), opt_ptr(gamma, "gamma", x, c),
                      sums.data_ptr<float>(), dx.data_ptr<float>(), dgamma.data_ptr<float>(),
-                     dbeta.data_ptr<float>(), false, false, n, c, s, cur_stream(x));
+                     dbeta.data_ptr<float>(), false, false, n, c, s, 0, cur_stream(x));
   return {dx, dgamma, dbeta};
 }
 
@@ -679,17 +697,20 @@ at::Tensor avgpool3_forward(const at::Tensor& x_in, int64_t stride,
 }
 
 at::Tensor avgpool3_backward(const at::Tensor& dy_in, int64_t h, int64_t w, int64_t stride) {
-  auto dy = dy_in.contiguous();
-  check_f32(dy, "dy", dy);
-  TORCH_CHECK(dy.dim() == 4 && dy.size(2) == (h - 1) / stride + 1 &&
-                  dy.size(3) == (w - 1) / stride + 1,
+  TORCH_CHECK(dy_in.dim() == 4 && dy_in.size(2) == (h - 1) / stride + 1 &&
+                  dy_in.size(3) == (w - 1) / stride + 1,
               "dy does not match the pooled shape");
+  // a channel slice (gradient of one input of a concatenation) is read in place
+  int64_t dy_img = avgpool3_backward_strided_ok(static_cast<int>(h), static_cast<int>(w))
+                       ? image_stride_if_channel_slice(dy_in) : 0;
+  auto dy = dy_img > 0 ? dy_in : dy_in.contiguous();
+  if (dy_img == 0) check_f32(dy, "dy", dy);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   auto dx = at::empty({dy.size(0), dy.size(1), h, w}, dy.options());
   if (dx.numel() > 0)
-    launch_avgpool3_backward(dy.data_ptr<float>(), dx.data_ptr<float>(), dy.size(0) * dy.size(1),
+    launch_avgpool3_backward(dy.data_ptr<float>(), dx.data_ptr<float>(), dy.size(0), dy.size(1),
                              static_cast<int>(h), static_cast<int>(w), static_cast<int>(stride),
-                             cur_stream(dy));
+                             dy_img, cur_stream(dy));
   return dx;
 }
 

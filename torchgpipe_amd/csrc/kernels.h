@@ -191,13 +191,16 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
                         bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
-                        hipStream_t stream);
+                        int64_t dy_img, hipStream_t stream);  // dy_img: dy's image stride
 
 // 3x3 average pool, padding 1, count_include_pad = False, stride 1 / 2 (pool.hip):
 // y = pool(x) (+ add) over `planes` = N*C planes of h x w; backward gathers dx.
 void launch_avgpool3_forward(const float* x, const float* add, float* y, int64_t planes, int h,
                              int w, int stride, hipStream_t stream);
-void launch_avgpool3_backward(const float* dy, float* dx, int64_t planes, int h, int w,
-                              int stride, hipStream_t stream);
+// dy may be a channel slice: plane (img, ch) at dy + img * dy_img + ch * ho * wo (only
+// when avgpool3_backward_strided_ok(h, w); otherwise dy must be dense)
+bool avgpool3_backward_strided_ok(int h, int w);
+void launch_avgpool3_backward(const float* dy, float* dx, int64_t images, int64_t channels,
+                              int h, int w, int stride, int64_t dy_img, hipStream_t stream);
 
 }  // namespace tgpipe

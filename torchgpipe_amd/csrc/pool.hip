@@ -115,11 +115,14 @@ __global__ __launch_bounds__(256) void avgpool3_fwd_plane_kernel(const float* __
 __global__ __launch_bounds__(256) void avgpool3_bwd_plane_kernel(const float* __restrict__ dy,
                                                                  float* __restrict__ dx, int h,
                                                                  int w, int ho, int wo,
-                                                                 int stride) {
+                                                                 int stride, int channels,
+                                                                 int64_t dy_img) {
   extern __shared__ float pl[];  // dy / window area, per output
   const int64_t plane = blockIdx.x;
   const int in = h * w, out = ho * wo, nt = blockDim.x;
-  const float* g = dy + plane * out;
+  // dy may be a channel slice of a wider gradient (image stride dy_img)
+  const int64_t img = plane / channels;
+  const float* g = dy + img * dy_img + (plane - img * channels) * out;
   for (int o = threadIdx.x; o < out; o += nt) {
     const int oy = o / wo, ox = o - oy * wo;
     const int cy = oy * stride, cx = ox * stride;
@@ -166,15 +169,23 @@ void launch_avgpool3_forward(const float* x, const float* add, float* y, int64_t
                      y, static_cast<int>(total), h, w, ho, wo, stride);
 }
 
-void launch_avgpool3_backward(const float* dy, float* dx, int64_t planes, int h, int w,
-                              int stride, hipStream_t stream) {
+bool avgpool3_backward_strided_ok(int h, int w) {
+  return static_cast<int64_t>(h) * w <= kPlaneMax;
+}
+
+void launch_avgpool3_backward(const float* dy, float* dx, int64_t images, int64_t channels,
+                              int h, int w, int stride, int64_t dy_img, hipStream_t stream) {
   const int ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
-  if (static_cast<int64_t>(h) * w <= kPlaneMax && planes < (int64_t{1} << 31)) {
+  const int64_t planes = images * channels;
+  if (dy_img <= 0) dy_img = channels * ho * wo;
+  if (avgpool3_backward_strided_ok(h, w) && planes < (int64_t{1} << 31)) {
     hipLaunchKernelGGL(avgpool3_bwd_plane_kernel, dim3(static_cast<unsigned>(planes)),
                        dim3(plane_threads(static_cast<int64_t>(h) * w)),
-                       static_cast<unsigned>(ho * wo * 4), stream, dy, dx, h, w, ho, wo, stride);
+                       static_cast<unsigned>(ho * wo * 4), stream, dy, dx, h, w, ho, wo, stride,
+                       static_cast<int>(channels), dy_img);
     return;
   }
+  // (dense dy only: the caller makes it contiguous when this path runs)
   const int64_t total = planes * h * w;
   hipLaunchKernelGGL(avgpool3_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, dy, dx,
                      static_cast<int>(total), h, w, ho, wo, stride);
