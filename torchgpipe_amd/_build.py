@@ -27,7 +27,7 @@ ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
 ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 
 KERNEL_SOURCES = ['kernels.hip', 'winograd.hip', 'winograd_f4.hip', 'conv_gemm.hip',
-                  'batchnorm.hip', 'pool.hip']
+                  'batchnorm.hip', 'pool.hip', 'unet_ops.hip']
 HOST_SOURCES = ['bindings.cpp', 'convbn.cpp']
 HEADERS = ['kernels.h', 'philox.h']
 

@@ -714,10 +714,82 @@ at::Tensor avgpool3_backward(const at::Tensor& dy_in, int64_t h, int64_t w, int6
   return dx;
 }
 
+// U-Net decoder: cat(upsample2x(x), skip) and its backward for x (unet_ops.hip).
+at::Tensor up2x_cat_forward(const at::Tensor& x_in, const at::Tensor& skip_in) {
+  auto x = x_in.contiguous();
+  auto skip = skip_in.contiguous();
+  check_f32(x, "x", x);
+  check_f32(skip, "skip", x);
+  TORCH_CHECK(x.dim() == 4 && skip.dim() == 4 && skip.size(0) == x.size(0) &&
+                  skip.size(2) == 2 * x.size(2) && skip.size(3) == 2 * x.size(3),
+              "skip must be [N][C2][2H][2W] for x [N][C1][H][W]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto out = at::empty({x.size(0), x.size(1) + skip.size(1), skip.size(2), skip.size(3)},
+                       x.options());
+  check_f32(out, "output", x);
+  launch_up2x_cat(x.data_ptr<float>(), skip.data_ptr<float>(), out.data_ptr<float>(), x.size(0),
+                  static_cast<int>(x.size(1)), static_cast<int>(skip.size(1)),
+                  static_cast<int>(x.size(2)), static_cast<int>(x.size(3)), cur_stream(x));
+  return out;
+}
+
+// dx = 2x2 block sums of dy[:, :c] (dy: the concatenation's gradient or its channel slice).
+at::Tensor up2x_backward(const at::Tensor& dy_in, int64_t c) {
+  TORCH_CHECK(dy_in.dim() == 4 && dy_in.size(1) >= c && dy_in.size(2) % 2 == 0 &&
+                  dy_in.size(3) % 2 == 0, "dy must be [N][>=C][2H][2W]");
+  auto dy = dy_in.narrow(1, 0, c);
+  int64_t dy_img = image_stride_if_channel_slice(dy);
+  if (dy_img == 0) {
+    dy = dy.contiguous();
+    dy_img = c * dy.size(2) * dy.size(3);
+  }
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kFloat, "dy must be float32 on the GPU");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  const int64_t h = dy.size(2) / 2, w = dy.size(3) / 2;
+  auto dx = at::empty({dy.size(0), c, h, w}, dy.options());
+  launch_up2x_backward(dy.data_ptr<float>(), dx.data_ptr<float>(), dy.size(0),
+                       static_cast<int>(c), static_cast<int>(h), static_cast<int>(w), dy_img,
+                       cur_stream(dy));
+  return dx;
+}
+
+at::Tensor maxpool2x2_forward(const at::Tensor& x_in) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({x.size(0), x.size(1), x.size(2) / 2, x.size(3) / 2}, x.options());
+  launch_maxpool2x2_forward(x.data_ptr<float>(), y.data_ptr<float>(), x.size(0) * x.size(1),
+                            static_cast<int>(x.size(2)), static_cast<int>(x.size(3)),
+                            cur_stream(x));
+  return y;
+}
+
+at::Tensor maxpool2x2_backward(const at::Tensor& x_in, const at::Tensor& dy_in) {
+  auto x = x_in.contiguous();
+  auto dy = dy_in.contiguous();
+  check_f32(x, "x", x);
+  check_f32(dy, "dy", x);
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(2) == x.size(2) / 2 &&
+                  dy.size(3) == x.size(3) / 2 && dy.size(1) == x.size(1),
+              "dy must be the pooled shape of x");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const bool odd = (x.size(2) & 1) || (x.size(3) & 1);
+  auto dx = odd ? at::zeros_like(x) : at::empty_like(x);
+  launch_maxpool2x2_backward(x.data_ptr<float>(), dy.data_ptr<float>(), dx.data_ptr<float>(),
+                             x.size(0) * x.size(1), static_cast<int>(x.size(2)),
+                             static_cast<int>(x.size(3)), cur_stream(x));
+  return dx;
+}
+
 }  // namespace
 }  // namespace tgpipe
 
 TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
+  m.def("up2x_cat_forward(Tensor x, Tensor skip) -> Tensor");
+  m.def("up2x_backward(Tensor dy, int c) -> Tensor");
+  m.def("maxpool2x2_forward(Tensor x) -> Tensor");
+  m.def("maxpool2x2_backward(Tensor x, Tensor dy) -> Tensor");
   m.def("avgpool3_forward(Tensor x, int stride, Tensor? add) -> Tensor");
   m.def("avgpool3_backward(Tensor dy, int h, int w, int stride) -> Tensor");
   m.def("bn_train_forward(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? acc, float eps) "
@@ -755,4 +827,8 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("dbn_commit64", &tgpipe::dbn_commit64);
   m.impl("avgpool3_forward", &tgpipe::avgpool3_forward);
   m.impl("avgpool3_backward", &tgpipe::avgpool3_backward);
+  m.impl("up2x_cat_forward", &tgpipe::up2x_cat_forward);
+  m.impl("up2x_backward", &tgpipe::up2x_backward);
+  m.impl("maxpool2x2_forward", &tgpipe::maxpool2x2_forward);
+  m.impl("maxpool2x2_backward", &tgpipe::maxpool2x2_backward);
 }

@@ -203,4 +203,18 @@ bool avgpool3_backward_strided_ok(int h, int w);
 void launch_avgpool3_backward(const float* dy, float* dx, int64_t images, int64_t channels,
                               int h, int w, int stride, int64_t dy_img, hipStream_t stream);
 
+// U-Net resolution changes (unet_ops.hip).  up2x_cat: out[n][c1+c2][2h][2w] =
+// cat(nearest 2x upsample of x[n][c1][h][w], skip[n][c2][2h][2w]); up2x_backward: dx = 2x2
+// block sums of dy's first c channels (image stride dy_img, elements); maxpool 2x2 / stride 2
+// without indices (the backward re-finds the argmax from x; dx is pre-zeroed by the caller
+// when h or w is odd).
+void launch_up2x_cat(const float* x, const float* skip, float* out, int64_t n, int c1, int c2,
+                     int h, int w, hipStream_t stream);
+void launch_up2x_backward(const float* dy, float* dx, int64_t n, int c, int h, int w,
+                          int64_t dy_img, hipStream_t stream);
+void launch_maxpool2x2_forward(const float* x, float* y, int64_t planes, int h, int w,
+                               hipStream_t stream);
+void launch_maxpool2x2_backward(const float* x, const float* dy, float* dx, int64_t planes,
+                                int h, int w, hipStream_t stream);
+
 }  // namespace tgpipe

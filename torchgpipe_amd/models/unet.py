@@ -32,9 +32,10 @@ from torchgpipe_amd.ops.conv import WinogradConv2d
 from torchgpipe_amd.ops.convbn import GemmConv2d
 from torchgpipe_amd.ops.dropout import Dropout2d
 from torchgpipe_amd.ops.fused import DropNormAct
+from torchgpipe_amd.ops.unet_ops import MaxPool2x2, up2x_cat
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
-__all__ = ['unet', 'Stash', 'PopCat']
+__all__ = ['unet', 'Stash', 'PopCat', 'PopUpCat']
 
 
 @skippable(stash=['skip'])
@@ -54,6 +55,16 @@ class PopCat(nn.Module):
                 pad += [0, want - have]
             input = F.pad(input, pad)
         return torch.cat((input, skipped), dim=1)
+
+
+@skippable(pop=['skip'])
+class PopUpCat(nn.Module):
+    """The decoder's ``up`` and ``skip`` layers in one pass (the preceding ``up`` layer is an
+    identity): ``cat(upsample_2x(input), skipped)`` on one HIP kernel (ops/unet_ops.py)."""
+
+    def forward(self, input: Tensor) -> Generator:  # type: ignore[override]
+        skipped = yield pop('skip')
+        return up2x_cat(input, skipped)
 
 
 def conv_block(in_channels: int, out_channels: int, fused: bool) -> nn.Sequential:
@@ -104,15 +115,15 @@ def unet(depth: int = 5, num_convs: int = 5, base_channels: int = 64, input_chan
         nn.Sequential(OrderedDict([
             ('encode', cell(enc(i))),
             ('skip', Stash().isolate(namespaces[i])),
-            ('down', nn.MaxPool2d(2, stride=2)),
+            ('down', MaxPool2x2() if fused else nn.MaxPool2d(2, stride=2)),
         ])) for i in range(depth)])
 
     bottleneck = nn.Sequential(cell(neck))
 
     decoder = nn.Sequential(*[
         nn.Sequential(OrderedDict([
-            ('up', nn.Upsample(scale_factor=2)),
-            ('skip', PopCat().isolate(namespaces[i])),
+            ('up', nn.Identity() if fused else nn.Upsample(scale_factor=2)),
+            ('skip', (PopUpCat() if fused else PopCat()).isolate(namespaces[i])),
             ('decode', cell(dec(i))),
         ])) for i in reversed(range(depth))])
 
