@@ -46,6 +46,7 @@ namespace tgpipe {
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 
 constexpr int kP = 36;                  // Winograd positions of a 6x6 tile
 constexpr int kC = 4;                   // reduction channels per step (MFMA K)
@@ -130,13 +131,14 @@ __global__ void f4_weight_kernel(const float* __restrict__ w, float* __restrict_
         floatx4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
 }
 
-// B^T of one 6-vector, in place.
-__device__ __forceinline__ void bt6(float& d0, float& d1, float& d2, float& d3, float& d4,
-                                    float& d5) {
-  const float p = d4 - 4.f * d2, q = d3 - 4.f * d1;
-  const float s = d4 - d2, t = 2.f * (d3 - d1);
-  const float r0 = 4.f * d0 - 5.f * d2 + d4;
-  const float r5 = 4.f * d1 - 5.f * d3 + d5;
+// B^T of one 6-vector, in place (T = float, or floatx2: two vectors at once on the packed
+// fp32 VALU, v_pk_fma_f32 / v_pk_add_f32).
+template <typename T>
+__device__ __forceinline__ void bt6(T& d0, T& d1, T& d2, T& d3, T& d4, T& d5) {
+  const T p = d4 - 4.f * d2, q = d3 - 4.f * d1;
+  const T s = d4 - d2, t = 2.f * (d3 - d1);
+  const T r0 = 4.f * d0 - 5.f * d2 + d4;
+  const T r5 = 4.f * d1 - 5.f * d3 + d5;
   d0 = r0;
   d1 = p + q;
   d2 = p - q;
@@ -184,15 +186,36 @@ __device__ __forceinline__ void f4_load_patch(F4Patch& p, __amdgpu_buffer_rsrc_t
   }
 }
 
-// V = B^T d B into the lane's 36 contiguous LDS floats.
+// V = B^T d B into the lane's 36 contiguous LDS floats.  Both passes run on pairs -- the
+// column pass on adjacent column pairs, the row pass on adjacent row pairs -- with the
+// packed fp32 VALU: 148 instead of 242 VALU instructions per patch (the patch waves'
+// VALU work is what their SIMDs stall on, profiles/pmc_f4_kernels.json valu_per_mfma).
 __device__ __forceinline__ void f4_transform_store(F4Patch& p, float* vdst) {
   float* d = p.d;
 #pragma unroll
-  for (int j = 0; j < 6; ++j)
-    bt6(d[0 * 6 + j], d[1 * 6 + j], d[2 * 6 + j], d[3 * 6 + j], d[4 * 6 + j], d[5 * 6 + j]);
+  for (int jp = 0; jp < 3; ++jp) {
+    floatx2 c[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
-    bt6(d[i * 6 + 0], d[i * 6 + 1], d[i * 6 + 2], d[i * 6 + 3], d[i * 6 + 4], d[i * 6 + 5]);
+    for (int i = 0; i < 6; ++i) c[i] = floatx2{d[i * 6 + 2 * jp], d[i * 6 + 2 * jp + 1]};
+    bt6(c[0], c[1], c[2], c[3], c[4], c[5]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      d[i * 6 + 2 * jp] = c[i][0];
+      d[i * 6 + 2 * jp + 1] = c[i][1];
+    }
+  }
+#pragma unroll
+  for (int ip = 0; ip < 3; ++ip) {
+    floatx2 r[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) r[j] = floatx2{d[2 * ip * 6 + j], d[(2 * ip + 1) * 6 + j]};
+    bt6(r[0], r[1], r[2], r[3], r[4], r[5]);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      d[2 * ip * 6 + j] = r[j][0];
+      d[(2 * ip + 1) * 6 + j] = r[j][1];
+    }
+  }
 #pragma unroll
   for (int k = 0; k < kP / 4; ++k)
     reinterpret_cast<floatx4*>(vdst)[k] = floatx4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
