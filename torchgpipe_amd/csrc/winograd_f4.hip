@@ -342,36 +342,44 @@ __device__ __forceinline__ void f4_output_transform(const floatx4 (&acc)[kP],
   const int py = 4 * pty;
   const int px = 4 * (prem - pty * TW);
   const bool full = (W & 3) == 0 && py + 4 <= H;
+  // two output channels at a time (adjacent accumulator registers) on the packed fp32 VALU
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int o = obase + r;
+  for (int rp = 0; rp < 2; ++rp) {
+    const int o = obase + 2 * rp;
     if (o >= O) continue;
     // A^T along rows (i), for every column j
-    float s[4][6];
+    floatx2 s[4][6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      const float m0 = acc[0 * 6 + j][r], m1 = acc[1 * 6 + j][r], m2 = acc[2 * 6 + j][r];
-      const float m3 = acc[3 * 6 + j][r], m4 = acc[4 * 6 + j][r], m5 = acc[5 * 6 + j][r];
-      const float a = m1 + m2, b = m1 - m2, c = m3 + m4, d = m3 - m4;
-      s[0][j] = m0 + a + c;
+      floatx2 m[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) m[i] = floatx2{acc[i * 6 + j][2 * rp], acc[i * 6 + j][2 * rp + 1]};
+      const floatx2 a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], d = m[3] - m[4];
+      s[0][j] = m[0] + a + c;
       s[1][j] = b + 2.f * d;
       s[2][j] = a + 4.f * c;
-      s[3][j] = b + 8.f * d + m5;
+      s[3][j] = b + 8.f * d + m[5];
     }
-    const float bv = bias ? bias[o] : 0.f;
-    float* yp = ydst + (static_cast<int64_t>(pn) * O + o) * HW + static_cast<int64_t>(py) * W + px;
+    const floatx2 bv{bias ? bias[o] : 0.f, bias && o + 1 < O ? bias[o + 1] : 0.f};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float a = s[k][1] + s[k][2], b = s[k][1] - s[k][2];
-      const float c = s[k][3] + s[k][4], d = s[k][3] - s[k][4];
-      const floatx4 out{s[k][0] + a + c + bv, b + 2.f * d + bv, a + 4.f * c + bv,
-                        b + 8.f * d + s[k][5] + bv};
-      if (full) {
-        *reinterpret_cast<floatx4*>(yp + k * W) = out;
-      } else if (py + k < H) {
+      const floatx2 a = s[k][1] + s[k][2], b = s[k][1] - s[k][2];
+      const floatx2 c = s[k][3] + s[k][4], d = s[k][3] - s[k][4];
+      const floatx2 v0 = s[k][0] + a + c + bv, v1 = b + 2.f * d + bv, v2 = a + 4.f * c + bv;
+      const floatx2 v3 = b + 8.f * d + s[k][5] + bv;
 #pragma unroll
-        for (int l = 0; l < 4; ++l)
-          if (px + l < W) yp[k * W + l] = out[l];
+      for (int e = 0; e < 2; ++e) {
+        if (o + e >= O) break;
+        float* yp = ydst + (static_cast<int64_t>(pn) * O + o + e) * HW +
+                    static_cast<int64_t>(py) * W + px;
+        const floatx4 out{v0[e], v1[e], v2[e], v3[e]};
+        if (full) {
+          *reinterpret_cast<floatx4*>(yp + k * W) = out;
+        } else if (py + k < H) {
+#pragma unroll
+          for (int l = 0; l < 4; ++l)
+            if (px + l < W) yp[k * W + l] = out[l];
+        }
       }
     }
   }
@@ -705,10 +713,12 @@ void launch_split_reduce(const float* ws, const float* bias, float* y, int64_t n
 // 2/3 two gradient waves each -- and waves 4-5 only multiply.  Lanes of one channel take 4
 // horizontally adjacent tiles, so a load instruction touches 16 channel planes.
 
-// A of one 4-vector: (y0, y0+y1+y2+y3, y0-y1+y2-y3, y0+2y1+4y2+8y3, y0-2y1+4y2-8y3, y3).
-__device__ __forceinline__ void a6(float y0, float y1, float y2, float y3, float (&o)[6]) {
-  const float e = y0 + y2, od = y1 + y3;
-  const float e2 = y0 + 4.f * y2, o2 = 2.f * y1 + 8.f * y3;
+// A of one 4-vector: (y0, y0+y1+y2+y3, y0-y1+y2-y3, y0+2y1+4y2+8y3, y0-2y1+4y2-8y3, y3)
+// (T = float, or floatx2 for two vectors on the packed fp32 VALU).
+template <typename T>
+__device__ __forceinline__ void a6(T y0, T y1, T y2, T y3, T (&o)[6]) {
+  const T e = y0 + y2, od = y1 + y3;
+  const T e2 = y0 + 4.f * y2, o2 = 2.f * y1 + 8.f * y3;
   o[0] = y0;
   o[1] = e + od;
   o[2] = e - od;
@@ -785,23 +795,34 @@ __device__ __forceinline__ void f4_load_dy(float (&g)[16], __amdgpu_buffer_rsrc_
   }
 }
 
-// M' = A g A^T into the lane's 36 contiguous LDS floats.
+// M' = A g A^T into the lane's 36 contiguous LDS floats (both passes on pairs, packed
+// fp32 VALU, like f4_transform_store).
 __device__ __forceinline__ void f4_dy_transform_store(const float (&g)[16], float* mdst) {
   float t[6][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float col[6];
-    a6(g[0 * 4 + j], g[1 * 4 + j], g[2 * 4 + j], g[3 * 4 + j], col);
+  for (int jp = 0; jp < 2; ++jp) {
+    floatx2 col[6];
+    a6(floatx2{g[0 * 4 + 2 * jp], g[0 * 4 + 2 * jp + 1]},
+       floatx2{g[1 * 4 + 2 * jp], g[1 * 4 + 2 * jp + 1]},
+       floatx2{g[2 * 4 + 2 * jp], g[2 * 4 + 2 * jp + 1]},
+       floatx2{g[3 * 4 + 2 * jp], g[3 * 4 + 2 * jp + 1]}, col);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) t[i][j] = col[i];
+    for (int i = 0; i < 6; ++i) {
+      t[i][2 * jp] = col[i][0];
+      t[i][2 * jp + 1] = col[i][1];
+    }
   }
   float m[kP];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    float row[6];
-    a6(t[i][0], t[i][1], t[i][2], t[i][3], row);
+  for (int ip = 0; ip < 3; ++ip) {
+    floatx2 row[6];
+    a6(floatx2{t[2 * ip][0], t[2 * ip + 1][0]}, floatx2{t[2 * ip][1], t[2 * ip + 1][1]},
+       floatx2{t[2 * ip][2], t[2 * ip + 1][2]}, floatx2{t[2 * ip][3], t[2 * ip + 1][3]}, row);
 #pragma unroll
-    for (int j = 0; j < 6; ++j) m[i * 6 + j] = row[j];
+    for (int j = 0; j < 6; ++j) {
+      m[2 * ip * 6 + j] = row[j][0];
+      m[(2 * ip + 1) * 6 + j] = row[j][1];
+    }
   }
 #pragma unroll
   for (int q = 0; q < kP / 4; ++q)
