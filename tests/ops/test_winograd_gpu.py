@@ -119,7 +119,7 @@ def test_direct_ops_small_channels():
                                    (1, 16, 8, 1, 1), (4, 32, 32, 33, 2), (2, 256, 128, 12, 12),
                                    (1, 64, 192, 20, 36)])
 @pytest.mark.parametrize('splits', [0, 1, 3])
-@pytest.mark.parametrize('variant', [4, 5, 6, 7, 12, 14, 15])
+@pytest.mark.parametrize('variant', [4, 5, 6, 7, 12, 14, 15, 18])
 def test_f4_forward_and_flip(shape, splits, variant):
     # Winograd F(4x4,3x3): edge tiles (H, W not multiples of 4), padded channels, split-K,
     # and backward-data through the flipped weight transform

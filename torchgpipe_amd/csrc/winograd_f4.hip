@@ -237,14 +237,15 @@ __device__ __forceinline__ void f4_store_slab(const floatx4 (&ur)[Cfg::kUVec], f
     *reinterpret_cast<floatx4*>(us + 4 * (i * Cfg::kSlabThreads + stid)) = ur[i];
 }
 
-// 36 MFMAs of one step: M[xi] += U[xi]^T V[xi] over the step's 4 channels.
+// 36 MFMAs of one step: M[xi] += U[xi]^T V[xi] over the step's 4 channels (U and V images
+// at separate LDS addresses).
 template <typename Cfg>
-__device__ __forceinline__ void f4_mfma(floatx4 (&acc)[kP], const float* buf, int lane, int wo,
-                                        int wt) {
+__device__ __forceinline__ void f4_mfma_uv(floatx4 (&acc)[kP], const float* ubuf,
+                                           const float* vbuf, int lane, int wo, int wt) {
   const floatx4* ua =
-      reinterpret_cast<const floatx4*>(buf + ((wo * kC + (lane >> 4)) * 16 + (lane & 15)) * kP);
+      reinterpret_cast<const floatx4*>(ubuf + ((wo * kC + (lane >> 4)) * 16 + (lane & 15)) * kP);
   const floatx4* vb = reinterpret_cast<const floatx4*>(
-      buf + Cfg::kUImg + ((lane >> 4) * kT + wt * 16 + (lane & 15)) * kP);
+      vbuf + ((lane >> 4) * kT + wt * 16 + (lane & 15)) * kP);
   // operand quad q+1 is read while quad q's 4 MFMAs issue
   floatx4 a = ua[0], b = vb[0];
 #pragma unroll
@@ -266,6 +267,13 @@ __device__ __forceinline__ void f4_mfma(floatx4 (&acc)[kP], const float* buf, in
     if (q + 1 < kP / 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
   }
+}
+
+// One LDS buffer = [U image][V image].
+template <typename Cfg>
+__device__ __forceinline__ void f4_mfma(floatx4 (&acc)[kP], const float* buf, int lane, int wo,
+                                        int wt) {
+  f4_mfma_uv<Cfg>(acc, buf, buf + Cfg::kUImg, lane, wo, wt);
 }
 
 // f4_mfma with the LDS operand quads read kAhead quads before their MFMAs (kAhead = 1 is
@@ -518,6 +526,120 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
   // -- output transform Y = A^T M A from the accumulators --------------------------------
   // Lane (wt*16 + j) holds tile t0 + wt*16 + j; register r of accumulator xi holds output
   // channel o0 + wo*16 + 4*(lane >> 4) + r.  Split-K partials go to slab z of y.
+  const int tp = t0 + wt * 16 + (lane & 15);
+  if (tp >= P) return;
+  float* ydst = y + static_cast<int64_t>(z) * (P / tpi) * O * HW;
+  f4_output_transform(acc, ydst, bias != nullptr && splits == 1 ? bias : nullptr, tp, tpi, TW,
+                      H, W, O, o0 + wo * 16 + 4 * (lane >> 4));
+}
+
+// Variant 18: variant 6 with the weight slab two steps ahead.  Variant 6 waits at every
+// step's barrier for the slab LDS-DMA issued at the start of that step (__syncthreads
+// drains vmcnt to 0; one step of MFMAs, ~0.5 us, does not cover an L2/HBM fetch).  Here
+// the U slab has a ring of three LDS images (3 x 36 KiB) next to the two V images
+// (2 x 18 KiB): 147 KiB.  The slab waves issue step s+2's DMA, run step s's MFMAs, and
+// retire only step s+1's DMA (counted s_waitcnt vmcnt) before a raw s_barrier, so one
+// slab stays in flight across every barrier; the patch waves retire their LDS writes
+// (lgkmcnt 0) before the same barrier.
+template <bool kVec>
+__global__ __launch_bounds__(512, 1) void f4_conv_ring_kernel(
+    const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ bias,
+    float* __restrict__ y, int R, int H, int W, int O, int Rp, int Op, int TH, int TW, int P,
+    int tblocks, int oblocks, int splits, uint32_t x_bytes) {
+  using Cfg = F4Cfg<4>;
+  constexpr int kO = Cfg::kO;
+  constexpr int kSlabWaves = Cfg::kSlabThreads / 64;                   // 6
+  constexpr int kDmaPerWave = Cfg::kUImg / 256 / kSlabWaves;           // 6 per step
+  static_assert(kDmaPerWave == 6, "the counted vmcnt below assumes 6 DMAs per wave");
+  __shared__ float lds[3 * Cfg::kUImg + 2 * kVImg];  // 147 KiB: one workgroup per CU
+  float* const uimg = lds;
+  float* const vimg = lds + 3 * Cfg::kUImg;
+
+  const int nwg = tblocks * oblocks * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int ob = wgid % oblocks;
+  const int tb = (wgid / oblocks) % tblocks;
+  const int z = wgid / (oblocks * tblocks);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wo = wave % 4;
+  const int wt = wave / 4;
+  const int t0 = tb * kT;
+  const int o0 = ob * kO;
+  const int HW = H * W;
+  const int tpi = TH * TW;
+
+  const int nsteps = Rp / kC;
+  const int s_begin = z * nsteps / splits;
+  const int s_end = (z + 1) * nsteps / splits;
+  floatx4 acc[kP];
+#pragma unroll
+  for (int i = 0; i < kP; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (wave < 2) {
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                          static_cast<int>(x_bytes), 0x00020000);
+    F4Patch p;
+    f4_fwd_offsets(p, t0 + wave * 16 + (lane & 15), lane >> 4, P, tpi, TW, R, H, W);
+    float* vmine = vimg + ((lane >> 4) * kT + wave * 16 + (lane & 15)) * kP;
+    const uint32_t step_bytes = static_cast<uint32_t>(kC) * HW * 4;
+    f4_load_patch<kVec>(p, xr, s_begin * step_bytes);
+    f4_transform_store(p, vmine);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    f4_load_patch<kVec>(p, xr, min(s_begin + 1, s_end - 1) * step_bytes);
+    int us = 0;
+    for (int s = s_begin; s < s_end; ++s) {
+      const int vb = (s - s_begin) & 1;
+      f4_transform_store(p, vmine + (vb ^ 1) * kVImg);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_load_patch<kVec>(p, xr, min(s + 2, s_end - 1) * step_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      f4_mfma_uv<Cfg>(acc, uimg + us * Cfg::kUImg, vimg + vb * kVImg, lane, wo, wt);
+      us = us == 2 ? 0 : us + 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    const int sw = wave - 2;
+    const int64_t slab_stride = static_cast<int64_t>(Op / 16) * (kC * 16 * kP);
+    const float* ubase = u + static_cast<int64_t>(o0 / 16) * (kC * 16 * kP);
+    f4_glds_slab<Cfg, kSlabWaves>(ubase + s_begin * slab_stride, uimg, sw, lane);
+    if (s_begin + 1 < s_end) {
+      f4_glds_slab<Cfg, kSlabWaves>(ubase + (s_begin + 1) * slab_stride, uimg + Cfg::kUImg, sw,
+                                    lane);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int us = 0;
+    for (int s = s_begin; s < s_end; ++s) {
+      const int vb = (s - s_begin) & 1;
+      const int un = us == 0 ? 2 : us - 1;  // (us + 2) % 3: the slot step s-1 read
+      const bool more = s + 2 < s_end;
+      if (more)
+        f4_glds_slab<Cfg, kSlabWaves>(ubase + (s + 2) * slab_stride, uimg + un * Cfg::kUImg,
+                                      sw, lane);
+      f4_mfma_uv<Cfg>(acc, uimg + us * Cfg::kUImg, vimg + vb * kVImg, lane, wo, wt);
+      us = us == 2 ? 0 : us + 1;
+      // retire step s+1's slab (leave step s+2's in flight), then the barrier
+      if (more)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+
   const int tp = t0 + wt * 16 + (lane & 15);
   if (tp >= P) return;
   float* ydst = y + static_cast<int64_t>(z) * (P / tpi) * O * HW;
@@ -1124,7 +1246,8 @@ void launch_wino4_weight(const float* w, float* u, int64_t out_channels, int64_t
 WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                     int variant, int splits) {
   WinoPlan plan;
-  plan.variant = (variant >= 4 && variant <= 12 && variant != 11) || variant == 14 || variant == 15 ? variant : 5;
+  plan.variant = (variant >= 4 && variant <= 12 && variant != 11) || variant == 14 ||
+                         variant == 15 || variant == 18 ? variant : 5;
   const int og = plan.variant == 5 || plan.variant == 7 || plan.variant == 15 ? 2 : 4;
   const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
   const int64_t blocks = ((P + kT - 1) / kT) * ((out_channels + 16 * og - 1) / (16 * og));
@@ -1155,6 +1278,22 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
   const int64_t P = n * th * tw;
   const int og = plan.variant == 5 || plan.variant == 7 || plan.variant == 15 ? 2 : 4;
   const int tblocks = static_cast<int>((P + kT - 1) / kT);
+  if (plan.variant == 18) {
+    const int oblocks4 = static_cast<int>((out_channels + 63) / 64);
+    const int64_t nwg4 = static_cast<int64_t>(tblocks) * oblocks4 * plan.splits;
+    auto kernel = f4_conv_ring_kernel<false>;  // (16-byte centre loads: see variant 12)
+    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg4)), dim3(512), 0, stream, x, u,
+                       bias, plan.splits > 1 ? ws : y, static_cast<int>(red_channels),
+                       static_cast<int>(h), static_cast<int>(w),
+                       static_cast<int>(out_channels), static_cast<int>(Rp),
+                       static_cast<int>(Op), static_cast<int>(th), static_cast<int>(tw),
+                       static_cast<int>(P), tblocks, oblocks4, plan.splits,
+                       static_cast<uint32_t>(n * red_channels * h * w * 4));
+    if (plan.splits > 1)
+      launch_split_reduce(ws, bias, y, n * out_channels * h * w, h * w,
+                          static_cast<int>(out_channels), plan.splits, stream);
+    return;
+  }
   const int oblocks = static_cast<int>((out_channels + 16 * og - 1) / (16 * og));
   const int splits = plan.splits;
   const int64_t nwg = static_cast<int64_t>(tblocks) * oblocks * splits;

@@ -141,6 +141,9 @@ def clear_winograd_caches(module: torch.nn.Module) -> None:
 # 1.17-1.45x faster than F(2x2) from 12^2 up, slower at 6^2 (a 4x4 tile wastes 5/9 of a
 # 6-pixel plane).  The F(4x4) kernel's 32-bit offsets need the input below 1 GiB.
 F4_MIN_PLANE = 8
+# Fused F(4x4) forward / backward-data kernel for < 512 channels: 6 (slab one step ahead)
+# or 18 (slab ring, two steps ahead; csrc/winograd_f4.hip).  TGPIPE_F4_FUSED_VARIANT.
+_F4_FUSED_VARIANT = int(os.environ.get('TGPIPE_F4_FUSED_VARIANT', '6'))
 F4_MAX_BYTES = (1 << 30) - 64
 
 
@@ -193,7 +196,7 @@ def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tens
             small = blocks < 160 or min(x.shape[2], x.shape[3]) < F4_MIN_PLANE
             variant = 15 if small else 14
         else:
-            variant = 7 if out_channels <= 32 or blocks < 160 else 6
+            variant = 7 if out_channels <= 32 or blocks < 160 else _F4_FUSED_VARIANT
         return ops.wino4_conv(x, cache.get(weight, flip, True), bias, out_channels, variant)
     return ops.wino_conv(x, cache.get(weight, flip), bias, out_channels)
 
