@@ -75,11 +75,18 @@ def test_fused_unet_matches_unfused_training_without_dropout():
     a.sum().backward()
     b.sum().backward()
     c.sum().backward()
+    errs = []
     for p, q, r in zip(fused.parameters(), plain.parameters(), ref.parameters()):
         scale = r.grad.norm().item() + 1e-6
         err_fused = (p.grad.double() - r.grad).norm().item() / scale
         err_plain = (q.grad.double() - r.grad).norm().item() / scale
-        assert err_fused < max(1e-3, 10 * err_plain), (p.shape, err_fused, err_plain)
+        errs.append((tuple(p.shape), err_fused, err_plain))
+    print('relative gradient errors vs fp64 (shape, fused, plain):', errs)
+    # pinned bound (verdict r1 #11): every parameter's relative gradient error vs the fp64
+    # model below 1.5e-4 (measured: fused max 4.9e-5, plain MIOpen 1.0e-5 -- Winograd
+    # F(4x4) fp32 transform rounding)
+    worst = max(errs, key=lambda e: e[1])
+    assert worst[1] < 1.5e-4, worst
 
 
 def test_deferred_batch_norm_on_gpu_matches_bn():

@@ -7,9 +7,9 @@ machines by repeating ``'cpu'`` as a device.
 Parity: ``torchgpipe/stream.py:12-101`` (CPUStream, new/current/default
 stream, use_device/use_stream, wait_stream, record_stream).  Differences:
 
-* ``wait_stream`` is implemented with an explicit HIP event record + stream
-  wait (``hipEventRecord``/``hipStreamWaitEvent``) through
-  ``torch.cuda.Event`` so the event can be pooled and reused.
+* ``wait_stream`` is ``torch.cuda.Stream.wait_stream`` (a HIP event record on the
+  target + ``hipStreamWaitEvent`` on the source, asynchronous for the host); a CPU
+  waiter synchronises on the target stream instead.
 * A small per-device **stream pool** (``StreamPool``) replaces "``chunks``
   streams per device" (the reference allocates ``chunks`` copy streams per
   device, 1667 for ResNet p2).  Ordering is carried by events, so stream
