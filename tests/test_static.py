@@ -9,11 +9,15 @@ checked with the standard library:
 * every public function and method of the package annotates all parameters and its
   return type (the part of ``mypy --strict``'s ``disallow_untyped_defs`` /
   ``disallow_incomplete_defs`` that needs no type inference);
-* no ``print`` in library code outside ``__main__`` blocks and the build script.
+* no ``print`` in library code outside ``__main__`` blocks and the build script;
+* the module-level imports of the package follow the reference's isort setting
+  (``force_sort_within_sections``): ``__future__``, standard library, third party, this
+  package, each section sorted by module name regardless of ``import`` / ``from``.
 """
 import ast
 import os
 import re
+import sys
 
 import pytest
 
@@ -117,3 +121,37 @@ def test_library_does_not_print(path):
               if isinstance(n, ast.Call) and isinstance(n.func, ast.Name)
               and n.func.id == 'print' and id(n) not in main_blocks]
     assert not prints, f'{_rel(path)}: print() at lines {prints}'
+
+
+FIRST_PARTY = {'torchgpipe_amd', 'tests', 'benchmarks', 'torchgpipe_amd_balancing'}
+
+
+def _import_key(node):
+    if isinstance(node, ast.Import):
+        module = node.names[0].name
+    else:
+        module = '.' * node.level + (node.module or '')
+    root = module.split('.')[0]
+    if root == '__future__':
+        section = 0
+    elif root in FIRST_PARTY or module.startswith('.'):
+        section = 3
+    elif root in sys.stdlib_module_names:
+        section = 1
+    else:
+        section = 2
+    return section, module.lower()
+
+
+@pytest.mark.parametrize('path', LIB, ids=_rel)
+def test_import_order(path):
+    tree = ast.parse(open(path).read())
+    block = []
+    for node in tree.body:
+        if isinstance(node, (ast.Import, ast.ImportFrom)):
+            block.append(node)
+        elif block and not (isinstance(node, ast.Expr) and isinstance(node.value, ast.Constant)):
+            break
+    keys = [_import_key(n) for n in block]
+    unsorted = [block[i].lineno for i in range(1, len(keys)) if keys[i] < keys[i - 1]]
+    assert not unsorted, f'{_rel(path)}: imports out of isort order at lines {unsorted}'

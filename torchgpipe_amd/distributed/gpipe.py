@@ -19,8 +19,8 @@ naming since ranks address each other through ``torch.distributed``.
 from typing import Dict, Iterable, Iterator, List, Optional, Sequence, Tuple, Union
 
 import torch
-import torch.distributed as dist
 from torch import Tensor, nn
+import torch.distributed as dist
 
 from torchgpipe_amd.gpipe import BalanceError, check_balance, partition_layers, \
     recommend_auto_balance, verify_module

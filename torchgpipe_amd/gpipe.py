@@ -26,11 +26,11 @@ from torch import Tensor, nn
 
 from torchgpipe_amd import microbatch
 from torchgpipe_amd.batchnorm import DeferredBatchNorm, set_micro_batches
+from torchgpipe_amd.ops.conv import new_step as wino_new_step
 from torchgpipe_amd.pipeline import Pipeline
 from torchgpipe_amd.skip.layout import inspect_skip_layout
 from torchgpipe_amd.skip.skippable import verify_skippables
 from torchgpipe_amd.stream import AbstractStream, StreamPool
-from torchgpipe_amd.ops.conv import new_step as wino_new_step
 from torchgpipe_amd.utils.meta import is_meta, materialize
 from torchgpipe_amd.worker import WorkerPool
 

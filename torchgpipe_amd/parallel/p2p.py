@@ -29,13 +29,13 @@ stream-ordered, so a missing peer is caught by the process group's watchdog
 (``init_process_group(timeout=...)``), which aborts the rank instead of
 hanging the job.
 """
-import datetime
 from dataclasses import dataclass
+import datetime
 from typing import Dict, Hashable, List, Optional, Sequence, Tuple
 
 import torch
-import torch.distributed as dist
 from torch import Tensor
+import torch.distributed as dist
 
 from torchgpipe_amd.ops import misc
 

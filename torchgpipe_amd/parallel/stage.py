@@ -27,13 +27,13 @@ Every cell is a function ``flat_inputs → flat_outputs`` where ``flat_inputs``
 output tensors + skips stashed for other ranks, so checkpointing
 (``Checkpointing``) treats cross-rank skips like any other input/output.
 """
-import datetime
 from collections import OrderedDict
+import datetime
 from typing import Any, Callable, Dict, Hashable, List, Optional, Sequence, Tuple, Union
 
 import torch
-import torch.distributed as dist
 from torch import Tensor, nn
+import torch.distributed as dist
 
 from torchgpipe_amd import microbatch
 from torchgpipe_amd.batchnorm import DeferredBatchNorm, set_micro_batches

@@ -15,10 +15,10 @@ format as the canonical on-disk layout and adds what pipelines need:
   device (``map_location``) — with a different balance than it was saved with
   if needed.
 """
+from collections import OrderedDict
 import json
 import os
 import re
-from collections import OrderedDict
 from typing import Dict, List, Mapping, Optional, Sequence
 
 import torch

@@ -18,9 +18,9 @@ from contextlib import contextmanager
 from queue import Queue
 import sys
 from threading import Thread
-import weakref
 from types import TracebackType
 from typing import Callable, Dict, Generator, List, Optional, Tuple, Type, Union
+import weakref
 
 import torch
 
