@@ -41,6 +41,10 @@ CASES = [
     (4, 1024, 7, 7, 256, 1, 1, 1, 0, 0),     # split reduction, 1x1
     (4, 96, 14, 14, 64, 1, 1, 2, 0, 1),      # strided scatter backward, even plane
     (2, 3, 32, 32, 16, 3, 3, 1, 1, 0),       # U-Net's 3-channel input convolution (2-D taps)
+    (4, 32, 28, 28, 32, 3, 3, 2, 1, 0),      # reduction-cell 3x3 stride 2 (stride holes)
+    (3, 16, 15, 15, 24, 3, 3, 2, 1, 0),      # 3x3 stride 2, odd plane
+    (2, 3, 32, 32, 16, 3, 3, 2, 1, 0),       # AmoebaNet stem (3 channels, stride 2)
+    (2, 16, 14, 14, 16, 1, 7, 2, 3, 0),      # 1x7 at stride 2
 ]
 
 

@@ -61,3 +61,22 @@ def test_maxpool2x2_matches_aten(hw):
     y.backward(g)
     yr.backward(g)
     torch.testing.assert_close(x.grad, xr.grad, equal_nan=True)
+
+
+@pytest.mark.parametrize('hw', [(14, 14), (7, 9)])
+def test_maxpool2x2_add_and_channel_sliced_gradient(hw):
+    """AmoebaNet's use: pool(x) + add in one pass, and the gradient of a concatenated cell
+    output (a channel slice) read in place."""
+    torch.manual_seed(2)
+    x = torch.randn(3, 8, *hw, device='cuda', requires_grad=True)
+    add = torch.randn(3, 8, hw[0] // 2, hw[1] // 2, device='cuda', requires_grad=True)
+    other = torch.randn(3, 5, hw[0] // 2, hw[1] // 2, device='cuda', requires_grad=True)
+    y = torch.cat([other, MaxPool2x2()(x, add)], 1)
+    xr, ar, orr = (t.detach().double().requires_grad_(True) for t in (x, add, other))
+    yr = torch.cat([orr, F.max_pool2d(xr, 2, 2) + ar], 1)
+    torch.testing.assert_close(y.double(), yr, rtol=1e-6, atol=1e-6)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.double())
+    torch.testing.assert_close(x.grad.double(), xr.grad, rtol=0, atol=0)
+    torch.testing.assert_close(add.grad.double(), ar.grad, rtol=0, atol=0)

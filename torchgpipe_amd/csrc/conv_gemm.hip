@@ -2,7 +2,9 @@
 // AmoebaNet-D cell operations: 1x1 (stride 1 / 2, input offset for FactorizedReduce)
 // and 1xk / kx1 convolutions, NCHW fp32, fused with the ReLU that precedes every
 // convolution of the model and with the statistics of the BatchNorm that follows it.
-// Any kh x kw kernel works at stride 1 (U-Net's 3-channel input convolution uses it).
+// Any kh x kw kernel at any stride (U-Net's 3-channel input convolution, AmoebaNet's stem
+// and the stride-2 3x3 of its reduction cells); strided kernels larger than 1x1 run the
+// backward-data over every input pixel, the taps that fall into stride holes reading 0.
 //
 //   forward      Z[n][co][p]    = sum_{ci,t} W[co][ci][t] * relu(X[n][ci][tap(p,t)])
 //                M = Co, N = images x output pixels, K = Ci x taps
@@ -397,15 +399,27 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
                                    ? static_cast<uint32_t>((col[e].base + coff) * 4) : kOOB);
           }
         } else {
-          // stride 1: output pixel = input pixel + pad - tap - offset
+          // output pixel * stride = input pixel + pad - tap - offset (stride holes: none)
           const int co = k / g.taps, t = k - co * g.taps;
           const int th = t / g.kw, tw = t - th * g.kw;
+          if (g.sh == 1 && g.sw == 1) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int y = col[e].y - th, x = col[e].x - tw;
-            const bool ok = col[e].ok && kin && y >= 0 && y < g.ho && x >= 0 && x < g.wo;
-            v[e] = bload(br, ok ? static_cast<uint32_t>(
-                                      (col[e].base + co * hw_out + y * g.wo + x) * 4) : kOOB);
+            for (int e = 0; e < 4; ++e) {
+              const int y = col[e].y - th, x = col[e].x - tw;
+              const bool ok = col[e].ok && kin && y >= 0 && y < g.ho && x >= 0 && x < g.wo;
+              v[e] = bload(br, ok ? static_cast<uint32_t>(
+                                        (col[e].base + co * hw_out + y * g.wo + x) * 4) : kOOB);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int ys = col[e].y - th, xs = col[e].x - tw;
+              const int y = ys / g.sh, x = xs / g.sw;
+              const bool ok = col[e].ok && kin && ys >= 0 && xs >= 0 && y * g.sh == ys &&
+                              x * g.sw == xs && y < g.ho && x < g.wo;
+              v[e] = bload(br, ok ? static_cast<uint32_t>(
+                                        (col[e].base + co * hw_out + y * g.wo + x) * 4) : kOOB);
+            }
           }
         }
         rb[i] = v;

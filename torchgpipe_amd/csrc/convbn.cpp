@@ -244,7 +244,6 @@ Parts make_parts(const at::Tensor& x, at::TensorList weights, at::IntArrayRef ge
                 "weight must be [Co][Ci][kh][kw] matching x and the geometry");
     TORCH_CHECK(sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && g[6] >= 0 && g[7] >= 0,
                 "bad stride / padding / offset");
-    TORCH_CHECK(kh * kw == 1 || (sh == 1 && sw == 1), "kernels larger than 1x1 need stride 1");
     const int64_t ho = (h + 2 * ph - kh) / sh + 1, wo = (w + 2 * pw - kw) / sw + 1;
     TORCH_CHECK(ho > 0 && wo > 0, "empty output");
     if (i == 0) {
@@ -753,13 +752,21 @@ at::Tensor up2x_backward(const at::Tensor& dy_in, int64_t c) {
   return dx;
 }
 
-at::Tensor maxpool2x2_forward(const at::Tensor& x_in) {
+at::Tensor maxpool2x2_forward(const at::Tensor& x_in, const c10::optional<at::Tensor>& add) {
   auto x = x_in.contiguous();
   check_f32(x, "x", x);
   TORCH_CHECK(x.dim() == 4, "x must be NCHW");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto y = at::empty({x.size(0), x.size(1), x.size(2) / 2, x.size(3) / 2}, x.options());
-  launch_maxpool2x2_forward(x.data_ptr<float>(), y.data_ptr<float>(), x.size(0) * x.size(1),
+  const float* ad = nullptr;
+  at::Tensor add_c;
+  if (add.has_value() && add->defined()) {
+    add_c = add->contiguous();
+    check_f32(add_c, "add", x);
+    TORCH_CHECK(add_c.sizes() == y.sizes(), "add must have the pooled shape");
+    ad = add_c.data_ptr<float>();
+  }
+  launch_maxpool2x2_forward(x.data_ptr<float>(), ad, y.data_ptr<float>(), x.size(0) * x.size(1),
                             static_cast<int>(x.size(2)), static_cast<int>(x.size(3)),
                             cur_stream(x));
   return y;
@@ -767,18 +774,24 @@ at::Tensor maxpool2x2_forward(const at::Tensor& x_in) {
 
 at::Tensor maxpool2x2_backward(const at::Tensor& x_in, const at::Tensor& dy_in) {
   auto x = x_in.contiguous();
-  auto dy = dy_in.contiguous();
   check_f32(x, "x", x);
-  check_f32(dy, "dy", x);
-  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(2) == x.size(2) / 2 &&
-                  dy.size(3) == x.size(3) / 2 && dy.size(1) == x.size(1),
+  TORCH_CHECK(x.dim() == 4 && dy_in.dim() == 4 && dy_in.size(2) == x.size(2) / 2 &&
+                  dy_in.size(3) == x.size(3) / 2 && dy_in.size(1) == x.size(1) &&
+                  dy_in.size(0) == x.size(0),
               "dy must be the pooled shape of x");
+  TORCH_CHECK(dy_in.scalar_type() == at::kFloat && dy_in.device() == x.device(),
+              "dy must be fp32 on x's device");
+  // a channel slice (gradient of one input of a concatenation) is read in place
+  const int64_t dy_img = image_stride_if_channel_slice(dy_in);
+  auto dy = dy_img > 0 ? dy_in : dy_in.contiguous();
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const bool odd = (x.size(2) & 1) || (x.size(3) & 1);
   auto dx = odd ? at::zeros_like(x) : at::empty_like(x);
+  const int64_t c = x.size(1);
   launch_maxpool2x2_backward(x.data_ptr<float>(), dy.data_ptr<float>(), dx.data_ptr<float>(),
-                             x.size(0) * x.size(1), static_cast<int>(x.size(2)),
-                             static_cast<int>(x.size(3)), cur_stream(x));
+                             x.size(0) * c, static_cast<int>(c), static_cast<int>(x.size(2)),
+                             static_cast<int>(x.size(3)),
+                             dy_img > 0 ? dy_img : c * dy.size(2) * dy.size(3), cur_stream(x));
   return dx;
 }
 
@@ -788,7 +801,7 @@ at::Tensor maxpool2x2_backward(const at::Tensor& x_in, const at::Tensor& dy_in) 
 TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("up2x_cat_forward(Tensor x, Tensor skip) -> Tensor");
   m.def("up2x_backward(Tensor dy, int c) -> Tensor");
-  m.def("maxpool2x2_forward(Tensor x) -> Tensor");
+  m.def("maxpool2x2_forward(Tensor x, Tensor? add=None) -> Tensor");
   m.def("maxpool2x2_backward(Tensor x, Tensor dy) -> Tensor");
   m.def("avgpool3_forward(Tensor x, int stride, Tensor? add) -> Tensor");
   m.def("avgpool3_backward(Tensor dy, int h, int w, int stride) -> Tensor");

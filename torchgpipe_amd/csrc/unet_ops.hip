@@ -87,6 +87,7 @@ __device__ __forceinline__ int argmax4(float v0, float v1, float v2, float v3, f
 }
 
 __global__ __launch_bounds__(256) void maxpool2x2_fwd_kernel(const float* __restrict__ x,
+                                                             const float* __restrict__ add,
                                                              float* __restrict__ y,
                                                              int64_t planes, int h, int w) {
   const int ho = h / 2, wo = w / 2;
@@ -99,17 +100,19 @@ __global__ __launch_bounds__(256) void maxpool2x2_fwd_kernel(const float* __rest
     const float* p = x + (plane * h + 2 * oy) * static_cast<int64_t>(w) + 2 * ox;
     float m;
     argmax4(p[0], p[1], p[w], p[w + 1], m);
-    y[i] = m;
+    y[i] = add != nullptr ? m + add[i] : m;  // AmoebaNet's cell-node sum folded in
   }
 }
 
 // One thread per 2x2 input block: writes all four input gradients (zeros but the argmax),
 // so every input element is written exactly once (odd trailing rows / columns, which no
-// window covers, are zeroed by the caller's allocation).
+// window covers, are zeroed by the caller's allocation).  dy may be a channel slice of a
+// larger gradient (image stride dy_img, e.g. AmoebaNet's concatenated cell output).
 __global__ __launch_bounds__(256) void maxpool2x2_bwd_kernel(const float* __restrict__ x,
                                                              const float* __restrict__ dy,
                                                              float* __restrict__ dx,
-                                                             int64_t planes, int h, int w) {
+                                                             int64_t planes, int channels,
+                                                             int h, int w, int64_t dy_img) {
   const int ho = h / 2, wo = w / 2;
   const int64_t total = planes * ho * wo;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
@@ -121,7 +124,8 @@ __global__ __launch_bounds__(256) void maxpool2x2_bwd_kernel(const float* __rest
     const float* p = x + base;
     float m;
     const int k = argmax4(p[0], p[1], p[w], p[w + 1], m);
-    const float g = dy[i];
+    const int64_t img = plane / channels;
+    const float g = dy[img * dy_img + (plane - img * channels) * ho * wo + r];
     float* q = dx + base;
     q[0] = k == 0 ? g : 0.f;
     q[1] = k == 1 ? g : 0.f;
@@ -148,20 +152,20 @@ void launch_up2x_backward(const float* dy, float* dx, int64_t n, int c, int h, i
                      h, w, dy_img);
 }
 
-void launch_maxpool2x2_forward(const float* x, float* y, int64_t planes, int h, int w,
-                               hipStream_t stream) {
+void launch_maxpool2x2_forward(const float* x, const float* add, float* y, int64_t planes, int h,
+                               int w, hipStream_t stream) {
   const int64_t total = planes * (h / 2) * static_cast<int64_t>(w / 2);
   if (total == 0) return;
-  hipLaunchKernelGGL(maxpool2x2_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, stream, x, y,
-                     planes, h, w);
+  hipLaunchKernelGGL(maxpool2x2_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, stream, x, add,
+                     y, planes, h, w);
 }
 
 void launch_maxpool2x2_backward(const float* x, const float* dy, float* dx, int64_t planes,
-                                int h, int w, hipStream_t stream) {
+                                int channels, int h, int w, int64_t dy_img, hipStream_t stream) {
   const int64_t total = planes * (h / 2) * static_cast<int64_t>(w / 2);
   if (total == 0) return;
   hipLaunchKernelGGL(maxpool2x2_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, stream, x, dy,
-                     dx, planes, h, w);
+                     dx, planes, channels, h, w, dy_img);
 }
 
 }  // namespace tgpipe

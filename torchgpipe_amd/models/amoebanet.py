@@ -28,6 +28,7 @@ from torch import Tensor, nn
 
 from torchgpipe_amd.ops.convbn import FusedChain, ReLUConvBN, fusable, relu_conv_bn
 from torchgpipe_amd.ops.pool import AvgPool3x3
+from torchgpipe_amd.ops.unet_ops import MaxPool2x2
 
 __all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS']
 
@@ -44,7 +45,7 @@ class Operation(nn.Module):
     @property
     def takes_add(self) -> bool:
         """Whether ``add`` folds into the module's own last pass (no separate add)."""
-        return isinstance(self.module, (FusedChain, FactorizedReduce, AvgPool3x3))
+        return isinstance(self.module, (FusedChain, FactorizedReduce, AvgPool3x3, MaxPool2x2))
 
     def forward(self, x: Tensor, add: Optional[Tensor] = None) -> Tensor:  # type: ignore[override]
         """``module(x)``, plus ``add`` (folded into a fused op's last pass when it can)."""
@@ -100,7 +101,9 @@ def op_max_pool_3x3(c: int, stride: int) -> Operation:
 
 
 def op_max_pool_2x2(c: int, stride: int) -> Operation:
-    return Operation('max_pool_2x2', nn.MaxPool2d(2, stride=stride, padding=0))
+    # stride 2 (every use in the genotypes) on the index-free HIP kernel (ops/unet_ops.py)
+    pool = MaxPool2x2() if stride == 2 else nn.MaxPool2d(2, stride=stride, padding=0)
+    return Operation('max_pool_2x2', pool)
 
 
 def _bottleneck(c: int, middle: List[nn.Module]) -> nn.Sequential:
@@ -178,6 +181,8 @@ class Stem(nn.Module):
         self.bn = nn.BatchNorm2d(channels)
 
     def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
+        if fusable(x, [self.conv], self.bn):
+            return relu_conv_bn(x, [(self.conv, 0)], self.bn)
         return self.bn(self.conv(self.relu(x)))
 
 

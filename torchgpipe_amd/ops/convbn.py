@@ -53,9 +53,8 @@ Geo = Tuple[int, int, int, int, int, int, int, int]  # kh, kw, sh, sw, ph, pw, o
 
 
 def conv_supported(conv: nn.Conv2d) -> bool:
-    """1×1 / 1×k / k×1, no bias, no groups / dilation, zero padding."""
-    kh, kw = conv.kernel_size
-    return ((kh == 1 or kw == 1) and conv.bias is None and conv.groups == 1
+    """Any kernel and stride; no bias, no groups / dilation, zero padding."""
+    return (conv.bias is None and conv.groups == 1
             and tuple(conv.dilation) == (1, 1) and conv.padding_mode == 'zeros'
             and isinstance(conv.padding, tuple))
 
@@ -172,8 +171,8 @@ class FusedChain(nn.Sequential):
     """A chain of (ReLU, Conv2d, BatchNorm2d) triplets run as fused ops.
 
     Children are the plain modules (the reference's state-dict keys); any triplet
-    whose convolution the GEMM kernels do not cover (e.g. the stride-2 3×3 of a
-    reduction cell's bottleneck) runs eagerly.  ``add`` is folded into the last
+    the fused op does not cover (biased / grouped / dilated convolutions, eval-mode
+    BatchNorm, CPU tensors) runs eagerly.  ``add`` is folded into the last
     triplet's normalisation pass.
     """
 
@@ -201,9 +200,8 @@ class ReLUConvBN(FusedChain):
 # -- plain convolutions on the same implicit-GEMM kernels --------------------------------
 
 def gemm_conv_eligible(x: Tensor, conv: nn.Conv2d) -> bool:
-    """Convolutions the implicit-GEMM kernels take without BatchNorm: any kernel at
-    stride 1 or a strided 1x1, no bias / groups / dilation, fp32 on the GPU."""
-    kh, kw = conv.kernel_size
+    """Convolutions the implicit-GEMM kernels take without BatchNorm: any kernel and
+    stride, no bias / groups / dilation, fp32 on the GPU."""
     limit = (1 << 31) - 64  # 32-bit buffer offsets of the kernels
     out_numel = x.numel() // max(1, x.shape[1]) * conv.out_channels if x.dim() == 4 else 0
     return (_ENABLED and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
@@ -211,8 +209,7 @@ def gemm_conv_eligible(x: Tensor, conv: nn.Conv2d) -> bool:
             and out_numel * 4 < limit
             and conv.weight.dtype == torch.float32 and conv.bias is None and conv.groups == 1
             and tuple(conv.dilation) == (1, 1) and conv.padding_mode == 'zeros'
-            and isinstance(conv.padding, tuple)
-            and (kh * kw == 1 or tuple(conv.stride) == (1, 1)) and _ext.available())
+            and isinstance(conv.padding, tuple) and _ext.available())
 
 
 class _GemmConv(torch.autograd.Function):

@@ -9,7 +9,7 @@
 
 Both fall back to the PyTorch ops off the GPU, for other dtypes and odd shapes.
 """
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -54,23 +54,30 @@ def up2x_cat(x: Tensor, skip: Tensor) -> Tensor:
 
 class _MaxPool2x2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x: Tensor) -> Tensor:  # type: ignore[override]
+    def forward(ctx, x: Tensor, add: Optional[Tensor]) -> Tensor:  # type: ignore[override]
         ctx.save_for_backward(x)
-        return _ext.require(x).maxpool2x2_forward(x)
+        ctx.has_add = add is not None
+        return _ext.require(x).maxpool2x2_forward(x, add)
 
     @staticmethod
-    def backward(ctx, dy: Tensor) -> Tensor:  # type: ignore[override]
+    def backward(ctx, dy: Tensor):  # type: ignore[override]
         (x,) = ctx.saved_tensors
-        return _ext.require(dy).maxpool2x2_backward(x, dy)
+        return _ext.require(dy).maxpool2x2_backward(x, dy), dy if ctx.has_add else None
 
 
 class MaxPool2x2(nn.MaxPool2d):
-    """``nn.MaxPool2d(2, stride=2)`` (floor mode, no padding / dilation / indices)."""
+    """``nn.MaxPool2d(2, stride=2)`` (floor mode, no padding / dilation / indices).
+
+    ``forward(x, add)`` returns ``pool(x) + add`` in the same pass (AmoebaNet's cell-node
+    sums, ``models/amoebanet.py``); the backward reads a channel-sliced gradient in place.
+    """
 
     def __init__(self) -> None:
         super().__init__(2, stride=2)
 
-    def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
-        if _fusable(x) and not self.return_indices and not self.ceil_mode:
-            return _MaxPool2x2.apply(x)
-        return super().forward(x)
+    def forward(self, x: Tensor, add: Optional[Tensor] = None) -> Tensor:  # type: ignore[override]
+        if _fusable(x) and not self.return_indices and not self.ceil_mode and \
+                (add is None or _fusable(add)):
+            return _MaxPool2x2.apply(x, add)
+        out = super().forward(x)
+        return out if add is None else out + add
