@@ -64,6 +64,13 @@ def main() -> None:
         per[n][1] += e - s
     total = sum(v[1] for v in per.values())
     span = ends[-1] - t0
+    # device idle: gaps between the end of everything launched so far and the next start
+    idle, big, horizon = 0, 0, t0
+    for _, s, e in timed:
+        if s > horizon:
+            idle += s - horizon
+            big += (s - horizon) > 50_000
+        horizon = max(horizon, e)
     ordered = sorted(per.items(), key=lambda kv: -kv[1][1])
     if args.csv:
         with open(args.csv, 'w', newline='') as f:
@@ -76,7 +83,9 @@ def main() -> None:
         groups[group_of(n)] += d
     lines = [f'# {args.title}', '',
              f'{steps} timed steps; kernel time {total / 1e6:.1f} ms '
-             f'({total / 1e6 / steps:.1f} ms/step); wall span {span / 1e6 / steps:.1f} ms/step.',
+             f'({total / 1e6 / steps:.1f} ms/step); wall span {span / 1e6 / steps:.1f} ms/step; '
+             f'device idle {idle / 1e6 / steps:.1f} ms/step ({big / steps:.0f} gaps > 50 us '
+             f'per step).',
              '', '| group | ms/step | share |', '|---|---:|---:|']
     for g, d in sorted(groups.items(), key=lambda kv: -kv[1]):
         lines.append(f'| {g} | {d / 1e6 / steps:.1f} | {100 * d / total:.1f}% |')
