@@ -53,12 +53,19 @@ def main() -> None:
         opt.zero_grad(set_to_none=True)
         torch.cuda.synchronize()
 
+    from torchgpipe_amd.ops import _ext
+    before = set(_ext.require().conv_gemm_plans_export().splitlines())
+    print(f'plans loaded {len(before)}', flush=True)
     prof = cProfile.Profile()
     t1 = time.time()
     prof.enable()
     step()
     prof.disable()
     print(f'step 1 {time.time() - t1:.2f}s', flush=True)
+    new = sorted(set(_ext.require().conv_gemm_plans_export().splitlines()) - before)
+    print(f'plans tuned in step 1: {len(new)}', flush=True)
+    for line in new:
+        print('  new plan:', line)
     t2 = time.time()
     step()
     print(f'step 2 {time.time() - t2:.2f}s', flush=True)

@@ -35,8 +35,11 @@ def main() -> None:
     p = argparse.ArgumentParser(description=__doc__)
     p.add_argument('--out', required=True)
     p.add_argument('--models', default='amoebanet,unet')
+    p.add_argument('--merge', action='store_true',
+                   help='seed from the shipped table and measure only the shapes it lacks')
     args = p.parse_args()
-    os.environ['TGPIPE_CG_DB'] = '0'  # measure, do not seed from the shipped table
+    if not args.merge:
+        os.environ['TGPIPE_CG_DB'] = '0'  # measure, do not seed from the shipped table
     from torchgpipe_amd.models import amoebanetd, unet
     from torchgpipe_amd.ops import _ext
     _ext.require()

@@ -29,6 +29,8 @@ def main() -> None:
     p.add_argument('--variants', type=int, nargs='+', default=[0, 2])
     p.add_argument('--iters', type=int, default=20)
     p.add_argument('--out', default=None)
+    p.add_argument('--splits', type=int, nargs='+', default=[0],
+                   help='split-K counts to time per variant (0 = the planner\'s choice)')
     p.add_argument('--shape', type=int, nargs=4, action='append', default=None,
                    help='N C K H (repeatable; default: the built-in table)')
     a = p.parse_args()
@@ -42,13 +44,13 @@ def main() -> None:
         u4 = ops.wino4_weight(w, False) if max(a.variants) >= 4 else None
         ref = F.conv2d(x.double(), w.double(), padding=1)
         row = {'shape': [n, c, k, h]}
-        for v in a.variants:
+        for v, sp in [(v, sp) for v in a.variants for sp in a.splits]:
             # variants >= 4 = Winograd F(4x4,3x3) (winograd_f4.hip; 8-10 are timing
             # ablations with wrong results), the rest F(2x2,3x3)
             def run():  # noqa: E306
                 if v >= 4:
-                    return ops.wino4_conv(x, u4, None, k, v, 0)
-                return ops.wino_conv(x, u, None, k, v, 0)
+                    return ops.wino4_conv(x, u4, None, k, v, sp)
+                return ops.wino_conv(x, u, None, k, v, sp)
             y = run()
             err = ((y.double() - ref).abs().max() / (ref.abs().max() + 1e-12)).item()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -61,7 +63,7 @@ def main() -> None:
             e.synchronize()
             ms = s.elapsed_time(e) / a.iters
             tf = 2.0 * n * k * c * 9 * h * h / ms / 1e9
-            row[f'v{v}'] = {'ms': round(ms, 4), 'direct_tflops': round(tf, 1), 'rel_err': err}
+            row[f'v{v}' + (f's{sp}' if sp else '')] = {'ms': round(ms, 4), 'direct_tflops': round(tf, 1), 'rel_err': err}
         rows.append(row)
         print(json.dumps(row), flush=True)
     if a.out:
