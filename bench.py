@@ -99,6 +99,10 @@ def parse() -> argparse.Namespace:
                    help='tiny model of the same family (CI smoke test of this script only)')
     p.add_argument('--channels-last', action='store_true',
                    help='NHWC activations and weights (MIOpen NHWC kernels; AmoebaNet)')
+    p.add_argument('--graph', action='store_true',
+                   help='one-GPU runs: capture the whole step (forward, backward, SGD) into a '
+                        'hipGraph after the warm-up and replay it (RNG-free models only: '
+                        'AmoebaNet; parallel/graph.py)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -216,7 +220,17 @@ def main() -> None:
         from torchgpipe_amd.parallel.stage import signature_of
         signature = signature_of(torch.empty(batch, *in_shape, device='meta'))
 
+        graph = None
+        if args.graph:
+            if world != 1:
+                raise SystemExit('--graph captures one-rank runs only')
+            from torchgpipe_amd.parallel import StepGraph
+            graph = StepGraph(stage, loss_fn, optimizer, warmup=max(1, args.warmup - 1))
+
         def step() -> None:
+            if graph is not None:
+                graph.step(x, target)  # type: ignore[arg-type]
+                return
             stage.train_step(x, target, loss_fn, signature=signature)
             optimizer.step()
             optimizer.zero_grad(set_to_none=True)
@@ -233,6 +247,9 @@ def main() -> None:
             if rank == 0:
                 print(f'[bench] {tag} warmup step {k + 1}/{args.warmup} done at '
                       f'{time.time() - t0:.1f}s', file=sys.stderr, flush=True)
+        while graph is not None and not graph.captured:  # the capture stays untimed
+            step()
+            sync()
         warm_s = time.time() - t0
 
         sync()
@@ -312,6 +329,7 @@ def main() -> None:
                 'warmup_s': round(warm_s, 1),
                 'first_step_s': round(main_run['first_step_s'], 2),
                 'timeout_s': args.timeout,
+                'hipgraph': bool(args.graph),
             },
             'tuned': tuned,
         }), file=result_out, flush=True)

@@ -30,7 +30,7 @@ def main() -> None:
     p.add_argument('--iters', type=int, default=20)
     p.add_argument('--out', default=None)
     p.add_argument('--splits', type=int, nargs='+', default=[0],
-                   help='split-K counts to time per variant (0 = the planner\'s choice)')
+                   help='split-K counts to time per variant (0: the planner picks)')
     p.add_argument('--shape', type=int, nargs=4, action='append', default=None,
                    help='N C K H (repeatable; default: the built-in table)')
     a = p.parse_args()
@@ -63,7 +63,8 @@ def main() -> None:
             e.synchronize()
             ms = s.elapsed_time(e) / a.iters
             tf = 2.0 * n * k * c * 9 * h * h / ms / 1e9
-            row[f'v{v}' + (f's{sp}' if sp else '')] = {'ms': round(ms, 4), 'direct_tflops': round(tf, 1), 'rel_err': err}
+            tag = f'v{v}' + (f's{sp}' if sp else '')
+            row[tag] = {'ms': round(ms, 4), 'direct_tflops': round(tf, 1), 'rel_err': err}
         rows.append(row)
         print(json.dumps(row), flush=True)
     if a.out:

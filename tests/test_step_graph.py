@@ -1,0 +1,93 @@
+"""Whole-step hipGraph capture (torchgpipe_amd/parallel/graph.py)."""
+import copy
+
+import pytest
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from torchgpipe_amd.ops.dropout import Dropout2d
+from torchgpipe_amd.parallel import PipelineStage, StepGraph
+from torchgpipe_amd.parallel.graph import rng_modules
+from torchgpipe_amd.utils import rng
+
+
+def _mlp() -> nn.Sequential:
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Linear(8, 16), nn.ReLU(), nn.Linear(16, 16), nn.ReLU(),
+                         nn.Linear(16, 4))
+
+
+def test_refuses_partitions_with_random_ops():
+    model = nn.Sequential(nn.Linear(4, 4), nn.Dropout(0.1), nn.Linear(4, 2))
+    stage = PipelineStage(model, [3], chunks=2)
+    with pytest.raises(ValueError, match='random numbers'):
+        StepGraph(stage, F.mse_loss)
+    ours = nn.Sequential(nn.Conv2d(3, 4, 1), Dropout2d(0.2))
+    assert rng_modules(ours) == ['1']
+    # p = 0 draws nothing
+    assert rng_modules(nn.Sequential(nn.Dropout(0.0))) == []
+
+
+def test_needs_a_warmup_step():
+    stage = PipelineStage(_mlp(), [5], chunks=2)
+    with pytest.raises(ValueError, match='warm-up'):
+        StepGraph(stage, F.mse_loss, warmup=0)
+
+
+def test_philox_pair_refuses_to_draw_inside_a_capture(monkeypatch):
+    monkeypatch.setattr(torch.cuda, 'is_current_stream_capturing', lambda: True)
+    with pytest.raises(RuntimeError, match='hipGraph capture'):
+        rng.philox_pair(torch.device('cuda', 0), 16)
+
+
+def test_cpu_steps_match_eager_training():
+    a, b = _mlp(), _mlp()
+    sa = PipelineStage(a, [5], chunks=4, checkpoint='except_last')
+    sb = PipelineStage(b, [5], chunks=4, checkpoint='except_last')
+    oa = torch.optim.SGD(sa.parameters(), lr=0.1)
+    ob = torch.optim.SGD(sb.parameters(), lr=0.1)
+    graph = StepGraph(sb, F.mse_loss, ob, warmup=1)
+    torch.manual_seed(1)
+    for _ in range(4):
+        x, y = torch.randn(16, 8), torch.randn(16, 4)
+        la = sa.train_step(x, y, F.mse_loss)
+        oa.step()
+        oa.zero_grad(set_to_none=True)
+        lb = graph.step(x, y)
+        assert torch.equal(la, lb)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa, pb)
+    assert not graph.captured  # nothing to capture on a CPU stage
+
+
+@pytest.mark.gpu
+def test_graph_replays_match_eager_steps_on_gpu():
+    """Tiny AmoebaNet-D (fused ReLU-Conv-BN ops, pools, BatchNorm running statistics,
+    checkpoint recomputation): eager steps vs warm-up + capture + replays, with a new
+    input every step (copied into the static buffers)."""
+    from torchgpipe_amd.models import amoebanetd
+    dev = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    base = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
+    a, b = copy.deepcopy(base), copy.deepcopy(base)
+    sa = PipelineStage(a, [len(a)], device=dev, chunks=4, checkpoint='except_last')
+    sb = PipelineStage(b, [len(b)], device=dev, chunks=4, checkpoint='except_last')
+    oa = torch.optim.SGD(sa.parameters(), lr=0.05)
+    ob = torch.optim.SGD(sb.parameters(), lr=0.05)
+    graph = StepGraph(sb, F.cross_entropy, ob, warmup=2)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    for k in range(6):
+        x = torch.rand(8, 3, 224, 224, device=dev, generator=gen)
+        y = torch.randint(10, (8,), device=dev, generator=gen)
+        la = sa.train_step(x, y, F.cross_entropy)
+        oa.step()
+        oa.zero_grad(set_to_none=True)
+        lb = graph.step(x, y)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(lb, la, rtol=1e-5, atol=1e-6, msg=f'loss of step {k}')
+    assert graph.captured
+    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pb, pa, rtol=1e-4, atol=1e-5, msg=name)
+    for (name, ba), bb in zip(a.named_buffers(), b.buffers()):
+        torch.testing.assert_close(bb, ba, rtol=1e-4, atol=1e-5, msg=name)

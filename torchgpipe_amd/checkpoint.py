@@ -105,12 +105,14 @@ class RNGSnapshot:
         self.device = device
         self.cpu_state = torch.get_rng_state()
         self.gpu_state: Optional[Tensor] = None
-        if device.type == 'cuda':
+        # Inside a hipGraph capture (parallel/graph.py, RNG-free partitions only) the
+        # device generator state can be neither read nor restored: skip it.
+        if device.type == 'cuda' and not torch.cuda.is_current_stream_capturing():
             self.gpu_state = torch.cuda.get_rng_state(device)
 
     @contextmanager
     def restored(self) -> Generator[None, None, None]:
-        devices = [self.device] if self.device.type == 'cuda' else []
+        devices = [self.device] if self.gpu_state is not None else []
         with torch.random.fork_rng(devices):
             torch.set_rng_state(self.cpu_state)
             if self.gpu_state is not None:

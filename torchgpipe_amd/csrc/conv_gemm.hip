@@ -29,8 +29,8 @@
 //
 // LDS images:
 //   K-major operand (k contiguous in HBM: weights, dZ in weight-grad, X in weight-grad)
-//     [BK/4][rows][4] with the 4 k of a quad stored (0, 2, 1, 3): lane half h of a
-//     32x32x2 MFMA pair (k-steps 2g, 2g+1) reads its two operands as one ds_read_b64.
+//     [BK/4][2][rows][2]: k quad g split into the pairs (k0, k2) / (k1, k3) that lane half
+//     h of a 32x32x2 MFMA pair (k-steps 2g, 2g+1) reads as one conflict-free ds_read_b64.
 //   N-major operand (pixels contiguous: X in forward, dZ in backward-data)
 //     [BK][cols + 32]: the two lane halves read rows k and k+1, 32 banks apart.
 // Out-of-range taps (padding, stride holes, tails) are raw buffer loads at an offset
@@ -129,9 +129,15 @@ struct Cfg {
 
 // ---- operand staging -----------------------------------------------------------------------
 // K-major operand: quad index i of thread t -> row r = (t >> 3) + (THREADS / 8) * i,
-// k quad q = t & 7, stored at slot [q][r ^ 2q]: the 16 lanes of a ds_write_b128 pass
-// (2 rows x 8 quads) hit 16 distinct 16-byte bank groups, and the 32 consecutive rows an
-// MFMA fragment read covers stay a permutation of one aligned 32-row block.
+// k quad q = t & 7 (k = 4q .. 4q+3).  The quad is split into the two k pairs the two lane
+// halves of a 32x32x2 MFMA pair consume -- half 0 = (k0, k2), half 1 = (k1, k3) -- each
+// stored as 8 bytes at slot [q][half][r ^ 2q]:
+//   * an MFMA fragment read (ds_read_b64, lane groups 0-31 / 32-63) is 32 consecutive
+//     rows of one half: 256 contiguous bytes, all 64 banks, no conflict (a [q][r][4]
+//     image puts rows r and r + 16 of a 16-byte-slot layout on the same banks: 2-way);
+//   * the two ds_write_b64 per quad (16-lane groups: 8 quads x 2 rows) land on 16
+//     distinct 8-byte bank pairs thanks to the r ^ 2q swizzle, which keeps every aligned
+//     32-row block a permutation of itself.
 __device__ __forceinline__ int kswz(int row, int q) { return row ^ (2 * q); }
 
 template <int ROWS, int Q, int THREADS>
@@ -140,8 +146,9 @@ __device__ __forceinline__ void store_kmajor(float* img, const floatx4 (&v)[Q], 
 #pragma unroll
   for (int i = 0; i < Q; ++i) {
     const int row = (tid >> 3) + (THREADS / 8) * i;
-    *reinterpret_cast<floatx4*>(img + (q * ROWS + kswz(row, q)) * 4) =
-        floatx4{v[i][0], v[i][2], v[i][1], v[i][3]};
+    float* base = img + ((2 * q) * ROWS + kswz(row, q)) * 2;
+    *reinterpret_cast<floatx2*>(base) = floatx2{v[i][0], v[i][2]};
+    *reinterpret_cast<floatx2*>(base + 2 * ROWS) = floatx2{v[i][1], v[i][3]};
   }
 }
 
@@ -173,12 +180,12 @@ __device__ __forceinline__ void mfma_stage(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG
 #pragma unroll
     for (int i = 0; i < WM; ++i)
       a[i] = *reinterpret_cast<const floatx2*>(
-          aimg + (g * C::BM + kswz(wm * 32 * WM + i * 32 + l32, g)) * 4 + 2 * h);
+          aimg + ((2 * g + h) * C::BM + kswz(wm * 32 * WM + i * 32 + l32, g)) * 2);
 #pragma unroll
     for (int j = 0; j < WN; ++j) {
       if constexpr (kBKMajor) {
         b[j] = *reinterpret_cast<const floatx2*>(
-            bimg + (g * C::BN + kswz(wn * 32 * WN + j * 32 + l32, g)) * 4 + 2 * h);
+            bimg + ((2 * g + h) * C::BN + kswz(wn * 32 * WN + j * 32 + l32, g)) * 2);
       } else {
         const int col = wn * 32 * WN + j * 32 + l32;
         b[j] = floatx2{bimg[(4 * g + h) * C::kBStrideN + col],

@@ -85,15 +85,17 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
   }
   if (!tune) return heuristic;
   const hipStream_t stream = cur_stream(like);
-  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &capture) != hipSuccess ||
-      capture != hipStreamCaptureStatusNone)
-    return heuristic;
   const PlanKey key{mode, g.n, g.ci, g.h, g.w, g.co, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.oh,
                     g.ow, g.co_total};
   std::lock_guard<std::mutex> lock(plan_mutex);
   auto hit = plan_cache.find(key);
   if (hit != plan_cache.end()) return hit->second;
+  // A stream capture (hipGraph) records launches, it cannot time them: a shape first met
+  // inside a capture runs the heuristic plan (warm-up steps before capturing tune it).
+  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &capture) != hipSuccess ||
+      capture != hipStreamCaptureStatusNone)
+    return heuristic;
   at::Tensor scratch;
   if (accumulate) {
     scratch = at::empty({out_numel}, like.options());

@@ -96,6 +96,11 @@ def philox_pair(device: torch.device, increment: int) -> SeedOffset:
     # Round up to a multiple of 4: one Philox call yields 4 x 32-bit values.
     increment = (int(increment) + 3) // 4 * 4
     tape = _state.tape
+    if device.type == 'cuda' and torch.cuda.is_current_stream_capturing():
+        # The pair becomes a constant of the captured kernels: every replay of the graph
+        # would draw the same mask (parallel/graph.py refuses such partitions up front).
+        raise RuntimeError('a framework RNG op drew random numbers inside a hipGraph '
+                           'capture; its replays would repeat the same mask every step')
     if tape is not None and tape.mode == 'replay':
         if tape.cursor >= len(tape.entries):
             raise RuntimeError('RNG tape exhausted: recomputation drew more random '
