@@ -103,6 +103,8 @@ def parse() -> argparse.Namespace:
                    help='one-GPU runs: capture the whole step (forward, backward, SGD) into a '
                         'hipGraph after the warm-up and replay it (RNG-free models only: '
                         'AmoebaNet; parallel/graph.py)')
+    p.add_argument('--cell-streams', action='store_true',
+                   help="AmoebaNet: run each cell's independent nodes on two HIP streams")
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -204,6 +206,9 @@ def main() -> None:
                               checkpoint=checkpoint, timeout=args.timeout)
         if args.channels_last:
             stage.partition.to(memory_format=torch.channels_last)
+        if args.cell_streams and args.model == 'amoebanet':
+            from torchgpipe_amd.models.amoebanet import set_cell_streams
+            set_cell_streams(stage.partition, True)
         optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
 
         gen = torch.Generator(device=device).manual_seed(0)
@@ -330,6 +335,7 @@ def main() -> None:
                 'first_step_s': round(main_run['first_step_s'], 2),
                 'timeout_s': args.timeout,
                 'hipgraph': bool(args.graph),
+                'cell_streams': bool(args.cell_streams and args.model == 'amoebanet'),
             },
             'tuned': tuned,
         }), file=result_out, flush=True)

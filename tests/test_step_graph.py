@@ -91,3 +91,43 @@ def test_graph_replays_match_eager_steps_on_gpu():
         torch.testing.assert_close(pb, pa, rtol=1e-4, atol=1e-5, msg=name)
     for (name, ba), bb in zip(a.named_buffers(), b.buffers()):
         torch.testing.assert_close(bb, ba, rtol=1e-4, atol=1e-5, msg=name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('graphed', [False, True])
+def test_two_stream_cells_match_one_stream(graphed):
+    """AmoebaNet cells with their independent nodes on two HIP streams (eager, and captured
+    into a hipGraph) train exactly like the one-stream model: losses, SGD-updated
+    parameters (whose gradients the fused ops on the side stream write themselves) and
+    BatchNorm buffers over several steps."""
+    from torchgpipe_amd.models import amoebanetd
+    from torchgpipe_amd.models.amoebanet import set_cell_streams
+    dev = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    base = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
+    a, b = copy.deepcopy(base), copy.deepcopy(base)
+    set_cell_streams(b, True)
+    sa = PipelineStage(a, [len(a)], device=dev, chunks=4, checkpoint='except_last')
+    sb = PipelineStage(b, [len(b)], device=dev, chunks=4, checkpoint='except_last')
+    oa = torch.optim.SGD(sa.parameters(), lr=0.05)
+    ob = torch.optim.SGD(sb.parameters(), lr=0.05)
+    graph = StepGraph(sb, F.cross_entropy, ob, warmup=2) if graphed else None
+    gen = torch.Generator(device=dev).manual_seed(5)
+    for k in range(5):
+        x = torch.rand(8, 3, 224, 224, device=dev, generator=gen)
+        y = torch.randint(10, (8,), device=dev, generator=gen)
+        la = sa.train_step(x, y, F.cross_entropy)
+        oa.step()
+        oa.zero_grad(set_to_none=True)
+        if graph is not None:
+            lb = graph.step(x, y)
+        else:
+            lb = sb.train_step(x, y, F.cross_entropy)
+            ob.step()
+            ob.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(lb, la, rtol=1e-5, atol=1e-6, msg=f'loss of step {k}')
+    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pb, pa, rtol=1e-4, atol=1e-5, msg=name)
+    for (name, ba), bb in zip(a.named_buffers(), b.buffers()):
+        torch.testing.assert_close(bb, ba, rtol=1e-4, atol=1e-5, msg=name)

@@ -21,7 +21,7 @@ keep the reference's children, so parameters and state-dict keys are the same
 as the plain model (``fused=False``), which also serves as the numerics oracle.
 """
 from collections import OrderedDict
-from typing import Callable, Iterator, List, Optional, Tuple, Union
+from typing import Callable, Dict, Iterator, List, Optional, Tuple, Union
 
 import torch
 from torch import Tensor, nn
@@ -30,7 +30,46 @@ from torchgpipe_amd.ops.convbn import FusedChain, ReLUConvBN, fusable, relu_conv
 from torchgpipe_amd.ops.pool import AvgPool3x3
 from torchgpipe_amd.ops.unet_ops import MaxPool2x2
 
-__all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS']
+__all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS', 'set_cell_streams']
+
+_SIDE_STREAMS: Dict[torch.device, torch.cuda.Stream] = {}
+
+
+def _side_stream(device: torch.device) -> torch.cuda.Stream:
+    stream = _SIDE_STREAMS.get(device)
+    if stream is None:
+        stream = _SIDE_STREAMS[device] = torch.cuda.Stream(device)
+    return stream
+
+
+class _JoinSideInBackward(torch.autograd.Function):
+    """Identity on the cell inputs whose backward makes the current stream wait for the side
+    stream: the fused ops on the side stream write ``param.grad`` themselves (gradient-
+    accumulation fusion), which autograd's end-of-backward stream sync does not see.  Every
+    op of the cell lies upstream of the inputs' gradients, so this backward runs after all
+    of them have been issued."""
+
+    @staticmethod
+    def forward(ctx, stream: torch.cuda.Stream, *xs: Tensor):  # type: ignore[override]
+        ctx.stream = stream
+        return tuple(x.view_as(x) for x in xs)
+
+    @staticmethod
+    def backward(ctx, *grads: Tensor):  # type: ignore[override]
+        torch.cuda.current_stream().wait_stream(ctx.stream)
+        return (None,) + grads
+
+
+def _op_cost(op: 'Operation') -> float:
+    """Rough relative device time of a cell operation (number of convolutions)."""
+    m = op.module
+    if isinstance(m, FusedChain):
+        return float(sum(isinstance(c, nn.Conv2d) for c in m.children()))
+    if isinstance(m, FactorizedReduce):
+        return 1.0
+    if isinstance(m, nn.Identity):
+        return 0.0
+    return 0.5  # pools
 
 
 class Operation(nn.Module):
@@ -202,23 +241,107 @@ class Cell(nn.Module):
         self.indices = [i for i, _ in genotype]
         self.operations = nn.ModuleList(
             factory(c, 2 if reduction and i < 2 else 1) for i, factory in genotype)
+        self.streams = False
+        self._plan = self._stream_plan()
+
+    def _stream_plan(self) -> List[int]:
+        """Stream (0 = current, 1 = side) of every node for the two-stream schedule.
+
+        The two input reductions go to different streams; every later node goes to the
+        less loaded of its inputs' streams (load = convolutions already placed there).
+        """
+        plan, load = [0, 1], [1.0, 1.0]
+        ops = list(self.operations)
+        for k in range(0, len(ops), 2):
+            ia, ib = self.indices[k], self.indices[k + 1]
+            choices = {plan[ia], plan[ib]}
+            s = min(choices, key=lambda c: load[c])
+            load[s] += _op_cost(ops[k]) + _op_cost(ops[k + 1])
+            plan.append(s)
+        return plan
 
     def extra_repr(self) -> str:
         return f'indices: {self.indices}'
+
+    def _node(self, k: int, nodes: List[Tensor]) -> Tensor:
+        # node = left + right: run the operation that cannot fold a sum first and hand
+        # its output to the other one's last pass
+        ops = self.operations
+        a, b = (k, k + 1) if ops[k + 1].takes_add or not ops[k].takes_add else (k + 1, k)
+        first = ops[a](nodes[self.indices[a]])
+        return ops[b](nodes[self.indices[b]], add=first)
 
     def forward(self, states: Union[Tensor, Tuple[Tensor, Tensor]]  # type: ignore[override]
                 ) -> Tuple[Tensor, Tensor]:
         s1, s2 = states if isinstance(states, tuple) else (states, states)
         skip = s1
+        if self.streams and s1.is_cuda:
+            return self._forward_two_streams(s1, s2), skip
         nodes = [self.reduce1(s1), self.reduce2(s2)]
-        ops = list(self.operations)
-        for k in range(0, len(ops), 2):
-            # node = left + right: run the operation that cannot fold a sum first and
-            # hand its output to the other one's last pass
-            a, b = (k, k + 1) if ops[k + 1].takes_add or not ops[k].takes_add else (k + 1, k)
-            first = ops[a](nodes[self.indices[a]])
-            nodes.append(ops[b](nodes[self.indices[b]], add=first))
+        for k in range(0, len(self.operations), 2):
+            nodes.append(self._node(k, nodes))
         return torch.cat([nodes[i] for i in self.concat], dim=1), skip
+
+    def _forward_two_streams(self, s1: Tensor, s2: Tensor) -> Tensor:
+        """The cell's independent nodes on two HIP streams (``set_cell_streams``).
+
+        Node k runs on stream ``self._plan[k]`` after waiting on the events of inputs
+        produced on the other stream; tensors crossing streams are ``record_stream``-ed so
+        the caching allocator does not hand their memory out early.  Autograd runs each
+        backward op on its forward op's stream.  Inside a hipGraph capture
+        (``parallel/graph.py``) the side stream forks from and joins the capturing stream,
+        so the graph keeps the two branches as parallel paths.
+        """
+        streams = [torch.cuda.current_stream(s1.device), _side_stream(s1.device)]
+        if torch.is_grad_enabled() and (s1.requires_grad or s2.requires_grad):
+            if s1 is s2:
+                s1 = s2 = _JoinSideInBackward.apply(streams[1], s1)[0]
+            else:
+                s1, s2 = _JoinSideInBackward.apply(streams[1], s1, s2)
+        streams[1].wait_stream(streams[0])
+        events: List[Optional[torch.cuda.Event]] = []
+        nodes: List[Tensor] = []
+
+        def run(k: int, fn: Callable[[], Tensor], inputs: List[int],
+                external: List[Tensor]) -> None:
+            s = self._plan[k]
+            stream = streams[s]
+            for i in inputs:
+                if self._plan[i] != s:
+                    ev = events[i]
+                    assert ev is not None
+                    stream.wait_event(ev)
+                    nodes[i].record_stream(stream)
+            if s == 1:
+                for t in external:
+                    t.record_stream(stream)
+            with torch.cuda.stream(stream):
+                out = fn()
+            ev = None
+            if any(self._plan[j] != s for j in range(k + 1, len(self._plan))) or \
+                    (s == 1 and k in self.concat):
+                ev = torch.cuda.Event()
+                ev.record(stream)
+            nodes.append(out)
+            events.append(ev)
+
+        run(0, lambda: self.reduce1(s1), [], [s1])
+        run(1, lambda: self.reduce2(s2), [], [s2])
+        for k in range(0, len(self.operations), 2):
+            ins = [self.indices[k], self.indices[k + 1]]
+            run(len(nodes), lambda k=k: self._node(k, nodes), ins, [])
+        streams[0].wait_stream(streams[1])
+        for i in self.concat:
+            if self._plan[i] == 1:
+                nodes[i].record_stream(streams[0])
+        return torch.cat([nodes[i] for i in self.concat], dim=1)
+
+
+def set_cell_streams(model: nn.Module, enabled: bool = True) -> None:
+    """Run every AmoebaNet cell's independent nodes on two HIP streams (GPU inputs)."""
+    for m in model.modules():
+        if isinstance(m, Cell):
+            m.streams = enabled
 
 
 def amoebanetd(num_classes: int = 10, num_layers: int = 4, num_filters: int = 512
