@@ -105,6 +105,9 @@ def parse() -> argparse.Namespace:
                         'AmoebaNet; parallel/graph.py)')
     p.add_argument('--cell-streams', action='store_true',
                    help="AmoebaNet: run each cell's independent nodes on two HIP streams")
+    p.add_argument('--overlap-recompute', action='store_true',
+                   help="recompute the next micro-batch on a second stream during this one's "
+                        'backward (PipelineStage(overlap_recompute=True))')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -203,7 +206,8 @@ def main() -> None:
     def measure(balance: list, tag: str) -> dict:
         """Build the stage for ``balance``, warm up, time ``--steps`` full SGD steps."""
         stage = PipelineStage(build_model(), balance, device=device, chunks=chunks,
-                              checkpoint=checkpoint, timeout=args.timeout)
+                              checkpoint=checkpoint, timeout=args.timeout,
+                              overlap_recompute=args.overlap_recompute)
         if args.channels_last:
             stage.partition.to(memory_format=torch.channels_last)
         if args.cell_streams and args.model == 'amoebanet':
@@ -336,6 +340,7 @@ def main() -> None:
                 'timeout_s': args.timeout,
                 'hipgraph': bool(args.graph),
                 'cell_streams': bool(args.cell_streams and args.model == 'amoebanet'),
+                'overlap_recompute': bool(args.overlap_recompute),
             },
             'tuned': tuned,
         }), file=result_out, flush=True)

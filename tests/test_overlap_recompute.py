@@ -1,0 +1,73 @@
+"""PipelineStage(overlap_recompute=True): the next micro-batch is recomputed on a second
+stream while the current one runs backward (torchgpipe_amd/parallel/stage.py)."""
+import copy
+
+import pytest
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from torchgpipe_amd.parallel import PipelineStage
+
+
+def test_cpu_stage_ignores_the_option():
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(4, 8), nn.ReLU(), nn.Linear(8, 2))
+    a, b = copy.deepcopy(model), copy.deepcopy(model)
+    sa = PipelineStage(a, [3], chunks=4, checkpoint='always')
+    sb = PipelineStage(b, [3], chunks=4, checkpoint='always', overlap_recompute=True)
+    x, y = torch.randn(8, 4), torch.randn(8, 2)
+    la = sa.train_step(x, y, F.mse_loss)
+    lb = sb.train_step(x, y, F.mse_loss)
+    assert torch.equal(la, lb)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa.grad, pb.grad)
+
+
+def _close_grads(a: nn.Module, b: nn.Module) -> None:
+    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert pb.grad is not None, name
+        scale = pa.grad.abs().max().item() + 1e-12
+        torch.testing.assert_close(pb.grad, pa.grad, rtol=1e-4, atol=1e-5 * scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('model_name,checkpoint', [('unet', 'except_last'),
+                                                   ('unet', 'always'),
+                                                   ('amoebanet', 'except_last')])
+def test_overlapped_recompute_matches_inline(model_name, checkpoint):
+    """Same losses and gradients with the recomputation on two lanes as inline, over three
+    steps (U-Net: Philox dropout replayed from the tape on the lane; AmoebaNet: fused
+    ops writing .grad from the lanes)."""
+    from torchgpipe_amd.models import amoebanetd, unet
+    dev = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    if model_name == 'unet':
+        base = unet(depth=3, num_convs=2, base_channels=16)
+        shape, classes = (3, 64, 64), None
+    else:
+        base = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
+        shape, classes = (3, 224, 224), 10
+    a, b = copy.deepcopy(base), copy.deepcopy(base)
+    sa = PipelineStage(a, [len(a)], device=dev, chunks=4, checkpoint=checkpoint)
+    sb = PipelineStage(b, [len(b)], device=dev, chunks=4, checkpoint=checkpoint,
+                       overlap_recompute=True)
+    gen = torch.Generator(device=dev).manual_seed(7)
+    for _ in range(3):
+        x = torch.rand(8, *shape, device=dev, generator=gen)
+        if classes is None:
+            y = torch.rand(8, 1, 64, 64, device=dev, generator=gen)
+            loss_fn = F.binary_cross_entropy_with_logits
+        else:
+            y = torch.randint(classes, (8,), device=dev, generator=gen)
+            loss_fn = F.cross_entropy
+        for p in list(a.parameters()) + list(b.parameters()):
+            p.grad = None
+        # the same Philox pairs for both models' dropout
+        state = torch.cuda.get_rng_state(dev)
+        la = sa.train_step(x, y, loss_fn)
+        torch.cuda.set_rng_state(state, dev)
+        lb = sb.train_step(x, y, loss_fn)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(lb, la, rtol=1e-5, atol=1e-6)
+        _close_grads(a, b)

@@ -117,7 +117,7 @@ class _RemoteSkipTracker(SkipTracker):
 class _Cell:
     """Bookkeeping of one micro-batch on this rank."""
 
-    __slots__ = ('index', 'inputs', 'outputs', 'out_atomic', 'chk', 'n_act_out')
+    __slots__ = ('index', 'inputs', 'outputs', 'out_atomic', 'chk', 'n_act_out', 'lane')
 
     def __init__(self, index: int) -> None:
         self.index = index
@@ -126,6 +126,7 @@ class _Cell:
         self.out_atomic = True
         self.chk: Optional[Checkpointing] = None
         self.n_act_out = 0
+        self.lane: Optional[torch.cuda.Stream] = None  # stream it was recomputed on
 
 
 class PipelineStage:
@@ -165,7 +166,8 @@ class PipelineStage:
                  deferred_batch_norm: bool = False, pack: bool = True,
                  links: Optional[bool] = None,
                  materialize: Optional[Callable[[nn.Module], None]] = None,
-                 timeout: Optional[float] = None) -> None:
+                 timeout: Optional[float] = None,
+                 overlap_recompute: bool = False) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
         if checkpoint not in ('always', 'except_last', 'never'):
@@ -242,6 +244,8 @@ class PipelineStage:
                        timeout=timeout)
 
         self._cells: List[_Cell] = []
+        self.overlap_recompute = overlap_recompute
+        self._lanes: Optional[List[torch.cuda.Stream]] = None
         self._sig: Optional[Signature] = None
         self._m = 0
         if distributed and self.n > 1:
@@ -494,7 +498,11 @@ class PipelineStage:
         prev = self.ranks[self.rank - 1] if self.rank > 0 else None
         me = self.ranks[self.rank]
 
-        for cell in reversed(self._cells):
+        cells = list(reversed(self._cells))
+        lanes = self._recompute_lanes()
+        main = torch.cuda.current_stream(self.device) if lanes is not None else None
+        prev_lane: Optional[torch.cuda.Stream] = None
+        for j, cell in enumerate(cells):
             i = cell.index
             # 1. post the gradient receives first ...
             grad_msg = None
@@ -506,9 +514,24 @@ class PipelineStage:
                 skip_grad_msgs.append(
                     (dst, self.p2p.recv(peer, self._key('gskip', i, peer, me))))
             # 2. ... then recompute while they are in flight
-            if cell.chk is not None:
-                with trace.range(f'recompute mb{i} stage{self.rank}'):
-                    cell.chk.recompute_now()
+            if lanes is None:
+                if cell.chk is not None:
+                    with trace.range(f'recompute mb{i} stage{self.rank}'):
+                        cell.chk.recompute_now()
+            else:
+                assert main is not None
+                self._recompute_on_lane(cell, lanes[j % 2], main)
+                if cell.lane is not None:
+                    # this backward (its recomputed ops run on cell.lane) must follow the
+                    # previous one: both accumulate into the same .grad buffers
+                    cell.lane.wait_stream(main)
+                    if prev_lane is not None:
+                        cell.lane.wait_stream(prev_lane)
+                    prev_lane = cell.lane
+                if j + 1 < len(cells):
+                    # the next micro-batch's recomputation (which touches no gradient) runs
+                    # on the other lane while this backward runs
+                    self._recompute_on_lane(cells[j + 1], lanes[(j + 1) % 2], main)
 
             # 3. backward through this cell
             tensors: List[Tensor] = []
@@ -553,8 +576,32 @@ class PipelineStage:
             cell.inputs = []
             cell.outputs = []
             cell.chk = None
+            cell.lane = None
+        if lanes is not None and main is not None:
+            # fused kernels on the lanes wrote .grad without autograd knowing
+            for lane in lanes:
+                main.wait_stream(lane)
         self._cells = []
         self.p2p.flush()
+
+    def _recompute_lanes(self) -> Optional[List[torch.cuda.Stream]]:
+        if not self.overlap_recompute or self.device.type != 'cuda':
+            return None
+        if self._lanes is None:
+            self._lanes = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
+        return self._lanes
+
+    def _recompute_on_lane(self, cell: _Cell, lane: torch.cuda.Stream,
+                           main: torch.cuda.Stream) -> None:
+        """Issue ``cell``'s recomputation on ``lane`` (once); its backward then runs there."""
+        if cell.chk is None or cell.lane is not None:
+            return
+        lane.wait_stream(main)
+        for t in cell.inputs:
+            t.record_stream(lane)
+        with torch.cuda.stream(lane), trace.range(f'recompute mb{cell.index} stage{self.rank}'):
+            cell.chk.recompute_now()
+        cell.lane = lane
 
     @staticmethod
     def _grad_of(t: Tensor) -> Tensor:
