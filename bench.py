@@ -103,11 +103,13 @@ def parse() -> argparse.Namespace:
                    help='one-GPU runs: capture the whole step (forward, backward, SGD) into a '
                         'hipGraph after the warm-up and replay it (RNG-free models only: '
                         'AmoebaNet; parallel/graph.py)')
-    p.add_argument('--cell-streams', action='store_true',
-                   help="AmoebaNet: run each cell's independent nodes on two HIP streams")
-    p.add_argument('--overlap-recompute', action='store_true',
+    p.add_argument('--cell-streams', choices=['auto', 'on', 'off'], default='auto',
+                   help="AmoebaNet: run each cell's independent nodes on two HIP streams "
+                        '(auto: on for one-GPU runs)')
+    p.add_argument('--overlap-recompute', choices=['auto', 'on', 'off'], default='auto',
                    help="recompute the next micro-batch on a second stream during this one's "
-                        'backward (PipelineStage(overlap_recompute=True))')
+                        'backward (PipelineStage(overlap_recompute=True); auto: on for '
+                        'one-GPU runs)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -196,6 +198,11 @@ def main() -> None:
     elif args.balance != 'ref':
         exp['balance'] = [int(v) for v in args.balance.split(',')]
     batch, chunks, balance = exp['batch'], exp['chunks'], list(exp['balance'])
+    # Intra-rank stream concurrency (measured on one GPU; multi-rank runs keep the
+    # one-stream schedule that the RCCL rehearsals exercised)
+    overlap = {'on': True, 'off': False}.get(args.overlap_recompute, world == 1 and gpu)
+    cell_streams = args.model == 'amoebanet' and {'on': True, 'off': False}.get(
+        args.cell_streams, world == 1 and gpu)
 
     def sync() -> None:
         if world > 1:
@@ -207,10 +214,10 @@ def main() -> None:
         """Build the stage for ``balance``, warm up, time ``--steps`` full SGD steps."""
         stage = PipelineStage(build_model(), balance, device=device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
-                              overlap_recompute=args.overlap_recompute)
+                              overlap_recompute=overlap)
         if args.channels_last:
             stage.partition.to(memory_format=torch.channels_last)
-        if args.cell_streams and args.model == 'amoebanet':
+        if cell_streams:
             from torchgpipe_amd.models.amoebanet import set_cell_streams
             set_cell_streams(stage.partition, True)
         optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
@@ -339,8 +346,8 @@ def main() -> None:
                 'first_step_s': round(main_run['first_step_s'], 2),
                 'timeout_s': args.timeout,
                 'hipgraph': bool(args.graph),
-                'cell_streams': bool(args.cell_streams and args.model == 'amoebanet'),
-                'overlap_recompute': bool(args.overlap_recompute),
+                'cell_streams': cell_streams,
+                'overlap_recompute': overlap,
             },
             'tuned': tuned,
         }), file=result_out, flush=True)

@@ -275,7 +275,9 @@ class Cell(nn.Module):
                 ) -> Tuple[Tensor, Tensor]:
         s1, s2 = states if isinstance(states, tuple) else (states, states)
         skip = s1
-        if self.streams and s1.is_cuda:
+        # (not inside a hipGraph capture: capturing the two-stream cells of the full model
+        # crashed the HIP runtime, profiles/r2/bench_amoeba_s13.md)
+        if self.streams and s1.is_cuda and not torch.cuda.is_current_stream_capturing():
             return self._forward_two_streams(s1, s2), skip
         nodes = [self.reduce1(s1), self.reduce2(s2)]
         for k in range(0, len(self.operations), 2):
@@ -288,9 +290,7 @@ class Cell(nn.Module):
         Node k runs on stream ``self._plan[k]`` after waiting on the events of inputs
         produced on the other stream; tensors crossing streams are ``record_stream``-ed so
         the caching allocator does not hand their memory out early.  Autograd runs each
-        backward op on its forward op's stream.  Inside a hipGraph capture
-        (``parallel/graph.py``) the side stream forks from and joins the capturing stream,
-        so the graph keeps the two branches as parallel paths.
+        backward op on its forward op's stream.
         """
         streams = [torch.cuda.current_stream(s1.device), _side_stream(s1.device)]
         if torch.is_grad_enabled() and (s1.requires_grad or s2.requires_grad):

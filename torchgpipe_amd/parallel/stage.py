@@ -587,6 +587,10 @@ class PipelineStage:
     def _recompute_lanes(self) -> Optional[List[torch.cuda.Stream]]:
         if not self.overlap_recompute or self.device.type != 'cuda':
             return None
+        if torch.cuda.is_current_stream_capturing():
+            # one stream inside hipGraph captures (parallel/graph.py): multi-stream captures
+            # of the full AmoebaNet step crashed the HIP runtime (profiles/r2/bench_amoeba_s13.md)
+            return None
         if self._lanes is None:
             self._lanes = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
         return self._lanes
