@@ -110,6 +110,9 @@ def parse() -> argparse.Namespace:
                    help="recompute the next micro-batch on a second stream during this one's "
                         'backward (PipelineStage(overlap_recompute=True); auto: on for '
                         'one-GPU runs)')
+    p.add_argument('--wgrad-stream', choices=['auto', 'on', 'off'], default='auto',
+                   help='run the fused ops\' weight-gradient GEMMs on a side stream '
+                        '(PipelineStage(wgrad_stream=True); experimental, auto: off)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -203,6 +206,7 @@ def main() -> None:
     overlap = {'on': True, 'off': False}.get(args.overlap_recompute, world == 1 and gpu)
     cell_streams = args.model == 'amoebanet' and {'on': True, 'off': False}.get(
         args.cell_streams, world == 1 and gpu)
+    wgrad_stream = {'on': True, 'off': False}.get(args.wgrad_stream, False)
 
     def sync() -> None:
         if world > 1:
@@ -214,7 +218,7 @@ def main() -> None:
         """Build the stage for ``balance``, warm up, time ``--steps`` full SGD steps."""
         stage = PipelineStage(build_model(), balance, device=device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
-                              overlap_recompute=overlap)
+                              overlap_recompute=overlap, wgrad_stream=wgrad_stream)
         if args.channels_last:
             stage.partition.to(memory_format=torch.channels_last)
         if cell_streams:
@@ -348,6 +352,7 @@ def main() -> None:
                 'hipgraph': bool(args.graph),
                 'cell_streams': cell_streams,
                 'overlap_recompute': overlap,
+                'wgrad_stream': wgrad_stream,
             },
             'tuned': tuned,
         }), file=result_out, flush=True)

@@ -74,6 +74,30 @@ __device__ __forceinline__ floatx4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 
+// Division by a per-launch constant without the ~20-instruction integer divide: the
+// implicit-GEMM gathers split flat indices into (channel, tap) / (image, pixel) / (row,
+// column) in their inner loops.  n / d = umulhi(n, mul) >> shr for 0 <= n < 2^31, with
+// shr = ceil(log2 d) - 1 and mul = ceil(2^(31 + ceil(log2 d)) / d) (d = 1: n itself).
+struct FastDiv {
+  uint32_t mul, shr;
+  int d;
+  __device__ __forceinline__ int div(int n) const {
+    return d == 1 ? n : static_cast<int>(__umulhi(static_cast<uint32_t>(n), mul) >> shr);
+  }
+};
+
+FastDiv make_fastdiv(int d) {
+  FastDiv f{0u, 0u, d};
+  if (d > 1) {
+    int l = 0;
+    while ((1ll << l) < d) ++l;  // ceil(log2 d)
+    f.mul = static_cast<uint32_t>(((1ull << (31 + l)) + static_cast<uint64_t>(d) - 1) /
+                                  static_cast<uint64_t>(d));
+    f.shr = static_cast<uint32_t>(l - 1);
+  }
+  return f;
+}
+
 // Geometry of one convolution (all byte offsets fit in 31 bits: checked on the host).
 struct Geo {
   int n, ci, h, w;       // input
@@ -85,6 +109,7 @@ struct Geo {
   int relu;              // ReLU on the input (forward / weight-grad) / its mask (bwd-data)
   int scatter;           // bwd-data over output pixels, results scattered (strided 1x1)
   int a_t;               // bwd-data: A is the transposed weight [ci][co*T] (row-major)
+  FastDiv fd_taps, fd_kw, fd_hwo, fd_wo, fd_hwi;  // / taps, / kw, / (ho*wo), / wo, / (h*w)
 };
 
 // Tile configurations.  CFG 0: 64 x 64 block, 4 waves (2 x 2) of one 32 x 32 MFMA tile;
@@ -339,7 +364,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
       } else {
         // dZ rows: A[co][k = (n, p)]
         if (quads && row < M && k + 3 < k_end) {
-          const int n = k / hw_out, p = k - n * hw_out;
+          const int n = g.fd_hwo.div(k), p = k - n * hw_out;
           ra[i] = bload4(ar, static_cast<uint32_t>(
                                  ((n * g.co_total + g.co_off + row) * hw_out + p) * 4));
         } else {
@@ -347,7 +372,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
           for (int e = 0; e < 4; ++e) {
             uint32_t off = kOOB;
             if (row < M && k + e < k_end) {
-              const int n = (k + e) / hw_out, p = k + e - n * hw_out;
+              const int n = g.fd_hwo.div(k + e), p = k + e - n * hw_out;
               off = static_cast<uint32_t>(((n * g.co_total + g.co_off + row) * hw_out + p) * 4);
             }
             ra[i][e] = bload(ar, off);
@@ -376,8 +401,8 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
                                    ? static_cast<uint32_t>((col[e].base + coff) * 4) : kOOB);
           }
         } else {
-          const int ci = k / g.taps, t = k - ci * g.taps;
-          const int th = t / g.kw, tw = t - th * g.kw;
+          const int ci = g.fd_taps.div(k), t = k - ci * g.taps;
+          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int yi = col[e].y + th, xi = col[e].x + tw;
@@ -407,8 +432,8 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
           }
         } else {
           // output pixel * stride = input pixel + pad - tap - offset (stride holes: none)
-          const int co = k / g.taps, t = k - co * g.taps;
-          const int th = t / g.kw, tw = t - th * g.kw;
+          const int co = g.fd_taps.div(k), t = k - co * g.taps;
+          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
           if (g.sh == 1 && g.sw == 1) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -437,19 +462,19 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
 #pragma unroll
       for (int i = 0; i < C::kBQuadsK; ++i) {
         const int j = n0 + (tid >> 3) + (kThreads / 8) * i;
-        const int ci = j / g.taps, t = j - ci * g.taps;
+        const int ci = g.fd_taps.div(j), t = j - ci * g.taps;
         floatx4 v;
         if (quads && j < N && k + 3 < k_end) {
-          const int n = k / hw_out, p = k - n * hw_out;
+          const int n = g.fd_hwo.div(k), p = k - n * hw_out;
           v = bload4(br, static_cast<uint32_t>(((n * g.ci + ci) * hw_in + p) * 4));
         } else {
-          const int th = t / g.kw, tw = t - th * g.kw;
+          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             uint32_t off = kOOB;
             if (j < N && k + e < k_end) {
-              const int n = (k + e) / hw_out, p = k + e - n * hw_out;
-              const int y = p / g.wo, x = p - y * g.wo;
+              const int n = g.fd_hwo.div(k + e), p = k + e - n * hw_out;
+              const int y = g.fd_wo.div(p), x = p - y * g.wo;
               const int yi = y * g.sh - g.ph + th + g.oh, xi = x * g.sw - g.pw + tw + g.ow;
               if (yi >= 0 && yi < g.h && xi >= 0 && xi < g.w)
                 off = static_cast<uint32_t>((((n * g.ci + ci) * g.h + yi) * g.w + xi) * 4);
@@ -557,6 +582,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
   constexpr int kQuads = C::BN / 4;
   const bool scatter = MODE == kBwdData && g.scatter;
   const int hw = (MODE == kFwd || scatter) ? hw_out : hw_in;
+  const FastDiv& fdh = (MODE == kFwd || scatter) ? g.fd_hwo : g.fd_hwi;
   const int ch_total = MODE == kFwd ? g.co_total : g.ci;
   const int ch_off = MODE == kFwd ? g.co_off : 0;
   const __amdgpu_buffer_rsrc_t mr = rsrc(x_mask, x_mask ? static_cast<int64_t>(g.n) * g.ci *
@@ -572,8 +598,8 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
       for (int e = 0; e < 4; ++e) {
         const int je = j + e;
         if (je >= N) break;
-        const int n = je / hw_out, p = je - n * hw_out;
-        const int y = p / g.wo, x = p - y * g.wo;
+        const int n = g.fd_hwo.div(je), p = je - n * hw_out;
+        const int y = g.fd_wo.div(p), x = p - y * g.wo;
         const int yi = y * g.sh - g.ph + g.oh, xi = x * g.sw - g.pw + g.ow;
         if (yi < 0 || yi >= g.h || xi < 0 || xi >= g.w) continue;
         const int64_t off = ((static_cast<int64_t>(n) * g.ci + m) * g.h + yi) * g.w + xi;
@@ -583,7 +609,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
       }
       continue;
     }
-    const int n = j / hw, p = j - n * hw;
+    const int n = fdh.div(j), p = j - n * hw;
     const int64_t base = (static_cast<int64_t>(n) * ch_total + ch_off + m) * hw + p;
     if ((hw & 3) == 0 && j + 3 < N) {
       if constexpr (MODE == kBwdData) {
@@ -600,7 +626,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
       for (int e = 0; e < 4; ++e) {
         const int je = j + e;
         if (je >= N) break;
-        const int ne = je / hw, pe = je - ne * hw;
+        const int ne = fdh.div(je), pe = je - ne * hw;
         const int64_t off = (static_cast<int64_t>(ne) * ch_total + ch_off + m) * hw + pe;
         float val = v[e];
         if constexpr (MODE == kBwdData) {
@@ -733,7 +759,12 @@ void launch_split_reduce(const float* ws, int splits, int64_t stride, float* out
 Geo make_geo(const ConvGemmGeo& cg) {
   Geo g{cg.n, cg.ci, cg.h, cg.w, cg.co, cg.ho, cg.wo, cg.co_total, cg.co_off, cg.kh, cg.kw,
         cg.kh * cg.kw, cg.sh, cg.sw, cg.ph, cg.pw, cg.oh, cg.ow, cg.relu ? 1 : 0, 0,
-        cg.a_t ? 1 : 0};
+        cg.a_t ? 1 : 0, {}, {}, {}, {}, {}};
+  g.fd_taps = make_fastdiv(g.taps);
+  g.fd_kw = make_fastdiv(g.kw);
+  g.fd_hwo = make_fastdiv(g.ho * g.wo);
+  g.fd_wo = make_fastdiv(g.wo);
+  g.fd_hwi = make_fastdiv(g.h * g.w);
   return g;
 }
 

@@ -361,6 +361,19 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
 // `sums` is the forward's zeroed [2][C] buffer (consumed).  `accum` is empty or holds one
 // optional entry per parameter gradient {dgamma, dbeta, dw_0, ...}: a given tensor (the
 // parameter's .grad across micro-batches) is accumulated into in place and returned.
+// One part's weight gradient: dw (+)= dz x relu(X) taps (accumulating into `into` when given).
+at::Tensor wgrad_part(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& weight,
+                      const ConvGemmGeo& g, const at::Tensor& into) {
+  const bool acc = into.defined();
+  auto dw = acc ? into : at::empty_like(weight);
+  const ConvGemmPlan plan =
+      tuned_plan(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
+                 nullptr, nullptr, g, acc, dz.numel() * 4, x.numel() * 4, x, dw.numel());
+  run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(), nullptr,
+           nullptr, g, plan, acc, dz.numel() * 4, x.numel() * 4, x);
+  return dw;
+}
+
 std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
                                         const at::Tensor& z, const at::Tensor& mean,
                                         const at::Tensor& invstd, at::Tensor& sums,
@@ -368,7 +381,7 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                                         at::TensorList weights, at::IntArrayRef geo, bool relu,
                                         bool need_dx,
                                         const c10::List<c10::optional<at::Tensor>>& accum,
-                                        at::TensorList weights_t) {
+                                        at::TensorList weights_t, bool defer_wgrad) {
   auto x = x_in.contiguous();
   // dy is read in place when it is a channel slice (a concatenated cell output's gradient)
   int64_t dy_img = image_stride_if_channel_slice(dy_in);
@@ -452,15 +465,44 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   out.push_back(dx);
   out.push_back(dgamma);
   out.push_back(dbeta);
+  if (defer_wgrad) {  // the caller runs convbn_wgrad (e.g. on a weight-gradient stream)
+    out.push_back(dz);
+    return out;
+  }
   for (size_t i = 0; i < p.geo.size(); ++i) {
     const bool acc = into[2 + i].defined();
-    auto dw = acc ? into[2 + i] : at::empty_like(weights[i]);
-    const ConvGemmPlan plan =
-        tuned_plan(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
-                   nullptr, nullptr, p.geo[i], acc, dz.numel() * 4, x.numel() * 4, x, dw.numel());
-    run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(), nullptr,
-             nullptr, p.geo[i], plan, acc, dz.numel() * 4, x.numel() * 4, x);
-    out.push_back(dw);
+    out.push_back(wgrad_part(dz, x, weights[i], p.geo[i], acc ? into[2 + i] : at::Tensor()));
+  }
+  return out;
+}
+
+// Weight gradients of a fused op from its BatchNorm-backward output dz (convbn_backward
+// with defer_wgrad), on the current stream: dW_i (+)= dz[:, part i] x relu(X) taps.
+std::vector<at::Tensor> convbn_wgrad(const at::Tensor& dz, const at::Tensor& x_in,
+                                     at::TensorList weights, at::IntArrayRef geo, bool relu,
+                                     const c10::List<c10::optional<at::Tensor>>& accum) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  check_f32(dz, "dz", x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Parts p = make_parts(x, weights, geo, relu);
+  TORCH_CHECK(dz.dim() == 4 && dz.size(0) == x.size(0) && dz.size(1) == p.co_total &&
+                  dz.size(2) == p.ho && dz.size(3) == p.wo,
+              "dz does not match the operation's output");
+  TORCH_CHECK(accum.empty() || accum.size() == p.geo.size(),
+              "accum must be empty or hold one gradient per weight");
+  std::vector<at::Tensor> out;
+  for (size_t i = 0; i < p.geo.size(); ++i) {
+    at::Tensor into;
+    if (!accum.empty()) {
+      const c10::optional<at::Tensor> t = accum.get(i);
+      if (t.has_value() && t->defined()) {
+        check_f32(*t, "accumulated gradient", x);
+        TORCH_CHECK(t->numel() == weights[i].numel(), "accumulated gradient has the wrong size");
+        into = *t;
+      }
+    }
+    out.push_back(wgrad_part(dz, x, weights[i], p.geo[i], into));
   }
   return out;
 }
@@ -818,7 +860,9 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
         "Tensor(c!)? num_batches_tracked, float momentum, float eps, Tensor? add) -> Tensor[]");
   m.def("convbn_backward(Tensor dy, Tensor x, Tensor z, Tensor mean, Tensor invstd, "
         "Tensor(a!) sums, Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx, "
-        "Tensor?[] accum, Tensor[] weights_t) -> Tensor[]");
+        "Tensor?[] accum, Tensor[] weights_t, bool defer_wgrad=False) -> Tensor[]");
+  m.def("convbn_wgrad(Tensor dz, Tensor x, Tensor[] weights, int[] geo, bool relu, "
+        "Tensor?[] accum) -> Tensor[]");
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
   m.def("conv_gemm_plans_export() -> str", &tgpipe::conv_gemm_plans_export);
   m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
@@ -833,6 +877,7 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("convbn_forward", &tgpipe::convbn_forward);
   m.impl("convbn_backward", &tgpipe::convbn_backward);
+  m.impl("convbn_wgrad", &tgpipe::convbn_wgrad);
   m.impl("conv_gemm_forward", &tgpipe::conv_gemm_forward);
   m.impl("conv_gemm_sweep", &tgpipe::conv_gemm_sweep);
   m.impl("conv_gemm_backward_data", &tgpipe::conv_gemm_backward_data);

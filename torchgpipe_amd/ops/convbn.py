@@ -22,7 +22,7 @@ eval mode, for non-fp32 tensors or unsupported convolutions.
 """
 import contextlib
 import os
-from typing import Iterator, List, Optional, Sequence, Tuple
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -72,6 +72,37 @@ def _bn_ok(bn: nn.Module, x: Tensor) -> bool:
             and (bn.momentum is not None or not bn.track_running_stats))
 
 
+_WGRAD = {'enabled': False}
+_WGRAD_STREAMS: Dict[torch.device, torch.cuda.Stream] = {}
+
+
+@contextlib.contextmanager
+def wgrad_stream_scope(enabled: bool = True) -> Iterator[None]:
+    """While active (process-wide: autograd runs backward on its own threads), fused ops
+    whose weight gradients are accumulated by the kernels themselves (``ops/gradacc.py``)
+    run the weight-gradient GEMMs on a per-device side stream, concurrently with the
+    backward chain (BatchNorm backward, backward-data) that continues on the op's stream.
+    On exit the caller's current stream waits for the side streams, so the gradients are
+    ready for the optimizer.  Not used inside hipGraph captures."""
+    prev = _WGRAD['enabled']
+    _WGRAD['enabled'] = enabled
+    try:
+        yield
+    finally:
+        _WGRAD['enabled'] = prev
+        for device, stream in _WGRAD_STREAMS.items():
+            torch.cuda.current_stream(device).wait_stream(stream)
+
+
+def _wgrad_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
+    if not _WGRAD['enabled'] or device.type != 'cuda' or torch.cuda.is_current_stream_capturing():
+        return None
+    stream = _WGRAD_STREAMS.get(device)
+    if stream is None:
+        stream = _WGRAD_STREAMS[device] = torch.cuda.Stream(device)
+    return stream
+
+
 class _ConvBN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: Tensor, add: Optional[Tensor], gamma: Optional[Tensor],  # type: ignore[override]
@@ -100,9 +131,20 @@ class _ConvBN(torch.autograd.Function):
         fused = [gradacc.target(p) for p in ctx.params]
         # the backward-data GEMM reads W^T: transposed once per step, not per micro-batch
         wts = [c.get_transposed(w) for c, w in zip(ctx.caches, weights)] if need_dx else []
-        dx, dgamma, dbeta, *dws = _ext.require(dy).convbn_backward(
+        ops = _ext.require(dy)
+        side = _wgrad_stream(dy.device) if all(f for f, _ in fused[2:]) else None
+        dx, dgamma, dbeta, *dws = ops.convbn_backward(
             dy, x, z, mean, invstd, sums, gamma, weights, ctx.geo, ctx.relu, need_dx,
-            [into for _, into in fused], wts)
+            [into for _, into in fused], wts, side is not None)
+        if side is not None:
+            # weight gradients on the side stream (written into .grad by the kernels)
+            dz = dws[0]
+            side.wait_stream(torch.cuda.current_stream(dy.device))
+            dz.record_stream(side)
+            x.record_stream(side)
+            with torch.cuda.stream(side):
+                dws = ops.convbn_wgrad(dz, x, weights, ctx.geo, ctx.relu,
+                                       [into for _, into in fused[2:]])
         grads = [dgamma, dbeta] + dws
         for k, ((fuse, into), p) in enumerate(zip(fused, ctx.params)):
             if fuse:  # written into p.grad by the kernels

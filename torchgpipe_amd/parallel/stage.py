@@ -167,7 +167,8 @@ class PipelineStage:
                  links: Optional[bool] = None,
                  materialize: Optional[Callable[[nn.Module], None]] = None,
                  timeout: Optional[float] = None,
-                 overlap_recompute: bool = False) -> None:
+                 overlap_recompute: bool = False,
+                 wgrad_stream: bool = False) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
         if checkpoint not in ('always', 'except_last', 'never'):
@@ -245,6 +246,7 @@ class PipelineStage:
 
         self._cells: List[_Cell] = []
         self.overlap_recompute = overlap_recompute
+        self.wgrad_stream = wgrad_stream
         self._lanes: Optional[List[torch.cuda.Stream]] = None
         self._sig: Optional[Signature] = None
         self._m = 0
@@ -490,8 +492,17 @@ class PipelineStage:
         """Back-propagate every micro-batch (reverse order) and ship input gradients.
 
         The last stage passes one scalar loss per micro-batch; the others pass
-        ``None``.
+        ``None``.  With ``wgrad_stream`` the fused ops' weight-gradient GEMMs run on a side
+        stream (``ops.convbn.wgrad_stream_scope``), joined before this returns.
         """
+        if self.wgrad_stream and self.device.type == 'cuda':
+            from torchgpipe_amd.ops.convbn import wgrad_stream_scope
+            with wgrad_stream_scope(True):
+                self._backward(losses)
+        else:
+            self._backward(losses)
+
+    def _backward(self, losses: Optional[Sequence[Tensor]] = None) -> None:
         if self.is_last and losses is None:
             raise ValueError('the last stage must pass the per-micro-batch losses')
         nxt = self.ranks[self.rank + 1] if not self.is_last else None
