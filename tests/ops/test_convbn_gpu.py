@@ -295,6 +295,32 @@ def test_fused_gradient_accumulation_matches_autograd(monkeypatch):
         torch.testing.assert_close(g, p.grad, rtol=1e-5, atol=1e-5)
 
 
+def test_single_split_weight_gradient_accumulates():
+    """A weight-gradient launch without split-K (small micro-batches: K = images x pixels
+    < 256 leaves only one split) must still add into an existing .grad."""
+    from torchgpipe_amd.ops.convbn import ReLUConvBN
+    ops = _ext.require()
+
+    def build():
+        torch.manual_seed(1)
+        return ReLUConvBN(nn.ReLU(), nn.Conv2d(16, 32, 1, bias=False), nn.BatchNorm2d(32)).cuda()
+
+    xs = [torch.randn(2, 16, 7, 7, device='cuda') for _ in range(3)]
+    fused, plain = build(), build()
+    ops.conv_gemm_force_cfg(0, 1)
+    try:
+        for x in xs:
+            fused(x).square().sum().backward()
+    finally:
+        ops.conv_gemm_force_cfg(-1, 1)
+    for x in xs:
+        y = F.batch_norm(F.conv2d(F.relu(x), plain[1].weight), None, None, plain[2].weight,
+                         plain[2].bias, training=True)
+        y.square().sum().backward()
+    torch.testing.assert_close(fused[1].weight.grad, plain[1].weight.grad, rtol=1e-4,
+                               atol=1e-5)
+
+
 def test_backward_reads_channel_sliced_gradients_in_place():
     """A cell output is a concatenation: its gradient reaches the fused ops as channel
     slices, which the BN backward and the pool backward read without a copy."""

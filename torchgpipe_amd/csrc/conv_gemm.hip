@@ -559,7 +559,11 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = m0 + wm * 32 * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (row < M && cj < N) out[static_cast<int64_t>(row) * N + cj] = acc[i][j][r];
+          if (row < M && cj < N) {
+            // (one split: this is the gradient itself, accumulated into .grad when asked)
+            float* o = out + static_cast<int64_t>(row) * N + cj;
+            *o = accumulate ? *o + acc[i][j][r] : acc[i][j][r];
+          }
         }
       }
     return;
