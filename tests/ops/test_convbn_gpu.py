@@ -317,8 +317,11 @@ def test_single_split_weight_gradient_accumulates():
         y = F.batch_norm(F.conv2d(F.relu(x), plain[1].weight), None, None, plain[2].weight,
                          plain[2].bias, training=True)
         y.square().sum().backward()
-    torch.testing.assert_close(fused[1].weight.grad, plain[1].weight.grad, rtol=1e-4,
-                               atol=1e-5)
+    # (the BatchNorm backward cancels: fp32 noise is ~1e-5 of the largest element; an
+    # overwritten instead of accumulated gradient is off by ~2/3 everywhere)
+    ref = plain[1].weight.grad
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(fused[1].weight.grad, ref, rtol=1e-3, atol=2e-4 * scale)
 
 
 def test_backward_reads_channel_sliced_gradients_in_place():
