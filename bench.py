@@ -109,7 +109,7 @@ def parse() -> argparse.Namespace:
     p.add_argument('--overlap-recompute', choices=['auto', 'on', 'off'], default='auto',
                    help="recompute the next micro-batch on a second stream during this one's "
                         'backward (PipelineStage(overlap_recompute=True); auto: on for '
-                        'one-GPU runs)')
+                        'one-GPU U-Net runs)')
     p.add_argument('--wgrad-stream', choices=['auto', 'on', 'off'], default='auto',
                    help='run the fused ops\' weight-gradient GEMMs on a side stream '
                         '(PipelineStage(wgrad_stream=True); experimental, auto: off)')
@@ -203,7 +203,10 @@ def main() -> None:
     batch, chunks, balance = exp['batch'], exp['chunks'], list(exp['balance'])
     # Intra-rank stream concurrency (measured on one GPU; multi-rank runs keep the
     # one-stream schedule that the RCCL rehearsals exercised)
-    overlap = {'on': True, 'off': False}.get(args.overlap_recompute, world == 1 and gpu)
+    # (auto: U-Net only -- AmoebaNet's two-stream cells already fill the CUs, and the extra
+    # recompute lane cost it 19 %: profiles/r2/bench_amoeba_s13.md)
+    overlap = {'on': True, 'off': False}.get(args.overlap_recompute,
+                                             world == 1 and gpu and args.model == 'unet')
     cell_streams = args.model == 'amoebanet' and {'on': True, 'off': False}.get(
         args.cell_streams, world == 1 and gpu)
     wgrad_stream = {'on': True, 'off': False}.get(args.wgrad_stream, False)

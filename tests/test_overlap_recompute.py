@@ -101,9 +101,6 @@ def test_overlap_with_two_stream_cells_matches_plain():
 
 
 @pytest.mark.gpu
-@pytest.mark.xfail(reason='weight-gradient stream: gradients differ (under investigation, '
-                          'scripts/debug/wgrad_stream_probe.py); bench.py keeps it off',
-                   strict=False)
 def test_weight_gradient_stream_matches_plain():
     """The fused ops' weight-gradient GEMMs on a side stream (with two-stream cells and
     recompute lanes, the one-GPU bench configuration) against the plain schedule."""
