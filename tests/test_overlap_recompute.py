@@ -122,11 +122,16 @@ def test_weight_gradient_stream_matches_plain():
         y = torch.randint(10, (8,), device=dev, generator=gen)
         la = sa.train_step(x, y, F.cross_entropy)
         lb = sb.train_step(x, y, F.cross_entropy)
-        # the update reads the side stream's gradients on the current stream
-        _close_grads(a, b)
+        # the update reads the side stream's gradients on the current stream.  Measured:
+        # < 1e-4 of each gradient's largest element after one step
+        # (profiles/r2/wgrad_stream_probe.log), drifting to ~4e-4 after two SGD updates;
+        # a lost or doubled micro-batch contribution would be ~1/4 of it.
+        for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+            scale = pa.grad.abs().max().item() + 1e-12
+            torch.testing.assert_close(pb.grad, pa.grad, rtol=1e-3, atol=2e-3 * scale)
         oa.step()
         ob.step()
         torch.cuda.synchronize()
-        torch.testing.assert_close(lb, la, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(lb, la, rtol=1e-3, atol=1e-4)
         oa.zero_grad(set_to_none=True)
         ob.zero_grad(set_to_none=True)
