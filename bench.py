@@ -110,6 +110,9 @@ def parse() -> argparse.Namespace:
                    help="recompute the next micro-batch on a second stream during this one's "
                         'backward (PipelineStage(overlap_recompute=True); auto: on for '
                         'one-GPU U-Net runs)')
+    p.add_argument('--overlap-forward', choices=['auto', 'on', 'off'], default='auto',
+                   help='alternate the forward micro-batches of a one-rank stateless partition '
+                        '(no running statistics: U-Net) between two streams (auto: off)')
     p.add_argument('--wgrad-stream', choices=['auto', 'on', 'off'], default='auto',
                    help='run the fused ops\' weight-gradient GEMMs on a side stream '
                         '(PipelineStage(wgrad_stream=True); experimental, auto: off)')
@@ -210,6 +213,7 @@ def main() -> None:
     cell_streams = args.model == 'amoebanet' and {'on': True, 'off': False}.get(
         args.cell_streams, world == 1 and gpu)
     wgrad_stream = {'on': True, 'off': False}.get(args.wgrad_stream, False)
+    overlap_fwd = {'on': True, 'off': False}.get(args.overlap_forward, False)
 
     def sync() -> None:
         if world > 1:
@@ -221,7 +225,8 @@ def main() -> None:
         """Build the stage for ``balance``, warm up, time ``--steps`` full SGD steps."""
         stage = PipelineStage(build_model(), balance, device=device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
-                              overlap_recompute=overlap, wgrad_stream=wgrad_stream)
+                              overlap_recompute=overlap, overlap_forward=overlap_fwd,
+                              wgrad_stream=wgrad_stream)
         if args.channels_last:
             stage.partition.to(memory_format=torch.channels_last)
         if cell_streams:
@@ -356,6 +361,7 @@ def main() -> None:
                 'cell_streams': cell_streams,
                 'overlap_recompute': overlap,
                 'wgrad_stream': wgrad_stream,
+                'overlap_forward': overlap_fwd,
             },
             'tuned': tuned,
         }), file=result_out, flush=True)

@@ -28,6 +28,7 @@ output tensors + skips stashed for other ranks, so checkpointing
 (``Checkpointing``) treats cross-rank skips like any other input/output.
 """
 from collections import OrderedDict
+import contextlib
 import datetime
 from typing import Any, Callable, Dict, Hashable, List, Optional, Sequence, Tuple, Union
 
@@ -168,6 +169,7 @@ class PipelineStage:
                  materialize: Optional[Callable[[nn.Module], None]] = None,
                  timeout: Optional[float] = None,
                  overlap_recompute: bool = False,
+                 overlap_forward: bool = False,
                  wgrad_stream: bool = False) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
@@ -246,8 +248,14 @@ class PipelineStage:
 
         self._cells: List[_Cell] = []
         self.overlap_recompute = overlap_recompute
+        self.overlap_forward = overlap_forward
         self.wgrad_stream = wgrad_stream
         self._lanes: Optional[List[torch.cuda.Stream]] = None
+        self._fwd_lanes: Optional[List[torch.cuda.Stream]] = None
+        # modules whose forward carries state across micro-batches (running statistics):
+        # their micro-batches must run in order on one stream
+        self._stateful = any(isinstance(m, nn.modules.batchnorm._BatchNorm)
+                             and m.track_running_stats for m in self.partition.modules())
         self._sig: Optional[Signature] = None
         self._m = 0
         if distributed and self.n > 1:
@@ -435,6 +443,8 @@ class PipelineStage:
         self._cells = []
         outputs: List[TensorOrTensors] = []
 
+        flanes = self._forward_lanes()
+        main = torch.cuda.current_stream(self.device) if flanes is not None else None
         for i in range(m):
             cell = _Cell(i)
             # 1. inputs: activations + cross-rank skips (posted before waiting on any)
@@ -458,13 +468,28 @@ class PipelineStage:
             flat = list(acts) + popped
             cell.inputs = flat
 
-            # 2. compute
+            # 2. compute (independent micro-batches of a one-rank, stateless partition
+            #    alternate between two forward lanes)
             fn = self._make_fn(cell, len(acts), in_atomic)
-            if i < stop:
-                cell.chk = Checkpointing(fn, Batch(tuple(flat)))
-                out = list(cell.chk.checkpoint())
-            else:
-                out = list(fn(tuple(flat)))
+            lane = None
+            if flanes is not None:
+                assert main is not None
+                lane = flanes[i % 2]
+                lane.wait_stream(main)
+                for t in flat:
+                    t.record_stream(lane)
+            with torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext():
+                if i < stop:
+                    cell.chk = Checkpointing(fn, Batch(tuple(flat)))
+                    out = list(cell.chk.checkpoint())
+                else:
+                    out = list(fn(tuple(flat)))
+            if lane is not None:
+                assert main is not None
+                for t in out:
+                    t.record_stream(main)
+                if cell.chk is None:
+                    cell.lane = lane  # its backward runs there (ordered like recomputed ones)
             cell.outputs = out
             self._cells.append(cell)
 
@@ -480,6 +505,9 @@ class PipelineStage:
                 self.p2p.send(by_dst[dst], self.ranks[dst],
                               self._key('skip', i, me, self.ranks[dst]))
             outputs.append(act_out[0] if cell.out_atomic else tuple(act_out))
+        if flanes is not None and main is not None:
+            for lane in flanes:
+                main.wait_stream(lane)
         if not torch.is_grad_enabled():
             # Inference: no backward will flush the sends; complete them now.
             self.p2p.flush()
@@ -588,10 +616,11 @@ class PipelineStage:
             cell.outputs = []
             cell.chk = None
             cell.lane = None
-        if lanes is not None and main is not None:
+        if self.device.type == 'cuda':
             # fused kernels on the lanes wrote .grad without autograd knowing
-            for lane in lanes:
-                main.wait_stream(lane)
+            cur = torch.cuda.current_stream(self.device)
+            for lane in (lanes or []) + (self._fwd_lanes or []):
+                cur.wait_stream(lane)
         self._cells = []
         self.p2p.flush()
 
@@ -605,6 +634,16 @@ class PipelineStage:
         if self._lanes is None:
             self._lanes = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
         return self._lanes
+
+    def _forward_lanes(self) -> Optional[List[torch.cuda.Stream]]:
+        """Two streams for the forward micro-batches of a one-rank stateless partition."""
+        if not self.overlap_forward or self.n != 1 or self._stateful:
+            return None
+        if self.device.type != 'cuda' or torch.cuda.is_current_stream_capturing():
+            return None
+        if self._fwd_lanes is None:
+            self._fwd_lanes = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
+        return self._fwd_lanes
 
     def _recompute_on_lane(self, cell: _Cell, lane: torch.cuda.Stream,
                            main: torch.cuda.Stream) -> None:
