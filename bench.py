@@ -112,7 +112,8 @@ def parse() -> argparse.Namespace:
                         'one-GPU U-Net runs)')
     p.add_argument('--overlap-forward', choices=['auto', 'on', 'off'], default='auto',
                    help='alternate the forward micro-batches of a one-rank stateless partition '
-                        '(no running statistics: U-Net) between two streams (auto: off)')
+                        '(no running statistics: U-Net) between two streams (auto: on for '
+                        'one-GPU U-Net runs)')
     p.add_argument('--wgrad-stream', choices=['auto', 'on', 'off'], default='auto',
                    help='run the fused ops\' weight-gradient GEMMs on a side stream '
                         '(PipelineStage(wgrad_stream=True); experimental, auto: off)')
@@ -213,7 +214,8 @@ def main() -> None:
     cell_streams = args.model == 'amoebanet' and {'on': True, 'off': False}.get(
         args.cell_streams, world == 1 and gpu)
     wgrad_stream = {'on': True, 'off': False}.get(args.wgrad_stream, False)
-    overlap_fwd = {'on': True, 'off': False}.get(args.overlap_forward, False)
+    overlap_fwd = {'on': True, 'off': False}.get(args.overlap_forward,
+                                                 world == 1 and gpu and args.model == 'unet')
 
     def sync() -> None:
         if world > 1:
