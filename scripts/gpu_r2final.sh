@@ -12,6 +12,4 @@ timeout -k 10 300 python bench.py --model amoebanet --gpus 1 --steps 10 --warmup
 echo "amoeba: $(tail -1 gpurun_out/final/amoeba.log | cut -c1-200)"
 bash scripts/profile_bench.sh unet_final --gpus 1 --steps 4 --warmup 2 || exit 1
 bash scripts/profile_bench.sh amoeba_final --model amoebanet --gpus 1 --steps 3 --warmup 2 || exit 1
-head -5 gpurun_out/prof_unet_final/summary.md | tail -2; head -5 gpurun_out/prof_amoeba_final/summary.md | tail -2
-timeout -k 10 300 python scripts/debug/wgrad_stream_probe.py > gpurun_out/final/wgrad_probe.log 2>&1
-grep -v amdgpu.ids gpurun_out/final/wgrad_probe.log | tail -8
+head -3 gpurun_out/prof_unet_final/summary.md | tail -1; head -3 gpurun_out/prof_amoeba_final/summary.md | tail -1
