@@ -1,0 +1,33 @@
+"""Two-stream schedule of the AmoebaNet cells (models/amoebanet.py, set_cell_streams)."""
+import torch
+
+from torchgpipe_amd.models import amoebanetd
+from torchgpipe_amd.models.amoebanet import Cell, set_cell_streams
+
+
+def test_stream_plans_split_the_cell_and_respect_dependencies():
+    model = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
+    cells = [m for m in model.modules() if isinstance(m, Cell)]
+    assert cells
+    for cell in cells:
+        plan = cell._plan
+        # the two input reductions on different streams, one stream per node
+        assert plan[:2] == [0, 1]
+        assert len(plan) == 2 + len(cell.operations) // 2
+        assert set(plan) == {0, 1}
+        # every node runs on the stream of one of its inputs
+        for k in range(0, len(cell.operations), 2):
+            node = 2 + k // 2
+            assert plan[node] in {plan[cell.indices[k]], plan[cell.indices[k + 1]]}
+
+
+def test_set_cell_streams_toggles_every_cell_and_cpu_runs_one_stream():
+    torch.manual_seed(0)
+    model = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
+    x = torch.rand(2, 3, 224, 224)
+    ref = model(x)
+    set_cell_streams(model, True)
+    assert all(m.streams for m in model.modules() if isinstance(m, Cell))
+    assert torch.equal(model(x), ref)  # CPU tensors: the one-stream path
+    set_cell_streams(model, False)
+    assert not any(m.streams for m in model.modules() if isinstance(m, Cell))
