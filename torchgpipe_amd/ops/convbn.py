@@ -84,9 +84,7 @@ def wgrad_stream_scope(enabled: bool = True) -> Iterator[None]:
     backward chain (BatchNorm backward, backward-data) that continues on the op's stream.
     On exit the caller's current stream waits for the side streams, so the gradients are
     ready for the optimizer.  Not used inside hipGraph captures.
-
-    Experimental: its parity test (``tests/test_overlap_recompute.py``) shows intermittent
-    gradient differences over several optimizer steps, so nothing enables it by default."""
+"""
     prev = _WGRAD['enabled']
     _WGRAD['enabled'] = enabled
     try:
