@@ -116,7 +116,7 @@ def parse() -> argparse.Namespace:
                         'one-GPU U-Net runs)')
     p.add_argument('--wgrad-stream', choices=['auto', 'on', 'off'], default='auto',
                    help='run the fused ops\' weight-gradient GEMMs on a side stream '
-                        '(PipelineStage(wgrad_stream=True); auto: on for one-GPU AmoebaNet runs)')
+                        '(PipelineStage(wgrad_stream=True); auto: off)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -213,8 +213,9 @@ def main() -> None:
                                              world == 1 and gpu and args.model == 'unet')
     cell_streams = args.model == 'amoebanet' and {'on': True, 'off': False}.get(
         args.cell_streams, world == 1 and gpu)
-    wgrad_stream = {'on': True, 'off': False}.get(args.wgrad_stream,
-                                                  world == 1 and gpu and args.model == 'amoebanet')
+    # (auto: off -- with the two-stream cells it measured 280.3 vs 328.6 samples/s on one box,
+    # profiles/r2/bench_amoeba_s13.md)
+    wgrad_stream = {'on': True, 'off': False}.get(args.wgrad_stream, False)
     overlap_fwd = {'on': True, 'off': False}.get(args.overlap_forward,
                                                  world == 1 and gpu and args.model == 'unet')
 
