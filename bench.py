@@ -1,15 +1,26 @@
 #!/usr/bin/env python
-"""Headline benchmark: U-Net(5,64) (or AmoebaNet-D(18,256)) GPipe training throughput.
+"""Headline benchmark: U-Net(5,64) GPipe training throughput, plus AmoebaNet-D(18,256).
 
 Metric (BASELINE.json): samples/sec of a full SGD training step (forward,
-backward with checkpoint recomputation, optimizer step) of U-Net(5,64) on
-3×192×192 synthetic images at 1/2/4/8 pipeline partitions, using the
-reference's experiment tables (``benchmarks/unet-speed/main.py:23-68``):
+backward with checkpoint recomputation, optimizer step) at 1/2/4/8 pipeline
+partitions, using the reference's experiment tables
+(``benchmarks/unet-speed/main.py:23-68``, ``benchmarks/amoebanetd-speed/main.py:35-96``):
 
-    N=1  pipeline-1  B=80,  chunks=2,  balance [241]
-    N=2  pipeline-2  B=512, chunks=32, balance [104, 137]
-    N=4  pipeline-4  B=512, chunks=16, balance [30, 66, 84, 61]
-    N=8  pipeline-8  B=640, chunks=40, balance [16, 27, 31, 44, 22, 57, 27, 17]
+    N=1  U-Net pipeline-1  B=80,  chunks=2,  balance [241]
+    N=2  U-Net pipeline-2  B=512, chunks=32, balance [104, 137]
+    N=4  U-Net pipeline-4  B=512, chunks=16, balance [30, 66, 84, 61]
+    N=8  U-Net pipeline-8  B=640, chunks=40, balance [16, 27, 31, 44, 22, 57, 27, 17]
+
+The top-level ``value`` is the U-Net headline.  After it, every run also times
+(``--sections``):
+
+* ``baseline``: the reference's speed-up denominator, U-Net(5,64) *without* GPipe
+  (plain model, B=40, no checkpointing) on rank 0's GPU, so ``speedup_vs_baseline``
+  is measured on the same box as the headline;
+* ``amoebanet``: AmoebaNet-D(18,256), n{N}m32 at the reference balance (n1m32, B=640
+  at N=1), and at N=2 the reference's own denominator n2m1 (B=96, ``always``);
+* for N > 1, one extra *diagnostic* step (not timed) in which every rank measures
+  how long its streams waited for activations / gradients (``per_rank``).
 
 One process per GPU (``torch.distributed.run``), RCCL point-to-point between
 stages; fp32 like the reference.  Rank 0 prints one JSON line.
@@ -24,11 +35,12 @@ import json
 import os
 import sys
 import time
+from typing import Any, Callable, Dict, List, Optional
 
 if int(os.environ.get('WORLD_SIZE', '1')) > 1:
-    # One HIP hardware queue per stream: a rank runs its compute stream plus one RCCL
-    # stream per pipeline link (up to 6 on U-Net p8 with long skips).  With HIP's
-    # default of 4 queues, streams beyond that share a queue and their kernels
+    # One HIP hardware queue per stream: a rank runs its compute stream and lanes plus
+    # one RCCL stream per pipeline link (up to 6 on U-Net p8 with long skips).  With
+    # HIP's default of 4 queues, streams beyond that share a queue and their kernels
     # serialise, so a spinning RCCL receive could hold up unrelated work.  Set before
     # the HIP runtime initialises (first CUDA call).
     os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
@@ -45,9 +57,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # (fused and non-fused): candidates from the per-layer device times
 # (profiles/unet_layer_profile_m1.json, benchmarks/layer_profile.py), then rounds of
 # benchmarks/stage_harness.py measurements fed back through
-# scripts/balance_from_harness.py (profiles/stage_harness_nf_p{2,4,8}.json): measured max
-# stage p8 206 ms, p4 283 ms, p2 643 ms (the reference's P40 balances measured a 613 ms
-# max stage at p8 with the earlier kernels).
+# scripts/balance_from_harness.py (profiles/stage_harness_nf_p{2,4,8}.json).
 UNET_EXPERIMENTS = {
     1: dict(name='pipeline-1', batch=80, chunks=2, balance=[241], tuned=[241], ref=24.456),
     2: dict(name='pipeline-2', batch=512, chunks=32, balance=[104, 137], tuned=[102, 139],
@@ -57,6 +67,8 @@ UNET_EXPERIMENTS = {
     8: dict(name='pipeline-8', batch=640, chunks=40, balance=[16, 27, 31, 44, 22, 57, 27, 17],
             tuned=[22, 23, 26, 30, 22, 37, 43, 38], ref=88.497),
 }
+# the reference's speed-up denominator: U-Net without GPipe, one GPU
+UNET_BASELINE = dict(name='baseline', batch=40, ref=28.500)
 # AmoebaNet tuned balances: profiles/amoebanet_layer_profile.json (micro-batch 40) through
 # the same simulator (n2 535 vs 492, n4 851 vs 814, n8 1539 vs 1503 simulated samples/s).
 AMOEBA_EXPERIMENTS = {
@@ -67,6 +79,8 @@ AMOEBA_EXPERIMENTS = {
     8: dict(name='n8m32', batch=1280, chunks=32, balance=[2, 2, 2, 3, 3, 4, 4, 4],
             tuned=[2, 2, 3, 3, 3, 3, 4, 4], ref=132.413),
 }
+# the reference's AmoebaNet speed-up denominator (benchmarks/amoebanetd-speed/main.py:39-45)
+AMOEBA_N2M1 = dict(name='n2m1', batch=96, chunks=1, balance=[7, 17], ref=26.733)
 
 
 def parse() -> argparse.Namespace:
@@ -86,6 +100,16 @@ def parse() -> argparse.Namespace:
     p.add_argument('--also-tuned', choices=['auto', 'yes', 'no'], default='auto',
                    help="after the headline timing, time the MI355X-tuned balance too and "
                         "report it as the 'tuned' field (auto: when N > 1 and it differs)")
+    p.add_argument('--sections', default='auto',
+                   help="comma-separated extra timings after the headline: 'baseline' "
+                        "(U-Net without GPipe, B=40, rank 0), 'amoebanet' (AmoebaNet-D n{N}m32 "
+                        "and, at N=2, n2m1); 'auto' = both when the headline is U-Net; "
+                        "'none'")
+    p.add_argument('--section-steps', type=int, default=None,
+                   help='timed steps of each extra section (default: --steps)')
+    p.add_argument('--probe', choices=['auto', 'on', 'off'], default='auto',
+                   help='one extra untimed step in which every rank measures its receive '
+                        'waits (auto: N > 1)')
     p.add_argument('--timeout', type=float, default=300.0,
                    help='seconds any pipeline wait may take before the run fails (RCCL '
                         'watchdog and gloo waits): a dead or stuck rank ends the job')
@@ -96,7 +120,7 @@ def parse() -> argparse.Namespace:
                         "messages through host memory and lets several ranks share one GPU "
                         "(functional rehearsal only, not a valid measurement)")
     p.add_argument('--tiny', action='store_true',
-                   help='tiny model of the same family (CI smoke test of this script only)')
+                   help='tiny models of the same families (CI smoke test of this script only)')
     p.add_argument('--channels-last', action='store_true',
                    help='NHWC activations and weights (MIOpen NHWC kernels; AmoebaNet)')
     p.add_argument('--graph', action='store_true',
@@ -105,15 +129,14 @@ def parse() -> argparse.Namespace:
                         'AmoebaNet; parallel/graph.py)')
     p.add_argument('--cell-streams', choices=['auto', 'on', 'off'], default='auto',
                    help="AmoebaNet: run each cell's independent nodes on two HIP streams "
-                        '(auto: on for one-GPU runs)')
+                        '(auto: on)')
     p.add_argument('--overlap-recompute', choices=['auto', 'on', 'off'], default='auto',
                    help="recompute the next micro-batch on a second stream during this one's "
                         'backward (PipelineStage(overlap_recompute=True); auto: on for '
-                        'one-GPU U-Net runs)')
+                        'U-Net)')
     p.add_argument('--overlap-forward', choices=['auto', 'on', 'off'], default='auto',
-                   help='alternate the forward micro-batches of a one-rank stateless partition '
-                        '(no running statistics: U-Net) between two streams (auto: on for '
-                        'one-GPU U-Net runs)')
+                   help='alternate the forward micro-batches of a stateless partition (no '
+                        'running statistics: U-Net) between two streams (auto: on for U-Net)')
     p.add_argument('--wgrad-stream', choices=['auto', 'on', 'off'], default='auto',
                    help='run the fused ops\' weight-gradient GEMMs on a side stream '
                         '(PipelineStage(wgrad_stream=True); auto: off)')
@@ -127,47 +150,65 @@ def even_balance(layers: int, parts: int) -> list:
     return [base + (1 if i < extra else 0) for i in range(parts)]
 
 
-def main() -> None:
-    args = parse()
-    # stdout carries exactly one JSON line (rank 0).  Libraries print to fd 1
-    # from native code (gloo's "[Gloo] Rank r is connected to ..." banner, RCCL
-    # info): point fd 1 at stderr for the whole run and keep a private handle
-    # on the real stdout for the result.
-    sys.stdout.flush()
-    result_out = os.fdopen(os.dup(1), 'w')
-    os.dup2(2, 1)
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != args.gpus:
-        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU')
+def choice(value: str, auto: bool) -> bool:
+    return {'on': True, 'off': False}.get(value, auto)
 
-    gpu = torch.cuda.is_available()
-    rehearsal = args.backend == 'gloo' and gpu and world > 1
-    if gpu and not rehearsal and local_rank >= torch.cuda.device_count():
-        raise SystemExit(f'LOCAL_RANK {local_rank} but only {torch.cuda.device_count()} GPUs')
-    device = (torch.device('cuda', local_rank % torch.cuda.device_count()) if gpu
-              else torch.device('cpu'))
-    if gpu:
-        torch.cuda.set_device(device)
-        torch.backends.cudnn.benchmark = args.cudnn_benchmark
-    if world > 1:
-        # Lazy RCCL init: each pipeline link (peer pair) then gets its own
-        # communicator and stream on first use.
-        backend = 'nccl' if gpu and not rehearsal else 'gloo'
-        dist.init_process_group(backend, rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=args.timeout))
 
-    from torchgpipe_amd.models import amoebanetd, unet
-    from torchgpipe_amd.parallel import PipelineStage
+class Bench:
+    """One bench job: process-group setup, model builders and the timing loops."""
 
-    table = UNET_EXPERIMENTS if args.model == 'unet' else AMOEBA_EXPERIMENTS
+    def __init__(self, args: argparse.Namespace) -> None:
+        self.args = args
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+        if self.world != args.gpus:
+            raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={self.world}: '
+                             'launch one rank per GPU')
+        self.gpu = torch.cuda.is_available()
+        self.rehearsal = args.backend == 'gloo' and self.gpu and self.world > 1
+        if self.gpu and not self.rehearsal and local_rank >= torch.cuda.device_count():
+            raise SystemExit(f'LOCAL_RANK {local_rank} but only {torch.cuda.device_count()} GPUs')
+        self.device = (torch.device('cuda', local_rank % torch.cuda.device_count()) if self.gpu
+                       else torch.device('cpu'))
+        if self.gpu:
+            torch.cuda.set_device(self.device)
+            torch.backends.cudnn.benchmark = args.cudnn_benchmark
+        self.ctrl = None
+        if self.world > 1:
+            # Lazy RCCL init: each pipeline link (peer pair) then gets its own
+            # communicator and stream on first use.
+            backend = 'nccl' if self.gpu and not self.rehearsal else 'gloo'
+            timeout = datetime.timedelta(seconds=args.timeout)
+            dist.init_process_group(backend, rank=self.rank, world_size=self.world,
+                                    timeout=timeout)
+            self.ctrl = (dist.group.WORLD if backend == 'gloo'
+                         else dist.new_group(backend='gloo', timeout=timeout))
 
-    def build_model() -> torch.nn.Sequential:
-        # Built on the meta device: each rank materialises (random-initialises) only
-        # its own partition inside PipelineStage.
-        with torch.device('meta'):
-            if args.model == 'unet':
+    def log(self, msg: str) -> None:
+        if self.rank == 0:
+            print(f'[bench] {msg}', file=sys.stderr, flush=True)
+
+    def sync(self) -> None:
+        if self.world > 1:
+            dist.barrier()
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+
+    def ctrl_barrier(self) -> None:
+        if self.world > 1:
+            dist.barrier(group=self.ctrl)
+
+    # -- models -----------------------------------------------------------------------------
+
+    def build(self, kind: str, meta: bool = True) -> torch.nn.Sequential:
+        from torchgpipe_amd.models import amoebanetd, unet
+        args = self.args
+        ctx = torch.device('meta') if meta else torch.device(self.device)
+        # Built on the meta device for pipelines: each rank materialises (random-initialises)
+        # only its own partition inside PipelineStage.
+        with ctx:
+            if kind == 'unet':
                 if args.tiny:
                     return unet(depth=2, num_convs=1, base_channels=4, input_channels=3,
                                 output_channels=1, fused=not args.unfused)
@@ -177,20 +218,203 @@ def main() -> None:
                 return amoebanetd(num_classes=10, num_layers=3, num_filters=8)
             return amoebanetd(num_classes=1000, num_layers=18, num_filters=256)
 
-    n_layers = len(build_model())
-    if args.model == 'unet':
+    def data(self, kind: str, batch: int, first: bool, last: bool):
+        gen = torch.Generator(device=self.device).manual_seed(0)
+        if kind == 'unet':
+            shape = (3, 192, 192)
+            x = torch.rand(batch, *shape, device=self.device, generator=gen) if first else None
+            t = torch.ones(batch, 1, 192, 192, device=self.device) if last else None
+            return x, t, F.binary_cross_entropy_with_logits, shape
+        shape = (3, 224, 224)
+        x = torch.rand(batch, *shape, device=self.device, generator=gen) if first else None
+        t = (torch.randint(10 if self.args.tiny else 1000, (batch,), device=self.device,
+                           generator=gen) if last else None)
+        if x is not None and self.args.channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
+        return x, t, F.cross_entropy, shape
+
+    # -- timing -----------------------------------------------------------------------------
+
+    def timed(self, step: Callable[[], None], steps: int, warmup: int, tag: str,
+              settle: Optional[Callable[[], bool]] = None) -> Dict[str, float]:
+        """``warmup`` untimed steps (plus any until ``settle()``), then ``steps`` timed steps
+        bracketed by a barrier and a device sync; elapsed = MAX over ranks."""
+        t0 = time.time()
+        first_s = 0.0
+        for k in range(warmup):
+            step()
+            self.sync()
+            if k == 0:
+                first_s = time.time() - t0
+            self.log(f'{tag} warmup step {k + 1}/{warmup} done at {time.time() - t0:.1f}s')
+        while settle is not None and not settle():  # e.g. a hipGraph capture: untimed
+            step()
+            self.sync()
+        warm_s = time.time() - t0
+        self.sync()
+        start = time.perf_counter()
+        for _ in range(steps):
+            step()
+        self.sync()
+        elapsed = time.perf_counter() - start
+        if self.world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        self.log(f'{tag}: {steps} steps in {elapsed:.3f}s')
+        return {'elapsed': elapsed, 'warm_s': warm_s, 'first_step_s': first_s}
+
+    def pipeline(self, kind: str, exp: Dict[str, Any], balance: List[int], checkpoint: str,
+                 steps: int, tag: str, probe: bool = False) -> Dict[str, Any]:
+        """Build the PipelineStage for ``balance``, warm up, time ``steps`` SGD steps."""
+        from torchgpipe_amd.parallel import PipelineStage
+        from torchgpipe_amd.parallel.stage import signature_of
+        args = self.args
+        batch, chunks = exp['batch'], exp['chunks']
+        unet = kind == 'unet'
+        # Intra-rank stream concurrency: U-Net alternates forward micro-batches between two
+        # lanes and recomputes the next micro-batch beside the current backward; AmoebaNet
+        # runs each cell's independent branches on two streams (its recompute lane cost 19 %
+        # on one GPU: profiles/r2/bench_amoeba_s13.md).  Multi-rank runs keep them: sends
+        # leave from the lane that computed them and backward passes are ordered across
+        # lanes (parallel/stage.py), parity-tested on shared-GPU gloo rehearsals.
+        overlap = choice(args.overlap_recompute, self.gpu and unet)
+        overlap_fwd = choice(args.overlap_forward, self.gpu and unet)
+        cell_streams = not unet and choice(args.cell_streams, self.gpu)
+        # (auto: off -- with the two-stream cells it measured 280.3 vs 328.6 samples/s on one
+        # box, profiles/r2/bench_amoeba_s13.md)
+        wgrad_stream = choice(args.wgrad_stream, False)
+        stage = PipelineStage(self.build(kind), balance, device=self.device, chunks=chunks,
+                              checkpoint=checkpoint, timeout=args.timeout,
+                              overlap_recompute=overlap, overlap_forward=overlap_fwd,
+                              wgrad_stream=wgrad_stream)
+        if args.channels_last and not unet:
+            stage.partition.to(memory_format=torch.channels_last)
+        if cell_streams:
+            from torchgpipe_amd.models.amoebanet import set_cell_streams
+            set_cell_streams(stage.partition, True)
+        optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
+        x, target, loss_fn, shape = self.data(kind, batch, stage.is_first, stage.is_last)
+        signature = signature_of(torch.empty(batch, *shape, device='meta'))
+
+        graph = None
+        if args.graph and tag == 'headline':
+            if self.world != 1:
+                raise SystemExit('--graph captures one-rank runs only')
+            from torchgpipe_amd.parallel import StepGraph
+            graph = StepGraph(stage, loss_fn, optimizer, warmup=max(1, args.warmup - 1))
+
+        def step() -> None:
+            if graph is not None:
+                graph.step(x, target)  # type: ignore[arg-type]
+                return
+            stage.train_step(x, target, loss_fn, signature=signature)
+            optimizer.step()
+            optimizer.zero_grad(set_to_none=True)
+
+        if self.gpu:
+            torch.cuda.reset_peak_memory_stats(self.device)
+        res: Dict[str, Any] = self.timed(
+            step, steps, args.warmup, tag,
+            settle=(lambda: graph.captured) if graph is not None else None)
+        res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
+                   steps=steps, cell_streams=cell_streams, overlap_recompute=overlap,
+                   overlap_forward=overlap_fwd, wgrad_stream=wgrad_stream)
+        if probe and graph is None:
+            # one untimed diagnostic step: per-rank receive waits and busy time
+            mine = stage.probe_step(step)
+            mine['rank'] = self.rank
+            gathered: List[Any] = [None] * self.world
+            if self.world > 1:
+                dist.all_gather_object(gathered, mine, group=self.ctrl)
+            else:
+                gathered = [mine]
+            res['per_rank'] = gathered
+        if args.profile_steps and self.rank == 0 and tag == 'headline':
+            from torch.profiler import ProfilerActivity, profile
+            acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if self.gpu else [])
+            with profile(activities=acts) as prof:
+                for _ in range(args.profile_steps):
+                    step()
+                self.sync()
+            print(prof.key_averages().table(
+                sort_by='cuda_time_total' if self.gpu else 'cpu_time_total', row_limit=30),
+                file=sys.stderr)
+        res['mem'] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30 if self.gpu else 0.0
+        del stage, optimizer, x, target, graph
+        if self.gpu:
+            torch.cuda.empty_cache()
+        return res
+
+    def plain(self, kind: str, batch: int, steps: int, tag: str) -> Optional[Dict[str, Any]]:
+        """The model without GPipe (no micro-batches, no checkpointing) on rank 0's GPU,
+        SGD like the pipelines: the reference's ``baseline`` experiment.  Other ranks wait."""
+        res = None
+        self.ctrl_barrier()
+        if self.rank == 0:
+            from torchgpipe_amd.ops.conv import new_step
+            model = self.build(kind, meta=False)
+            optimizer = torch.optim.SGD(model.parameters(), lr=0.1)
+            x, target, loss_fn, _ = self.data(kind, batch, True, True)
+
+            def step() -> None:
+                new_step()
+                loss = loss_fn(model(x), target)
+                loss.backward()
+                optimizer.step()
+                optimizer.zero_grad(set_to_none=True)
+
+            world, self.world = self.world, 1  # rank 0 alone: no collective in its timing
+            try:
+                res = self.timed(step, steps, self.args.warmup, tag)
+            finally:
+                self.world = world
+            res.update(batch=batch, steps=steps)
+            del model, optimizer, x, target
+            if self.gpu:
+                torch.cuda.empty_cache()
+        self.ctrl_barrier()
+        return res
+
+
+def summary(res: Dict[str, Any], ref: Optional[float]) -> Dict[str, Any]:
+    value = res['batch'] * res['steps'] / res['elapsed']
+    out = {'value': round(value, 3), 'ms_per_step': round(1000 * res['elapsed'] / res['steps'], 3),
+           'steps': res['steps'], 'batch': res['batch']}
+    if 'chunks' in res:
+        out.update(chunks=res['chunks'], balance=res['balance'], checkpoint=res['checkpoint'])
+    out['vs_p40'] = round(value / ref, 3) if ref else None
+    return out
+
+
+def main() -> None:
+    args = parse()
+    # stdout carries exactly one JSON line (rank 0).  Libraries print to fd 1
+    # from native code (gloo's "[Gloo] Rank r is connected to ..." banner, RCCL
+    # info): point fd 1 at stderr for the whole run and keep a private handle
+    # on the real stdout for the result.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), 'w')
+    os.dup2(2, 1)
+    b = Bench(args)
+    world = b.world
+
+    kind = args.model
+    n_layers = len(b.build(kind))
+    table = UNET_EXPERIMENTS if kind == 'unet' else AMOEBA_EXPERIMENTS
+    if kind == 'unet':
         exp = dict(table.get(world) or dict(name=f'pipeline-{world}', batch=80 * world,
                                             chunks=4 * world,
                                             balance=even_balance(n_layers, world), ref=None))
-        in_shape = (3, 192, 192)
         checkpoint = 'except_last'
         model_name = 'U-Net(5,64)'
+        in_shape = '3x192x192'
     else:
         exp = dict(table.get(world) or dict(name=f'n{world}m32', batch=160 * world, chunks=32,
                                             balance=even_balance(n_layers, world), ref=None))
-        in_shape = (3, 224, 224)
         checkpoint = 'except_last' if exp['chunks'] > 1 else 'always'
         model_name = 'AmoebaNet-D(18,256)'
+        in_shape = '3x224x224'
     if args.tiny:
         exp['balance'] = exp['tuned'] = even_balance(n_layers, world)
     if args.checkpoint:
@@ -205,131 +429,59 @@ def main() -> None:
     elif args.balance != 'ref':
         exp['balance'] = [int(v) for v in args.balance.split(',')]
     batch, chunks, balance = exp['batch'], exp['chunks'], list(exp['balance'])
-    # Intra-rank stream concurrency (measured on one GPU; multi-rank runs keep the
-    # one-stream schedule that the RCCL rehearsals exercised)
-    # (auto: U-Net only -- AmoebaNet's two-stream cells already fill the CUs, and the extra
-    # recompute lane cost it 19 %: profiles/r2/bench_amoeba_s13.md)
-    overlap = {'on': True, 'off': False}.get(args.overlap_recompute,
-                                             world == 1 and gpu and args.model == 'unet')
-    cell_streams = args.model == 'amoebanet' and {'on': True, 'off': False}.get(
-        args.cell_streams, world == 1 and gpu)
-    # (auto: off -- with the two-stream cells it measured 280.3 vs 328.6 samples/s on one box,
-    # profiles/r2/bench_amoeba_s13.md)
-    wgrad_stream = {'on': True, 'off': False}.get(args.wgrad_stream, False)
-    overlap_fwd = {'on': True, 'off': False}.get(args.overlap_forward,
-                                                 world == 1 and gpu and args.model == 'unet')
+    probe = choice(args.probe, world > 1)
 
-    def sync() -> None:
-        if world > 1:
-            dist.barrier()
-        if gpu:
-            torch.cuda.synchronize(device)
-
-    def measure(balance: list, tag: str) -> dict:
-        """Build the stage for ``balance``, warm up, time ``--steps`` full SGD steps."""
-        stage = PipelineStage(build_model(), balance, device=device, chunks=chunks,
-                              checkpoint=checkpoint, timeout=args.timeout,
-                              overlap_recompute=overlap, overlap_forward=overlap_fwd,
-                              wgrad_stream=wgrad_stream)
-        if args.channels_last:
-            stage.partition.to(memory_format=torch.channels_last)
-        if cell_streams:
-            from torchgpipe_amd.models.amoebanet import set_cell_streams
-            set_cell_streams(stage.partition, True)
-        optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
-
-        gen = torch.Generator(device=device).manual_seed(0)
-        x = torch.rand(batch, *in_shape, device=device, generator=gen) if stage.is_first else None
-        if x is not None and args.channels_last:
-            x = x.contiguous(memory_format=torch.channels_last)
-        if args.model == 'unet':
-            target = torch.ones(batch, 1, 192, 192, device=device) if stage.is_last else None
-            loss_fn = F.binary_cross_entropy_with_logits
-        else:
-            target = (torch.randint(10 if args.tiny else 1000, (batch,), device=device,
-                                    generator=gen) if stage.is_last else None)
-            loss_fn = F.cross_entropy
-        from torchgpipe_amd.parallel.stage import signature_of
-        signature = signature_of(torch.empty(batch, *in_shape, device='meta'))
-
-        graph = None
-        if args.graph:
-            if world != 1:
-                raise SystemExit('--graph captures one-rank runs only')
-            from torchgpipe_amd.parallel import StepGraph
-            graph = StepGraph(stage, loss_fn, optimizer, warmup=max(1, args.warmup - 1))
-
-        def step() -> None:
-            if graph is not None:
-                graph.step(x, target)  # type: ignore[arg-type]
-                return
-            stage.train_step(x, target, loss_fn, signature=signature)
-            optimizer.step()
-            optimizer.zero_grad(set_to_none=True)
-
-        if gpu:
-            torch.cuda.reset_peak_memory_stats(device)
-        t0 = time.time()
-        first_s = 0.0
-        for k in range(args.warmup):
-            step()
-            sync()
-            if k == 0:
-                first_s = time.time() - t0
-            if rank == 0:
-                print(f'[bench] {tag} warmup step {k + 1}/{args.warmup} done at '
-                      f'{time.time() - t0:.1f}s', file=sys.stderr, flush=True)
-        while graph is not None and not graph.captured:  # the capture stays untimed
-            step()
-            sync()
-        warm_s = time.time() - t0
-
-        sync()
-        start = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        sync()
-        elapsed = time.perf_counter() - start
-
-        if world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
-
-        if args.profile_steps and rank == 0 and tag == 'headline':
-            from torch.profiler import ProfilerActivity, profile
-            acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if gpu else [])
-            with profile(activities=acts) as prof:
-                for _ in range(args.profile_steps):
-                    step()
-                sync()
-            print(prof.key_averages().table(
-                sort_by='cuda_time_total' if gpu else 'cpu_time_total', row_limit=30),
-                file=sys.stderr)
-        mem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if gpu else 0.0
-        del stage, optimizer, x, target
-        if gpu:
-            torch.cuda.empty_cache()
-        return {'elapsed': elapsed, 'warm_s': warm_s, 'first_step_s': first_s, 'mem': mem}
-
-    main_run = measure(balance, 'headline')
-    elapsed, warm_s = main_run['elapsed'], main_run['warm_s']
+    main_run = b.pipeline(kind, exp, balance, checkpoint, args.steps, 'headline', probe=probe)
+    elapsed = main_run['elapsed']
     tuned = None
     also = args.also_tuned == 'yes' or (args.also_tuned == 'auto' and world > 1
                                          and args.balance == 'ref' and tuned_balance != balance)
     if also:
-        t = measure(tuned_balance, 'tuned')
+        t = b.pipeline(kind, exp, tuned_balance, checkpoint, args.steps, 'tuned')
         tuned = {'balance': tuned_balance,
                  'value': round(batch * args.steps / t['elapsed'], 3),
                  'ms_per_step': round(1000 * t['elapsed'] / args.steps, 3)}
 
+    sections = ({'baseline', 'amoebanet'} if kind == 'unet' else set()) \
+        if args.sections == 'auto' else \
+        (set() if args.sections == 'none' else set(args.sections.split(',')))
+    sec_steps = args.section_steps or args.steps
     samples_per_s = batch * args.steps / elapsed
-    if rank == 0:
+
+    baseline = None
+    if 'baseline' in sections and kind == 'unet':
+        bl = b.plain('unet', 4 if args.tiny else UNET_BASELINE['batch'], sec_steps, 'baseline')
+        if bl is not None:
+            baseline = summary(bl, None if args.tiny else UNET_BASELINE['ref'])
+            baseline['experiment'] = 'baseline (no GPipe, rank 0 GPU)'
+
+    amoeba = None
+    if 'amoebanet' in sections and kind == 'unet':
+        a_layers = len(b.build('amoebanet'))
+        aexp = dict(AMOEBA_EXPERIMENTS.get(world) or dict(
+            name=f'n{world}m32', batch=160 * world, chunks=32,
+            balance=even_balance(a_layers, world), ref=None))
+        if args.tiny:
+            aexp.update(batch=4, chunks=2, balance=even_balance(a_layers, world))
+        ar = b.pipeline('amoebanet', aexp, aexp['balance'],
+                        'except_last' if aexp['chunks'] > 1 else 'always', sec_steps,
+                        'amoebanet')
+        amoeba = summary(ar, None if args.tiny else aexp['ref'])
+        amoeba['experiment'] = aexp['name']
+        amoeba['cell_streams'] = ar['cell_streams']
+        if world == 2:
+            d = dict(AMOEBA_N2M1)
+            if args.tiny:
+                d.update(batch=4, balance=even_balance(a_layers, 2))
+            dr = b.pipeline('amoebanet', d, d['balance'], 'always', sec_steps, 'amoebanet-n2m1')
+            amoeba['n2m1'] = summary(dr, None if args.tiny else d['ref'])
+            amoeba['speedup_vs_n2m1'] = round(amoeba['value'] / amoeba['n2m1']['value'], 3)
+
+    if b.rank == 0:
         ref = None if args.tiny else exp.get('ref')
         if args.tiny:
             model_name += ' TINY smoke-test variant (not a measurement)'
-        mem = main_run['mem']
-        print(json.dumps({
+        record = {
             'metric': f'{model_name} GPipe training throughput (samples/sec)',
             'value': round(samples_per_s, 3),
             'unit': 'samples/sec',
@@ -347,28 +499,38 @@ def main() -> None:
                 'experiment': exp['name'],
                 'global_batch': batch,
                 'seq_len': None,
-                'input': 'x'.join(map(str, in_shape)),
+                'input': in_shape,
                 'chunks': chunks,
                 'balance': balance,
                 'balance_source': args.balance,
                 'checkpoint': checkpoint,
                 'parallelism': f'pp{world}',
-                'transport': 'gloo-host-staged (rehearsal)' if rehearsal else
-                             ('rccl' if gpu and world > 1 else 'none'),
-                'fused_cells': args.model == 'unet' and not args.unfused,
+                'transport': 'gloo-host-staged (rehearsal)' if b.rehearsal else
+                             ('rccl' if b.gpu and world > 1 else 'none'),
+                'fused_cells': kind == 'unet' and not args.unfused,
                 'baseline_samples_per_sec_p40': ref,
-                'rank0_peak_mem_gib': round(mem, 2),
-                'warmup_s': round(warm_s, 1),
+                'rank0_peak_mem_gib': round(main_run['mem'], 2),
+                'warmup_s': round(main_run['warm_s'], 1),
                 'first_step_s': round(main_run['first_step_s'], 2),
                 'timeout_s': args.timeout,
                 'hipgraph': bool(args.graph),
-                'cell_streams': cell_streams,
-                'overlap_recompute': overlap,
-                'wgrad_stream': wgrad_stream,
-                'overlap_forward': overlap_fwd,
+                'cell_streams': main_run['cell_streams'],
+                'overlap_recompute': main_run['overlap_recompute'],
+                'wgrad_stream': main_run['wgrad_stream'],
+                'overlap_forward': main_run['overlap_forward'],
             },
             'tuned': tuned,
-        }), file=result_out, flush=True)
+        }
+        if baseline is not None:
+            # same-box speed-up over the reference's own denominator (no GPipe, B=40)
+            record['baseline_samples_per_sec'] = baseline['value']
+            record['speedup_vs_baseline'] = round(samples_per_s / baseline['value'], 3)
+            record['baseline'] = baseline
+        if amoeba is not None:
+            record['amoebanet'] = amoeba
+        if 'per_rank' in main_run:
+            record['per_rank'] = main_run['per_rank']
+        print(json.dumps(record), file=result_out, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -76,12 +76,28 @@ def reference(kind: str, device: torch.device, chunks: int):
 
 
 def stage_worker(rank: int, world: int, kind: str, chunks: int, checkpoint: str,
-                 device_type: str):
-    """One rank: two training steps (the second on cached message metadata)."""
+                 device_type: str, options: dict = None):
+    """One rank: two training steps (the second on cached message metadata).
+
+    ``device_type``: 'cpu', 'cuda' (rank r on cuda:r) or 'cuda-shared' (every rank on
+    cuda:0, host-staged gloo transport: the one-GPU rehearsal of a multi-rank run, which
+    exercises the stage's stream logic -- lanes, two-stream cells -- for real).
+    ``options``: extra PipelineStage keywords, plus ``cell_streams`` (AmoebaNet).
+    """
     from torchgpipe_amd.parallel import PipelineStage
-    device = torch.device('cuda', rank) if device_type == 'cuda' else torch.device('cpu')
+    options = dict(options or {})
+    cell_streams = options.pop('cell_streams', False)
+    if device_type == 'cuda':
+        device = torch.device('cuda', rank)
+    elif device_type == 'cuda-shared':
+        device = torch.device('cuda', 0)
+    else:
+        device = torch.device('cpu')
     stage = PipelineStage(build(kind), balance(kind, world), device=device, chunks=chunks,
-                          checkpoint=checkpoint, timeout=60)
+                          checkpoint=checkpoint, timeout=60, **options)
+    if cell_streams:
+        from torchgpipe_amd.models.amoebanet import set_cell_streams
+        set_cell_streams(stage.partition, True)
     x, t = data(kind, device)
     loss = None
     for _ in range(2):

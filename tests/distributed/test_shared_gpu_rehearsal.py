@@ -1,0 +1,40 @@
+"""Multi-rank pipelines with intra-rank stream overlap, rehearsed on ONE GPU.
+
+Two or three ranks share ``cuda:0`` and exchange host-staged messages over gloo, so
+every stream decision of :class:`~torchgpipe_amd.parallel.PipelineStage` runs on a real
+device: forward lanes (micro-batches alternating between two streams, their sends
+leaving from the lane), the recompute lane beside the gradient receive, backward
+ordering across lanes (the fused ops add into ``.grad`` outside autograd) and
+AmoebaNet's two-stream cells.  Gradients of every rank and the loss are checked
+against the whole model on one GPU with the same micro-batching
+(``tests/distributed/parity.py``).  These are the schedules ``bench.py`` runs on
+multi-GPU nodes over RCCL.
+"""
+import pytest
+import torch
+
+from tests.distributed import parity
+from tests.distributed.mp_util import run
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ('unet', 'except_last', dict(overlap_recompute=True, overlap_forward=True)),
+    ('unet', 'except_last', dict(overlap_forward=True)),
+    ('unet', 'never', dict(overlap_forward=True)),
+    ('unet', 'always', dict(overlap_recompute=True)),
+    ('amoebanet', 'except_last', dict(cell_streams=True)),
+    ('amoebanet', 'except_last', dict(cell_streams=True, overlap_recompute=True)),
+]
+
+
+@pytest.mark.parametrize('kind,checkpoint,options', CASES,
+                         ids=[f'{k}-{c}-{"+".join(o)}' for k, c, o in CASES])
+def test_overlapped_stage_matches_one_gpu(tmp_path, kind, checkpoint, options):
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    chunks = 3
+    results = run(parity.stage_worker, 2, tmp_path, kind, chunks, checkpoint, 'cuda-shared',
+                  options, backend='gloo', timeout=120)
+    grads, loss = parity.reference(kind, torch.device('cuda', 0), chunks)
+    parity.assert_parity(results, grads, loss, rel=1e-4)

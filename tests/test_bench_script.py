@@ -50,6 +50,23 @@ def test_bench_json_contract(nproc, model):
     assert 'TINY' in rec['metric'] and rec['vs_baseline'] is None
     # value is the whole-job aggregate: batch * steps / elapsed
     assert rec['value'] == pytest.approx(4 * 1000 / rec['ms_per_step'], rel=1e-2)
+    if model == 'unet':
+        # same-box speed-up denominator and the AmoebaNet section ride along
+        assert rec['baseline']['value'] > 0 and rec['speedup_vs_baseline'] > 0
+        assert rec['speedup_vs_baseline'] == pytest.approx(
+            rec['value'] / rec['baseline_samples_per_sec'], rel=1e-2)
+        amoeba = rec['amoebanet']
+        assert amoeba['value'] > 0 and amoeba['steps'] == 1
+        if nproc == 2:
+            assert amoeba['n2m1']['chunks'] == 1 and amoeba['speedup_vs_n2m1'] > 0
+    if nproc > 1:
+        ranks = rec['per_rank']
+        assert [r['rank'] for r in ranks] == list(range(nproc))
+        for r in ranks:
+            assert r['step_ms'] > 0 and r['busy_ms'] <= r['step_ms'] + 1e-6
+            assert min(r['fwd_wait_ms'], r['bwd_wait_ms'], r['fill_ms'], r['drain_ms']) >= 0
+        # rank 1 waits for rank 0's activations, rank 0 for rank 1's gradients
+        assert ranks[1]['fwd_wait_ms'] > 0 and ranks[0]['bwd_wait_ms'] > 0
 
 
 def test_bench_headline_uses_reference_balance_and_reports_tuned():

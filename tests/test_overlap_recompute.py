@@ -32,10 +32,16 @@ def _close_grads(a: nn.Module, b: nn.Module) -> None:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('model_name,checkpoint', [('unet', 'except_last'),
-                                                   ('unet', 'always'),
-                                                   ('amoebanet', 'except_last')])
-def test_overlapped_recompute_matches_inline(model_name, checkpoint):
+@pytest.mark.parametrize('model_name,checkpoint,recompute', [
+    ('unet', 'except_last', True),
+    ('unet', 'always', True),
+    ('amoebanet', 'except_last', True),
+    # forward lanes alone: the non-checkpointed cells' backward passes run on the two
+    # lanes and must still be ordered (fused ops add into .grad outside autograd)
+    ('unet', 'except_last', False),
+    ('unet', 'never', False),
+])
+def test_overlapped_recompute_matches_inline(model_name, checkpoint, recompute):
     """Same losses and gradients with the recomputation on two lanes as inline, over three
     steps (U-Net: Philox dropout replayed from the tape on the lane; AmoebaNet: fused
     ops writing .grad from the lanes)."""
@@ -51,7 +57,7 @@ def test_overlapped_recompute_matches_inline(model_name, checkpoint):
     a, b = copy.deepcopy(base), copy.deepcopy(base)
     sa = PipelineStage(a, [len(a)], device=dev, chunks=4, checkpoint=checkpoint)
     sb = PipelineStage(b, [len(b)], device=dev, chunks=4, checkpoint=checkpoint,
-                       overlap_recompute=True, overlap_forward=True)
+                       overlap_recompute=recompute, overlap_forward=True)
     gen = torch.Generator(device=dev).manual_seed(7)
     for _ in range(3):
         x = torch.rand(8, *shape, device=dev, generator=gen)

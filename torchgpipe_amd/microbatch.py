@@ -204,18 +204,24 @@ class Gatherer:
             for t, b in zip(tensors, self.buffers):
                 b[lo:hi].copy_(t.detach(), non_blocking=True)
                 record_stream(t, side)  # type: ignore[arg-type]
+                # the buffers were allocated on the compute stream: keep them alive until
+                # the side stream's copies are done, even if result() falls back
+                record_stream(b, side)  # type: ignore[arg-type]
         self.used.append(side)
 
     def result(self, outputs: List[Batch]) -> TensorOrTensors:
         from torchgpipe_amd.stream import current_stream, wait_stream
+        if self.buffers is not None:
+            # fence the side-stream copies on both return paths (a later micro-batch may
+            # have failed the shape check after earlier ones were already queued)
+            compute = current_stream(self.buffers[0].device)
+            seen = set()
+            for side in self.used:
+                if id(side) not in seen:
+                    seen.add(id(side))
+                    wait_stream(compute, side)  # type: ignore[arg-type]
         if not self.ok or self.buffers is None:
             return gather(outputs)
-        compute = current_stream(self.buffers[0].device)
-        seen = set()
-        for side in self.used:
-            if id(side) not in seen:
-                seen.add(id(side))
-                wait_stream(compute, side)  # type: ignore[arg-type]
         flat = [t for b in outputs for t in b]
         out = _GatherInto.apply(self.bounds, len(self.buffers), *self.buffers, *flat)
         return out[0] if self.atomic else tuple(out)

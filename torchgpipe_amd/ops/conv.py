@@ -42,9 +42,13 @@ _BUDGET: Optional[int] = None
 
 
 def new_step() -> None:
-    """Start a new pipeline step: every cached weight transform is re-validated."""
+    """Start a new pipeline step: every cached weight transform is re-validated, and the
+    ``AccumulateGrad`` nodes pinned by the previous step's fused backward are released
+    (``ops/gradacc.py``), so this step's graph gets nodes bound to its own streams."""
     global _STEP
     _STEP += 1
+    from torchgpipe_amd.ops import gradacc
+    gradacc.release()
 
 
 def cache_bytes() -> int:

@@ -72,31 +72,42 @@ def _bn_ok(bn: nn.Module, x: Tensor) -> bool:
             and (bn.momentum is not None or not bn.track_running_stats))
 
 
-_WGRAD = {'enabled': False}
+# devices whose backward currently runs weight gradients on a side stream -> scope depth
+_WGRAD: Dict[torch.device, int] = {}
 _WGRAD_STREAMS: Dict[torch.device, torch.cuda.Stream] = {}
 
 
 @contextlib.contextmanager
-def wgrad_stream_scope(enabled: bool = True) -> Iterator[None]:
-    """While active (process-wide: autograd runs backward on its own threads), fused ops
-    whose weight gradients are accumulated by the kernels themselves (``ops/gradacc.py``)
-    run the weight-gradient GEMMs on a per-device side stream, concurrently with the
-    backward chain (BatchNorm backward, backward-data) that continues on the op's stream.
-    On exit the caller's current stream waits for the side streams, so the gradients are
-    ready for the optimizer.  Not used inside hipGraph captures.
-"""
-    prev = _WGRAD['enabled']
-    _WGRAD['enabled'] = enabled
+def wgrad_stream_scope(device: torch.device, enabled: bool = True) -> Iterator[None]:
+    """While active for ``device`` (read on autograd's device threads, so keyed by device
+    rather than by thread), fused ops on that device whose weight gradients are
+    accumulated by the kernels themselves (``ops/gradacc.py``) run the weight-gradient
+    GEMMs on a per-device side stream, concurrently with the backward chain (BatchNorm
+    backward, backward-data) that continues on the op's stream.  Pipelines on other
+    devices of the process are unaffected.  On exit the caller's current stream on
+    ``device`` waits for that side stream, so the gradients are ready for the optimizer.
+    Not used inside hipGraph captures.
+    """
+    device = torch.device(device)
+    if device.type == 'cuda' and device.index is None:
+        device = torch.device('cuda', torch.cuda.current_device())
+    if not enabled:
+        yield
+        return
+    _WGRAD[device] = _WGRAD.get(device, 0) + 1
     try:
         yield
     finally:
-        _WGRAD['enabled'] = prev
-        for device, stream in _WGRAD_STREAMS.items():
+        _WGRAD[device] -= 1
+        if not _WGRAD[device]:
+            del _WGRAD[device]
+        stream = _WGRAD_STREAMS.get(device)
+        if stream is not None:
             torch.cuda.current_stream(device).wait_stream(stream)
 
 
 def _wgrad_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
-    if not _WGRAD['enabled'] or device.type != 'cuda' or torch.cuda.is_current_stream_capturing():
+    if device not in _WGRAD or device.type != 'cuda' or torch.cuda.is_current_stream_capturing():
         return None
     stream = _WGRAD_STREAMS.get(device)
     if stream is None:

@@ -19,17 +19,27 @@ It only applies when the result is indistinguishable from autograd's:
 * an existing ``.grad`` is a plain contiguous fp32 tensor on the same device.
 
 ``TGPIPE_FUSED_GRAD_ACCUM=0`` turns it off (plain autograd accumulation).
+
+The parameter's ``AccumulateGrad`` node is looked up once per step and pinned on the
+parameter until :func:`release` (called when the next pipeline step starts,
+``ops.conv.new_step``).  Pinning it longer would hand the next step's forward the old
+node, which PyTorch bound to the stream it was created on: under forward / recompute
+lanes that node's stream differs from the producer's, and the engine then warns ("The
+AccumulateGrad node's stream does not match ...") and inserts cross-stream syncs.
 """
 import os
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
+import weakref
 
 import torch
 from torch import Tensor
 
-__all__ = ['target', 'commit', 'enabled']
+__all__ = ['target', 'commit', 'enabled', 'release']
 
 _ENABLED = os.environ.get('TGPIPE_FUSED_GRAD_ACCUM', '1') != '0'
 _ATTR = '_tgpipe_grad_accumulator'
+# id(param) -> weak reference (tensors compare elementwise, so no WeakSet)
+_PINNED: Dict[int, 'weakref.ref[Tensor]'] = {}
 
 
 def enabled() -> bool:
@@ -44,9 +54,19 @@ def _accumulator(param: Tensor) -> Optional[object]:
         if fn is None or not fn.next_functions:
             return None
         node = fn.next_functions[0][0]
-        # the tensor only holds its AccumulateGrad weakly; keep it alive with the parameter
+        # the tensor only holds its AccumulateGrad weakly; keep it for the rest of the step
         setattr(param, _ATTR, node)
+        _PINNED[id(param)] = weakref.ref(param)
     return node
+
+
+def release() -> None:
+    """Drop every pinned ``AccumulateGrad`` node (start of a new step)."""
+    for ref in _PINNED.values():
+        param = ref()
+        if param is not None and hasattr(param, _ATTR):
+            delattr(param, _ATTR)
+    _PINNED.clear()
 
 
 def target(param: Optional[Tensor]) -> Tuple[bool, Optional[Tensor]]:

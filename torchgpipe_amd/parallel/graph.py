@@ -26,11 +26,23 @@ Requirements, checked up front:
 
 Each replay computes the step's gradients from scratch (the first micro-batch writes
 ``param.grad``, later ones accumulate), i.e. the eager step that follows
-``optimizer.zero_grad()``; ``param.grad`` holds them after the replay.  Shapes first met
-inside the capture would run the implicit-GEMM kernels' heuristic plans, which is why the
-warm-up steps (which autotune them) come first.
+``optimizer.zero_grad()``; ``param.grad`` holds them after the replay.
+
+What a replay does not see, and how it is handled:
+
+* ``.grad`` ownership: the gradients live in the graph's memory pool.  Replays write
+  those tensors whatever ``param.grad`` points to, so :meth:`StepGraph.step` re-attaches
+  them before each replay (a ``zero_grad(set_to_none=True)`` in between is harmless).
+* Optimizer hyperparameters are baked into the captured kernels as constants: an LR
+  scheduler or a change to ``param_groups`` after the capture would be silently ignored.
+  The scalar hyperparameters are snapshotted at capture and every replay checks them;
+  a change raises instead of training with stale values (re-create the StepGraph, or use
+  an optimizer built with ``capturable=True`` and tensor hyperparameters).
+
+Shapes first met inside the capture would run the implicit-GEMM kernels' heuristic plans,
+which is why the warm-up steps (which autotune them) come first.
 """
-from typing import Callable, List, Optional
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -86,6 +98,8 @@ class StepGraph:
         self._input: Optional[Tensor] = None
         self._target: Optional[Tensor] = None
         self._loss: Optional[Tensor] = None
+        self._grads: List[Tuple[Tensor, Tensor]] = []
+        self._hyper: List[Dict[str, object]] = []
 
     @property
     def captured(self) -> bool:
@@ -134,6 +148,14 @@ class StepGraph:
         if self._graph is None:
             self._capture(input, target)
         assert self._graph is not None and self._input is not None and self._target is not None
+        if self._hyperparameters() != self._hyper:
+            raise RuntimeError('StepGraph: optimizer hyperparameters changed since the capture '
+                               '(the replay would keep the captured values); re-create the '
+                               'StepGraph or use a capturable optimizer with tensor '
+                               'hyperparameters')
+        for param, grad in self._grads:
+            if param.grad is not grad:
+                param.grad = grad
         if input is not self._input:
             self._input.copy_(input)
         if target is not self._target:
@@ -153,6 +175,16 @@ class StepGraph:
         self._zero_grad()
         torch.cuda.synchronize(device)
         graph = torch.cuda.CUDAGraph()
+        self._hyper = self._hyperparameters()
         with torch.cuda.graph(graph):
             self._loss = self._eager(self._input, self._target)
         self._graph = graph
+        self._grads = [(p, p.grad) for p in self.stage.parameters() if p.grad is not None]
+
+    def _hyperparameters(self) -> List[Dict[str, object]]:
+        """The optimizer's scalar hyperparameters, per parameter group."""
+        if self.optimizer is None:
+            return []
+        return [{k: v for k, v in group.items()
+                 if k != 'params' and isinstance(v, (int, float, bool, tuple, str, type(None)))}
+                for group in self.optimizer.param_groups]

@@ -30,6 +30,7 @@ output tensors + skips stashed for other ranks, so checkpointing
 from collections import OrderedDict
 import contextlib
 import datetime
+import time
 from typing import Any, Callable, Dict, Hashable, List, Optional, Sequence, Tuple, Union
 
 import torch
@@ -258,6 +259,7 @@ class PipelineStage:
                              and m.track_running_stats for m in self.partition.modules())
         self._sig: Optional[Signature] = None
         self._m = 0
+        self._probe: Optional[List[Tuple[str, Any, Any]]] = None
         if distributed and self.n > 1:
             self.connect()
 
@@ -459,12 +461,14 @@ class PipelineStage:
                 in_atomic = True
             skip_msgs = [self.p2p.recv(self.ranks[src], self._key('skip', i, self.ranks[src], me))
                          for src in sorted({s for s, _ in self.in_skips})]
+            mark = self._probe_begin() if act_msg is not None or skip_msgs else None
             if act_msg is not None:
                 acts = act_msg.wait()
                 in_atomic = act_msg.atomic
             popped: List[Tensor] = []
             for msg in skip_msgs:
                 popped += msg.wait()
+            self._probe_end('fwd', mark)
             flat = list(acts) + popped
             cell.inputs = flat
 
@@ -489,21 +493,24 @@ class PipelineStage:
                 for t in out:
                     t.record_stream(main)
                 if cell.chk is None:
-                    cell.lane = lane  # its backward runs there (ordered like recomputed ones)
+                    cell.lane = lane  # its backward runs there (ordered in _backward)
             cell.outputs = out
             self._cells.append(cell)
 
-            # 3. outputs: activation to the next stage, skips to their pop ranks
+            # 3. outputs: activation to the next stage, skips to their pop ranks.  Sends
+            #    are ordered after the stream that computed them (RCCL syncs with the
+            #    current stream), so a lane's outputs leave without holding up main.
             act_out = out[:cell.n_act_out]
-            if nxt is not None:
-                self.p2p.send(act_out, nxt, self._key('act', i, me, nxt),
-                              atomic=cell.out_atomic)
-            by_dst: Dict[int, List[Tensor]] = OrderedDict()
-            for (dst, _), t in zip(self.out_skips, out[cell.n_act_out:]):
-                by_dst.setdefault(dst, []).append(t)
-            for dst in sorted(by_dst):
-                self.p2p.send(by_dst[dst], self.ranks[dst],
-                              self._key('skip', i, me, self.ranks[dst]))
+            with torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext():
+                if nxt is not None:
+                    self.p2p.send(act_out, nxt, self._key('act', i, me, nxt),
+                                  atomic=cell.out_atomic)
+                by_dst: Dict[int, List[Tensor]] = OrderedDict()
+                for (dst, _), t in zip(self.out_skips, out[cell.n_act_out:]):
+                    by_dst.setdefault(dst, []).append(t)
+                for dst in sorted(by_dst):
+                    self.p2p.send(by_dst[dst], self.ranks[dst],
+                                  self._key('skip', i, me, self.ranks[dst]))
             outputs.append(act_out[0] if cell.out_atomic else tuple(act_out))
         if flanes is not None and main is not None:
             for lane in flanes:
@@ -525,7 +532,7 @@ class PipelineStage:
         """
         if self.wgrad_stream and self.device.type == 'cuda':
             from torchgpipe_amd.ops.convbn import wgrad_stream_scope
-            with wgrad_stream_scope(True):
+            with wgrad_stream_scope(self.device):
                 self._backward(losses)
         else:
             self._backward(losses)
@@ -539,8 +546,10 @@ class PipelineStage:
 
         cells = list(reversed(self._cells))
         lanes = self._recompute_lanes()
-        main = torch.cuda.current_stream(self.device) if lanes is not None else None
-        prev_lane: Optional[torch.cuda.Stream] = None
+        on_gpu = self.device.type == 'cuda'
+        main = torch.cuda.current_stream(self.device) if on_gpu else None
+        # stream that ran the previous micro-batch's backward (None: main / CPU)
+        prev_run: Optional[torch.cuda.Stream] = None
         for j, cell in enumerate(cells):
             i = cell.index
             # 1. post the gradient receives first ...
@@ -560,22 +569,17 @@ class PipelineStage:
             else:
                 assert main is not None
                 self._recompute_on_lane(cell, lanes[j % 2], main)
-                if cell.lane is not None:
-                    # this backward (its recomputed ops run on cell.lane) must follow the
-                    # previous one: both accumulate into the same .grad buffers
-                    cell.lane.wait_stream(main)
-                    if prev_lane is not None:
-                        cell.lane.wait_stream(prev_lane)
-                    prev_lane = cell.lane
                 if j + 1 < len(cells):
                     # the next micro-batch's recomputation (which touches no gradient) runs
-                    # on the other lane while this backward runs
+                    # on the other lane while this backward runs; issued before this
+                    # cell's gradient wait so it never queues behind the transfer
                     self._recompute_on_lane(cells[j + 1], lanes[(j + 1) % 2], main)
 
             # 3. backward through this cell
             tensors: List[Tensor] = []
             grads: List[Tensor] = []
             act_out = cell.outputs[:cell.n_act_out]
+            mark = self._probe_begin() if grad_msg is not None or skip_grad_msgs else None
             if self.is_last:
                 assert losses is not None
                 tensors.append(losses[i])
@@ -596,9 +600,22 @@ class PipelineStage:
                         if t.requires_grad:
                             tensors.append(t)
                             grads.append(g)
+            self._probe_end('bwd', mark)
+            # A cell computed or recomputed on a lane runs its backward there (autograd
+            # replays each op on its forward stream).  Order it after main (received
+            # gradients, the loss) and after the previous micro-batch's backward,
+            # whichever stream ran it: the fused ops add into the same .grad buffers
+            # outside autograd, so nothing else would order the two.
+            run = cell.lane if cell.lane is not None else main
+            if cell.lane is not None:
+                assert main is not None
+                cell.lane.wait_stream(main)
+            if run is not None and prev_run is not None and prev_run is not run:
+                run.wait_stream(prev_run)
             with trace.range(f'bwd mb{i} stage{self.rank}'):
                 if tensors:
                     torch.autograd.backward(tensors, grads)
+            prev_run = run
 
             # 4. ship input gradients upstream
             n_in_act = len(cell.inputs) - len(self.in_skips)
@@ -616,7 +633,7 @@ class PipelineStage:
             cell.outputs = []
             cell.chk = None
             cell.lane = None
-        if self.device.type == 'cuda':
+        if on_gpu:
             # fused kernels on the lanes wrote .grad without autograd knowing
             cur = torch.cuda.current_stream(self.device)
             for lane in (lanes or []) + (self._fwd_lanes or []):
@@ -636,8 +653,16 @@ class PipelineStage:
         return self._lanes
 
     def _forward_lanes(self) -> Optional[List[torch.cuda.Stream]]:
-        """Two streams for the forward micro-batches of a one-rank stateless partition."""
-        if not self.overlap_forward or self.n != 1 or self._stateful:
+        """Two streams for the forward micro-batches of a stateless partition.
+
+        Micro-batch i runs on lane i % 2 after main (which holds its received inputs), and
+        its outputs are sent from that lane, so consecutive micro-batches overlap whenever
+        their inputs are already here: on the first stage, and on a stage slower than its
+        upstream (the pipeline's bottleneck, where inputs queue).  Partitions with running
+        statistics (BatchNorm) keep one stream: their micro-batches update shared state
+        in order.
+        """
+        if not self.overlap_forward or self._stateful:
             return None
         if self.device.type != 'cuda' or torch.cuda.is_current_stream_capturing():
             return None
@@ -656,6 +681,84 @@ class PipelineStage:
         with torch.cuda.stream(lane), trace.range(f'recompute mb{cell.index} stage{self.rank}'):
             cell.chk.recompute_now()
         cell.lane = lane
+
+    # -- diagnostics ------------------------------------------------------------------------
+
+    def _streams(self) -> List[torch.cuda.Stream]:
+        return ([torch.cuda.current_stream(self.device)] + list(self._lanes or [])
+                + list(self._fwd_lanes or []))
+
+    def _probe_begin(self) -> Any:
+        """Marker before a receive wait: events on main and every lane (GPU), or the host
+        clock (host-blocking transports)."""
+        if self._probe is None:
+            return None
+        if self.device.type == 'cuda':
+            events = []
+            for s in self._streams():
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(s)
+                events.append(e)
+            return events
+        return time.perf_counter()
+
+    def _probe_end(self, kind: str, mark: Any) -> None:
+        if self._probe is None or mark is None:
+            return
+        if self.device.type == 'cuda':
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(self.device))
+            self._probe.append((kind, mark, e))
+        else:
+            self._probe.append((kind, mark, time.perf_counter()))
+
+    def probe_step(self, step: Callable[[], Any]) -> Dict[str, float]:
+        """Run ``step()`` (one training step of this stage) with its receive waits timed.
+
+        Returns, in ms: ``step_ms`` (the step on this rank, from the first kernel it queues
+        to the last), ``fwd_wait_ms`` / ``bwd_wait_ms`` (time every stream of this stage
+        sat idle waiting for activations / gradients to arrive: each wait is measured from
+        the moment the last of main and the lanes reached it, so lane compute is not
+        counted), ``fill_ms`` / ``drain_ms`` (the first forward and first backward wait:
+        the pipeline fill and drain bubbles this rank sees) and ``busy_ms`` (``step_ms``
+        minus the waits).  Meant for one diagnostic step outside the timed ones: the
+        events add a little host work per micro-batch.
+        """
+        gpu = self.device.type == 'cuda'
+        self._probe = []
+        try:
+            if gpu:
+                torch.cuda.synchronize(self.device)
+                start = torch.cuda.Event(enable_timing=True)
+                start.record(torch.cuda.current_stream(self.device))
+                step()
+                end = torch.cuda.Event(enable_timing=True)
+                end.record(torch.cuda.current_stream(self.device))
+                for s in self._streams():
+                    torch.cuda.current_stream(self.device).wait_stream(s)
+                torch.cuda.synchronize(self.device)
+                total = start.elapsed_time(end)
+
+                def wait_of(mark: Any, stop: Any) -> float:
+                    began = max(start.elapsed_time(e) for e in mark)
+                    return max(0.0, start.elapsed_time(stop) - began)
+            else:
+                t0 = time.perf_counter()
+                step()
+                total = 1000 * (time.perf_counter() - t0)
+
+                def wait_of(mark: Any, stop: Any) -> float:
+                    return 1000 * (stop - mark)
+            waits = [(kind, wait_of(m, e)) for kind, m, e in self._probe]
+        finally:
+            self._probe = None
+        fwd = [w for k, w in waits if k == 'fwd']
+        bwd = [w for k, w in waits if k == 'bwd']
+        return {'step_ms': round(total, 3),
+                'fwd_wait_ms': round(sum(fwd), 3), 'bwd_wait_ms': round(sum(bwd), 3),
+                'fill_ms': round(fwd[0], 3) if fwd else 0.0,
+                'drain_ms': round(bwd[0], 3) if bwd else 0.0,
+                'busy_ms': round(total - sum(fwd) - sum(bwd), 3)}
 
     @staticmethod
     def _grad_of(t: Tensor) -> Tensor:
