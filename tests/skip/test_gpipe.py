@@ -125,3 +125,29 @@ def test_1to3_across_gpus(devices):
     piped = GPipe(copy.deepcopy(plain), [1, 1, 1], devices=devices, chunks=3)
     x = torch.rand(6, 4)
     torch.testing.assert_close(plain(x), piped(x.cuda(0)).cpu())
+
+
+@pytest.mark.parametrize('balance', [[104, 137], [30, 66, 84, 61]])
+def test_same_route_skips_travel_as_one_hop(balance):
+    """K7: every skip a micro-batch carries from one partition to another is one
+    PortalCopy (one packed peer copy between GPUs), not one per skip.  U-Net(5, 2) has
+    U-Net(5, 64)'s 241 layers, so the reference pipeline-4 balance applies."""
+    from torchgpipe_amd import GPipe
+    from torchgpipe_amd.models import unet
+    from torchgpipe_amd.skip import portal
+    from torchgpipe_amd.skip.layout import layout_from_balance
+
+    model = unet(depth=5, num_convs=5, base_channels=2, input_channels=3, output_channels=1)
+    n = len(balance)
+    layout = layout_from_balance(model, balance)
+    routes = sum(len(list(layout.copy_policy(j))) for j in range(n))
+    groups = sum(len(layout.copy_groups(j)) for j in range(n))
+    # p2: all 4 skips on route 0 -> 1; p4: 4 skips on 3 routes
+    assert (routes, groups) == {2: (4, 1), 4: (4, 3)}[n]
+    chunks = 2
+    gpipe = GPipe(model, balance, devices=['cpu'] * n, chunks=chunks)
+    before = portal.portal_hops
+    out = gpipe(torch.rand(4, 3, 64, 64))
+    assert portal.portal_hops - before == groups * chunks
+    out.mean().backward()
+    assert all(p.grad is not None for p in gpipe.parameters())

@@ -77,3 +77,46 @@ def test_disabled_switch(monkeypatch):
     assert gradacc.target(w) == (False, None)
     _Scale.apply(x, w).sum().backward()
     torch.testing.assert_close(w.grad, x.detach().sum(0))
+
+
+def test_release_drops_pinned_nodes():
+    """new_step() unpins the previous step's AccumulateGrad nodes (stream binding)."""
+    from torchgpipe_amd.ops.conv import new_step
+    x, w = _data()
+    _Scale.apply(x, w).sum().backward()
+    assert getattr(w, gradacc._ATTR, None) is not None
+    new_step()
+    assert getattr(w, gradacc._ATTR, None) is None and not gradacc._PINNED
+    _Scale.apply(x, w).sum().backward()  # re-acquired on the next backward
+    torch.testing.assert_close(w.grad, 2 * x.detach().sum(0))
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [
+    (2, 64, 64, 16), (3, 32, 48, 20),        # F(4x4) fused, one split
+    (8, 64, 64, 32),                          # F(4x4) fused, split-K reduction
+    (2, 512, 512, 12), (2, 512, 512, 6),      # F(4x4) non-fused
+    (2, 64, 96, 6), (32, 64, 96, 6),          # F(2x2), without / with split-K
+])
+def test_winograd_weight_gradient_accumulates_in_kernel(shape):
+    """WinogradConv2d applied to three inputs (three backward calls into one .grad, the
+    GPipe micro-batch pattern): the F(4x4) / F(2x2) weight-gradient kernels add into the
+    existing .grad themselves; the result matches fp64 PyTorch, and the AccumulateGrad
+    node never runs (no autograd accumulation)."""
+    from torchgpipe_amd.ops.conv import WinogradConv2d
+    n, c, k, hw = shape
+    dev = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    conv = WinogradConv2d(c, k, 3, padding=1, bias=False).to(dev)
+    ref = nn.Conv2d(c, k, 3, padding=1, bias=False).to(dev).double()
+    ref.weight.data.copy_(conv.weight.data)
+    xs = [torch.randn(n, c, hw, hw, device=dev) for _ in range(3)]
+    for x in xs:
+        conv(x).square().mean().backward()
+        ref(x.double()).square().mean().backward()
+    torch.cuda.synchronize()
+    err = (conv.weight.grad.double() - ref.weight.grad).norm() / ref.weight.grad.norm()
+    assert err < 1e-5, err.item()

@@ -237,8 +237,21 @@ at::Tensor wino4_conv(const at::Tensor& x_in, const at::Tensor& u,
   return y;
 }
 
+// Weight-gradient destination: a new tensor, or `into` (an existing .grad, contiguous
+// fp32 [K][C][3][3]) that the kernels add into (gradient-accumulation fusion).
+at::Tensor wgrad_destination(const c10::optional<at::Tensor>& into, const at::Tensor& x,
+                             int64_t k, int64_t c) {
+  if (!into.has_value()) return at::empty({k, c, 3, 3}, x.options());
+  const at::Tensor& d = *into;
+  TORCH_CHECK(d.is_contiguous() && d.scalar_type() == at::kFloat && d.device() == x.device() &&
+                  d.dim() == 4 && d.size(0) == k && d.size(1) == c && d.size(2) == 3 &&
+                  d.size(3) == 3,
+              "into must be a contiguous fp32 [K][C][3][3] tensor on x's device");
+  return d;
+}
+
 at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits,
-                      int64_t variant) {
+                      int64_t variant, const c10::optional<at::Tensor>& into) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   check_f32_gpu(x, "x");
@@ -251,8 +264,9 @@ at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t s
   TORCH_CHECK(c * h * w < (int64_t{1} << 31) && k * h * w < (int64_t{1} << 31),
               "plane too large for 32-bit channel offsets");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  auto dw = at::empty({k, c, 3, 3}, x.options());
-  if (n == 0 || h == 0 || w == 0) return dw.zero_();
+  const bool accum = into.has_value();
+  auto dw = wgrad_destination(into, x, k, c);
+  if (n == 0 || h == 0 || w == 0) return accum ? dw : dw.zero_();
   TORCH_CHECK(variant == -1 || variant == 0 || variant == 2, "variant must be -1, 0 or 2");
   // auto: the 64 x 64 double-buffered kernel, except for <= 32 output channels where
   // half of its 64-wide k block would idle (benchmarks/wgrad_variants.py).  Variant 2
@@ -267,12 +281,13 @@ at::Tensor wino_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t s
   at::Tensor ws;
   if (s > 1) ws = at::empty({s * k * c * 9}, x.options());
   launch_wino_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), dw.data_ptr<float>(),
-                    s > 1 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s, v, stream_of(x));
+                    s > 1 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s, v, accum,
+                    stream_of(x));
   return dw;
 }
 
 at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t splits,
-                       int64_t variant) {
+                       int64_t variant, const c10::optional<at::Tensor>& into) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   check_f32_gpu(x, "x");
@@ -283,8 +298,9 @@ at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t 
               "dy must be [N][K][H][W] of a 3x3/s1/p1 convolution of x");
   TORCH_CHECK(dy.device() == x.device(), "x and dy must share a device");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  auto dw = at::empty({k, c, 3, 3}, x.options());
-  if (n == 0 || h == 0 || w == 0 || c == 0 || k == 0) return dw.zero_();
+  const bool accum = into.has_value();
+  auto dw = wgrad_destination(into, x, k, c);
+  if (n == 0 || h == 0 || w == 0 || c == 0 || k == 0) return accum ? dw : dw.zero_();
   // 32-bit buffer offsets and tile indices
   TORCH_CHECK(wino4_wgrad_supported(n, c, k, h, w),
               "input too large for the F(4x4) weight-gradient kernel (needs < 1 GiB); "
@@ -299,7 +315,7 @@ at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t 
   if (wsize > 0) ws = at::empty({wsize}, x.options());
   launch_wino4_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), dw.data_ptr<float>(),
                      wsize > 0 ? ws.data_ptr<float>() : nullptr, n, c, k, h, w, s,
-                     static_cast<int>(variant), stream_of(x));
+                     static_cast<int>(variant), accum, stream_of(x));
   return dw;
 }
 
@@ -319,11 +335,11 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("spin(int ns, Device device) -> ()");
   m.def("copy_segments(Tensor[] srcs, Tensor(a!)[] dsts) -> ()");
   m.def("wino_weight(Tensor w, bool flip) -> Tensor");
-  m.def("wino_wgrad(Tensor x, Tensor dy, int splits=0, int variant=-1) -> Tensor");
+  m.def("wino_wgrad(Tensor x, Tensor dy, int splits=0, int variant=-1, Tensor? into=None) -> Tensor");
   m.def("wino_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
   m.def("wino4_weight(Tensor w, bool flip) -> Tensor");
-  m.def("wino4_wgrad(Tensor x, Tensor dy, int splits=0, int variant=0) -> Tensor");
+  m.def("wino4_wgrad(Tensor x, Tensor dy, int splits=0, int variant=0, Tensor? into=None) -> Tensor");
   m.def("wino4_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
 }

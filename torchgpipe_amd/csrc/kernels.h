@@ -102,9 +102,10 @@ int wino4_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
 // holds the split-K partials (splits > 1) and, for variant 1, the transformed operands.
 int64_t wino4_wgrad_workspace(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int splits,
                               int variant);
+// accum: add into dw (an existing gradient) instead of overwriting it.
 void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
                         int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
-                        hipStream_t stream);
+                        bool accum, hipStream_t stream);
 
 // Weight gradient of the same convolution: dw[K][C][3][3] from x[N][C][H][W] and
 // dy[N][K][H][W]; `splits` > 1 needs a workspace of splits*K*C*9 floats.
@@ -113,7 +114,7 @@ void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, i
 int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int variant);
 void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
                        int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
-                       hipStream_t stream);
+                       bool accum, hipStream_t stream);
 
 // ---- AmoebaNet cell operations (conv_gemm.hip, batchnorm.hip) -----------------------------
 

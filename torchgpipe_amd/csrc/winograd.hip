@@ -817,9 +817,16 @@ __device__ __forceinline__ void wgrad_fetch(float (&xr)[2][16], float (&yr)[4], 
   }
 }
 
+// Weight-gradient store: overwrite, or add into an existing .grad (gradient-accumulation
+// fusion, ops/gradacc.py: no separate `grad += new` pass per micro-batch).
+__device__ __forceinline__ void wg_store(float* o, float v, bool accum) {
+  *o = accum ? *o + v : v;
+}
+
 __global__ __launch_bounds__(kThreads, 2) void wino_wgrad_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dw, int C,
-    int K, int H, int W, int TH, int TW_, int64_t P, int cblocks, int kblocks, int splits) {
+    int K, int H, int W, int TH, int TW_, int64_t P, int cblocks, int kblocks, int splits,
+    bool accum) {
   __shared__ float Vs[kWT * kWC * kWS];
   __shared__ float Ms[kWT * kWK * kWS];
 
@@ -969,9 +976,9 @@ __global__ __launch_bounds__(kThreads, 2) void wino_wgrad_kernel(
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const float s12 = 0.5f * (t[i][1] + t[i][2]);
-        o[i * 3 + 0] = t[i][0] + s12;
-        o[i * 3 + 1] = 0.5f * (t[i][1] - t[i][2]);
-        o[i * 3 + 2] = s12 + t[i][3];
+        wg_store(o + i * 3 + 0, t[i][0] + s12, accum);
+        wg_store(o + i * 3 + 1, 0.5f * (t[i][1] - t[i][2]), accum);
+        wg_store(o + i * 3 + 2, s12 + t[i][3], accum);
       }
     }
   }
@@ -1221,7 +1228,8 @@ __device__ __forceinline__ void wd_step(floatx4 (&acc)[16][2], WdStage& s, float
 
 __global__ __launch_bounds__(kDBThreads, 1) void wino_wgrad_db_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dw, int C,
-    int K, int H, int W, int TH, int TW_, int64_t P, int cblocks, int kblocks, int splits) {
+    int K, int H, int W, int TH, int TW_, int64_t P, int cblocks, int kblocks, int splits,
+    bool accum) {
   __shared__ float lds[2 * 2 * kWDImg];  // [buffer][V | M'][8 tiles][64][20]: 160 KiB
 
   const int nwg = cblocks * kblocks * splits;
@@ -1307,20 +1315,20 @@ __global__ __launch_bounds__(kDBThreads, 1) void wino_wgrad_db_kernel(
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         const float s12 = 0.5f * (t[a][1] + t[a][2]);
-        o[a * 3 + 0] = t[a][0] + s12;
-        o[a * 3 + 1] = 0.5f * (t[a][1] - t[a][2]);
-        o[a * 3 + 2] = s12 + t[a][3];
+        wg_store(o + a * 3 + 0, t[a][0] + s12, accum);
+        wg_store(o + a * 3 + 1, 0.5f * (t[a][1] - t[a][2]), accum);
+        wg_store(o + a * 3 + 2, s12 + t[a][3], accum);
       }
     }
 }
 
 __global__ void wino_wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
-                                         int64_t numel, int splits) {
+                                         int64_t numel, int splits, bool accum) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= numel) return;
   float v = 0.f;
   for (int z = 0; z < splits; ++z) v += ws[z * numel + i];
-  dw[i] = v;
+  wg_store(dw + i, v, accum);
 }
 
 }  // namespace
@@ -1399,7 +1407,7 @@ int wino_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int
 
 void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
                        int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
-                       hipStream_t stream) {
+                       bool accum, hipStream_t stream) {
   const int64_t th = (h + 1) / 2, tw = (w + 1) / 2;
   const int64_t P = n * th * tw;
   if (variant == 2) {
@@ -1410,7 +1418,7 @@ void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, in
                        dim3(kDBThreads), 0, stream, x, dy, splits > 1 ? ws : dw,
                        static_cast<int>(c), static_cast<int>(k), static_cast<int>(h),
                        static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw), P,
-                       cblocks, kblocks, splits);
+                       cblocks, kblocks, splits, accum && splits == 1);
   } else {
     const int cblocks = static_cast<int>((c + kWC - 1) / kWC);
     const int kblocks = static_cast<int>((k + kWK - 1) / kWK);
@@ -1419,13 +1427,13 @@ void launch_wino_wgrad(const float* x, const float* dy, float* dw, float* ws, in
                        stream, x, dy, splits > 1 ? ws : dw, static_cast<int>(c),
                        static_cast<int>(k), static_cast<int>(h), static_cast<int>(w),
                        static_cast<int>(th), static_cast<int>(tw), P, cblocks, kblocks,
-                       splits);
+                       splits, accum && splits == 1);
   }
   if (splits > 1) {
     const int64_t numel = k * c * 9;
     hipLaunchKernelGGL(wino_wgrad_reduce_kernel,
                        dim3(static_cast<unsigned>((numel + 255) / 256)), dim3(256), 0, stream,
-                       ws, dw, numel, splits);
+                       ws, dw, numel, splits, accum);
   }
 }
 

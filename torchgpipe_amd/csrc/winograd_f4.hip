@@ -768,7 +768,7 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_gemm_kernel(
 template <bool kVec>
 __global__ __launch_bounds__(256) void f4_split_reduce_kernel(
     const float* __restrict__ ws, const float* __restrict__ bias, float* __restrict__ y,
-    int64_t numel, int64_t hw, int O, int splits) {
+    int64_t numel, int64_t hw, int O, int splits, bool accum) {
   typedef std::conditional_t<kVec, floatx4, float> T;
   constexpr int kW = kVec ? 4 : 1;
   __shared__ T part[3][64];
@@ -799,24 +799,25 @@ __global__ __launch_bounds__(256) void f4_split_reduce_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += bias[((i + e) / hw) % O];
     }
+    if (accum) v += *reinterpret_cast<const floatx4*>(y + i);
     *reinterpret_cast<floatx4*>(y + i) = v;
   } else {
     if (bias) v += bias[(i / hw) % O];
-    y[i] = v;
+    y[i] = accum ? y[i] + v : v;
   }
 }
 
 void launch_split_reduce(const float* ws, const float* bias, float* y, int64_t numel, int64_t hw,
-                         int O, int splits, hipStream_t stream) {
+                         int O, int splits, hipStream_t stream, bool accum = false) {
   const bool vec = (numel & 3) == 0;
   const int64_t cols = vec ? numel / 4 : numel;
   const dim3 grid(static_cast<unsigned>((cols + 63) / 64));
   if (vec)
     hipLaunchKernelGGL(f4_split_reduce_kernel<true>, grid, dim3(256), 0, stream, ws, bias, y,
-                       numel, hw, O, splits);
+                       numel, hw, O, splits, accum);
   else
     hipLaunchKernelGGL(f4_split_reduce_kernel<false>, grid, dim3(256), 0, stream, ws, bias, y,
-                       numel, hw, O, splits);
+                       numel, hw, O, splits, accum);
 }
 
 // ---- weight gradient: dW = G^T [ sum_t (A dY_t A^T) (.) (B^T d_t B) ] G ------------------
@@ -962,8 +963,9 @@ __device__ __forceinline__ void gt6(const float (&u)[6], float (&w)[3]) {
 constexpr int kWgThreads = 512;
 
 // dW[k][c] = G^T dU G for the lane's column c and rows kbase + r of its 36 accumulators.
+// accum: add into the existing gradient (gradient-accumulation fusion, ops/gradacc.py).
 __device__ __forceinline__ void f4_wgrad_epilogue(const floatx4 (&acc)[kP], float* __restrict__ out,
-                                                  int c, int kbase, int C, int K) {
+                                                  int c, int kbase, int C, int K, bool accum) {
   if (c >= C) return;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -984,9 +986,8 @@ __device__ __forceinline__ void f4_wgrad_epilogue(const floatx4 (&acc)[kP], floa
     for (int a = 0; a < 3; ++a) {
       float w3[3];
       gt6(t[a], w3);
-      o[a * 3 + 0] = w3[0];
-      o[a * 3 + 1] = w3[1];
-      o[a * 3 + 2] = w3[2];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) o[a * 3 + e] = accum ? o[a * 3 + e] + w3[e] : w3[e];
     }
   }
 }
@@ -1053,7 +1054,7 @@ __global__ __launch_bounds__(256) void f4_wg_mdy_kernel(const float* __restrict_
 template <int kAhead = 2>
 __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_gemm_kernel(
     const float* __restrict__ vx, const float* __restrict__ m, float* __restrict__ dw, int C,
-    int K, int nsteps, int cblocks, int kblocks, int splits) {
+    int K, int nsteps, int cblocks, int kblocks, int splits, bool accum) {
   using Cfg = F4Cfg<4>;
   constexpr int kBuf = Cfg::kBuf;
   constexpr int kMPieces = Cfg::kUImg / 256;  // 36
@@ -1103,7 +1104,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_gemm_kernel(
     __syncthreads();
   }
   f4_wgrad_epilogue(acc, dw + static_cast<int64_t>(z) * K * C * 9, cb * 32 + wt * 16 + (lane & 15),
-                    kb * 64 + wo * 16 + 4 * (lane >> 4), C, K);
+                    kb * 64 + wo * 16 + 4 * (lane >> 4), C, K, accum);
 }
 
 
@@ -1112,7 +1113,7 @@ template <bool kVec>
 __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dw, int N,
     int C, int K, int H, int W, int TH, int TW, int P, int cblocks, int kblocks, int splits,
-    uint32_t x_bytes, uint32_t dy_bytes) {
+    uint32_t x_bytes, uint32_t dy_bytes, bool accum) {
   using Cfg = F4Cfg<4>;
   constexpr int kBuf = Cfg::kBuf;
   __shared__ float lds[2 * kBuf];  // [buffer][M' 64k x 4t x 36 | V 4t x 32c x 36]: 108 KiB
@@ -1215,7 +1216,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_kernel(
 
   // -- dW = G^T dU G; lane holds c = c0 + wt*16 + (lane & 15), k = k0 + wo*16 + 4(lane>>4) + r
   f4_wgrad_epilogue(acc, dw + static_cast<int64_t>(z) * K * C * 9, c0 + wt * 16 + (lane & 15),
-                    k0 + wo * 16 + 4 * (lane >> 4), C, K);
+                    k0 + wo * 16 + 4 * (lane >> 4), C, K, accum);
 }
 
 }  // namespace
@@ -1369,7 +1370,7 @@ int64_t wino4_wgrad_workspace(int64_t n, int64_t c, int64_t k, int64_t h, int64_
 
 void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, int64_t n,
                         int64_t c, int64_t k, int64_t h, int64_t w, int splits, int variant,
-                        hipStream_t stream) {
+                        bool accum, hipStream_t stream) {
   const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
   const int64_t P = n * th * tw;
   const int cblocks = static_cast<int>((c + 31) / 32);
@@ -1396,17 +1397,20 @@ void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, i
                        static_cast<int>(ppad), kblocks, mt, dy_bytes);
     hipLaunchKernelGGL(f4_wgrad_gemm_kernel<>, dim3(static_cast<unsigned>(nwg)), dim3(kWgThreads), 0,
                        stream, vx, m, splits > 1 ? partial : dw, static_cast<int>(c),
-                       static_cast<int>(k), static_cast<int>(nsteps), cblocks, kblocks, splits);
+                       static_cast<int>(k), static_cast<int>(nsteps), cblocks, kblocks, splits,
+                       accum && splits == 1);
   } else {
     auto kernel = (w & 3) == 0 ? f4_wgrad_kernel<true> : f4_wgrad_kernel<false>;
     hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(kWgThreads), 0,
                        stream, x, dy, splits > 1 ? partial : dw, static_cast<int>(n),
                        static_cast<int>(c), static_cast<int>(k), static_cast<int>(h),
                        static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw),
-                       static_cast<int>(P), cblocks, kblocks, splits, x_bytes, dy_bytes);
+                       static_cast<int>(P), cblocks, kblocks, splits, x_bytes, dy_bytes,
+                       accum && splits == 1);
   }
   if (splits > 1) {
-    launch_split_reduce(partial, nullptr, dw, k * c * 9, 9, static_cast<int>(k), splits, stream);
+    launch_split_reduce(partial, nullptr, dw, k * c * 9, 9, static_cast<int>(k), splits, stream,
+                        accum);
   }
 }
 

@@ -31,7 +31,7 @@ import torch
 from torch import Tensor, nn
 import torch.nn.functional as F
 
-from torchgpipe_amd.ops import _ext
+from torchgpipe_amd.ops import _ext, gradacc
 
 __all__ = ['WinogradConv2d', 'winograd_conv2d', 'wino_eligible', 'new_step',
            'clear_winograd_caches', 'cache_bytes']
@@ -213,6 +213,7 @@ class _WinogradConv(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.cache = cache
         ctx.has_bias = bias is not None
+        ctx.param = weight  # gradient-accumulation fusion (ops/gradacc.py)
         return y
 
     @staticmethod
@@ -220,7 +221,8 @@ class _WinogradConv(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         dy = dy.contiguous()
         dx, dw = _conv_grads(x, weight, dy, ctx.cache, ctx.needs_input_grad[0],
-                             ctx.needs_input_grad[1])
+                             ctx.needs_input_grad[1], ctx.param)
+        del ctx.param
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum((0, 2, 3))
@@ -228,24 +230,43 @@ class _WinogradConv(torch.autograd.Function):
 
 
 def _conv_grads(x: Tensor, weight: Tensor, dy: Tensor, cache: _TransformCache, need_x: bool,
-                need_w: bool) -> Tuple[Optional[Tensor], Optional[Tensor]]:
-    """Backward-data and weight gradient of the 3x3 / stride 1 / pad 1 convolution."""
+                need_w: bool, param: Optional[Tensor] = None
+                ) -> Tuple[Optional[Tensor], Optional[Tensor]]:
+    """Backward-data and weight gradient of the 3x3 / stride 1 / pad 1 convolution.
+
+    With ``param`` (the weight as an autograd leaf) the Winograd weight-gradient kernels
+    add straight into ``param.grad`` when autograd would accumulate there anyway
+    (``ops/gradacc.py``): a GPipe step then spends no ``grad += new`` pass over the
+    weights per micro-batch (U-Net p8's stage 3: 105 M parameters, 39 extra passes), and
+    the parameter's AccumulateGrad node never runs, so micro-batches back-propagating on
+    different streams (forward / recompute lanes) need no cross-stream sync for it.
+    Returns ``dw = None`` when the kernels wrote the gradient themselves.
+    """
     dx = dw = None
     if need_x:
         dx = _conv(dy, cache, weight, None, True)
     if need_w:
-        if _wgrad_f4(x, dy, weight):
+        ops = _ext.require(dy)
+        f4, mfma = _wgrad_f4(x, dy, weight), _wgrad_on_mfma(x, weight)
+        fuse, into = gradacc.target(param) if param is not None and (f4 or mfma) else \
+            (False, None)
+        if f4:
             # non-fused (transform passes + LDS-DMA GEMM) from 512 channels on both
             # sides: 11-23 % faster there, 1.2-3.6x slower on the wide shallow planes
             # (profiles/wgrad_f4_variants.json)
             nonfused = min(weight.shape[0], weight.shape[1]) >= 512
-            dw = _ext.require(dy).wino4_wgrad(x, dy, 0, 1 if nonfused else 0)
-        elif _wgrad_on_mfma(x, weight):
-            dw = _ext.require(dy).wino_wgrad(x, dy, 0)
+            dw = ops.wino4_wgrad(x, dy, 0, 1 if nonfused else 0, into)
+        elif mfma:
+            dw = ops.wino_wgrad(x, dy, 0, -1, into)
         else:
             dw = torch.ops.aten.convolution_backward(
                 dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                 [False, True, False])[1]
+        if fuse:
+            assert param is not None
+            if into is None:
+                gradacc.commit(param, dw)
+            dw = None
     return dx, dw
 
 

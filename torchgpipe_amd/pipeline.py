@@ -128,8 +128,10 @@ class Pipeline:
             if i != 0:
                 depend(batches[i - 1], batches[i])
             next_stream = copy_streams[j][i]
-            for prev_j, ns, name in self.skip_layout.copy_policy(j):
-                skip_trackers[i].copy(batches[i], copy_streams[prev_j][i], next_stream, ns, name)
+            # every skip from one source partition into j travels as one packed hop
+            for prev_j, keys in self.skip_layout.copy_groups(j):
+                skip_trackers[i].copy_many(batches[i], copy_streams[prev_j][i], next_stream,
+                                           keys)
             if j != 0:
                 copy(batches[i], copy_streams[j - 1][i], next_stream)
 

@@ -42,6 +42,15 @@ class SkipLayout:
             if src != next_j:
                 yield (src, ns, name)
 
+    def copy_groups(self, next_j: int) -> List[Tuple[int, List[Tuple[Namespace, str]]]]:
+        """:meth:`copy_policy` grouped by source partition: one transfer per route."""
+        groups: List[Tuple[int, List[Tuple[Namespace, str]]]] = []
+        for src, ns, name in self.copy_policy(next_j):
+            if not groups or groups[-1][0] != src:
+                groups.append((src, []))
+            groups[-1][1].append((ns, name))
+        return groups
+
     def send_policy(self, prev_j: int) -> Iterable[Tuple[int, Namespace, str]]:
         """Cross-partition routes out of ``prev_j``, ascending by destination."""
         for dst, ns, name in self.by_source[prev_j]:

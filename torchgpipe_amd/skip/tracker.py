@@ -14,7 +14,7 @@ Parity: ``torchgpipe/skip/tracker.py:19-179``.
 """
 from contextlib import contextmanager
 import threading
-from typing import Dict, Generator, List, Optional, Tuple
+from typing import Dict, Generator, List, Optional, Sequence, Tuple
 
 from torch import Tensor
 
@@ -23,7 +23,7 @@ from torchgpipe_amd.dependency import fork, join
 from torchgpipe_amd.microbatch import Batch
 from torchgpipe_amd.skip.layout import SkipLayout
 from torchgpipe_amd.skip.namespace import Namespace
-from torchgpipe_amd.skip.portal import Portal
+from torchgpipe_amd.skip.portal import Portal, copy_portals
 from torchgpipe_amd.stream import AbstractStream
 
 __all__: List[str] = []
@@ -43,6 +43,10 @@ class SkipTracker:
 
     def copy(self, batch: Batch, prev_stream: AbstractStream, next_stream: AbstractStream,
              ns: Namespace, name: str) -> None:
+        raise TypeError('copy is not supported for non-portal skip tensors')
+
+    def copy_many(self, batch: Batch, prev_stream: AbstractStream,
+                  next_stream: AbstractStream, keys: Sequence[Key]) -> None:
         raise TypeError('copy is not supported for non-portal skip tensors')
 
 
@@ -79,9 +83,16 @@ class SkipTrackerThroughPotals(SkipTracker):
 
     def copy(self, batch: Batch, prev_stream: AbstractStream, next_stream: AbstractStream,
              ns: Namespace, name: str) -> None:
-        assert self.skip_layout.requires_copy(ns, name)
+        self.copy_many(batch, prev_stream, next_stream, [(ns, name)])
+
+    def copy_many(self, batch: Batch, prev_stream: AbstractStream,
+                  next_stream: AbstractStream, keys: Sequence[Key]) -> None:
+        """Move the portals of ``keys`` (one source partition, one destination) as one
+        hop, packed into a single transfer between two GPUs."""
+        assert all(self.skip_layout.requires_copy(ns, name) for ns, name in keys)
         batch[0], phony = fork(batch[0])
-        phony = self.portals[(ns, name)].copy(prev_stream, next_stream, phony)
+        phony = copy_portals([self.portals[key] for key in keys], prev_stream, next_stream,
+                             phony)
         batch[0] = join(batch[0], phony)
 
 
