@@ -210,3 +210,51 @@ def test_cache_budget_zero_keeps_no_transforms(monkeypatch):
     assert convmod.cache_bytes() == before
     want = F.conv2d(x.double(), layer.weight.double(), padding=1)
     assert ((y.double() - want).norm() / want.norm()).item() < 1e-5
+
+
+# -- batched-GEMM F(4x4) (bg_weight / bg_conv): every N-tile width and split-K --------------
+
+BG_SHAPES = [  # (N, C, K, H, W)
+    (16, 512, 512, 24, 24),    # 576 tiles: BN 96
+    (16, 1024, 1024, 12, 12),  # 144 tiles: BN 48
+    (16, 256, 512, 6, 6),      # 64 tiles: BN 64
+    (3, 70, 130, 13, 11),      # ragged channels / planes: every padding path
+    (1, 16, 8, 5, 7),
+    (40, 128, 96, 12, 12),     # 360 tiles: BN 128
+]
+
+
+@pytest.mark.parametrize('shape', BG_SHAPES)
+@pytest.mark.parametrize('flip', [False, True])
+def test_batched_gemm_winograd_matches_conv2d(shape, flip):
+    """Forward (flip=False) and backward-data (flip=True: the rotated, transposed weights)
+    of the batched-GEMM path against fp64 PyTorch."""
+    n, c, k, h, w = shape
+    ops = _ext.require(torch.empty(0, device=cuda))
+    torch.manual_seed(0)
+    wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
+    if flip:  # dx = conv_transpose(dy, w): input has k channels, output c
+        x = torch.randn(n, k, h, w, device=cuda)
+        want = F.conv_transpose2d(x.double(), wt.double(), padding=1)
+        got = ops.bg_conv(x, ops.bg_weight(wt, True), None, c)
+    else:
+        x = torch.randn(n, c, h, w, device=cuda)
+        b = torch.randn(k, device=cuda)
+        want = _ref(x, wt, b)
+        got = ops.bg_conv(x, ops.bg_weight(wt, False), b, k)
+    torch.testing.assert_close(got.double(), want, rtol=1e-4,
+                               atol=2e-5 * (want.abs().max().item() + 1))
+
+
+@pytest.mark.parametrize('bn', [48, 64, 96, 128])
+@pytest.mark.parametrize('splits', [1, 3])
+def test_batched_gemm_tile_widths_and_splits(bn, splits):
+    n, c, k, h, w = 4, 96, 136, 20, 20
+    ops = _ext.require(torch.empty(0, device=cuda))
+    torch.manual_seed(1)
+    x = torch.randn(n, c, h, w, device=cuda)
+    wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
+    got = ops.bg_conv(x, ops.bg_weight(wt, False), None, k, bn, splits)
+    want = _ref(x, wt)
+    torch.testing.assert_close(got.double(), want, rtol=1e-4,
+                               atol=2e-5 * (want.abs().max().item() + 1))

@@ -76,12 +76,10 @@ constexpr uint32_t kBadRow = 0x80000000u;
 constexpr uint32_t kBadCol = 0x40000000u;
 
 // U4[Rp/4][Op/16][4 c][16 o][36] = G g G^T of (output channel o, reduction channel r).
-__global__ void f4_weight_kernel(const float* __restrict__ w, float* __restrict__ u, int O,
-                                 int R, int Op, int Rp, bool flip) {
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (idx >= static_cast<int64_t>(Rp) * Op) return;
-  const int r = static_cast<int>(idx / Op);
-  const int o = static_cast<int>(idx % Op);
+// v = G g G^T (36 values, row-major 6x6) of (output channel o, reduction channel r);
+// zeros outside [0, O) x [0, R).
+__device__ __forceinline__ void f4_weight_tile(const float* __restrict__ w, int O, int R, int o,
+                                               int r, bool flip, float (&v)[kP]) {
   float g[3][3] = {};
   if (r < R && o < O) {
     if (!flip) {  // w = [O][R][3][3]
@@ -115,7 +113,6 @@ __global__ void f4_weight_kernel(const float* __restrict__ w, float* __restrict_
 #pragma unroll
     for (int i = 0; i < 6; ++i) t[i][j] = col[i];
   }
-  float v[kP];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     float row[6];
@@ -123,6 +120,16 @@ __global__ void f4_weight_kernel(const float* __restrict__ w, float* __restrict_
 #pragma unroll
     for (int j = 0; j < 6; ++j) v[i * 6 + j] = row[j];
   }
+}
+
+__global__ void f4_weight_kernel(const float* __restrict__ w, float* __restrict__ u, int O,
+                                 int R, int Op, int Rp, bool flip) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(Rp) * Op) return;
+  const int r = static_cast<int>(idx / Op);
+  const int o = static_cast<int>(idx % Op);
+  float v[kP];
+  f4_weight_tile(w, O, R, o, r, flip, v);
   float* dst = u + (static_cast<int64_t>(r / kC) * (Op / 16) + o / 16) * (kC * 16 * kP) +
                ((r % kC) * 16 + o % 16) * kP;
 #pragma unroll
@@ -190,7 +197,7 @@ __device__ __forceinline__ void f4_load_patch(F4Patch& p, __amdgpu_buffer_rsrc_t
 // column pass on adjacent column pairs, the row pass on adjacent row pairs -- with the
 // packed fp32 VALU: 148 instead of 242 VALU instructions per patch (the patch waves'
 // VALU work is what their SIMDs stall on, profiles/pmc_f4_kernels.json valu_per_mfma).
-__device__ __forceinline__ void f4_transform_store(F4Patch& p, float* vdst) {
+__device__ __forceinline__ void f4_transform(F4Patch& p) {
   float* d = p.d;
 #pragma unroll
   for (int jp = 0; jp < 3; ++jp) {
@@ -216,6 +223,11 @@ __device__ __forceinline__ void f4_transform_store(F4Patch& p, float* vdst) {
       d[(2 * ip + 1) * 6 + j] = r[j][1];
     }
   }
+}
+
+__device__ __forceinline__ void f4_transform_store(F4Patch& p, float* vdst) {
+  f4_transform(p);
+  const float* d = p.d;
 #pragma unroll
   for (int k = 0; k < kP / 4; ++k)
     reinterpret_cast<floatx4*>(vdst)[k] = floatx4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
@@ -1219,6 +1231,265 @@ __global__ __launch_bounds__(kWgThreads, 1) void f4_wgrad_kernel(
                     k0 + wo * 16 + 4 * (lane >> 4), C, K, accum);
 }
 
+// ---- batched-GEMM Winograd: transform passes + 36 independent MFMA GEMMs ----------------
+//
+// The fused kernels above keep all 36 positions of a 64-channel x 32-tile block in
+// registers so the output transform can run in the epilogue; per 4-channel step they
+// move 54 KiB through LDS for 0.59 MFLOP (11 FLOP/byte).  On the deep, low-resolution
+// U-Net levels (512-2048 channels at 6-24 pixels, 16 images per micro-batch) that made
+// f4_gemm_kernel 61 % of a pipeline stage's device time at ~40 % of the matrix peak
+// (profiles/r3).  Here the 36 positions are independent GEMMs
+//     M[b][o][t] = sum_c U[b][c][o] V[b][c][t]          (b = 0..35)
+// run as one batched launch with 128 x BN output tiles (32 FLOP/byte at BN = 128), the
+// products written to HBM, and the output transform (A^T M A, + bias) a separate pass that
+// also sums split-K slabs.  The weights U are transformed once per step (cached) and the
+// input V by its own pass, both straight into the GEMM's per-step LDS image:
+//     X[b][step][row][16]   row = output channel (U) or tile (V), 16 reduction values
+// with the 16 values of a row permuted (bg_slot) so that the lane of MFMA k-group q reads
+// its four k sub-steps as one float4, and the 16 lanes of each ds_read_b128 bank group hit
+// 64 distinct banks.  A step's tile is then one contiguous block in memory, copied by
+// LDS-DMA (global_load_lds_dwordx4) into a three-stage ring.
+
+// position of reduction index k (0..15 within a step) in the 16 floats of row r
+__device__ __forceinline__ int bg_quad(int q, int r) {
+  // quad order per 4-row group: [0, 2, 3, 1] (see the bank argument above)
+  constexpr int kTbl = 0 | (2 << 2) | (3 << 4) | (1 << 6);
+  return q ^ ((kTbl >> (((r >> 2) & 3) * 2)) & 3);
+}
+__device__ __forceinline__ int bg_slot(int k, int r) { return (bg_quad(k & 3, r) << 2) | (k >> 2); }
+
+// U[b][step][Mp][16] = G g G^T of (output channel m, reduction channel step*16 + k).
+__global__ __launch_bounds__(256) void bg_weight_f4_kernel(const float* __restrict__ w,
+                                                          float* __restrict__ a, int O, int R,
+                                                          int Mp, int ksteps, bool flip) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 16 * Mp) return;
+  const int k = static_cast<int>(idx & 15);
+  const int64_t rest = idx >> 4;
+  const int m = static_cast<int>(rest % Mp);
+  const int st = static_cast<int>(rest / Mp);
+  float v[kP];
+  f4_weight_tile(w, O, R, m, st * 16 + k, flip, v);
+  const int64_t plane = static_cast<int64_t>(ksteps) * Mp * 16;
+  float* dst = a + (static_cast<int64_t>(st) * Mp + m) * 16 + bg_slot(k, m);
+#pragma unroll
+  for (int b = 0; b < kP; ++b) dst[b * plane] = v[b];
+}
+
+// V[b][step][Np][16] = B^T d B of (tile t, channel step*16 + k); zeros in the padding.
+// Lanes: 16 channels x 4 consecutive tiles, so each position's store is 256 contiguous B.
+__global__ __launch_bounds__(256) void bg_input_f4_kernel(const float* __restrict__ x,
+                                                         float* __restrict__ v, int R, int H,
+                                                         int W, int TW, int tpi, int P, int Np,
+                                                         int ksteps, uint32_t x_bytes) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 16 * Np) return;
+  const int k = static_cast<int>(idx & 15);
+  const int64_t rest = idx >> 4;
+  const int t = static_cast<int>(rest % Np);
+  const int st = static_cast<int>(rest / Np);
+  const int c = st * 16 + k;
+  F4Patch p;
+  if (t < P && c < R) {
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                          static_cast<int>(x_bytes), 0x00020000);
+    f4_fwd_offsets(p, t, c, P, tpi, TW, R, H, W);
+    f4_load_patch<false>(p, xr, 0);
+    f4_transform(p);
+  } else {
+#pragma unroll
+    for (int b = 0; b < kP; ++b) p.d[b] = 0.f;
+  }
+  const int64_t plane = static_cast<int64_t>(ksteps) * Np * 16;
+  float* dst = v + (static_cast<int64_t>(st) * Np + t) * 16 + bg_slot(k, t);
+#pragma unroll
+  for (int b = 0; b < kP; ++b) dst[b * plane] = p.d[b];
+}
+
+template <int N>
+__device__ __forceinline__ void bg_wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+}
+
+// C[z][b][Mp][Np] = sum over the split's steps of A[b]^T B[b].  Workgroup: 4 waves, a 128 x BN
+// tile; wave w owns rows 32w..32w+31 (two 16-row MFMA blocks) and all BN columns, i.e.
+// 2 x BN/16 accumulator tiles of v_mfma_f32_16x16x4f32.  Per 16-deep step: 2 + BN/16
+// ds_read_b128 and 8 * BN/16 MFMAs per wave; the step's (128 + BN) x 64 B arrive by LDS-DMA
+// two steps ahead.
+template <int BN>
+__global__ __launch_bounds__(256, 2) void bg_gemm_kernel(
+    const float* __restrict__ a, const float* __restrict__ bmat, float* __restrict__ c, int Mp,
+    int Np, int ksteps, int mtiles, int ntiles, int batch, int splits) {
+  constexpr int BM = 128;
+  constexpr int kA = BM * 16, kB = BN * 16, kStage = kA + kB;
+  constexpr int kPieces = kStage / 256;  // 1 KiB LDS-DMA pieces per step
+  constexpr int kAPieces = kA / 256;
+  constexpr int kNJ = BN / 16;
+  static_assert(BN % 16 == 0 && kStage % 256 == 0, "tile shape");
+  __shared__ float lds[3 * kStage];
+
+  const int nwg = ntiles * mtiles * batch * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  // consecutive work ids (same A tile, consecutive N tiles) on one XCD: one L2 serves them
+  int wid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int nt = wid % ntiles;
+  wid /= ntiles;
+  const int mt = wid % mtiles;
+  wid /= mtiles;
+  const int bb = wid % batch;
+  const int z = wid / batch;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int64_t astep = static_cast<int64_t>(Mp) * 16, bstep = static_cast<int64_t>(Np) * 16;
+  const float* abase = a + bb * ksteps * astep + static_cast<int64_t>(mt) * kA;
+  const float* bbase = bmat + bb * ksteps * bstep + static_cast<int64_t>(nt) * kB;
+  const int s0 = static_cast<int>(static_cast<int64_t>(z) * ksteps / splits);
+  const int s1 = static_cast<int>(static_cast<int64_t>(z + 1) * ksteps / splits);
+
+  auto issue = [&](int st, int buf) {
+    float* dst = lds + buf * kStage;
+#pragma unroll
+    for (int i = 0; i < (kPieces + 3) / 4; ++i) {
+      const int piece = i * 4 + wave;
+      if (piece < kPieces) {
+        const float* src = piece < kAPieces ? abase + st * astep + piece * 256
+                                            : bbase + st * bstep + (piece - kAPieces) * 256;
+        __builtin_amdgcn_global_load_lds((glob_void_t*)(src + lane * 4),
+                                         (lds_void_t*)(dst + piece * 256), 16, 0, 0);
+      }
+    }
+  };
+  // this wave's pieces per step (wave-uniform): the counted vmcnt keeps the next step's
+  // DMA in flight across the barrier
+  const int mine = (kPieces - wave + 3) / 4;
+  auto retire_all_but_next = [&]() {
+    switch (mine) {
+      case 1: bg_wait_vm<1>(); break;
+      case 2: bg_wait_vm<2>(); break;
+      case 3: bg_wait_vm<3>(); break;
+      default: bg_wait_vm<4>(); break;
+    }
+  };
+
+  floatx4 acc[2][kNJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < kNJ; ++jj) acc[i][jj] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int q = lane >> 4, j = lane & 15;
+  int aoff[2], boff[kNJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 32 + i * 16 + j;
+    aoff[i] = row * 16 + (bg_quad(q, row) << 2);
+  }
+#pragma unroll
+  for (int jj = 0; jj < kNJ; ++jj) {
+    const int row = jj * 16 + j;
+    boff[jj] = kA + row * 16 + (bg_quad(q, row) << 2);
+  }
+
+  if (s0 < s1) issue(s0, 0);
+  if (s0 + 1 < s1) issue(s0 + 1, 1);
+  int buf = 0;
+  for (int st = s0; st < s1; ++st) {
+    if (st + 1 < s1)
+      retire_all_but_next();
+    else
+      bg_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (st + 2 < s1) issue(st + 2, buf == 0 ? 2 : buf - 1);
+    const float* base = lds + buf * kStage;
+    floatx4 af[2], bf[kNJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const floatx4*>(base + aoff[i]);
+#pragma unroll
+    for (int jj = 0; jj < kNJ; ++jj) bf[jj] = *reinterpret_cast<const floatx4*>(base + boff[jj]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int jj = 0; jj < kNJ; ++jj)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][kk], bf[jj][kk], acc[i][jj], 0, 0, 0);
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+
+  float* cz = c + (static_cast<int64_t>(z) * batch + bb) * Mp * Np;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m0 = mt * BM + wave * 32 + i * 16 + 4 * q;
+#pragma unroll
+    for (int jj = 0; jj < kNJ; ++jj) {
+      const int n = nt * BN + jj * 16 + j;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cz[static_cast<int64_t>(m0 + r) * Np + n] = acc[i][jj][r];
+    }
+  }
+}
+
+// Y = A^T (sum_z M[z]) A (+ bias): one thread per (output channel, tile), consecutive
+// threads on consecutive tiles (coalesced reads of each position's M row).
+__global__ __launch_bounds__(256) void bg_output_f4_kernel(
+    const float* __restrict__ cbuf, const float* __restrict__ bias, float* __restrict__ y, int O,
+    int Mp, int Np, int P, int tpi, int TW, int H, int W, int splits) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(O) * P) return;
+  const int t = static_cast<int>(idx % P);
+  const int o = static_cast<int>(idx / P);
+  const int64_t pos = static_cast<int64_t>(Mp) * Np;
+  const float* src = cbuf + static_cast<int64_t>(o) * Np + t;
+  float m[kP];
+#pragma unroll
+  for (int b = 0; b < kP; ++b) m[b] = src[b * pos];
+  for (int z = 1; z < splits; ++z) {
+    const float* sz = src + static_cast<int64_t>(z) * kP * pos;
+#pragma unroll
+    for (int b = 0; b < kP; ++b) m[b] += sz[b * pos];
+  }
+  float s[4][6];
+#pragma unroll
+  for (int jc = 0; jc < 6; ++jc) {
+    const float a = m[6 + jc] + m[12 + jc], bq = m[6 + jc] - m[12 + jc];
+    const float cc = m[18 + jc] + m[24 + jc], d = m[18 + jc] - m[24 + jc];
+    s[0][jc] = m[jc] + a + cc;
+    s[1][jc] = bq + 2.f * d;
+    s[2][jc] = a + 4.f * cc;
+    s[3][jc] = bq + 8.f * d + m[30 + jc];
+  }
+  const float bv = bias ? bias[o] : 0.f;
+  const int n = t / tpi;
+  const int rem = t - n * tpi;
+  const int ty = rem / TW;
+  const int py = 4 * ty, px = 4 * (rem - ty * TW);
+  float* yp = y + (static_cast<int64_t>(n) * O + o) * H * W + static_cast<int64_t>(py) * W + px;
+  const bool full = (W & 3) == 0 && py + 4 <= H;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float a = s[k][1] + s[k][2], bq = s[k][1] - s[k][2];
+    const float cc = s[k][3] + s[k][4], d = s[k][3] - s[k][4];
+    const floatx4 out{s[k][0] + a + cc + bv, bq + 2.f * d + bv, a + 4.f * cc + bv,
+                      bq + 8.f * d + s[k][5] + bv};
+    if (full) {
+      *reinterpret_cast<floatx4*>(yp + k * W) = out;
+    } else if (py + k < H) {
+#pragma unroll
+      for (int l = 0; l < 4; ++l)
+        if (px + l < W) yp[k * W + l] = out[l];
+    }
+  }
+}
+
 }  // namespace
 
 int64_t wino4_pad_reduction(int64_t r) { return (r + kC - 1) / kC * kC; }
@@ -1412,6 +1683,95 @@ void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, i
     launch_split_reduce(partial, nullptr, dw, k * c * 9, 9, static_cast<int>(k), splits, stream,
                         accum);
   }
+}
+
+// ---- batched-GEMM Winograd host side ---------------------------------------------------
+
+namespace {
+constexpr int kBgBM = 128;
+int64_t bg_round(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+}  // namespace
+
+int bg_pick_bn(int64_t tiles) {
+  // the N tile that pads the tile count least (ties: the larger tile)
+  int best = 128;
+  int64_t best_pad = bg_round(tiles, 128);
+  for (int bn : {96, 64, 48}) {
+    const int64_t pad = bg_round(tiles, bn);
+    if (pad < best_pad) {
+      best = bn;
+      best_pad = pad;
+    }
+  }
+  return best;
+}
+
+BgPlan bg_plan_f4(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                  int bn, int splits) {
+  BgPlan plan;
+  const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
+  plan.bn = bn == 48 || bn == 64 || bn == 96 || bn == 128 ? bn : bg_pick_bn(P);
+  plan.mp = bg_round(out_channels, kBgBM);
+  plan.np = bg_round(P, plan.bn);
+  plan.ksteps = (red_channels + 15) / 16;
+  const int64_t tiles = (plan.mp / kBgBM) * (plan.np / plan.bn) * kP;
+  if (splits > 0) {
+    plan.splits = static_cast<int>(std::min<int64_t>(splits, plan.ksteps));
+  } else {
+    // two workgroups per CU: >= 512 workgroups, >= 16 steps per split
+    int64_t s = 1;
+    while (tiles * s < 512 && plan.ksteps / (s * 2) >= 16) s *= 2;
+    plan.splits = static_cast<int>(s);
+  }
+  plan.workspace = kP * plan.ksteps * 16 * plan.np + plan.splits * kP * plan.mp * plan.np;
+  return plan;
+}
+
+int64_t bg_weight_f4_numel(int64_t out_channels, int64_t red_channels) {
+  return kP * ((red_channels + 15) / 16) * 16 * bg_round(out_channels, kBgBM);
+}
+
+void launch_bg_weight_f4(const float* w, float* a, int64_t out_channels, int64_t red_channels,
+                         bool flip, hipStream_t stream) {
+  const int64_t mp = bg_round(out_channels, kBgBM);
+  const int64_t ksteps = (red_channels + 15) / 16;
+  const int64_t total = ksteps * 16 * mp;
+  hipLaunchKernelGGL(bg_weight_f4_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
+                     dim3(256), 0, stream, w, a, static_cast<int>(out_channels),
+                     static_cast<int>(red_channels), static_cast<int>(mp),
+                     static_cast<int>(ksteps), flip);
+}
+
+void launch_bg_conv_f4(const float* x, const float* a, const float* bias, float* y, float* ws,
+                       int64_t n, int64_t red_channels, int64_t h, int64_t w,
+                       int64_t out_channels, const BgPlan& plan, hipStream_t stream) {
+  const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
+  const int64_t P = n * th * tw;
+  float* v = ws;
+  float* cbuf = ws + kP * plan.ksteps * 16 * plan.np;
+  const int64_t vt = plan.ksteps * 16 * plan.np;
+  hipLaunchKernelGGL(bg_input_f4_kernel, dim3(static_cast<unsigned>((vt + 255) / 256)), dim3(256),
+                     0, stream, x, v, static_cast<int>(red_channels), static_cast<int>(h),
+                     static_cast<int>(w), static_cast<int>(tw), static_cast<int>(th * tw),
+                     static_cast<int>(P), static_cast<int>(plan.np),
+                     static_cast<int>(plan.ksteps),
+                     static_cast<uint32_t>(n * red_channels * h * w * 4));
+  const int mtiles = static_cast<int>(plan.mp / kBgBM);
+  const int ntiles = static_cast<int>(plan.np / plan.bn);
+  const int64_t nwg = static_cast<int64_t>(mtiles) * ntiles * kP * plan.splits;
+  auto gemm = plan.bn == 128 ? bg_gemm_kernel<128>
+              : plan.bn == 96 ? bg_gemm_kernel<96>
+              : plan.bn == 64 ? bg_gemm_kernel<64>
+                              : bg_gemm_kernel<48>;
+  hipLaunchKernelGGL(gemm, dim3(static_cast<unsigned>(nwg)), dim3(256), 0, stream, a, v, cbuf,
+                     static_cast<int>(plan.mp), static_cast<int>(plan.np),
+                     static_cast<int>(plan.ksteps), mtiles, ntiles, kP, plan.splits);
+  const int64_t ot = out_channels * P;
+  hipLaunchKernelGGL(bg_output_f4_kernel, dim3(static_cast<unsigned>((ot + 255) / 256)), dim3(256),
+                     0, stream, cbuf, bias, y, static_cast<int>(out_channels),
+                     static_cast<int>(plan.mp), static_cast<int>(plan.np), static_cast<int>(P),
+                     static_cast<int>(th * tw), static_cast<int>(tw), static_cast<int>(h),
+                     static_cast<int>(w), plan.splits);
 }
 
 }  // namespace tgpipe
