@@ -58,17 +58,23 @@ def main() -> None:
         flops = 2.0 * n * k * c * 9 * h * h
         cache = _TransformCache()
         cur = timed(lambda: _conv(x, cache, w, None, False), a.iters)
-        wb = ops.bg_weight(w, False)
         ref = torch.nn.functional.conv2d(x, w, padding=1)
         row = {'shape': [n, c, k, h], 'current_ms': round(cur, 4),
                'current_tflops': round(flops / cur / 1e9, 1)}
-        for bn in (0, 48, 64, 96, 128):
-            got = ops.bg_conv(x, wb, None, k, bn, 0)
-            err = ((got - ref).norm() / ref.norm()).item()
-            ms = timed(lambda: ops.bg_conv(x, wb, None, k, bn, 0), a.iters)
-            row[f'bg{bn or "auto"}_ms'] = round(ms, 4)
-            row[f'bg{bn or "auto"}_err'] = float(f'{err:.2e}')
-        row['bg_auto_tflops'] = round(flops / row['bgauto_ms'] / 1e9, 1)
+        for kind in (4, 2):
+            wb = ops.bg_weight(w, False, kind)
+            for waves, bn in ((0, 0), (4, 48), (4, 64), (4, 96), (4, 128), (8, 64), (8, 96),
+                              (8, 128), (8, 144), (8, 192)):
+                tag = f'f{kind}_{"auto" if not waves else f"{waves}x{bn}"}'
+                got = ops.bg_conv(x, wb, None, k, bn, 0, kind, waves)
+                err = ((got - ref).norm() / ref.norm()).item()
+                if err > 1e-4:
+                    raise SystemExit(f'{tag} {n, c, k, h}: relative error {err:.2e}')
+                ms = timed(lambda: ops.bg_conv(x, wb, None, k, bn, 0, kind, waves), a.iters)
+                row[tag] = round(ms, 4)
+            best = min((v, t) for t, v in row.items() if t.startswith(f'f{kind}_'))
+            row[f'f{kind}_best'] = best[1]
+        row['f4_auto_tflops'] = round(flops / row['f4_auto'] / 1e9, 1)
         rows.append(row)
         print(json.dumps(row), flush=True)
     if a.out:

@@ -226,9 +226,10 @@ BG_SHAPES = [  # (N, C, K, H, W)
 
 @pytest.mark.parametrize('shape', BG_SHAPES)
 @pytest.mark.parametrize('flip', [False, True])
-def test_batched_gemm_winograd_matches_conv2d(shape, flip):
+@pytest.mark.parametrize('kind', [4, 2])
+def test_batched_gemm_winograd_matches_conv2d(shape, flip, kind):
     """Forward (flip=False) and backward-data (flip=True: the rotated, transposed weights)
-    of the batched-GEMM path against fp64 PyTorch."""
+    of the batched-GEMM path, F(4x4) and F(2x2), against fp64 PyTorch."""
     n, c, k, h, w = shape
     ops = _ext.require(torch.empty(0, device=cuda))
     torch.manual_seed(0)
@@ -236,25 +237,26 @@ def test_batched_gemm_winograd_matches_conv2d(shape, flip):
     if flip:  # dx = conv_transpose(dy, w): input has k channels, output c
         x = torch.randn(n, k, h, w, device=cuda)
         want = F.conv_transpose2d(x.double(), wt.double(), padding=1)
-        got = ops.bg_conv(x, ops.bg_weight(wt, True), None, c)
+        got = ops.bg_conv(x, ops.bg_weight(wt, True, kind), None, c, 0, 0, kind)
     else:
         x = torch.randn(n, c, h, w, device=cuda)
         b = torch.randn(k, device=cuda)
         want = _ref(x, wt, b)
-        got = ops.bg_conv(x, ops.bg_weight(wt, False), b, k)
+        got = ops.bg_conv(x, ops.bg_weight(wt, False, kind), b, k, 0, 0, kind)
     torch.testing.assert_close(got.double(), want, rtol=1e-4,
                                atol=2e-5 * (want.abs().max().item() + 1))
 
 
-@pytest.mark.parametrize('bn', [48, 64, 96, 128])
+@pytest.mark.parametrize('waves,bn', [(4, 48), (4, 64), (4, 96), (4, 128), (8, 64), (8, 96),
+                                      (8, 128), (8, 144), (8, 192)])
 @pytest.mark.parametrize('splits', [1, 3])
-def test_batched_gemm_tile_widths_and_splits(bn, splits):
-    n, c, k, h, w = 4, 96, 136, 20, 20
+def test_batched_gemm_tile_shapes_and_splits(waves, bn, splits):
+    n, c, k, h, w = 4, 96, 300, 20, 20
     ops = _ext.require(torch.empty(0, device=cuda))
     torch.manual_seed(1)
     x = torch.randn(n, c, h, w, device=cuda)
     wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
-    got = ops.bg_conv(x, ops.bg_weight(wt, False), None, k, bn, splits)
+    got = ops.bg_conv(x, ops.bg_weight(wt, False), None, k, bn, splits, 4, waves)
     want = _ref(x, wt)
     torch.testing.assert_close(got.double(), want, rtol=1e-4,
                                atol=2e-5 * (want.abs().max().item() + 1))

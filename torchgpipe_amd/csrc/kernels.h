@@ -92,24 +92,26 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
                        int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                        const WinoPlan& plan, hipStream_t stream);
 
-// Batched-GEMM Winograd F(4x4, 3x3) (winograd_f4.hip): input-transform pass, 36 independent
+// Batched-GEMM Winograd F(4x4, 3x3) / F(2x2, 3x3) (winograd_f4.hip): input-transform pass, 36 / 16 independent
 // MFMA GEMMs with 128 x bn output tiles, output-transform pass (also sums split-K slabs).
 struct BgPlan {
-  int bn = 64;            // N (tile) width of a GEMM tile: 48, 64, 96 or 128
+  int kind = 4;           // 4: F(4x4) (36 positions), 2: F(2x2) (16 positions)
+  int waves = 8;          // GEMM tile height 32 * waves: 4 (128 rows) or 8 (256 rows)
+  int bn = 64;            // GEMM tile width (tiles): 48-128 (4 waves), 64-192 (8 waves)
   int splits = 1;         // split-K slabs
   int64_t mp = 0, np = 0, ksteps = 0;
   int64_t workspace = 0;  // floats: V + split slabs of M
 };
 int bg_pick_bn(int64_t tiles);
-BgPlan bg_plan_f4(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
-                  int bn, int splits);
-// weights in the GEMM's operand layout U[36][ceil(R/16)][round(O, 128)][16]
-int64_t bg_weight_f4_numel(int64_t out_channels, int64_t red_channels);
-void launch_bg_weight_f4(const float* w, float* a, int64_t out_channels, int64_t red_channels,
-                         bool flip, hipStream_t stream);
-void launch_bg_conv_f4(const float* x, const float* a, const float* bias, float* y, float* ws,
-                       int64_t n, int64_t red_channels, int64_t h, int64_t w,
-                       int64_t out_channels, const BgPlan& plan, hipStream_t stream);
+BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+               int bn, int splits, int kind, int waves);
+// weights in the GEMM's operand layout U[36 or 16][ceil(R/16)][round(O, 256)][16]
+int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind);
+void launch_bg_weight(const float* w, float* a, int64_t out_channels, int64_t red_channels,
+                      bool flip, int kind, hipStream_t stream);
+void launch_bg_conv(const float* x, const float* a, const float* bias, float* y, float* ws,
+                    int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                    const BgPlan& plan, hipStream_t stream);
 
 
 // F(4x4,3x3) weight gradient (winograd_f4.hip): dw[K][C][3][3], 36 MFMA multiplies per

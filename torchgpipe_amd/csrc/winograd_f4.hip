@@ -1313,24 +1313,30 @@ __device__ __forceinline__ void bg_wait_vm() {
   else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
   else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 }
 
-// C[z][b][Mp][Np] = sum over the split's steps of A[b]^T B[b].  Workgroup: 4 waves, a 128 x BN
-// tile; wave w owns rows 32w..32w+31 (two 16-row MFMA blocks) and all BN columns, i.e.
-// 2 x BN/16 accumulator tiles of v_mfma_f32_16x16x4f32.  Per 16-deep step: 2 + BN/16
-// ds_read_b128 and 8 * BN/16 MFMAs per wave; the step's (128 + BN) x 64 B arrive by LDS-DMA
-// two steps ahead.
-template <int BN>
-__global__ __launch_bounds__(256, 2) void bg_gemm_kernel(
+// C[z][b][Mp][Np] = sum over the split's steps of A[b]^T B[b].  Workgroup: kWaves waves, a
+// (32 kWaves) x BN tile; wave w owns rows 32w..32w+31 (two 16-row MFMA blocks) and all BN
+// columns, i.e. 2 x BN/16 accumulator tiles of v_mfma_f32_16x16x4f32.  Per 16-deep step:
+// 2 + BN/16 ds_read_b128 and 8 * BN/16 MFMAs per wave; the step's (BM + BN) x 64 B arrive
+// by LDS-DMA two steps ahead.  Bigger tiles cut the bytes per FLOP the CUs pull from L2 /
+// the Infinity Cache: 128 x 48 moves 57 B per KFLOP, 256 x 144 only 22.
+template <int kWaves, int BN>
+__global__ __launch_bounds__(64 * kWaves, 512 / (64 * kWaves)) void bg_gemm_kernel(
     const float* __restrict__ a, const float* __restrict__ bmat, float* __restrict__ c, int Mp,
     int Np, int ksteps, int mtiles, int ntiles, int batch, int splits) {
-  constexpr int BM = 128;
+  constexpr int BM = 32 * kWaves;
   constexpr int kA = BM * 16, kB = BN * 16, kStage = kA + kB;
   constexpr int kPieces = kStage / 256;  // 1 KiB LDS-DMA pieces per step
   constexpr int kAPieces = kA / 256;
   constexpr int kNJ = BN / 16;
-  static_assert(BN % 16 == 0 && kStage % 256 == 0, "tile shape");
+  constexpr int kPer = (kPieces + kWaves - 1) / kWaves;
+  static_assert(BN % 16 == 0 && kStage % 256 == 0 && kPer <= 4, "tile shape");
   __shared__ float lds[3 * kStage];
 
   const int nwg = ntiles * mtiles * batch * splits;
@@ -1347,19 +1353,21 @@ __global__ __launch_bounds__(256, 2) void bg_gemm_kernel(
   const int z = wid / batch;
 
   const int tid = threadIdx.x;
-  const int wave = tid >> 6;
+  // wave-uniform in a scalar register: the DMA issue and counted waits below then branch
+  // on SCC instead of running every path under an exec mask
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int64_t astep = static_cast<int64_t>(Mp) * 16, bstep = static_cast<int64_t>(Np) * 16;
-  const float* abase = a + bb * ksteps * astep + static_cast<int64_t>(mt) * kA;
-  const float* bbase = bmat + bb * ksteps * bstep + static_cast<int64_t>(nt) * kB;
+  const float* abase = a + static_cast<int64_t>(bb) * ksteps * astep + static_cast<int64_t>(mt) * kA;
+  const float* bbase = bmat + static_cast<int64_t>(bb) * ksteps * bstep + static_cast<int64_t>(nt) * kB;
   const int s0 = static_cast<int>(static_cast<int64_t>(z) * ksteps / splits);
   const int s1 = static_cast<int>(static_cast<int64_t>(z + 1) * ksteps / splits);
 
   auto issue = [&](int st, int buf) {
     float* dst = lds + buf * kStage;
 #pragma unroll
-    for (int i = 0; i < (kPieces + 3) / 4; ++i) {
-      const int piece = i * 4 + wave;
+    for (int i = 0; i < kPer; ++i) {
+      const int piece = i * kWaves + wave;
       if (piece < kPieces) {
         const float* src = piece < kAPieces ? abase + st * astep + piece * 256
                                             : bbase + st * bstep + (piece - kAPieces) * 256;
@@ -1368,15 +1376,20 @@ __global__ __launch_bounds__(256, 2) void bg_gemm_kernel(
       }
     }
   };
-  // this wave's pieces per step (wave-uniform): the counted vmcnt keeps the next step's
-  // DMA in flight across the barrier
-  const int mine = (kPieces - wave + 3) / 4;
-  auto retire_all_but_next = [&]() {
-    switch (mine) {
+  // this wave's pieces per step: waiting for vmcnt <= k * mine leaves the last k issued
+  // steps in flight
+  const int mine = (kPieces - wave + kWaves - 1) / kWaves;
+  auto wait_steps_in_flight = [&](int k) {
+    switch (k * mine) {
+      case 0: bg_wait_vm<0>(); break;
       case 1: bg_wait_vm<1>(); break;
       case 2: bg_wait_vm<2>(); break;
       case 3: bg_wait_vm<3>(); break;
-      default: bg_wait_vm<4>(); break;
+      case 4: bg_wait_vm<4>(); break;
+      case 5: bg_wait_vm<5>(); break;
+      case 6: bg_wait_vm<6>(); break;
+      case 7: bg_wait_vm<7>(); break;
+      default: bg_wait_vm<8>(); break;
     }
   };
 
@@ -1398,31 +1411,51 @@ __global__ __launch_bounds__(256, 2) void bg_gemm_kernel(
     const int row = jj * 16 + j;
     boff[jj] = kA + row * 16 + (bg_quad(q, row) << 2);
   }
-
-  if (s0 < s1) issue(s0, 0);
-  if (s0 + 1 < s1) issue(s0 + 1, 1);
-  int buf = 0;
-  for (int st = s0; st < s1; ++st) {
-    if (st + 1 < s1)
-      retire_all_but_next();
-    else
-      bg_wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    if (st + 2 < s1) issue(st + 2, buf == 0 ? 2 : buf - 1);
+  floatx4 af[2], bf[kNJ];
+  auto fetch = [&](int buf) {
     const float* base = lds + buf * kStage;
-    floatx4 af[2], bf[kNJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const floatx4*>(base + aoff[i]);
 #pragma unroll
     for (int jj = 0; jj < kNJ; ++jj) bf[jj] = *reinterpret_cast<const floatx4*>(base + boff[jj]);
+  };
+
+  // Software pipeline over a three-slot ring: at step st the fragments of st are already
+  // in registers (read during step st-1); after one barrier (step st+1 landed, every wave
+  // done reading slot st) the wave issues step st+3's DMA into slot st, reads step st+1's
+  // fragments and runs step st's MFMAs while those reads return.
+  const int nst = s1 - s0;
+  if (nst > 0) {
+    issue(s0, 0);
+    if (nst > 1) issue(s0 + 1, 1);
+    if (nst > 2) issue(s0 + 2, 2);
+    wait_steps_in_flight(nst > 2 ? 2 : nst - 1);
+    __builtin_amdgcn_s_barrier();
+    fetch(0);
+  }
+  int buf = 0;
+  for (int k = 0; k < nst; ++k) {
+    floatx4 ac[2], bc[kNJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ac[i] = af[i];
+#pragma unroll
+    for (int jj = 0; jj < kNJ; ++jj) bc[jj] = bf[jj];
+    const int nb = buf == 2 ? 0 : buf + 1;
+    if (k + 1 < nst) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's reads are done
+      wait_steps_in_flight(k + 2 < nst ? 1 : 0);           // step k+1 landed
+      __builtin_amdgcn_s_barrier();
+      if (k + 3 < nst) issue(s0 + k + 3, buf);
+      fetch(nb);
+    }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
       for (int jj = 0; jj < kNJ; ++jj)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][kk], bf[jj][kk], acc[i][jj], 0, 0, 0);
-    buf = buf == 2 ? 0 : buf + 1;
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[i][kk], bc[jj][kk], acc[i][jj], 0, 0, 0);
+    buf = nb;
   }
 
   float* cz = c + (static_cast<int64_t>(z) * batch + bb) * Mp * Np;
@@ -1487,6 +1520,145 @@ __global__ __launch_bounds__(256) void bg_output_f4_kernel(
       for (int l = 0; l < 4; ++l)
         if (px + l < W) yp[k * W + l] = out[l];
     }
+  }
+}
+
+// ---- the same batched GEMM for F(2x2, 3x3): 16 positions, 4x4 patches, 2x2 outputs ------
+// On 6x6 planes a 4x4 output tile covers 8x8 (5/9 of its multiplies wasted), so F(2x2)
+// does the same matrix-core work with a transformed weight 16/36 the size: the bottom
+// U-Net level's 2048 x 2048 layers read 268 MB of U per call instead of 604 MB.
+constexpr int kP2 = 16;
+
+__global__ __launch_bounds__(256) void bg_weight_f2_kernel(const float* __restrict__ w,
+                                                          float* __restrict__ a, int O, int R,
+                                                          int Mp, int ksteps, bool flip) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 16 * Mp) return;
+  const int k = static_cast<int>(idx & 15);
+  const int64_t rest = idx >> 4;
+  const int m = static_cast<int>(rest % Mp);
+  const int st = static_cast<int>(rest / Mp);
+  const int r = st * 16 + k;
+  float g[3][3] = {};
+  if (r < R && m < O) {
+    const float* src = flip ? w + (static_cast<int64_t>(r) * O + m) * 9
+                            : w + (static_cast<int64_t>(m) * R + r) * 9;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jc = 0; jc < 3; ++jc) g[i][jc] = flip ? src[(2 - i) * 3 + (2 - jc)] : src[i * 3 + jc];
+  }
+  // G = [[1, 0, 0], [1/2, 1/2, 1/2], [1/2, -1/2, 1/2], [0, 0, 1]]
+  float t[4][3];
+#pragma unroll
+  for (int jc = 0; jc < 3; ++jc) {
+    t[0][jc] = g[0][jc];
+    t[1][jc] = 0.5f * (g[0][jc] + g[1][jc] + g[2][jc]);
+    t[2][jc] = 0.5f * (g[0][jc] - g[1][jc] + g[2][jc]);
+    t[3][jc] = g[2][jc];
+  }
+  float v[kP2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i * 4 + 0] = t[i][0];
+    v[i * 4 + 1] = 0.5f * (t[i][0] + t[i][1] + t[i][2]);
+    v[i * 4 + 2] = 0.5f * (t[i][0] - t[i][1] + t[i][2]);
+    v[i * 4 + 3] = t[i][2];
+  }
+  const int64_t plane = static_cast<int64_t>(ksteps) * Mp * 16;
+  float* dst = a + (static_cast<int64_t>(st) * Mp + m) * 16 + bg_slot(k, m);
+#pragma unroll
+  for (int b = 0; b < kP2; ++b) dst[b * plane] = v[b];
+}
+
+__global__ __launch_bounds__(256) void bg_input_f2_kernel(const float* __restrict__ x,
+                                                         float* __restrict__ v, int R, int H,
+                                                         int W, int TW, int tpi, int P, int Np,
+                                                         int ksteps) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 16 * Np) return;
+  const int k = static_cast<int>(idx & 15);
+  const int64_t rest = idx >> 4;
+  const int t = static_cast<int>(rest % Np);
+  const int st = static_cast<int>(rest / Np);
+  const int c = st * 16 + k;
+  float d[4][4] = {};
+  if (t < P && c < R) {
+    const int n = t / tpi;
+    const int rem = t - n * tpi;
+    const int ty = rem / TW;
+    const int y0 = 2 * ty - 1, x0 = 2 * (rem - ty * TW) - 1;
+    const float* src = x + (static_cast<int64_t>(n) * R + c) * H * W;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int yy = y0 + i;
+#pragma unroll
+      for (int jc = 0; jc < 4; ++jc) {
+        const int xx = x0 + jc;
+        d[i][jc] = yy >= 0 && yy < H && xx >= 0 && xx < W ? src[yy * W + xx] : 0.f;
+      }
+    }
+  }
+  // B^T = [[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]]
+  float e[4][4];
+#pragma unroll
+  for (int jc = 0; jc < 4; ++jc) {
+    e[0][jc] = d[0][jc] - d[2][jc];
+    e[1][jc] = d[1][jc] + d[2][jc];
+    e[2][jc] = d[2][jc] - d[1][jc];
+    e[3][jc] = d[1][jc] - d[3][jc];
+  }
+  float vv[kP2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    vv[i * 4 + 0] = e[i][0] - e[i][2];
+    vv[i * 4 + 1] = e[i][1] + e[i][2];
+    vv[i * 4 + 2] = e[i][2] - e[i][1];
+    vv[i * 4 + 3] = e[i][1] - e[i][3];
+  }
+  const int64_t plane = static_cast<int64_t>(ksteps) * Np * 16;
+  float* dst = v + (static_cast<int64_t>(st) * Np + t) * 16 + bg_slot(k, t);
+#pragma unroll
+  for (int b = 0; b < kP2; ++b) dst[b * plane] = vv[b];
+}
+
+__global__ __launch_bounds__(256) void bg_output_f2_kernel(
+    const float* __restrict__ cbuf, const float* __restrict__ bias, float* __restrict__ y, int O,
+    int Mp, int Np, int P, int tpi, int TW, int H, int W, int splits) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(O) * P) return;
+  const int t = static_cast<int>(idx % P);
+  const int o = static_cast<int>(idx / P);
+  const int64_t pos = static_cast<int64_t>(Mp) * Np;
+  const float* src = cbuf + static_cast<int64_t>(o) * Np + t;
+  float m[kP2];
+#pragma unroll
+  for (int b = 0; b < kP2; ++b) m[b] = src[b * pos];
+  for (int z = 1; z < splits; ++z) {
+    const float* sz = src + static_cast<int64_t>(z) * kP2 * pos;
+#pragma unroll
+    for (int b = 0; b < kP2; ++b) m[b] += sz[b * pos];
+  }
+  // A^T = [[1, 1, 1, 0], [0, 1, -1, -1]]
+  float s[2][4];
+#pragma unroll
+  for (int jc = 0; jc < 4; ++jc) {
+    s[0][jc] = m[jc] + m[4 + jc] + m[8 + jc];
+    s[1][jc] = m[4 + jc] - m[8 + jc] - m[12 + jc];
+  }
+  const float bv = bias ? bias[o] : 0.f;
+  const int n = t / tpi;
+  const int rem = t - n * tpi;
+  const int ty = rem / TW;
+  const int py = 2 * ty, px = 2 * (rem - ty * TW);
+  float* yp = y + (static_cast<int64_t>(n) * O + o) * H * W + static_cast<int64_t>(py) * W + px;
+#pragma unroll
+  for (int kr = 0; kr < 2; ++kr) {
+    if (py + kr >= H) break;
+    const float v0 = s[kr][0] + s[kr][1] + s[kr][2] + bv;
+    const float v1 = s[kr][1] - s[kr][2] - s[kr][3] + bv;
+    yp[kr * W] = v0;
+    if (px + 1 < W) yp[kr * W + 1] = v1;
   }
 }
 
@@ -1688,15 +1860,18 @@ void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, i
 // ---- batched-GEMM Winograd host side ---------------------------------------------------
 
 namespace {
-constexpr int kBgBM = 128;
+constexpr int kBgRowPad = 256;  // weight rows (output channels) padded for either tile height
 int64_t bg_round(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+// (waves, BN) instantiations of bg_gemm_kernel
+constexpr int kBgTiles[][2] = {{4, 48}, {4, 64}, {4, 96}, {4, 128},
+                               {8, 64}, {8, 96}, {8, 128}, {8, 144}, {8, 192}};
 }  // namespace
 
 int bg_pick_bn(int64_t tiles) {
   // the N tile that pads the tile count least (ties: the larger tile)
-  int best = 128;
-  int64_t best_pad = bg_round(tiles, 128);
-  for (int bn : {96, 64, 48}) {
+  int best = 192;
+  int64_t best_pad = bg_round(tiles, 192);
+  for (int bn : {144, 128, 96, 64, 48}) {
     const int64_t pad = bg_round(tiles, bn);
     if (pad < best_pad) {
       best = bn;
@@ -1706,68 +1881,107 @@ int bg_pick_bn(int64_t tiles) {
   return best;
 }
 
-BgPlan bg_plan_f4(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
-                  int bn, int splits) {
+BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+               int bn, int splits, int kind, int waves) {
   BgPlan plan;
-  const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
-  plan.bn = bn == 48 || bn == 64 || bn == 96 || bn == 128 ? bn : bg_pick_bn(P);
-  plan.mp = bg_round(out_channels, kBgBM);
-  plan.np = bg_round(P, plan.bn);
+  plan.kind = kind == 2 ? 2 : 4;
+  const int tile = plan.kind;
+  const int64_t npos = plan.kind == 2 ? kP2 : kP;
+  const int64_t P = n * ((h + tile - 1) / tile) * ((w + tile - 1) / tile);
   plan.ksteps = (red_channels + 15) / 16;
-  const int64_t tiles = (plan.mp / kBgBM) * (plan.np / plan.bn) * kP;
+  plan.mp = bg_round(out_channels, kBgRowPad);
+  bool valid = false;
+  for (const auto& t : kBgTiles) valid |= t[0] == waves && t[1] == bn;
+  if (!valid) {
+    // Auto: 256-row tiles (8 waves) from 256 output channels up, the N tile that pads the
+    // tile count least; 128-row tiles keep their narrower N set.
+    waves = out_channels > 128 ? 8 : 4;
+    bn = bg_pick_bn(P);
+    if (waves == 4 && bn > 128) bn = 128;
+    if (waves == 8 && bn == 48) bn = 64;
+  }
+  plan.waves = waves;
+  plan.bn = bn;
+  plan.np = bg_round(P, plan.bn);
+  const int64_t bm = 32 * waves;
+  const int64_t tiles = (plan.mp / bm) * (plan.np / plan.bn) * npos;
   if (splits > 0) {
     plan.splits = static_cast<int>(std::min<int64_t>(splits, plan.ksteps));
   } else {
-    // two workgroups per CU: >= 512 workgroups, >= 16 steps per split
+    // >= 2 workgroups per CU (one of 8 waves holds 77-84 KiB of LDS), >= 16 steps per split
+    const int64_t target = waves == 8 ? 512 : 768;
     int64_t s = 1;
-    while (tiles * s < 512 && plan.ksteps / (s * 2) >= 16) s *= 2;
+    while (tiles * s < target && plan.ksteps / (s * 2) >= 16) s *= 2;
     plan.splits = static_cast<int>(s);
   }
-  plan.workspace = kP * plan.ksteps * 16 * plan.np + plan.splits * kP * plan.mp * plan.np;
+  plan.workspace = npos * plan.ksteps * 16 * plan.np + plan.splits * npos * plan.mp * plan.np;
   return plan;
 }
 
-int64_t bg_weight_f4_numel(int64_t out_channels, int64_t red_channels) {
-  return kP * ((red_channels + 15) / 16) * 16 * bg_round(out_channels, kBgBM);
+int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind) {
+  return (kind == 2 ? kP2 : kP) * ((red_channels + 15) / 16) * 16 *
+         bg_round(out_channels, kBgRowPad);
 }
 
-void launch_bg_weight_f4(const float* w, float* a, int64_t out_channels, int64_t red_channels,
-                         bool flip, hipStream_t stream) {
-  const int64_t mp = bg_round(out_channels, kBgBM);
+void launch_bg_weight(const float* w, float* a, int64_t out_channels, int64_t red_channels,
+                      bool flip, int kind, hipStream_t stream) {
+  const int64_t mp = bg_round(out_channels, kBgRowPad);
   const int64_t ksteps = (red_channels + 15) / 16;
   const int64_t total = ksteps * 16 * mp;
-  hipLaunchKernelGGL(bg_weight_f4_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
-                     dim3(256), 0, stream, w, a, static_cast<int>(out_channels),
-                     static_cast<int>(red_channels), static_cast<int>(mp),
-                     static_cast<int>(ksteps), flip);
+  hipLaunchKernelGGL(kind == 2 ? bg_weight_f2_kernel : bg_weight_f4_kernel,
+                     dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, stream, w, a,
+                     static_cast<int>(out_channels), static_cast<int>(red_channels),
+                     static_cast<int>(mp), static_cast<int>(ksteps), flip);
 }
 
-void launch_bg_conv_f4(const float* x, const float* a, const float* bias, float* y, float* ws,
-                       int64_t n, int64_t red_channels, int64_t h, int64_t w,
-                       int64_t out_channels, const BgPlan& plan, hipStream_t stream) {
-  const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
+void launch_bg_conv(const float* x, const float* a, const float* bias, float* y, float* ws,
+                    int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
+                    const BgPlan& plan, hipStream_t stream) {
+  const int tile = plan.kind;
+  const int npos = plan.kind == 2 ? kP2 : kP;
+  const int64_t th = (h + tile - 1) / tile, tw = (w + tile - 1) / tile;
   const int64_t P = n * th * tw;
   float* v = ws;
-  float* cbuf = ws + kP * plan.ksteps * 16 * plan.np;
+  float* cbuf = ws + npos * plan.ksteps * 16 * plan.np;
   const int64_t vt = plan.ksteps * 16 * plan.np;
-  hipLaunchKernelGGL(bg_input_f4_kernel, dim3(static_cast<unsigned>((vt + 255) / 256)), dim3(256),
-                     0, stream, x, v, static_cast<int>(red_channels), static_cast<int>(h),
-                     static_cast<int>(w), static_cast<int>(tw), static_cast<int>(th * tw),
-                     static_cast<int>(P), static_cast<int>(plan.np),
-                     static_cast<int>(plan.ksteps),
-                     static_cast<uint32_t>(n * red_channels * h * w * 4));
-  const int mtiles = static_cast<int>(plan.mp / kBgBM);
+  if (plan.kind == 2) {
+    hipLaunchKernelGGL(bg_input_f2_kernel, dim3(static_cast<unsigned>((vt + 255) / 256)),
+                       dim3(256), 0, stream, x, v, static_cast<int>(red_channels),
+                       static_cast<int>(h), static_cast<int>(w), static_cast<int>(tw),
+                       static_cast<int>(th * tw), static_cast<int>(P),
+                       static_cast<int>(plan.np), static_cast<int>(plan.ksteps));
+  } else {
+    hipLaunchKernelGGL(bg_input_f4_kernel, dim3(static_cast<unsigned>((vt + 255) / 256)),
+                       dim3(256), 0, stream, x, v, static_cast<int>(red_channels),
+                       static_cast<int>(h), static_cast<int>(w), static_cast<int>(tw),
+                       static_cast<int>(th * tw), static_cast<int>(P),
+                       static_cast<int>(plan.np), static_cast<int>(plan.ksteps),
+                       static_cast<uint32_t>(n * red_channels * h * w * 4));
+  }
+  const int mtiles = static_cast<int>(plan.mp / (32 * plan.waves));
   const int ntiles = static_cast<int>(plan.np / plan.bn);
-  const int64_t nwg = static_cast<int64_t>(mtiles) * ntiles * kP * plan.splits;
-  auto gemm = plan.bn == 128 ? bg_gemm_kernel<128>
-              : plan.bn == 96 ? bg_gemm_kernel<96>
-              : plan.bn == 64 ? bg_gemm_kernel<64>
-                              : bg_gemm_kernel<48>;
-  hipLaunchKernelGGL(gemm, dim3(static_cast<unsigned>(nwg)), dim3(256), 0, stream, a, v, cbuf,
-                     static_cast<int>(plan.mp), static_cast<int>(plan.np),
-                     static_cast<int>(plan.ksteps), mtiles, ntiles, kP, plan.splits);
+  const int64_t nwg = static_cast<int64_t>(mtiles) * ntiles * npos * plan.splits;
+  using Gemm = void (*)(const float*, const float*, float*, int, int, int, int, int, int, int);
+  Gemm gemm = bg_gemm_kernel<4, 48>;
+  switch (plan.waves * 1000 + plan.bn) {
+    case 4048: gemm = bg_gemm_kernel<4, 48>; break;
+    case 4064: gemm = bg_gemm_kernel<4, 64>; break;
+    case 4096: gemm = bg_gemm_kernel<4, 96>; break;
+    case 4128: gemm = bg_gemm_kernel<4, 128>; break;
+    case 8064: gemm = bg_gemm_kernel<8, 64>; break;
+    case 8096: gemm = bg_gemm_kernel<8, 96>; break;
+    case 8128: gemm = bg_gemm_kernel<8, 128>; break;
+    case 8144: gemm = bg_gemm_kernel<8, 144>; break;
+    case 8192: gemm = bg_gemm_kernel<8, 192>; break;
+    default: break;
+  }
+  hipLaunchKernelGGL(gemm, dim3(static_cast<unsigned>(nwg)), dim3(64 * plan.waves), 0, stream, a,
+                     v, cbuf, static_cast<int>(plan.mp), static_cast<int>(plan.np),
+                     static_cast<int>(plan.ksteps), mtiles, ntiles, static_cast<int>(npos),
+                     plan.splits);
   const int64_t ot = out_channels * P;
-  hipLaunchKernelGGL(bg_output_f4_kernel, dim3(static_cast<unsigned>((ot + 255) / 256)), dim3(256),
+  hipLaunchKernelGGL(plan.kind == 2 ? bg_output_f2_kernel : bg_output_f4_kernel,
+                     dim3(static_cast<unsigned>((ot + 255) / 256)), dim3(256),
                      0, stream, cbuf, bias, y, static_cast<int>(out_channels),
                      static_cast<int>(plan.mp), static_cast<int>(plan.np), static_cast<int>(P),
                      static_cast<int>(th * tw), static_cast<int>(tw), static_cast<int>(h),
