@@ -102,7 +102,7 @@ struct BgPlan {
   int64_t mp = 0, np = 0, ksteps = 0;
   int64_t workspace = 0;  // floats: V + split slabs of M
 };
-int bg_pick_bn(int64_t tiles);
+int bg_pick_bn(int64_t tiles, int kind);
 BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                int bn, int splits, int kind, int waves);
 // weights in the GEMM's operand layout U[36 or 16][ceil(R/16)][round(O, 256)][16]

@@ -1867,14 +1867,19 @@ constexpr int kBgTiles[][2] = {{4, 48}, {4, 64}, {4, 96}, {4, 128},
                                {8, 64}, {8, 96}, {8, 128}, {8, 144}, {8, 192}};
 }  // namespace
 
-int bg_pick_bn(int64_t tiles) {
-  // the N tile that pads the tile count least (ties: the larger tile)
-  int best = 192;
-  int64_t best_pad = bg_round(tiles, 192);
-  for (int bn : {144, 128, 96, 64, 48}) {
-    const int64_t pad = bg_round(tiles, bn);
+int bg_pick_bn(int64_t tiles, int kind) {
+  // The 4-wave (128-row) tile width that pads the tile count least; ties go to the width
+  // measured fastest (benchmarks/bg_bench.py, profiles/r3/bg_bench.json): 64 for F(4x4),
+  // 96 for F(2x2).
+  static constexpr int kF4[] = {64, 48, 96, 128};
+  static constexpr int kF2[] = {96, 64, 48, 128};
+  const int* order = kind == 2 ? kF2 : kF4;
+  int best = order[0];
+  int64_t best_pad = bg_round(tiles, best);
+  for (int i = 1; i < 4; ++i) {
+    const int64_t pad = bg_round(tiles, order[i]);
     if (pad < best_pad) {
-      best = bn;
+      best = order[i];
       best_pad = pad;
     }
   }
@@ -1893,12 +1898,10 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
   bool valid = false;
   for (const auto& t : kBgTiles) valid |= t[0] == waves && t[1] == bn;
   if (!valid) {
-    // Auto: 256-row tiles (8 waves) from 256 output channels up, the N tile that pads the
-    // tile count least; 128-row tiles keep their narrower N set.
-    waves = out_channels > 128 ? 8 : 4;
-    bn = bg_pick_bn(P);
-    if (waves == 4 && bn > 128) bn = 128;
-    if (waves == 8 && bn == 48) bn = 64;
+    // Auto: 128-row tiles (4 waves), which beat the 256-row ones on every measured U-Net
+    // shape once the fragment reads were software-pipelined (profiles/r3/bg_bench.json)
+    waves = 4;
+    bn = bg_pick_bn(P, plan.kind);
   }
   plan.waves = waves;
   plan.bn = bn;
@@ -1908,7 +1911,7 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
   if (splits > 0) {
     plan.splits = static_cast<int>(std::min<int64_t>(splits, plan.ksteps));
   } else {
-    // >= 2 workgroups per CU (one of 8 waves holds 77-84 KiB of LDS), >= 16 steps per split
+    // >= 2-3 workgroups per CU, >= 16 steps per split
     const int64_t target = waves == 8 ? 512 : 768;
     int64_t s = 1;
     while (tiles * s < target && plan.ksteps / (s * 2) >= 16) s *= 2;

@@ -78,22 +78,29 @@ class _TransformCache:
     def __init__(self) -> None:
         self._entries: Dict[Tuple, Tuple[Tuple[int, int, torch.device, int], Tensor]] = {}
 
-    def get(self, weight: Tensor, flip: bool, f4: bool = False) -> Tensor:
+    def get(self, weight: Tensor, flip: bool, f4: bool = False, bg: int = 0) -> Tensor:
+        """The transformed weight for ``flip`` (backward-data) and the kernel family:
+        F(2x2) (default), F(4x4) fused (``f4``) or the batched-GEMM layout of F(4x4) /
+        F(2x2) (``bg`` = 4 / 2)."""
         global _CACHE_BYTES
         key = (weight.data_ptr(), weight._version, weight.device, _STEP)
-        hit = self._entries.get((flip, f4))
+        slot = (flip, f4, bg)
+        hit = self._entries.get(slot)
         if hit is not None and hit[0] == key:
             return hit[1]
         if hit is not None:  # stale: release before transforming again
             _CACHE_BYTES -= hit[1].numel() * hit[1].element_size()
-            del self._entries[(flip, f4)]
+            del self._entries[slot]
         ops = _ext.require(weight)
         with torch.no_grad():
             w = weight.detach().contiguous()
-            u = ops.wino4_weight(w, flip) if f4 else ops.wino_weight(w, flip)
+            if bg:
+                u = ops.bg_weight(w, flip, bg)
+            else:
+                u = ops.wino4_weight(w, flip) if f4 else ops.wino_weight(w, flip)
         size = u.numel() * u.element_size()
         if _CACHE_BYTES + size <= _budget(weight.device):
-            self._entries[(flip, f4)] = (key, u)
+            self._entries[slot] = (key, u)
             _CACHE_BYTES += size
         return u
 
@@ -177,11 +184,43 @@ def _use_f4(x: Tensor, out_channels: int = 0) -> bool:
     return (plane >= F4_MIN_PLANE or wide) and x.numel() * x.element_size() < F4_MAX_BYTES
 
 
+# Batched-GEMM Winograd (csrc/winograd_f4.hip bg_*: input-transform pass, 36 / 16 independent
+# 128 x 48-128 MFMA GEMMs, output-transform pass) for convolutions with >= 256 channels on
+# both sides: 1.1-1.9x faster than the fused / non-fused F(4x4) kernels and the F(2x2)
+# kernel on every such U-Net shape at 16-40 images (benchmarks/bg_bench.py,
+# profiles/r3/bg_bench.json), F(2x2) on 6x6 planes (a 4x4 tile grid wastes 5/9 there).
+# TGPIPE_WINOGRAD_BG=0 keeps the older kernels.
+BG_ENABLED = os.environ.get('TGPIPE_WINOGRAD_BG', '1') != '0'
+BG_MIN_CHANNELS = 256
+
+
+def _bg_kind(x: Tensor, out_channels: int) -> int:
+    """4 (F(4x4)), 2 (F(2x2)) or 0 (not the batched-GEMM path) for this convolution."""
+    r = x.shape[1]
+    plane = min(x.shape[2], x.shape[3])
+    if not BG_ENABLED or r < BG_MIN_CHANNELS or out_channels < BG_MIN_CHANNELS or plane < 6:
+        return 0
+    kind = 2 if plane < 8 else 4
+    positions = 16 if kind == 2 else 36
+    if r * out_channels * positions * 4 > F4_MAX_CACHE_BYTES or \
+            x.numel() * x.element_size() >= F4_MAX_BYTES:
+        return 0
+    tiles = x.shape[0] * -(-x.shape[2] // kind) * -(-x.shape[3] // kind)
+    # the GEMM's padded operands and products (positions x channels x tiles) stay in the
+    # kernels' 32-bit index range
+    if positions * max(r, out_channels) * (tiles + 192) >= (1 << 31):
+        return 0
+    return kind
+
+
 def _conv(x: Tensor, cache: _TransformCache, weight: Tensor, bias: Optional[Tensor],
           flip: bool) -> Tensor:
     """One Winograd convolution launch: forward (flip=False) or backward-data (flip=True)."""
     ops = _ext.require(x)
     out_channels = weight.shape[1] if flip else weight.shape[0]
+    kind = _bg_kind(x, out_channels)
+    if kind:
+        return ops.bg_conv(x, cache.get(weight, flip, bg=kind), bias, out_channels, 0, 0, kind)
     if _use_f4(x, out_channels):
         # 32-channel workgroups (variant 7) when a 64-channel one (variant 6) would idle
         # half its waves, or when the 64-channel grid covers well under one workgroup per
