@@ -63,14 +63,14 @@ def main() -> None:
                'current_tflops': round(flops / cur / 1e9, 1)}
         for kind in (4, 2):
             wb = ops.bg_weight(w, False, kind)
-            for waves, bn in ((0, 0), (4, 48), (4, 64), (4, 96), (4, 128), (8, 64), (8, 96),
-                              (8, 128), (8, 144), (8, 192)):
-                tag = f'f{kind}_{"auto" if not waves else f"{waves}x{bn}"}'
-                got = ops.bg_conv(x, wb, None, k, bn, 0, kind, waves)
+            for waves, bn, sub in [(0, 0, 0)] + [(4, b, u) for b in (48, 64, 96, 128)
+                                                for u in (1, 2)] + [(8, 128, 1)]:
+                tag = f'f{kind}_{"auto" if not waves else f"{waves}x{bn}s{sub}"}'
+                got = ops.bg_conv(x, wb, None, k, bn, 0, kind, waves, sub)
                 err = ((got - ref).norm() / ref.norm()).item()
                 if err > 1e-4:
                     raise SystemExit(f'{tag} {n, c, k, h}: relative error {err:.2e}')
-                ms = timed(lambda: ops.bg_conv(x, wb, None, k, bn, 0, kind, waves), a.iters)
+                ms = timed(lambda: ops.bg_conv(x, wb, None, k, bn, 0, kind, waves, sub), a.iters)
                 row[tag] = round(ms, 4)
             best = min((v, t) for t, v in row.items() if t.startswith(f'f{kind}_'))
             row[f'f{kind}_best'] = best[1]

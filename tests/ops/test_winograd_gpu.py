@@ -247,16 +247,17 @@ def test_batched_gemm_winograd_matches_conv2d(shape, flip, kind):
                                atol=2e-5 * (want.abs().max().item() + 1))
 
 
-@pytest.mark.parametrize('waves,bn', [(4, 48), (4, 64), (4, 96), (4, 128), (8, 64), (8, 96),
-                                      (8, 128), (8, 144), (8, 192)])
+@pytest.mark.parametrize('waves,bn,sub', [(4, 48, 1), (4, 64, 1), (4, 96, 1), (4, 128, 1),
+                                          (4, 48, 2), (4, 64, 2), (4, 96, 2), (4, 128, 2),
+                                          (8, 64, 1), (8, 96, 1), (8, 128, 1), (8, 144, 1)])
 @pytest.mark.parametrize('splits', [1, 3])
-def test_batched_gemm_tile_shapes_and_splits(waves, bn, splits):
+def test_batched_gemm_tile_shapes_and_splits(waves, bn, sub, splits):
     n, c, k, h, w = 4, 96, 300, 20, 20
     ops = _ext.require(torch.empty(0, device=cuda))
     torch.manual_seed(1)
     x = torch.randn(n, c, h, w, device=cuda)
     wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
-    got = ops.bg_conv(x, ops.bg_weight(wt, False), None, k, bn, splits, 4, waves)
+    got = ops.bg_conv(x, ops.bg_weight(wt, False), None, k, bn, splits, 4, waves, sub)
     want = _ref(x, wt)
     torch.testing.assert_close(got.double(), want, rtol=1e-4,
                                atol=2e-5 * (want.abs().max().item() + 1))

@@ -338,7 +338,7 @@ at::Tensor bg_weight(const at::Tensor& w, bool flip, int64_t kind) {
 
 at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
                    const c10::optional<at::Tensor>& bias, int64_t out_channels, int64_t bn,
-                   int64_t splits, int64_t kind, int64_t waves) {
+                   int64_t splits, int64_t kind, int64_t waves, int64_t sub) {
   auto x = x_in.contiguous();
   check_f32_gpu(x, "x");
   check_f32_gpu(a, "a");
@@ -361,7 +361,7 @@ at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
   if (n == 0 || h == 0 || w == 0 || out_channels == 0) return y;
   const BgPlan plan = bg_plan(n, r, h, w, out_channels, static_cast<int>(bn),
                               static_cast<int>(splits), static_cast<int>(kind),
-                              static_cast<int>(waves));
+                              static_cast<int>(waves), static_cast<int>(sub));
   // 32-bit tile / element indices of the GEMM and transform kernels
   TORCH_CHECK(plan.ksteps * 16 * plan.np < (int64_t{1} << 31) &&
                   plan.mp * plan.np < (int64_t{1} << 31),
@@ -397,7 +397,7 @@ TORCH_LIBRARY(tgpipe, m) {
         "int splits=0) -> Tensor");
   m.def("bg_weight(Tensor w, bool flip, int kind=4) -> Tensor");
   m.def("bg_conv(Tensor x, Tensor a, Tensor? bias, int out_channels, int bn=0, int splits=0, "
-        "int kind=4, int waves=0) -> Tensor");
+        "int kind=4, int waves=0, int sub=0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {

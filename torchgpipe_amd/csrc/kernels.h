@@ -97,15 +97,16 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
 struct BgPlan {
   int kind = 4;           // 4: F(4x4) (36 positions), 2: F(2x2) (16 positions)
   int waves = 8;          // GEMM tile height 32 * waves: 4 (128 rows) or 8 (256 rows)
-  int bn = 64;            // GEMM tile width (tiles): 48-128 (4 waves), 64-192 (8 waves)
+  int bn = 64;            // GEMM tile width (tiles): 48-128 (4 waves), 64-144 (8 waves)
+  int sub = 2;            // 16-deep reduction steps per pipeline stage (1 or 2)
   int splits = 1;         // split-K slabs
   int64_t mp = 0, np = 0, ksteps = 0;
   int64_t workspace = 0;  // floats: V + split slabs of M
 };
 int bg_pick_bn(int64_t tiles, int kind);
 BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
-               int bn, int splits, int kind, int waves);
-// weights in the GEMM's operand layout U[36 or 16][ceil(R/16)][round(O, 256)][16]
+               int bn, int splits, int kind, int waves, int sub);
+// weights in the GEMM's operand layout U[36 or 16][2 ceil(R/32)][round(O, 256)][16]
 int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind);
 void launch_bg_weight(const float* w, float* a, int64_t out_channels, int64_t red_channels,
                       bool flip, int kind, hipStream_t stream);

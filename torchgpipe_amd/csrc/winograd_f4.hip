@@ -1317,26 +1317,37 @@ __device__ __forceinline__ void bg_wait_vm() {
   else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N == 11) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+  else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 }
 
 // C[z][b][Mp][Np] = sum over the split's steps of A[b]^T B[b].  Workgroup: kWaves waves, a
 // (32 kWaves) x BN tile; wave w owns rows 32w..32w+31 (two 16-row MFMA blocks) and all BN
-// columns, i.e. 2 x BN/16 accumulator tiles of v_mfma_f32_16x16x4f32.  Per 16-deep step:
-// 2 + BN/16 ds_read_b128 and 8 * BN/16 MFMAs per wave; the step's (BM + BN) x 64 B arrive
-// by LDS-DMA two steps ahead.  Bigger tiles cut the bytes per FLOP the CUs pull from L2 /
-// the Infinity Cache: 128 x 48 moves 57 B per KFLOP, 256 x 144 only 22.
-template <int kWaves, int BN>
+// columns, i.e. 2 x BN/16 accumulator tiles of v_mfma_f32_16x16x4f32.  A pipeline stage is
+// kSub 16-deep steps: per stage and wave kSub (2 + BN/16) ds_read_b128 and 8 kSub BN/16
+// MFMAs, one barrier, and the stage's kSub (BM + BN) x 64 B arriving by LDS-DMA into a
+// three-slot ring two stages ahead.  The fragments of stage st+1 are read while stage st's
+// MFMAs run.  (256-row tiles of 8 waves move fewer bytes per FLOP but ran slower on every
+// U-Net shape: profiles/r3/bg_bench.json.)
+template <int kWaves, int BN, int kSub>
 __global__ __launch_bounds__(64 * kWaves, 512 / (64 * kWaves)) void bg_gemm_kernel(
     const float* __restrict__ a, const float* __restrict__ bmat, float* __restrict__ c, int Mp,
     int Np, int ksteps, int mtiles, int ntiles, int batch, int splits) {
   constexpr int BM = 32 * kWaves;
-  constexpr int kA = BM * 16, kB = BN * 16, kStage = kA + kB;
-  constexpr int kPieces = kStage / 256;  // 1 KiB LDS-DMA pieces per step
+  constexpr int kA = BM * 16, kB = BN * 16, kSubStage = kA + kB, kStage = kSub * kSubStage;
+  constexpr int kSubPieces = kSubStage / 256;  // 1 KiB LDS-DMA pieces per step
+  constexpr int kPieces = kSub * kSubPieces;
   constexpr int kAPieces = kA / 256;
   constexpr int kNJ = BN / 16;
   constexpr int kPer = (kPieces + kWaves - 1) / kWaves;
-  static_assert(BN % 16 == 0 && kStage % 256 == 0 && kPer <= 4, "tile shape");
+  static_assert(BN % 16 == 0 && kSubStage % 256 == 0 && kPer <= 8, "tile shape");
   __shared__ float lds[3 * kStage];
 
   const int nwg = ntiles * mtiles * batch * splits;
@@ -1360,26 +1371,31 @@ __global__ __launch_bounds__(64 * kWaves, 512 / (64 * kWaves)) void bg_gemm_kern
   const int64_t astep = static_cast<int64_t>(Mp) * 16, bstep = static_cast<int64_t>(Np) * 16;
   const float* abase = a + static_cast<int64_t>(bb) * ksteps * astep + static_cast<int64_t>(mt) * kA;
   const float* bbase = bmat + static_cast<int64_t>(bb) * ksteps * bstep + static_cast<int64_t>(nt) * kB;
-  const int s0 = static_cast<int>(static_cast<int64_t>(z) * ksteps / splits);
-  const int s1 = static_cast<int>(static_cast<int64_t>(z + 1) * ksteps / splits);
+  // stages of kSub steps (ksteps is a multiple of 2: the transforms pad to 32 channels)
+  const int nstages = ksteps / kSub;
+  const int s0 = static_cast<int>(static_cast<int64_t>(z) * nstages / splits);
+  const int s1 = static_cast<int>(static_cast<int64_t>(z + 1) * nstages / splits);
 
-  auto issue = [&](int st, int buf) {
+  auto issue = [&](int sg, int buf) {
     float* dst = lds + buf * kStage;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int piece = i * kWaves + wave;
       if (piece < kPieces) {
-        const float* src = piece < kAPieces ? abase + st * astep + piece * 256
-                                            : bbase + st * bstep + (piece - kAPieces) * 256;
+        const int sub = piece / kSubPieces;
+        const int pc = piece - sub * kSubPieces;
+        const int st = sg * kSub + sub;
+        const float* src = pc < kAPieces ? abase + st * astep + pc * 256
+                                         : bbase + st * bstep + (pc - kAPieces) * 256;
         __builtin_amdgcn_global_load_lds((glob_void_t*)(src + lane * 4),
                                          (lds_void_t*)(dst + piece * 256), 16, 0, 0);
       }
     }
   };
-  // this wave's pieces per step: waiting for vmcnt <= k * mine leaves the last k issued
-  // steps in flight
+  // this wave's pieces per stage: waiting for vmcnt <= k * mine leaves the last k issued
+  // stages in flight
   const int mine = (kPieces - wave + kWaves - 1) / kWaves;
-  auto wait_steps_in_flight = [&](int k) {
+  auto wait_stages_in_flight = [&](int k) {
     switch (k * mine) {
       case 0: bg_wait_vm<0>(); break;
       case 1: bg_wait_vm<1>(); break;
@@ -1389,7 +1405,15 @@ __global__ __launch_bounds__(64 * kWaves, 512 / (64 * kWaves)) void bg_gemm_kern
       case 5: bg_wait_vm<5>(); break;
       case 6: bg_wait_vm<6>(); break;
       case 7: bg_wait_vm<7>(); break;
-      default: bg_wait_vm<8>(); break;
+      case 8: bg_wait_vm<8>(); break;
+      case 9: bg_wait_vm<9>(); break;
+      case 10: bg_wait_vm<10>(); break;
+      case 11: bg_wait_vm<11>(); break;
+      case 12: bg_wait_vm<12>(); break;
+      case 13: bg_wait_vm<13>(); break;
+      case 14: bg_wait_vm<14>(); break;
+      case 15: bg_wait_vm<15>(); break;
+      default: bg_wait_vm<16>(); break;
     }
   };
 
@@ -1411,50 +1435,61 @@ __global__ __launch_bounds__(64 * kWaves, 512 / (64 * kWaves)) void bg_gemm_kern
     const int row = jj * 16 + j;
     boff[jj] = kA + row * 16 + (bg_quad(q, row) << 2);
   }
-  floatx4 af[2], bf[kNJ];
+  floatx4 af[kSub][2], bf[kSub][kNJ];
   auto fetch = [&](int buf) {
     const float* base = lds + buf * kStage;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const floatx4*>(base + aoff[i]);
+    for (int u = 0; u < kSub; ++u) {
 #pragma unroll
-    for (int jj = 0; jj < kNJ; ++jj) bf[jj] = *reinterpret_cast<const floatx4*>(base + boff[jj]);
+      for (int i = 0; i < 2; ++i)
+        af[u][i] = *reinterpret_cast<const floatx4*>(base + u * kSubStage + aoff[i]);
+#pragma unroll
+      for (int jj = 0; jj < kNJ; ++jj)
+        bf[u][jj] = *reinterpret_cast<const floatx4*>(base + u * kSubStage + boff[jj]);
+    }
   };
 
-  // Software pipeline over a three-slot ring: at step st the fragments of st are already
-  // in registers (read during step st-1); after one barrier (step st+1 landed, every wave
-  // done reading slot st) the wave issues step st+3's DMA into slot st, reads step st+1's
-  // fragments and runs step st's MFMAs while those reads return.
+  // Software pipeline over the three-slot ring: at stage k the fragments of k are already
+  // in registers (read during stage k-1); after one barrier (stage k+1 landed, every wave
+  // done reading slot k) the wave issues stage k+3's DMA into slot k, reads stage k+1's
+  // fragments and runs stage k's MFMAs while those reads return.
   const int nst = s1 - s0;
   if (nst > 0) {
     issue(s0, 0);
     if (nst > 1) issue(s0 + 1, 1);
     if (nst > 2) issue(s0 + 2, 2);
-    wait_steps_in_flight(nst > 2 ? 2 : nst - 1);
+    wait_stages_in_flight(nst > 2 ? 2 : nst - 1);
     __builtin_amdgcn_s_barrier();
     fetch(0);
   }
   int buf = 0;
   for (int k = 0; k < nst; ++k) {
-    floatx4 ac[2], bc[kNJ];
+    floatx4 ac[kSub][2], bc[kSub][kNJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) ac[i] = af[i];
+    for (int u = 0; u < kSub; ++u) {
 #pragma unroll
-    for (int jj = 0; jj < kNJ; ++jj) bc[jj] = bf[jj];
+      for (int i = 0; i < 2; ++i) ac[u][i] = af[u][i];
+#pragma unroll
+      for (int jj = 0; jj < kNJ; ++jj) bc[u][jj] = bf[u][jj];
+    }
     const int nb = buf == 2 ? 0 : buf + 1;
     if (k + 1 < nst) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's reads are done
-      wait_steps_in_flight(k + 2 < nst ? 1 : 0);           // step k+1 landed
+      wait_stages_in_flight(k + 2 < nst ? 1 : 0);          // stage k+1 landed
       __builtin_amdgcn_s_barrier();
       if (k + 3 < nst) issue(s0 + k + 3, buf);
       fetch(nb);
     }
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
+    for (int u = 0; u < kSub; ++u)
 #pragma unroll
-      for (int jj = 0; jj < kNJ; ++jj)
+      for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[i][kk], bc[jj][kk], acc[i][jj], 0, 0, 0);
+        for (int jj = 0; jj < kNJ; ++jj)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[u][i][kk], bc[u][jj][kk],
+                                                             acc[i][jj], 0, 0, 0);
     buf = nb;
   }
 
@@ -1864,7 +1899,10 @@ constexpr int kBgRowPad = 256;  // weight rows (output channels) padded for eith
 int64_t bg_round(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // (waves, BN) instantiations of bg_gemm_kernel
 constexpr int kBgTiles[][2] = {{4, 48}, {4, 64}, {4, 96}, {4, 128},
-                               {8, 64}, {8, 96}, {8, 128}, {8, 144}, {8, 192}};
+                               {8, 64}, {8, 96}, {8, 128}, {8, 144}};
+// 16-deep steps of the transformed operands: the reduction padded to 32 channels, so a
+// pipeline stage may hold one or two steps
+int64_t bg_ksteps(int64_t red_channels) { return (red_channels + 31) / 32 * 2; }
 }  // namespace
 
 int bg_pick_bn(int64_t tiles, int kind) {
@@ -1887,13 +1925,13 @@ int bg_pick_bn(int64_t tiles, int kind) {
 }
 
 BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
-               int bn, int splits, int kind, int waves) {
+               int bn, int splits, int kind, int waves, int sub) {
   BgPlan plan;
   plan.kind = kind == 2 ? 2 : 4;
   const int tile = plan.kind;
   const int64_t npos = plan.kind == 2 ? kP2 : kP;
   const int64_t P = n * ((h + tile - 1) / tile) * ((w + tile - 1) / tile);
-  plan.ksteps = (red_channels + 15) / 16;
+  plan.ksteps = bg_ksteps(red_channels);
   plan.mp = bg_round(out_channels, kBgRowPad);
   bool valid = false;
   for (const auto& t : kBgTiles) valid |= t[0] == waves && t[1] == bn;
@@ -1905,11 +1943,12 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
   }
   plan.waves = waves;
   plan.bn = bn;
+  plan.sub = sub == 1 || sub == 2 ? sub : 2;
   plan.np = bg_round(P, plan.bn);
   const int64_t bm = 32 * waves;
   const int64_t tiles = (plan.mp / bm) * (plan.np / plan.bn) * npos;
   if (splits > 0) {
-    plan.splits = static_cast<int>(std::min<int64_t>(splits, plan.ksteps));
+    plan.splits = splits;
   } else {
     // >= 2-3 workgroups per CU, >= 16 steps per split
     const int64_t target = waves == 8 ? 512 : 768;
@@ -1917,19 +1956,22 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
     while (tiles * s < target && plan.ksteps / (s * 2) >= 16) s *= 2;
     plan.splits = static_cast<int>(s);
   }
+  // every split owns >= 1 pipeline stage
+  plan.splits = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(plan.splits,
+                                                                        plan.ksteps / plan.sub)));
   plan.workspace = npos * plan.ksteps * 16 * plan.np + plan.splits * npos * plan.mp * plan.np;
   return plan;
 }
 
 int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind) {
-  return (kind == 2 ? kP2 : kP) * ((red_channels + 15) / 16) * 16 *
+  return (kind == 2 ? kP2 : kP) * bg_ksteps(red_channels) * 16 *
          bg_round(out_channels, kBgRowPad);
 }
 
 void launch_bg_weight(const float* w, float* a, int64_t out_channels, int64_t red_channels,
                       bool flip, int kind, hipStream_t stream) {
   const int64_t mp = bg_round(out_channels, kBgRowPad);
-  const int64_t ksteps = (red_channels + 15) / 16;
+  const int64_t ksteps = bg_ksteps(red_channels);
   const int64_t total = ksteps * 16 * mp;
   hipLaunchKernelGGL(kind == 2 ? bg_weight_f2_kernel : bg_weight_f4_kernel,
                      dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, stream, w, a,
@@ -1965,17 +2007,20 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
   const int ntiles = static_cast<int>(plan.np / plan.bn);
   const int64_t nwg = static_cast<int64_t>(mtiles) * ntiles * npos * plan.splits;
   using Gemm = void (*)(const float*, const float*, float*, int, int, int, int, int, int, int);
-  Gemm gemm = bg_gemm_kernel<4, 48>;
-  switch (plan.waves * 1000 + plan.bn) {
-    case 4048: gemm = bg_gemm_kernel<4, 48>; break;
-    case 4064: gemm = bg_gemm_kernel<4, 64>; break;
-    case 4096: gemm = bg_gemm_kernel<4, 96>; break;
-    case 4128: gemm = bg_gemm_kernel<4, 128>; break;
-    case 8064: gemm = bg_gemm_kernel<8, 64>; break;
-    case 8096: gemm = bg_gemm_kernel<8, 96>; break;
-    case 8128: gemm = bg_gemm_kernel<8, 128>; break;
-    case 8144: gemm = bg_gemm_kernel<8, 144>; break;
-    case 8192: gemm = bg_gemm_kernel<8, 192>; break;
+  Gemm gemm = bg_gemm_kernel<4, 64, 2>;
+  switch (plan.waves * 10000 + plan.bn * 10 + plan.sub) {
+    case 40481: gemm = bg_gemm_kernel<4, 48, 1>; break;
+    case 40641: gemm = bg_gemm_kernel<4, 64, 1>; break;
+    case 40961: gemm = bg_gemm_kernel<4, 96, 1>; break;
+    case 41281: gemm = bg_gemm_kernel<4, 128, 1>; break;
+    case 40482: gemm = bg_gemm_kernel<4, 48, 2>; break;
+    case 40642: gemm = bg_gemm_kernel<4, 64, 2>; break;
+    case 40962: gemm = bg_gemm_kernel<4, 96, 2>; break;
+    case 41282: gemm = bg_gemm_kernel<4, 128, 2>; break;
+    case 80641: gemm = bg_gemm_kernel<8, 64, 1>; break;
+    case 80961: gemm = bg_gemm_kernel<8, 96, 1>; break;
+    case 81281: gemm = bg_gemm_kernel<8, 128, 1>; break;
+    case 81441: gemm = bg_gemm_kernel<8, 144, 1>; break;
     default: break;
   }
   hipLaunchKernelGGL(gemm, dim3(static_cast<unsigned>(nwg)), dim3(64 * plan.waves), 0, stream, a,
