@@ -98,7 +98,7 @@ struct BgPlan {
   int kind = 4;           // 4: F(4x4) (36 positions), 2: F(2x2) (16 positions)
   int waves = 8;          // GEMM tile height 32 * waves: 4 (128 rows) or 8 (256 rows)
   int bn = 64;            // GEMM tile width (tiles): 48-128 (4 waves), 64-144 (8 waves)
-  int sub = 2;            // 16-deep reduction steps per pipeline stage (1 or 2)
+  int sub = 1;            // 16-deep reduction steps per pipeline stage (1 or 2)
   int splits = 1;         // split-K slabs
   int64_t mp = 0, np = 0, ksteps = 0;
   int64_t workspace = 0;  // floats: V + split slabs of M

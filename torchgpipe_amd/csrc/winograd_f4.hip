@@ -1277,34 +1277,45 @@ __global__ __launch_bounds__(256) void bg_weight_f4_kernel(const float* __restri
 }
 
 // V[b][step][Np][16] = B^T d B of (tile t, channel step*16 + k); zeros in the padding.
-// Lanes: 16 channels x 4 consecutive tiles, so each position's store is 256 contiguous B.
+// A thread transforms the four channels k = q, q+4, q+8, q+12 of a step (q = 0..3) for one
+// tile: bg_slot puts those four at consecutive floats, so each position is one 16-byte
+// store, and a wave (16 tiles x 4 q) writes 1 KiB contiguous per position.  The pass is
+// bandwidth-bound (it writes 2.25x the input), so the store width is what matters.
+template <bool kVec>
 __global__ __launch_bounds__(256) void bg_input_f4_kernel(const float* __restrict__ x,
                                                          float* __restrict__ v, int R, int H,
                                                          int W, int TW, int tpi, int P, int Np,
                                                          int ksteps, uint32_t x_bytes) {
   const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (idx >= static_cast<int64_t>(ksteps) * 16 * Np) return;
-  const int k = static_cast<int>(idx & 15);
-  const int64_t rest = idx >> 4;
+  if (idx >= static_cast<int64_t>(ksteps) * 4 * Np) return;
+  const int q = static_cast<int>(idx & 3);
+  const int64_t rest = idx >> 2;
   const int t = static_cast<int>(rest % Np);
   const int st = static_cast<int>(rest / Np);
-  const int c = st * 16 + k;
-  F4Patch p;
-  if (t < P && c < R) {
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
-                                          static_cast<int>(x_bytes), 0x00020000);
-    f4_fwd_offsets(p, t, c, P, tpi, TW, R, H, W);
-    f4_load_patch<false>(p, xr, 0);
-    f4_transform(p);
-  } else {
-#pragma unroll
-    for (int b = 0; b < kP; ++b) p.d[b] = 0.f;
-  }
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                        static_cast<int>(x_bytes), 0x00020000);
   const int64_t plane = static_cast<int64_t>(ksteps) * Np * 16;
-  float* dst = v + (static_cast<int64_t>(st) * Np + t) * 16 + bg_slot(k, t);
+  float* dst = v + (static_cast<int64_t>(st) * Np + t) * 16 + (bg_quad(q, t) << 2);
+  float out[4][kP];
 #pragma unroll
-  for (int b = 0; b < kP; ++b) dst[b * plane] = p.d[b];
+  for (int e = 0; e < 4; ++e) {
+    const int c = st * 16 + q + 4 * e;
+    F4Patch p;
+    if (t < P && c < R) {
+      f4_fwd_offsets(p, t, c, P, tpi, TW, R, H, W);
+      f4_load_patch<kVec>(p, xr, 0);
+      f4_transform(p);
+    } else {
+#pragma unroll
+      for (int b = 0; b < kP; ++b) p.d[b] = 0.f;
+    }
+#pragma unroll
+    for (int b = 0; b < kP; ++b) out[e][b] = p.d[b];
+  }
+#pragma unroll
+  for (int b = 0; b < kP; ++b)
+    *reinterpret_cast<floatx4*>(dst + b * plane) = floatx4{out[0][b], out[1][b], out[2][b], out[3][b]};
 }
 
 template <int N>
@@ -1906,11 +1917,11 @@ int64_t bg_ksteps(int64_t red_channels) { return (red_channels + 31) / 32 * 2; }
 }  // namespace
 
 int bg_pick_bn(int64_t tiles, int kind) {
-  // The 4-wave (128-row) tile width that pads the tile count least; ties go to the width
-  // measured fastest (benchmarks/bg_bench.py, profiles/r3/bg_bench.json): 64 for F(4x4),
-  // 96 for F(2x2).
-  static constexpr int kF4[] = {64, 48, 96, 128};
-  static constexpr int kF2[] = {96, 64, 48, 128};
+  // The 128-row tile width that pads the tile count least; ties go to the width measured
+  // fastest (benchmarks/bg_bench.py, profiles/r3/bg_bench.json): 48 for F(4x4) (128 on
+  // the widest grids), 128 then 96 for F(2x2).
+  static constexpr int kF4[] = {48, 64, 128, 96};
+  static constexpr int kF2[] = {128, 96, 48, 64};
   const int* order = kind == 2 ? kF2 : kF4;
   int best = order[0];
   int64_t best_pad = bg_round(tiles, best);
@@ -1921,6 +1932,7 @@ int bg_pick_bn(int64_t tiles, int kind) {
       best_pad = pad;
     }
   }
+  if (kind != 2 && tiles >= 4096 && tiles % 128 == 0) best = 128;
   return best;
 }
 
@@ -1943,7 +1955,9 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
   }
   plan.waves = waves;
   plan.bn = bn;
-  plan.sub = sub == 1 || sub == 2 ? sub : 2;
+  // one 16-deep step per stage: two halved the resident workgroups per CU and ran 2-20 %
+  // slower on every shape (profiles/r3/bg_bench.json)
+  plan.sub = sub == 1 || sub == 2 ? sub : 1;
   plan.np = bg_round(P, plan.bn);
   const int64_t bm = 32 * waves;
   const int64_t tiles = (plan.mp / bm) * (plan.np / plan.bn) * npos;
@@ -1996,10 +2010,11 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
                        static_cast<int>(th * tw), static_cast<int>(P),
                        static_cast<int>(plan.np), static_cast<int>(plan.ksteps));
   } else {
-    hipLaunchKernelGGL(bg_input_f4_kernel, dim3(static_cast<unsigned>((vt + 255) / 256)),
-                       dim3(256), 0, stream, x, v, static_cast<int>(red_channels),
-                       static_cast<int>(h), static_cast<int>(w), static_cast<int>(tw),
-                       static_cast<int>(th * tw), static_cast<int>(P),
+    const int64_t vt4 = plan.ksteps * 4 * plan.np;
+    hipLaunchKernelGGL((w & 3) == 0 ? bg_input_f4_kernel<true> : bg_input_f4_kernel<false>,
+                       dim3(static_cast<unsigned>((vt4 + 255) / 256)), dim3(256), 0, stream, x, v,
+                       static_cast<int>(red_channels), static_cast<int>(h), static_cast<int>(w),
+                       static_cast<int>(tw), static_cast<int>(th * tw), static_cast<int>(P),
                        static_cast<int>(plan.np), static_cast<int>(plan.ksteps),
                        static_cast<uint32_t>(n * red_channels * h * w * 4));
   }
