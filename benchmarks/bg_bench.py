@@ -25,9 +25,6 @@ SHAPES = [  # (N, C, K, H)
     (16, 512, 256, 24), (16, 256, 256, 48),
     (32, 1024, 1024, 12), (32, 2048, 2048, 6), (32, 512, 512, 24),
     (40, 1024, 1024, 12), (40, 2048, 2048, 6), (40, 512, 512, 24), (40, 256, 256, 48),
-    # the shallower levels (fused F(4x4) kernels today)
-    (16, 128, 128, 96), (32, 128, 128, 96), (40, 128, 128, 96), (40, 128, 128, 48),
-    (16, 512, 128, 48), (40, 256, 64, 96), (16, 64, 64, 192), (40, 64, 64, 192),
 ]
 
 
@@ -66,7 +63,8 @@ def main() -> None:
                'current_tflops': round(flops / cur / 1e9, 1)}
         for kind in (4, 2):
             wb = ops.bg_weight(w, False, kind)
-            for waves, bn, sub in [(0, 0, 0)] + [(4, b, 1) for b in (48, 64, 96, 128)]:
+            for waves, bn, sub in [(0, 0, 0)] + [(w_, b, 1) for w_ in (4, 1)
+                                                for b in (48, 64, 96, 128)]:
                 tag = f'f{kind}_{"auto" if not waves else f"{waves}x{bn}s{sub}"}'
                 got = ops.bg_conv(x, wb, None, k, bn, 0, kind, waves, sub)
                 err = ((got - ref).norm() / ref.norm()).item()
