@@ -63,8 +63,7 @@ def main() -> None:
                'current_tflops': round(flops / cur / 1e9, 1)}
         for kind in (4, 2):
             wb = ops.bg_weight(w, False, kind)
-            for waves, bn, sub in [(0, 0, 0)] + [(w_, b, 1) for w_ in (4, 1)
-                                                for b in (48, 64, 96, 128)]:
+            for waves, bn, sub in [(0, 0, 0)] + [(4, b, 1) for b in (48, 64, 96, 128)]:
                 tag = f'f{kind}_{"auto" if not waves else f"{waves}x{bn}s{sub}"}'
                 got = ops.bg_conv(x, wb, None, k, bn, 0, kind, waves, sub)
                 err = ((got - ref).norm() / ref.norm()).item()

@@ -249,8 +249,7 @@ def test_batched_gemm_winograd_matches_conv2d(shape, flip, kind):
 
 @pytest.mark.parametrize('waves,bn,sub', [(4, 48, 1), (4, 64, 1), (4, 96, 1), (4, 128, 1),
                                           (4, 48, 2), (4, 64, 2), (4, 96, 2), (4, 128, 2),
-                                          (8, 64, 1), (8, 96, 1), (8, 128, 1), (8, 144, 1),
-                                          (1, 48, 1), (1, 64, 1), (1, 96, 1), (1, 128, 1)])
+                                          (8, 64, 1), (8, 96, 1), (8, 128, 1), (8, 144, 1)])
 @pytest.mark.parametrize('splits', [1, 3])
 def test_batched_gemm_tile_shapes_and_splits(waves, bn, sub, splits):
     n, c, k, h, w = 4, 96, 300, 20, 20

@@ -1517,97 +1517,6 @@ __global__ __launch_bounds__(64 * kWaves, 512 / (64 * kWaves)) void bg_gemm_kern
   }
 }
 
-// The same GEMM without LDS: each wave streams its own A rows and the whole B tile straight
-// into registers, three steps ahead (the compiler's vmcnt tracking orders each use after
-// its load).  Nothing is shared through LDS, so there is no barrier: the four waves of a
-// workgroup run independently and read the same B lines, which the CU's L1 serves after
-// the first wave.  A step's fragments are one contiguous 2 KiB (A) and BN x 64 B (B) block.
-template <int BN>
-__global__ __launch_bounds__(256, 2) void bg_gemm_direct_kernel(
-    const float* __restrict__ a, const float* __restrict__ bmat, float* __restrict__ c, int Mp,
-    int Np, int ksteps, int mtiles, int ntiles, int batch, int splits) {
-  constexpr int BM = 128;
-  constexpr int kNJ = BN / 16;
-  constexpr int kDepth = 3;
-  const int nwg = ntiles * mtiles * batch * splits;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int qq = nwg >> 3, rr = nwg & 7;
-  int wid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  const int nt = wid % ntiles;
-  wid /= ntiles;
-  const int mt = wid % mtiles;
-  wid /= mtiles;
-  const int bb = wid % batch;
-  const int z = wid / batch;
-
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int64_t astep = static_cast<int64_t>(Mp) * 16, bstep = static_cast<int64_t>(Np) * 16;
-  const int q = lane >> 4, j = lane & 15;
-  const float* ap[2];
-  const float* bp[kNJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = mt * BM + wave * 32 + i * 16 + j;
-    ap[i] = a + static_cast<int64_t>(bb) * ksteps * astep + row * 16 + (bg_quad(q, row) << 2);
-  }
-#pragma unroll
-  for (int jj = 0; jj < kNJ; ++jj) {
-    const int row = nt * BN + jj * 16 + j;
-    bp[jj] = bmat + static_cast<int64_t>(bb) * ksteps * bstep + row * 16 + (bg_quad(q, row) << 2);
-  }
-  const int s0 = static_cast<int>(static_cast<int64_t>(z) * ksteps / splits);
-  const int s1 = static_cast<int>(static_cast<int64_t>(z + 1) * ksteps / splits);
-
-  floatx4 acc[2][kNJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int jj = 0; jj < kNJ; ++jj) acc[i][jj] = floatx4{0.f, 0.f, 0.f, 0.f};
-  floatx4 ra[kDepth][2], rb[kDepth][kNJ];
-  auto load = [&](int st, floatx4 (&fa)[2], floatx4 (&fb)[kNJ]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const floatx4*>(ap[i] + st * astep);
-#pragma unroll
-    for (int jj = 0; jj < kNJ; ++jj) fb[jj] = *reinterpret_cast<const floatx4*>(bp[jj] + st * bstep);
-  };
-  auto mma = [&](const floatx4 (&fa)[2], const floatx4 (&fb)[kNJ]) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-      for (int jj = 0; jj < kNJ; ++jj)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][kk], fb[jj][kk], acc[i][jj], 0, 0, 0);
-  };
-#pragma unroll
-  for (int u = 0; u < kDepth; ++u)
-    if (s0 + u < s1) load(s0 + u, ra[u], rb[u]);
-  for (int st = s0; st < s1; st += kDepth) {
-#pragma unroll
-    for (int u = 0; u < kDepth; ++u) {
-      if (st + u < s1) {
-        mma(ra[u], rb[u]);
-        if (st + u + kDepth < s1) load(st + u + kDepth, ra[u], rb[u]);
-      }
-    }
-  }
-
-  float* cz = c + (static_cast<int64_t>(z) * batch + bb) * Mp * Np;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m0 = mt * BM + wave * 32 + i * 16 + 4 * q;
-#pragma unroll
-    for (int jj = 0; jj < kNJ; ++jj) {
-      const int n = nt * BN + jj * 16 + j;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cz[static_cast<int64_t>(m0 + r) * Np + n] = acc[i][jj][r];
-    }
-  }
-}
-
 // Y = A^T (sum_z M[z]) A (+ bias): one thread per (output channel, tile), consecutive
 // threads on consecutive tiles (coalesced reads of each position's M row).
 __global__ __launch_bounds__(256) void bg_output_f4_kernel(
@@ -2000,10 +1909,8 @@ namespace {
 constexpr int kBgRowPad = 256;  // weight rows (output channels) padded for either tile height
 int64_t bg_round(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // (waves, BN) instantiations of bg_gemm_kernel
-// waves = 1: bg_gemm_direct_kernel (4 independent waves, no LDS), 128 rows
 constexpr int kBgTiles[][2] = {{4, 48}, {4, 64}, {4, 96}, {4, 128},
-                               {8, 64}, {8, 96}, {8, 128}, {8, 144},
-                               {1, 48}, {1, 64}, {1, 96}, {1, 128}};
+                               {8, 64}, {8, 96}, {8, 128}, {8, 144}};
 // 16-deep steps of the transformed operands: the reduction padded to 32 channels, so a
 // pipeline stage may hold one or two steps
 int64_t bg_ksteps(int64_t red_channels) { return (red_channels + 31) / 32 * 2; }
@@ -2050,9 +1957,9 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
   plan.bn = bn;
   // one 16-deep step per stage: two halved the resident workgroups per CU and ran 2-20 %
   // slower on every shape (profiles/r3/bg_bench.json)
-  plan.sub = (sub == 1 || sub == 2) && waves != 1 ? sub : 1;
+  plan.sub = sub == 1 || sub == 2 ? sub : 1;
   plan.np = bg_round(P, plan.bn);
-  const int64_t bm = waves == 1 ? 128 : 32 * waves;
+  const int64_t bm = 32 * waves;
   const int64_t tiles = (plan.mp / bm) * (plan.np / plan.bn) * npos;
   if (splits > 0) {
     plan.splits = splits;
@@ -2111,7 +2018,7 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
                        static_cast<int>(plan.np), static_cast<int>(plan.ksteps),
                        static_cast<uint32_t>(n * red_channels * h * w * 4));
   }
-  const int mtiles = static_cast<int>(plan.mp / (plan.waves == 1 ? 128 : 32 * plan.waves));
+  const int mtiles = static_cast<int>(plan.mp / (32 * plan.waves));
   const int ntiles = static_cast<int>(plan.np / plan.bn);
   const int64_t nwg = static_cast<int64_t>(mtiles) * ntiles * npos * plan.splits;
   using Gemm = void (*)(const float*, const float*, float*, int, int, int, int, int, int, int);
@@ -2129,13 +2036,9 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
     case 80961: gemm = bg_gemm_kernel<8, 96, 1>; break;
     case 81281: gemm = bg_gemm_kernel<8, 128, 1>; break;
     case 81441: gemm = bg_gemm_kernel<8, 144, 1>; break;
-    case 10481: gemm = bg_gemm_direct_kernel<48>; break;
-    case 10641: gemm = bg_gemm_direct_kernel<64>; break;
-    case 10961: gemm = bg_gemm_direct_kernel<96>; break;
-    case 11281: gemm = bg_gemm_direct_kernel<128>; break;
     default: break;
   }
-  const int block = plan.waves == 1 ? 256 : 64 * plan.waves;
+  const int block = 64 * plan.waves;
   hipLaunchKernelGGL(gemm, dim3(static_cast<unsigned>(nwg)), dim3(block), 0, stream, a,
                      v, cbuf, static_cast<int>(plan.mp), static_cast<int>(plan.np),
                      static_cast<int>(plan.ksteps), mtiles, ntiles, static_cast<int>(npos),
