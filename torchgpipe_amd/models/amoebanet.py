@@ -21,6 +21,7 @@ keep the reference's children, so parameters and state-dict keys are the same
 as the plain model (``fused=False``), which also serves as the numerics oracle.
 """
 from collections import OrderedDict
+import os
 from typing import Callable, Dict, Iterator, List, Optional, Tuple, Union
 
 import torch
@@ -33,6 +34,7 @@ from torchgpipe_amd.ops.unet_ops import MaxPool2x2
 __all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS', 'set_cell_streams']
 
 _SIDE_STREAMS: Dict[Tuple[torch.device, int], torch.cuda.Stream] = {}
+_CAPTURE_STREAMS = os.environ.get('TGPIPE_CAPTURE_STREAMS', '0') == '1'
 
 
 def _side_stream(device: torch.device, main: torch.cuda.Stream) -> torch.cuda.Stream:
@@ -279,9 +281,11 @@ class Cell(nn.Module):
                 ) -> Tuple[Tensor, Tensor]:
         s1, s2 = states if isinstance(states, tuple) else (states, states)
         skip = s1
-        # (not inside a hipGraph capture: capturing the two-stream cells of the full model
-        # crashed the HIP runtime, profiles/r2/bench_amoeba_s13.md)
-        if self.streams and s1.is_cuda and not torch.cuda.is_current_stream_capturing():
+        # (not inside a hipGraph capture unless TGPIPE_CAPTURE_STREAMS=1: capturing the
+        # two-stream cells of the full model crashed the HIP runtime,
+        # profiles/r2/bench_amoeba_s13.md)
+        if self.streams and s1.is_cuda and (_CAPTURE_STREAMS or
+                                            not torch.cuda.is_current_stream_capturing()):
             return self._forward_two_streams(s1, s2), skip
         nodes = [self.reduce1(s1), self.reduce2(s2)]
         for k in range(0, len(self.operations), 2):
