@@ -123,10 +123,10 @@ def parse() -> argparse.Namespace:
                    help='tiny models of the same families (CI smoke test of this script only)')
     p.add_argument('--channels-last', action='store_true',
                    help='NHWC activations and weights (MIOpen NHWC kernels; AmoebaNet)')
-    p.add_argument('--graph', action='store_true',
+    p.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
                    help='one-GPU runs: capture the whole step (forward, backward, SGD) into a '
                         'hipGraph after the warm-up and replay it (RNG-free models only: '
-                        'AmoebaNet; parallel/graph.py)')
+                        'AmoebaNet; parallel/graph.py; auto: on for one-GPU AmoebaNet)')
     p.add_argument('--cell-streams', choices=['auto', 'on', 'off'], default='auto',
                    help="AmoebaNet: run each cell's independent nodes on two HIP streams "
                         '(auto: on)')
@@ -298,7 +298,10 @@ class Bench:
         signature = signature_of(torch.empty(batch, *shape, device='meta'))
 
         graph = None
-        if args.graph and tag == 'headline':
+        # whole-step hipGraph: AmoebaNet (no RNG) on one GPU (two-stream cells included,
+        # launched from a big-stack thread: profiles/r3/capture_crash.md)
+        use_graph = choice(args.graph, self.world == 1 and self.gpu and not unet)
+        if use_graph:
             if self.world != 1:
                 raise SystemExit('--graph captures one-rank runs only')
             from torchgpipe_amd.parallel import StepGraph
@@ -319,7 +322,8 @@ class Bench:
             settle=(lambda: graph.captured) if graph is not None else None)
         res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
                    steps=steps, cell_streams=cell_streams, overlap_recompute=overlap,
-                   overlap_forward=overlap_fwd, wgrad_stream=wgrad_stream)
+                   overlap_forward=overlap_fwd, wgrad_stream=wgrad_stream,
+                   hipgraph=graph is not None)
         if probe and graph is None:
             # one untimed diagnostic step: per-rank receive waits and busy time
             mine = stage.probe_step(step)
@@ -469,6 +473,7 @@ def main() -> None:
         amoeba = summary(ar, None if args.tiny else aexp['ref'])
         amoeba['experiment'] = aexp['name']
         amoeba['cell_streams'] = ar['cell_streams']
+        amoeba['hipgraph'] = ar['hipgraph']
         if world == 2:
             d = dict(AMOEBA_N2M1)
             if args.tiny:
@@ -513,7 +518,7 @@ def main() -> None:
                 'warmup_s': round(main_run['warm_s'], 1),
                 'first_step_s': round(main_run['first_step_s'], 2),
                 'timeout_s': args.timeout,
-                'hipgraph': bool(args.graph),
+                'hipgraph': main_run['hipgraph'],
                 'cell_streams': main_run['cell_streams'],
                 'overlap_recompute': main_run['overlap_recompute'],
                 'wgrad_stream': main_run['wgrad_stream'],

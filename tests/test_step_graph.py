@@ -135,3 +135,56 @@ def test_two_stream_cells_match_one_stream(graphed):
             torch.testing.assert_close(pb.grad, pa.grad, rtol=1e-4, atol=1e-5 * scale)
     for (name, ba), bb in zip(a.named_buffers(), b.buffers()):
         torch.testing.assert_close(bb, ba, rtol=1e-4, atol=1e-5)
+
+
+def test_big_stack_worker_runs_calls_and_reraises():
+    import threading
+    from torchgpipe_amd.utils.bigstack import call_with_big_stack
+    names = []
+    assert call_with_big_stack(lambda: names.append(threading.current_thread().name) or 7) == 7
+    assert names == ['tgpipe-big-stack']
+
+    def deep(n):  # ~100 k Python frames would not fit the default thread stack
+        return 0 if n == 0 else 1 + deep(n - 1)
+
+    import sys
+    limit = sys.getrecursionlimit()
+    sys.setrecursionlimit(60000)
+    try:
+        assert call_with_big_stack(lambda: deep(50000)) == 50000
+    finally:
+        sys.setrecursionlimit(limit)
+    with pytest.raises(ZeroDivisionError):
+        call_with_big_stack(lambda: 1 / 0)
+
+
+@pytest.mark.gpu
+def test_deep_two_stream_graph_replays_from_the_big_stack_thread():
+    """A captured graph of ~40 k kernels forked and joined across two streams (the shape
+    of the full AmoebaNet two-stream step that crashed hipGraphLaunch on the main thread,
+    profiles/r3/capture_crash.md) replays from the big-stack worker with the exact
+    result of its eager twin."""
+    from torchgpipe_amd.utils.bigstack import call_with_big_stack
+    dev = torch.device('cuda', 0)
+    x = torch.zeros(64, device=dev)
+    side = torch.cuda.Stream(dev)
+    graph = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+
+    def capture():
+        with torch.cuda.graph(graph):
+            main = torch.cuda.current_stream()
+            for i in range(10000):
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    x.add_(1.0)
+                main.wait_stream(side)
+                x.mul_(1.0)
+                x.add_(1.0)
+
+    call_with_big_stack(capture)
+    x.zero_()
+    for _ in range(2):
+        call_with_big_stack(graph.replay)
+    torch.cuda.synchronize()
+    assert torch.all(x == 40000.0)

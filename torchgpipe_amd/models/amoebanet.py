@@ -34,7 +34,7 @@ from torchgpipe_amd.ops.unet_ops import MaxPool2x2
 __all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS', 'set_cell_streams']
 
 _SIDE_STREAMS: Dict[Tuple[torch.device, int], torch.cuda.Stream] = {}
-_CAPTURE_STREAMS = os.environ.get('TGPIPE_CAPTURE_STREAMS', '0') == '1'
+_CAPTURE_STREAMS = os.environ.get('TGPIPE_CAPTURE_STREAMS', '1') != '0'
 
 
 def _side_stream(device: torch.device, main: torch.cuda.Stream) -> torch.cuda.Stream:
@@ -281,9 +281,10 @@ class Cell(nn.Module):
                 ) -> Tuple[Tensor, Tensor]:
         s1, s2 = states if isinstance(states, tuple) else (states, states)
         skip = s1
-        # (not inside a hipGraph capture unless TGPIPE_CAPTURE_STREAMS=1: capturing the
-        # two-stream cells of the full model crashed the HIP runtime,
-        # profiles/r2/bench_amoeba_s13.md)
+        # (also inside hipGraph captures: the replay crash of round 2 was the runtime's
+        # recursive DAG walk overflowing the main thread's stack, now launched from a
+        # big-stack thread, utils/bigstack.py; TGPIPE_CAPTURE_STREAMS=0 keeps captures on
+        # one stream)
         if self.streams and s1.is_cuda and (_CAPTURE_STREAMS or
                                             not torch.cuda.is_current_stream_capturing()):
             return self._forward_two_streams(s1, s2), skip

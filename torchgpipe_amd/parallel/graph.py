@@ -48,6 +48,7 @@ import torch
 from torch import Tensor, nn
 
 from torchgpipe_amd.parallel.stage import PipelineStage
+from torchgpipe_amd.utils.bigstack import call_with_big_stack
 
 __all__ = ['StepGraph', 'rng_modules']
 
@@ -146,7 +147,9 @@ class StepGraph:
             self._warm += 1
             return loss
         if self._graph is None:
-            self._capture(input, target)
+            # capture (whose end instantiates the graph) and replays on a big-stack thread:
+            # the runtime walks a multi-stream graph recursively (utils/bigstack.py)
+            call_with_big_stack(lambda: self._capture(input, target))
         assert self._graph is not None and self._input is not None and self._target is not None
         if self._hyperparameters() != self._hyper:
             raise RuntimeError('StepGraph: optimizer hyperparameters changed since the capture '
@@ -160,7 +163,7 @@ class StepGraph:
             self._input.copy_(input)
         if target is not self._target:
             self._target.copy_(target)
-        self._graph.replay()
+        call_with_big_stack(self._graph.replay)
         assert self._loss is not None
         return self._loss
 

@@ -645,8 +645,8 @@ class PipelineStage:
         if not self.overlap_recompute or self.device.type != 'cuda':
             return None
         if torch.cuda.is_current_stream_capturing():
-            # one stream inside hipGraph captures (parallel/graph.py): multi-stream captures
-            # of the full AmoebaNet step crashed the HIP runtime (profiles/r2/bench_amoeba_s13.md)
+            # the recompute lanes stay out of hipGraph captures (parallel/graph.py): only the
+            # two-stream cells are verified inside captures (profiles/r3/capture_crash.md)
             return None
         if self._lanes is None:
             self._lanes = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]

@@ -1,0 +1,78 @@
+"""Run a call on a worker thread with a large native stack.
+
+Why: replaying a large *multi-stream* hipGraph crashed with SIGSEGV inside
+``hipGraphLaunch`` -- the full AmoebaNet-D(18,256) step with two-stream cells,
+~100 k kernel nodes joined by cross-stream event edges
+(``profiles/r2/bench_amoeba_n1m32_s13_streams_graph_crash.log``).  A faulthandler
+stack put the fault in ``torch.cuda.CUDAGraph.replay`` with no Python frame below
+it, the tiny model of the same code replayed fine, and the same full-size run
+with ``ulimit -s unlimited`` completed and ran at 343.5 samples/s
+(``profiles/r3/capture_crash.md``): the runtime walks the graph's DAG
+recursively when it launches it, and a deep fork/join DAG overflows the default
+8 MiB main-thread stack.  A single-stream capture is a plain chain and does not
+recurse that deep, which is why the one-stream workaround of round 2 hid it.
+
+The fix here does not depend on the caller's ``ulimit``: graph launches (and the
+capture, whose end instantiates the graph) run on one persistent worker thread
+whose stack is reserved at 1 GiB of address space (pages are committed only when
+touched).  The caller's device and current stream are propagated, exceptions are
+re-raised in the caller, and the call is synchronous from the caller's point of
+view (the worker only *enqueues* GPU work, like the caller would have).
+"""
+import queue
+import threading
+from typing import Any, Callable, Optional, Tuple
+
+import torch
+
+__all__ = ['call_with_big_stack', 'STACK_BYTES']
+
+STACK_BYTES = 1 << 30
+
+_lock = threading.Lock()
+_worker: Optional['_Worker'] = None
+
+
+class _Worker:
+    def __init__(self) -> None:
+        self.requests: 'queue.Queue[Tuple[Callable[[], Any], queue.Queue]]' = queue.Queue()
+        prev = threading.stack_size()
+        threading.stack_size(STACK_BYTES)
+        try:
+            self.thread = threading.Thread(target=self._run, name='tgpipe-big-stack',
+                                           daemon=True)
+            self.thread.start()
+        finally:
+            threading.stack_size(prev)
+
+    def _run(self) -> None:
+        while True:
+            fn, reply = self.requests.get()
+            try:
+                reply.put((True, fn()))
+            except BaseException as exc:  # re-raised in the caller
+                reply.put((False, exc))
+
+
+def call_with_big_stack(fn: Callable[[], Any]) -> Any:
+    """``fn()`` on the big-stack worker, under the caller's CUDA device and stream."""
+    global _worker
+    with _lock:
+        if _worker is None:
+            _worker = _Worker()
+        worker = _worker
+    device = torch.cuda.current_device() if torch.cuda.is_available() else None
+    stream = torch.cuda.current_stream() if device is not None else None
+
+    def wrapped() -> Any:
+        if device is None:
+            return fn()
+        with torch.cuda.device(device), torch.cuda.stream(stream):
+            return fn()
+
+    reply: 'queue.Queue' = queue.Queue(maxsize=1)
+    worker.requests.put((wrapped, reply))
+    ok, value = reply.get()
+    if not ok:
+        raise value
+    return value
