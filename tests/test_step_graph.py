@@ -182,7 +182,7 @@ def test_deep_two_stream_graph_replays_from_the_big_stack_thread():
                 x.mul_(1.0)
                 x.add_(1.0)
 
-    call_with_big_stack(capture)
+    capture()
     x.zero_()
     for _ in range(2):
         call_with_big_stack(graph.replay)

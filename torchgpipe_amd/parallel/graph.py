@@ -147,9 +147,10 @@ class StepGraph:
             self._warm += 1
             return loss
         if self._graph is None:
-            # capture (whose end instantiates the graph) and replays on a big-stack thread:
-            # the runtime walks a multi-stream graph recursively (utils/bigstack.py)
-            call_with_big_stack(lambda: self._capture(input, target))
+            # captured on the calling thread, whose library handles (hipBLASLt, MIOpen) the
+            # warm-up steps created: a first library call inside a capture on a fresh thread
+            # would have to create them there
+            self._capture(input, target)
         assert self._graph is not None and self._input is not None and self._target is not None
         if self._hyperparameters() != self._hyper:
             raise RuntimeError('StepGraph: optimizer hyperparameters changed since the capture '
@@ -163,6 +164,8 @@ class StepGraph:
             self._input.copy_(input)
         if target is not self._target:
             self._target.copy_(target)
+        # replays from a big-stack thread: the runtime walks a multi-stream graph
+        # recursively when it launches it (utils/bigstack.py)
         call_with_big_stack(self._graph.replay)
         assert self._loss is not None
         return self._loss

@@ -12,10 +12,11 @@ recursively when it launches it, and a deep fork/join DAG overflows the default
 8 MiB main-thread stack.  A single-stream capture is a plain chain and does not
 recurse that deep, which is why the one-stream workaround of round 2 hid it.
 
-The fix here does not depend on the caller's ``ulimit``: graph launches (and the
-capture, whose end instantiates the graph) run on one persistent worker thread
-whose stack is reserved at 1 GiB of address space (pages are committed only when
-touched).  The caller's device and current stream are propagated, exceptions are
+The fix here does not depend on the caller's ``ulimit``: graph launches run on one
+persistent worker thread whose stack is reserved at 1 GiB of address space (pages are
+committed only when touched).  Captures stay on the caller's thread: a library call
+(hipBLASLt for a Linear layer) made for the first time on a fresh thread inside a
+capture has to create its per-thread handle there, which crashed.  The caller's device and current stream are propagated, exceptions are
 re-raised in the caller, and the call is synchronous from the caller's point of
 view (the worker only *enqueues* GPU work, like the caller would have).
 """
