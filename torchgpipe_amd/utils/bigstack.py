@@ -16,9 +16,10 @@ The fix here does not depend on the caller's ``ulimit``: graph launches run on o
 persistent worker thread whose stack is reserved at 1 GiB of address space (pages are
 committed only when touched).  Captures stay on the caller's thread: a library call
 (hipBLASLt for a Linear layer) made for the first time on a fresh thread inside a
-capture has to create its per-thread handle there, which crashed.  The caller's device and current stream are propagated, exceptions are
-re-raised in the caller, and the call is synchronous from the caller's point of
-view (the worker only *enqueues* GPU work, like the caller would have).
+capture has to create its per-thread handle there, which crashed.  The caller's
+device and current stream are propagated, exceptions are re-raised in the caller, and
+the call is synchronous from the caller's point of view (the worker only *enqueues*
+GPU work, like the caller would have).
 """
 import queue
 import threading
