@@ -7,7 +7,7 @@ import torch.nn.functional as F
 
 from common import parser, run_speed
 
-from torchgpipe_amd.models import resnet101
+from torchgpipe_amd.models.resnet import build_resnet
 
 EXPERIMENTS = {
     'baseline': dict(batch=118),
@@ -21,8 +21,13 @@ EXPERIMENTS = {
 
 
 def main() -> None:
-    args = parser(__doc__, EXPERIMENTS).parse_args()
-    run_speed(args, EXPERIMENTS[args.experiment], lambda: resnet101(num_classes=1000),
+    p = parser(__doc__, EXPERIMENTS)
+    p.add_argument('--plain', action='store_true',
+                   help='plain nn layers (MIOpen convolutions / BatchNorm) instead of the fused '
+                        'Conv-BN-ReLU runs (ops/fusion.py)')
+    args = p.parse_args()
+    run_speed(args, EXPERIMENTS[args.experiment],
+              lambda: build_resnet([3, 4, 23, 3], num_classes=1000, fused=not args.plain),
               (3, 224, 224), lambda b, d: torch.randint(1000, (b,), device=d),
               F.cross_entropy, dataset_size=50000)
 

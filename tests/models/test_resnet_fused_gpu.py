@@ -1,0 +1,120 @@
+"""Fused ResNet layers (ops/fusion.py: ConvBN2d -> BatchNormAct2d -> ReLU runs) against fp64
+``nn`` references of the same layers, and the fused ResNet-50 against the plain model."""
+import copy
+
+import pytest
+import torch
+from torch import nn
+
+from torchgpipe_amd.ops import _ext
+from torchgpipe_amd.ops.fusion import BatchNormAct2d, ConvBN2d, ReLU, relink
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    assert _ext.available(), _ext.load_error()
+
+
+def rel_err(a, b):
+    return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
+
+
+# (n, ci, hw, co, kernel, stride, padding)
+CASES = [
+    (4, 64, 28, 96, 1, 1, 0),     # 1x1: implicit GEMM, statistics in the epilogue
+    (4, 64, 28, 128, 1, 2, 0),    # strided 1x1 (downsample)
+    (4, 64, 28, 64, 3, 1, 1),     # 3x3 stride 1: Winograd F(4x4) + native BN(+ReLU)
+    (4, 256, 14, 256, 3, 1, 1),   # 3x3 stride 1, >= 256 channels: batched-GEMM Winograd
+    (4, 32, 28, 32, 3, 2, 1),     # 3x3 stride 2: implicit GEMM
+    (2, 3, 64, 64, 7, 2, 3),      # the stem's 7x7 stride 2
+    (4, 512, 7, 512, 1, 1, 0),    # 7x7 planes: split reduction, fused split statistics
+]
+
+
+@pytest.mark.parametrize('relu', [True, False])
+@pytest.mark.parametrize('case', CASES, ids=[f'{c[4]}x{c[4]}s{c[5]}_{c[1]}to{c[3]}@{c[2]}'
+                                            for c in CASES])
+def test_conv_bn_relu_run_matches_fp64(case, relu):
+    n, ci, hw, co, k, stride, pad = case
+    torch.manual_seed(0)
+    mods = [ConvBN2d(ci, co, k, stride=stride, padding=pad, bias=False), BatchNormAct2d(co)]
+    if relu:
+        mods.append(ReLU())
+    seq = nn.Sequential(*mods).cuda()
+    with torch.no_grad():
+        seq[1].weight.uniform_(0.5, 1.5)
+        seq[1].bias.uniform_(-0.5, 0.5)
+    assert relink(seq) == 1
+    ref = nn.Sequential(nn.Conv2d(ci, co, k, stride=stride, padding=pad, bias=False),
+                        nn.BatchNorm2d(co), *([nn.ReLU()] if relu else [])).cuda().double()
+    ref.load_state_dict(seq.state_dict())
+    x = torch.randn(n, ci, hw, hw, device='cuda', requires_grad=True)
+    x64 = x.detach().double().requires_grad_(True)
+    y = seq(x)
+    y64 = ref(x64)
+    assert getattr(y, '_tgpipe_bn_done', None) == id(seq[1]), 'the fused path must run'
+    assert rel_err(y, y64) < 1e-5
+    g = torch.randn_like(y)
+    y.backward(g)
+    y64.backward(g.double())
+    assert rel_err(x.grad, x64.grad) < 1e-5
+    for (name, p), q in zip(seq.named_parameters(), ref.parameters()):
+        assert rel_err(p.grad, q.grad) < 2e-5, name
+    assert rel_err(seq[1].running_mean, ref[1].running_mean) < 1e-6
+    assert rel_err(seq[1].running_var, ref[1].running_var) < 1e-6
+    assert seq[1].num_batches_tracked.item() == 1
+
+
+def test_unlinked_layers_run_on_their_own():
+    """A balance that separates the convolution from its BatchNorm: each layer runs alone
+    (implicit-GEMM convolution, native BatchNorm + ReLU) and computes the same function."""
+    torch.manual_seed(0)
+    full = nn.Sequential(ConvBN2d(32, 48, 1, bias=False), BatchNormAct2d(48), ReLU()).cuda()
+    other = copy.deepcopy(full)
+    assert relink(full) == 1
+    a, b = nn.Sequential(other[0]), nn.Sequential(other[1], other[2])
+    assert relink(a) == 0 and relink(b) == 0
+    x = torch.randn(4, 32, 14, 14, device='cuda', requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    y_fused = full(x)
+    y_split = b(a(x2))
+    assert getattr(y_split, '_tgpipe_bn_done', None) is None
+    assert rel_err(y_split, y_fused) < 1e-5
+    y_fused.square().sum().backward()
+    y_split.square().sum().backward()
+    assert rel_err(x2.grad, x.grad) < 1e-5
+    for p, q in zip(full.parameters(), other.parameters()):
+        assert rel_err(q.grad, p.grad) < 1e-5
+    assert rel_err(other[1].running_var, full[1].running_var) < 1e-6
+
+
+def test_fused_resnet50_matches_plain_model():
+    """Whole fused ResNet-50 (training mode) vs the plain nn model with the same weights:
+    loss, input gradient and every parameter gradient; then one SGD step each and the
+    BatchNorm running statistics."""
+    from torchgpipe_amd.models.resnet import build_resnet
+    torch.manual_seed(0)
+    fused = build_resnet([3, 4, 6, 3], num_classes=10, fused=True).cuda()
+    plain = build_resnet([3, 4, 6, 3], num_classes=10, fused=False).cuda()
+    plain.load_state_dict(fused.state_dict())
+    x = torch.randn(16, 3, 96, 96, device='cuda')
+    t = torch.randint(10, (16,), device='cuda')
+    losses = []
+    for model in (fused, plain):
+        xi = x.clone().requires_grad_(True)
+        loss = nn.functional.cross_entropy(model(xi), t)
+        loss.backward()
+        losses.append((loss.detach(), xi.grad))
+    assert rel_err(losses[0][0], losses[1][0]) < 1e-5
+    assert rel_err(losses[0][1], losses[1][1]) < 1e-3
+    for (name, p), q in zip(fused.named_parameters(), plain.parameters()):
+        assert rel_err(p.grad, q.grad) < 1e-3, name
+    for (name, b), c in zip(fused.named_buffers(), plain.buffers()):
+        if b.is_floating_point():
+            assert rel_err(b, c) < 1e-4, name
+        else:
+            assert torch.equal(b, c), name

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
 // all of them hold bit-identical statistics), workgroup (channel, 0) publishes mean /
 // invstd / running statistics, and every workgroup normalises its own images.  Saves the
 // separate finalize launch per BatchNorm (AmoebaNet: ~17 k launches per training step).
-template <bool kVec, bool kAdd>
+template <bool kVec, bool kAdd, bool kRelu>
 __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
     const float* __restrict__ pm, const float* __restrict__ pm2, int blocks, int width,
     int cols, int n, int c, int s, int n_per, float eps, double momentum,
@@ -156,9 +156,17 @@ __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
     for (int q = tid; q < quads; q += 256) {
       const int img = n0 + q / sq;
       const int64_t off = (static_cast<int64_t>(img) * c + ch) * sq + (q - (img - n0) * sq);
-      // (z - mean) * k, not z * k - mean * k: no cancellation when |mean| >> std
-      floatx4 v = (reinterpret_cast<const floatx4*>(z)[off] - mu) * k + bb;
+      // (z - mean) * k, not z * k - mean * k: no cancellation when |mean| >> std; one
+      // fma, the same rounding the backward's ReLU mask recomputes (bn_relu_mask)
+      const floatx4 zv = reinterpret_cast<const floatx4*>(z)[off];
+      floatx4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(zv[e] - mu, k, bb);
       if constexpr (kAdd) v += reinterpret_cast<const floatx4*>(add)[off];
+      if constexpr (kRelu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+      }
       reinterpret_cast<floatx4*>(y)[off] = v;
     }
   } else {
@@ -166,11 +174,18 @@ __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
     for (int e = tid; e < elems; e += 256) {
       const int img = n0 + e / s;
       const int64_t off = (static_cast<int64_t>(img) * c + ch) * s + (e - (img - n0) * s);
-      float v = (z[off] - mu) * k + bb;
+      float v = __builtin_fmaf(z[off] - mu, k, bb);
       if constexpr (kAdd) v += add[off];
+      if constexpr (kRelu) v = v > 0.f ? v : 0.f;
       y[off] = v;
     }
   }
+}
+
+// The ReLU after a BatchNorm (relu_out), re-derived in the backward from the saved
+// convolution output: the forward's normalised value > 0, computed with the same fma.
+__device__ __forceinline__ bool bn_relu_mask(float z, float mu, float k, float b) {
+  return __builtin_fmaf(z - mu, k, b) > 0.f;
 }
 
 template <bool kVec, bool kAdd>
@@ -207,12 +222,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
 // One workgroup per (channel, image range): sums of dy and dy * (z - mean).
 // dy may be a channel slice of a wider tensor (the gradient of a concatenated cell
 // output): image `img` of dy starts at dy + img * dy_img (z and dz are dense).
+// relu_out: dy is the gradient of relu(bn(z)); the ReLU's mask is re-derived from z.
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const float* __restrict__ dy, const float* __restrict__ z, const float* __restrict__ mean,
-    float* __restrict__ sums, int64_t n, int64_t c, int64_t s, int64_t n_per, int64_t dy_img) {
+    float* __restrict__ sums, int64_t n, int64_t c, int64_t s, int64_t n_per, int64_t dy_img,
+    int relu_out, const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta) {
   const int64_t ch = blockIdx.x;
   const int64_t n0 = blockIdx.y * n_per, n1 = min(n, n0 + n_per);
   const float mu = mean[ch];
+  const float rk = relu_out ? invstd[ch] * (gamma ? gamma[ch] : 1.f) : 0.f;
+  const float rb = relu_out && beta ? beta[ch] : 0.f;
   float sd = 0.f, sdz = 0.f;
   for (int64_t img = n0; img < n1; ++img) {
     const int64_t base = (img * c + ch) * s;
@@ -223,15 +243,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         const floatx4 v = reinterpret_cast<const floatx4*>(z + base)[q];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          sd += g[e];
-          sdz += g[e] * (v[e] - mu);
+          const float ge = !relu_out || bn_relu_mask(v[e], mu, rk, rb) ? g[e] : 0.f;
+          sd += ge;
+          sdz += ge * (v[e] - mu);
         }
       }
     } else {
       for (int64_t i = threadIdx.x; i < s; i += 256) {
-        const float g = dyp[i];
+        const float zv = z[base + i];
+        const float g = !relu_out || bn_relu_mask(zv, mu, rk, rb) ? dyp[i] : 0.f;
         sd += g;
-        sdz += g * (z[base + i] - mu);
+        sdz += g * (zv - mu);
       }
     }
   }
@@ -259,7 +281,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ sums, float* __restrict__ dz, float* __restrict__ dgamma,
     float* __restrict__ dbeta, int acc_gamma, int acc_beta, int64_t total, int64_t c, int64_t s,
-    float inv_m, int64_t dy_img) {
+    float inv_m, int64_t dy_img, int relu_out, const float* __restrict__ beta) {
   const int64_t cs = c * s;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
   const int64_t first = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
@@ -277,8 +299,13 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
       const float k3 = is * is * sums[c + ch] * inv_m;
       const float mu = mean[ch];
       const int64_t img = 4 * q / cs;
-      const floatx4 g = *reinterpret_cast<const floatx4*>(dy + img * dy_img + (4 * q - img * cs));
+      floatx4 g = *reinterpret_cast<const floatx4*>(dy + img * dy_img + (4 * q - img * cs));
       const floatx4 v = reinterpret_cast<const floatx4*>(z)[q];
+      if (relu_out) {
+        const float rb = beta ? beta[ch] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] = bn_relu_mask(v[e], mu, k1, rb) ? g[e] : 0.f;
+      }
       floatx4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = k1 * (g[e] - k2 - (v[e] - mu) * k3);
@@ -290,7 +317,8 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
       const float is = invstd[ch];
       const float k1 = (gamma ? gamma[ch] : 1.f) * is;
       const int64_t img = i / cs;
-      const float g = dy[img * dy_img + (i - img * cs)];
+      float g = dy[img * dy_img + (i - img * cs)];
+      if (relu_out && !bn_relu_mask(z[i], mean[ch], k1, beta ? beta[ch] : 0.f)) g = 0.f;
       dz[i] = k1 * (g - sums[ch] * inv_m - (z[i] - mean[ch]) * is * is * sums[c + ch] * inv_m);
     }
   }
@@ -384,7 +412,7 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
                               double momentum, float* mean, float* invstd, float* running_mean,
                               float* running_var, int64_t* tracked, double* acc, float* zero2c,
                               const float* z, const float* gamma, const float* beta,
-                              const float* add, float* y, hipStream_t stream) {
+                              const float* add, float* y, hipStream_t stream, bool relu) {
   if (c == 0) return;
   // enough (channel, image range) workgroups to cover the chip ~4x
   int64_t splits = (1024 + c - 1) / c;
@@ -401,10 +429,13 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
                        running_var, tracked, acc, zero2c, z, gamma, beta, add, y);
   };
   const bool vec = (s & 3) == 0;
-  if (vec && add) go(bn_finalize_apply_kernel<true, true>);
-  else if (vec) go(bn_finalize_apply_kernel<true, false>);
-  else if (add) go(bn_finalize_apply_kernel<false, true>);
-  else go(bn_finalize_apply_kernel<false, false>);
+  if (relu) {  // (ResNet's BatchNorm -> ReLU; never with a node sum)
+    if (vec) go(bn_finalize_apply_kernel<true, false, true>);
+    else go(bn_finalize_apply_kernel<false, false, true>);
+  } else if (vec && add) go(bn_finalize_apply_kernel<true, true, false>);
+  else if (vec) go(bn_finalize_apply_kernel<true, false, false>);
+  else if (add) go(bn_finalize_apply_kernel<false, true, false>);
+  else go(bn_finalize_apply_kernel<false, false, false>);
 }
 
 void launch_dbn_commit64(double* acc, float* running_mean, float* running_var, int64_t c,
@@ -453,7 +484,7 @@ void launch_bn_apply(const float* z, const float* mean, const float* invstd, con
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
                         bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
-                        int64_t dy_img, hipStream_t stream) {
+                        int64_t dy_img, hipStream_t stream, bool relu_out, const float* beta) {
   if (dy_img <= 0) dy_img = c * s;
   const int64_t total = n * c * s;
   if (total == 0) return;
@@ -465,7 +496,8 @@ void launch_bn_backward(const float* dy, const float* z, const float* mean, cons
   splits = (n + n_per - 1) / n_per;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(static_cast<unsigned>(c),
                                                 static_cast<unsigned>(splits)),
-                     dim3(256), 0, stream, dy, z, mean, sums, n, c, s, n_per, dy_img);
+                     dim3(256), 0, stream, dy, z, mean, sums, n, c, s, n_per, dy_img,
+                     relu_out ? 1 : 0, invstd, gamma, beta);
   const bool vec = (s & 3) == 0;
   int64_t work = vec ? total / 4 : total;
   if (work < c) work = c;
@@ -474,11 +506,11 @@ void launch_bn_backward(const float* dy, const float* z, const float* mean, cons
   if (vec)
     hipLaunchKernelGGL((bn_bwd_dz_kernel<true>), dim3(grid), dim3(256), 0, stream, dy, z, mean,
                        invstd, gamma, sums, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
-                       acc_beta ? 1 : 0, total, c, s, inv_m, dy_img);
+                       acc_beta ? 1 : 0, total, c, s, inv_m, dy_img, relu_out ? 1 : 0, beta);
   else
     hipLaunchKernelGGL((bn_bwd_dz_kernel<false>), dim3(grid), dim3(256), 0, stream, dy, z, mean,
                        invstd, gamma, sums, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
-                       acc_beta ? 1 : 0, total, c, s, inv_m, dy_img);
+                       acc_beta ? 1 : 0, total, c, s, inv_m, dy_img, relu_out ? 1 : 0, beta);
 }
 
 }  // namespace tgpipe

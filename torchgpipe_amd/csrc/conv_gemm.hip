@@ -760,6 +760,149 @@ void launch_split_reduce(const float* ws, int splits, int64_t stride, float* out
                        c_off);
 }
 
+// Forward split reduction fused with the BatchNorm statistics pass: one wave per (image,
+// channel) plane of this convolution sums the split partials ws[s][img][ch][p] in split
+// order, stores the plane into z[img][c_off + ch], and writes the plane's mean and centred
+// M2 to pm / pm2[img][c_off + ch] (per-image partials, like launch_bn_stats): one launch
+// where split_reduce + bn_stats took two.  kPer > 0: the plane (<= 64 * kPer pixels) stays
+// in registers for the M2 pass; kPer = 0: each lane re-reads the pixels it stored.
+template <int kPer>
+__global__ __launch_bounds__(256) void split_reduce_stats_kernel(
+    const float* __restrict__ ws, int splits, int64_t stride, float* __restrict__ z,
+    float* __restrict__ pm, float* __restrict__ pm2, int64_t planes, int c, int hw, int c_total,
+    int c_off) {
+  const int lane = threadIdx.x & 63;
+  const int64_t plane = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (plane >= planes) return;
+  const int64_t img = plane / c;
+  const int ch = static_cast<int>(plane - img * c);
+  const float* src = ws + plane * hw;
+  float* dst = z + (img * c_total + c_off + ch) * hw;
+  float sum = 0.f;
+  float v[kPer > 0 ? kPer : 1];
+  if constexpr (kPer > 0) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) v[i] = 0.f;
+    for (int s = 0; s < splits; ++s) {
+      const float* sp = src + s * stride;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int p = lane + 64 * i;
+        if (p < hw) v[i] += sp[p];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = lane + 64 * i;
+      if (p < hw) {
+        dst[p] = v[i];
+        sum += v[i];
+      }
+    }
+  } else {
+    for (int p = lane; p < hw; p += 64) {
+      float a0 = 0.f, a1 = 0.f;
+      int s = 0;
+      for (; s + 1 < splits; s += 2) {
+        a0 += src[s * stride + p];
+        a1 += src[(s + 1) * stride + p];
+      }
+      if (s < splits) a0 += src[s * stride + p];
+      const float t = a0 + a1;
+      dst[p] = t;
+      sum += t;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+  const float mean = sum / static_cast<float>(hw);
+  float m2 = 0.f;
+  if constexpr (kPer > 0) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = lane + 64 * i;
+      if (p < hw) {
+        const float d = v[i] - mean;
+        m2 += d * d;
+      }
+    }
+  } else {
+    for (int p = lane; p < hw; p += 64) {  // this lane's own stores: program-order reads
+      const float d = dst[p] - mean;
+      m2 += d * d;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m2 += __shfl_xor(m2, off);
+  if (lane == 0) {
+    pm[img * c_total + c_off + ch] = mean;
+    pm2[img * c_total + c_off + ch] = m2;
+  }
+}
+
+void launch_split_reduce_stats(const float* ws, int splits, int64_t stride, float* z, float* pm,
+                               float* pm2, int64_t n, int c, int hw, int c_total, int c_off,
+                               hipStream_t stream) {
+  const int64_t planes = n * c;
+  if (planes == 0 || hw == 0) return;
+  const dim3 grid(static_cast<unsigned>((planes + 3) / 4)), block(256);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, block, 0, stream, ws, splits, stride, z, pm, pm2, planes, c, hw,
+                       c_total, c_off);
+  };
+  if (hw <= 64) go(split_reduce_stats_kernel<1>);
+  else if (hw <= 256) go(split_reduce_stats_kernel<4>);
+  else if (hw <= 1024) go(split_reduce_stats_kernel<16>);
+  else go(split_reduce_stats_kernel<0>);
+}
+
+// Deferred weight gradients (launch_conv_gemm_wgrad_slab): grad[i] (+)= sum_s slab[s][i] for a
+// table of parameters in one launch, splits summed in order (bitwise reproducible).  Each
+// workgroup covers 1024 floats of one entry; the entry is found from the prefix of block
+// counts in the (by-value) table.
+struct SlabTable {
+  const float* slab[kSlabFlushMax];
+  float* grad[kSlabFlushMax];
+  int64_t numel[kSlabFlushMax];
+  int splits[kSlabFlushMax];
+  int accumulate[kSlabFlushMax];
+  int block_end[kSlabFlushMax];  // exclusive prefix of workgroups per entry
+  int count;
+};
+
+__global__ __launch_bounds__(256) void slab_flush_kernel(SlabTable t) {
+  int e = 0;
+  while (e + 1 < t.count && static_cast<int>(blockIdx.x) >= t.block_end[e]) ++e;
+  const int first_block = e == 0 ? 0 : t.block_end[e - 1];
+  const int64_t numel = t.numel[e];
+  const int64_t base = static_cast<int64_t>(blockIdx.x - first_block) * 1024 + 4 * threadIdx.x;
+  const float* slab = t.slab[e];
+  float* grad = t.grad[e];
+  const int splits = t.splits[e];
+  if ((numel & 3) == 0) {
+    if (base >= numel) return;
+    floatx4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+    int s = 0;
+    for (; s + 1 < splits; s += 2) {
+      a0 += *reinterpret_cast<const floatx4*>(slab + s * numel + base);
+      a1 += *reinterpret_cast<const floatx4*>(slab + (s + 1) * numel + base);
+    }
+    if (s < splits) a0 += *reinterpret_cast<const floatx4*>(slab + s * numel + base);
+    floatx4 v = a0 + a1;
+    if (t.accumulate[e]) v += *reinterpret_cast<const floatx4*>(grad + base);
+    *reinterpret_cast<floatx4*>(grad + base) = v;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = base + k;
+      if (i >= numel) break;
+      float a = 0.f;
+      for (int s = 0; s < splits; ++s) a += slab[s * numel + i];
+      grad[i] = t.accumulate[e] ? grad[i] + a : a;
+    }
+  }
+}
+
 Geo make_geo(const ConvGemmGeo& cg) {
   Geo g{cg.n, cg.ci, cg.h, cg.w, cg.co, cg.ho, cg.wo, cg.co_total, cg.co_off, cg.kh, cg.kw,
         cg.kh * cg.kw, cg.sh, cg.sw, cg.ph, cg.pw, cg.oh, cg.ow, cg.relu ? 1 : 0, 0,
@@ -939,6 +1082,12 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
   else
     by_cfg(W{}, nullptr, nullptr, nullptr);
   if (!split) return;
+  if (mode == kFwd && part_mean != nullptr) {
+    // split forward with statistics: reduction and per-image BatchNorm partials in one pass
+    launch_split_reduce_stats(ws, plan.splits, stride, out, part_mean, part_m2, g.n, g.co,
+                              g.ho * g.wo, g.co_total, g.co_off, stream);
+    return;
+  }
   // out[dst(i)] = (accumulate ? out : 0) + mask * sum_s ws[s][i]
   int64_t planes, c, hw, c_total = 0, c_off = 0;
   if (mode == kFwd) {
@@ -951,6 +1100,51 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
   }
   launch_split_reduce(ws, plan.splits, stride, out, mode == kBwdData && g.relu ? x_mask : nullptr,
                       accumulate, planes, c, hw, c_total, c_off, stream);
+}
+
+void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
+                                 const ConvGemmGeo& cg, const ConvGemmPlan& plan, bool accumulate,
+                                 int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
+  Geo g = make_geo(cg);
+  int M, N, K;
+  gemm_dims(kWgrad, g, M, N, K);
+  if (M == 0 || N == 0) return;
+  const int64_t stride = static_cast<int64_t>(M) * N;
+  // every split block read-modify-writes its own slice: no reduction pass
+  auto go = [&](auto cfg_c) {
+    launch_cfg<kWgrad, decltype(cfg_c)::value>(a, b, nullptr, slab, nullptr, nullptr, g, M, N, K,
+                                               plan.splits, stride, accumulate, a_bytes, b_bytes,
+                                               stream);
+  };
+  switch (plan.cfg) {
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;
+    default: go(std::integral_constant<int, 0>{}); break;
+  }
+}
+
+void launch_slab_flush(const SlabFlushEntry* entries, int count, hipStream_t stream) {
+  for (int first = 0; first < count; first += kSlabFlushMax) {
+    SlabTable t{};
+    t.count = std::min(kSlabFlushMax, count - first);
+    int blocks = 0;
+    for (int k = 0; k < t.count; ++k) {
+      const SlabFlushEntry& e = entries[first + k];
+      t.slab[k] = e.slab;
+      t.grad[k] = e.grad;
+      t.numel[k] = e.numel;
+      t.splits[k] = e.splits;
+      t.accumulate[k] = e.accumulate ? 1 : 0;
+      blocks += static_cast<int>((e.numel + 1023) / 1024);
+      t.block_end[k] = blocks;
+    }
+    if (blocks > 0)
+      hipLaunchKernelGGL(slab_flush_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                         stream, t);
+  }
 }
 
 }  // namespace tgpipe

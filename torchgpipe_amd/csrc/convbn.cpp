@@ -289,7 +289,7 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
                                        const c10::optional<at::Tensor>& running_var,
                                        const c10::optional<at::Tensor>& num_batches_tracked,
                                        double momentum, double eps,
-                                       const c10::optional<at::Tensor>& add) {
+                                       const c10::optional<at::Tensor>& add, bool relu_out) {
   auto x = x_in.contiguous();
   check_f32(x, "x", x);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -307,21 +307,24 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     split = split || plans.back().splits > 1;
   }
   // statistics partials: from the GEMM epilogue (all parts share one column tiling), or
-  // per (image, channel) from a separate pass when a reduction is split
+  // per (image, channel) when a reduction is split -- from the split reduction itself for a
+  // single convolution, from a separate pass for several
   for (const auto& pl : plans)
     split = split || pl.col_width != plans[0].col_width;
+  const bool fused_stats = split && p.geo.size() == 1;
   const int width = split ? static_cast<int>(s) : plans[0].col_width;
   const int blocks = split ? static_cast<int>(n) : plans[0].col_blocks;
   auto part = at::empty({2, blocks, c}, x.options());
+  const bool epilogue_stats = !split || fused_stats;
   for (size_t i = 0; i < p.geo.size(); ++i) {
     const auto wt = weights[i];
     const ConvGemmPlan& pl = plans[i];
     run_gemm(0, wt.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
-             split ? nullptr : part[0].data_ptr<float>(),
-             split ? nullptr : part[1].data_ptr<float>(), p.geo[i], pl, false, wt.numel() * 4,
-             x.numel() * 4, x);
+             epilogue_stats ? part[0].data_ptr<float>() : nullptr,
+             epilogue_stats ? part[1].data_ptr<float>() : nullptr, p.geo[i], pl, false,
+             wt.numel() * 4, x.numel() * 4, x);
   }
-  if (split)
+  if (split && !fused_stats)
     launch_bn_stats(z.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n,
                     c, s, stream);
   auto mean = at::empty({c}, x.options());
@@ -348,12 +351,13 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     TORCH_CHECK(add_c.sizes() == z.sizes(), "add must have the output's shape");
     ad = add_c.data_ptr<float>();
   }
+  TORCH_CHECK(!(relu_out && ad != nullptr), "relu_out with a node sum is not supported");
   auto y = at::empty_like(z);
   launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, n,
                            c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), const_cast<float*>(rm),
                            const_cast<float*>(rv), tracked, nullptr, sums.data_ptr<float>(),
-                           z.data_ptr<float>(), ga, be, ad, y.data_ptr<float>(), stream);
+                           z.data_ptr<float>(), ga, be, ad, y.data_ptr<float>(), stream, relu_out);
   return {y, z, mean, invstd, sums};
 }
 
@@ -362,16 +366,77 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
 // optional entry per parameter gradient {dgamma, dbeta, dw_0, ...}: a given tensor (the
 // parameter's .grad across micro-batches) is accumulated into in place and returned.
 // One part's weight gradient: dw (+)= dz x relu(X) taps (accumulating into `into` when given).
+//
+// `slab` (optional, ops/gradacc.py deferred weight gradients): when the plan splits the
+// reduction, the split partials go into this per-parameter buffer of `splits` weight-sized
+// slices instead of a workspace + reduction pass -- stored when `slab_first` (the step's
+// first use; the slab is resized to fit), added otherwise -- and the slab itself is
+// returned; wgrad_slab_flush sums its slices into .grad at the end of the step.  A later
+// call whose plan splits differently reduces into the slab's first slice.
 at::Tensor wgrad_part(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& weight,
-                      const ConvGemmGeo& g, const at::Tensor& into) {
+                      const ConvGemmGeo& g, const at::Tensor& into,
+                      c10::optional<at::Tensor> slab = c10::nullopt, bool slab_first = false) {
   const bool acc = into.defined();
   auto dw = acc ? into : at::empty_like(weight);
   const ConvGemmPlan plan =
       tuned_plan(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
                  nullptr, nullptr, g, acc, dz.numel() * 4, x.numel() * 4, x, dw.numel());
+  if (slab.has_value() && slab->defined() && plan.splits > 1) {
+    at::Tensor sb = *slab;
+    TORCH_CHECK(sb.is_cuda() && sb.device() == x.device() && sb.scalar_type() == at::kFloat &&
+                    sb.dim() == 1,
+                "slab must be a 1-D float32 tensor on the input's device");
+    const int64_t need = static_cast<int64_t>(plan.splits) * weight.numel();
+    TORCH_CHECK(need * 4 <= kMaxBytes, "slab too large");
+    if (slab_first) {
+      if (sb.numel() != need) sb.resize_({need});
+    }
+    if (slab_first || sb.numel() == need) {
+      launch_conv_gemm_wgrad_slab(dz.data_ptr<float>(), x.data_ptr<float>(), sb.data_ptr<float>(),
+                                  g, plan, !slab_first, dz.numel() * 4, x.numel() * 4,
+                                  cur_stream(x));
+    } else {
+      TORCH_CHECK(sb.numel() >= weight.numel() && sb.numel() % weight.numel() == 0,
+                  "slab does not hold whole weight-sized slices");
+      run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, sb.data_ptr<float>(),
+               nullptr, nullptr, g, plan, true, dz.numel() * 4, x.numel() * 4, x);
+    }
+    return sb;
+  }
   run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(), nullptr,
            nullptr, g, plan, acc, dz.numel() * 4, x.numel() * 4, x);
   return dw;
+}
+
+c10::optional<at::Tensor> slab_of(const c10::List<c10::optional<at::Tensor>>& slabs, size_t i) {
+  if (i >= slabs.size()) return c10::nullopt;
+  return slabs.get(i);
+}
+
+bool first_of(at::IntArrayRef slab_first, size_t i) {
+  return i < slab_first.size() && slab_first[i] != 0;
+}
+
+// End of a step with deferred weight gradients: grads[i] (+)= sum of slabs[i]'s slices
+// (accumulate[i]: add to the existing gradient), for every parameter in one launch per
+// kSlabFlushMax entries.
+void wgrad_slab_flush(at::TensorList slabs, at::TensorList grads, at::IntArrayRef accumulate) {
+  TORCH_CHECK(slabs.size() == grads.size() && grads.size() == accumulate.size(),
+              "slabs, grads and accumulate must have one entry per parameter");
+  if (slabs.empty()) return;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(grads[0].device());
+  std::vector<SlabFlushEntry> entries;
+  for (size_t i = 0; i < slabs.size(); ++i) {
+    const auto& g = grads[i];
+    const auto& sb = slabs[i];
+    check_f32(g, "grad", grads[0]);
+    check_f32(sb, "slab", grads[0]);
+    TORCH_CHECK(g.numel() > 0 && sb.numel() % g.numel() == 0 && sb.numel() >= g.numel(),
+                "slab must hold whole gradient-sized slices");
+    entries.push_back({sb.data_ptr<float>(), g.data_ptr<float>(), g.numel(),
+                       static_cast<int>(sb.numel() / g.numel()), accumulate[i] != 0});
+  }
+  launch_slab_flush(entries.data(), static_cast<int>(entries.size()), cur_stream(grads[0]));
 }
 
 std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
@@ -381,7 +446,10 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                                         at::TensorList weights, at::IntArrayRef geo, bool relu,
                                         bool need_dx,
                                         const c10::List<c10::optional<at::Tensor>>& accum,
-                                        at::TensorList weights_t, bool defer_wgrad) {
+                                        at::TensorList weights_t, bool defer_wgrad,
+                                        const c10::List<c10::optional<at::Tensor>>& slabs,
+                                        at::IntArrayRef slab_first,
+                                        const c10::optional<at::Tensor>& beta, bool relu_out) {
   auto x = x_in.contiguous();
   // dy is read in place when it is a channel slice (a concatenated cell output's gradient)
   int64_t dy_img = image_stride_if_channel_slice(dy_in);
@@ -423,7 +491,8 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   launch_bn_backward(dy.data_ptr<float>(), z.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), ga, sums.data_ptr<float>(), dz.data_ptr<float>(),
                      dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), into[0].defined(),
-                     into[1].defined(), n, c, s, dy_img, stream);
+                     into[1].defined(), n, c, s, dy_img, stream, relu_out,
+                     opt_ptr(beta, "beta", x, c));
   std::vector<at::Tensor> out;
   at::Tensor dx;
   if (need_dx) {
@@ -471,7 +540,8 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   }
   for (size_t i = 0; i < p.geo.size(); ++i) {
     const bool acc = into[2 + i].defined();
-    out.push_back(wgrad_part(dz, x, weights[i], p.geo[i], acc ? into[2 + i] : at::Tensor()));
+    out.push_back(wgrad_part(dz, x, weights[i], p.geo[i], acc ? into[2 + i] : at::Tensor(),
+                             slab_of(slabs, i), first_of(slab_first, i)));
   }
   return out;
 }
@@ -480,7 +550,9 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
 // with defer_wgrad), on the current stream: dW_i (+)= dz[:, part i] x relu(X) taps.
 std::vector<at::Tensor> convbn_wgrad(const at::Tensor& dz, const at::Tensor& x_in,
                                      at::TensorList weights, at::IntArrayRef geo, bool relu,
-                                     const c10::List<c10::optional<at::Tensor>>& accum) {
+                                     const c10::List<c10::optional<at::Tensor>>& accum,
+                                     const c10::List<c10::optional<at::Tensor>>& slabs,
+                                     at::IntArrayRef slab_first) {
   auto x = x_in.contiguous();
   check_f32(x, "x", x);
   check_f32(dz, "dz", x);
@@ -502,7 +574,8 @@ std::vector<at::Tensor> convbn_wgrad(const at::Tensor& dz, const at::Tensor& x_i
         into = *t;
       }
     }
-    out.push_back(wgrad_part(dz, x, weights[i], p.geo[i], into));
+    out.push_back(wgrad_part(dz, x, weights[i], p.geo[i], into, slab_of(slabs, i),
+                             first_of(slab_first, i)));
   }
   return out;
 }
@@ -616,7 +689,8 @@ at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_
 // `accum` (optional): accumulate into this tensor (the weight's .grad) and return it.
 at::Tensor conv_gemm_backward_weight(const at::Tensor& dz_in, const at::Tensor& x_in,
                                      const at::Tensor& weight, at::IntArrayRef geo, bool relu,
-                                     const c10::optional<at::Tensor>& accum) {
+                                     const c10::optional<at::Tensor>& accum,
+                                     const c10::optional<at::Tensor>& slab, bool slab_first) {
   auto x = x_in.contiguous();
   auto dz = dz_in.contiguous();
   check_f32(x, "x", x);
@@ -630,22 +704,25 @@ at::Tensor conv_gemm_backward_weight(const at::Tensor& dz_in, const at::Tensor& 
     check_f32(*accum, "accum", x);
     TORCH_CHECK(accum->numel() == weight.numel(), "accum must have the weight's size");
   }
-  auto dw = acc ? *accum : at::empty_like(weight);
-  const ConvGemmPlan plan =
-      tuned_plan(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(),
-                 nullptr, nullptr, p.geo[0], acc, dz.numel() * 4, x.numel() * 4, x, dw.numel());
-  run_gemm(2, dz.data_ptr<float>(), x.data_ptr<float>(), nullptr, dw.data_ptr<float>(), nullptr,
-           nullptr, p.geo[0], plan, acc, dz.numel() * 4, x.numel() * 4, x);
-  return dw;
+  return wgrad_part(dz, x, weight, p.geo[0], acc ? *accum : at::Tensor(), slab, slab_first);
 }
 
 // BatchNorm (training) of x[N][C][*] with micro-batch statistics, for DeferredBatchNorm:
 // statistics partials per (image, channel), Chan/fp64 finalize (folded into the fp64
 // accumulators `acc` [3][C] when given), one normalising pass.  Returns {y, mean, invstd}.
+//
+// Plain BatchNorm2d training (ops/fusion.py): running_mean / running_var (EMA with
+// `momentum`, unbiased variance) and num_batches_tracked are updated by the finalize when
+// given; `relu` applies a ReLU after the normalisation (its backward: bn_train_backward
+// with relu).
 std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
                                          const c10::optional<at::Tensor>& gamma,
                                          const c10::optional<at::Tensor>& beta,
-                                         const c10::optional<at::Tensor>& acc, double eps) {
+                                         const c10::optional<at::Tensor>& acc, double eps,
+                                         const c10::optional<at::Tensor>& running_mean,
+                                         const c10::optional<at::Tensor>& running_var,
+                                         const c10::optional<at::Tensor>& num_batches_tracked,
+                                         double momentum, bool relu) {
   auto x = x_in.contiguous();
   check_f32(x, "x", x);
   TORCH_CHECK(x.dim() >= 2, "x must be [N][C][*]");
@@ -664,16 +741,28 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
                 "acc must be a contiguous float64 [3][C] tensor on the input's device");
     accp = acc->data_ptr<double>();
   }
+  const float* rm = opt_ptr(running_mean, "running_mean", x, c);
+  const float* rv = opt_ptr(running_var, "running_var", x, c);
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean and running_var go together");
+  int64_t* tracked = nullptr;
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->device() == x.device() &&
+                    num_batches_tracked->scalar_type() == at::kLong &&
+                    num_batches_tracked->numel() == 1,
+                "num_batches_tracked must be a 1-element int64 tensor on the input's device");
+    tracked = num_batches_tracked->data_ptr<int64_t>();
+  }
   launch_bn_stats(x.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n, c,
                   s, stream);
   auto sums = at::empty({2, c}, x.options());  // zeroed by the finalize, for the backward
   launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(),
                            static_cast<int>(n), static_cast<int>(s), n, c, s,
-                           static_cast<float>(eps), 0.0, mean.data_ptr<float>(),
-                           invstd.data_ptr<float>(), nullptr, nullptr, nullptr, accp,
+                           static_cast<float>(eps), rm != nullptr ? momentum : 0.0,
+                           mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                           const_cast<float*>(rm), const_cast<float*>(rv), tracked, accp,
                            sums.data_ptr<float>(), x.data_ptr<float>(),
                            opt_ptr(gamma, "gamma", x, c), opt_ptr(beta, "beta", x, c), nullptr,
-                           y.data_ptr<float>(), stream);
+                           y.data_ptr<float>(), stream, relu);
   return {y, mean, invstd, sums};
 }
 
@@ -681,7 +770,8 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
 std::vector<at::Tensor> bn_train_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
                                           const at::Tensor& mean, const at::Tensor& invstd,
                                           at::Tensor& sums,
-                                          const c10::optional<at::Tensor>& gamma) {
+                                          const c10::optional<at::Tensor>& gamma,
+                                          const c10::optional<at::Tensor>& beta, bool relu) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   check_f32(x, "x", x);
@@ -697,7 +787,8 @@ std::vector<at::Tensor> bn_train_backward(const at::Tensor& dy_in, const at::Ten
   launch_bn_backward(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), opt_ptr(gamma, "gamma", x, c),
                      sums.data_ptr<float>(), dx.data_ptr<float>(), dgamma.data_ptr<float>(),
-                     dbeta.data_ptr<float>(), false, false, n, c, s, 0, cur_stream(x));
+                     dbeta.data_ptr<float>(), false, false, n, c, s, 0, cur_stream(x), relu,
+                     opt_ptr(beta, "beta", x, c));
   return {dx, dgamma, dbeta};
 }
 
@@ -849,20 +940,25 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("maxpool2x2_backward(Tensor x, Tensor dy) -> Tensor");
   m.def("avgpool3_forward(Tensor x, int stride, Tensor? add) -> Tensor");
   m.def("avgpool3_backward(Tensor dy, int h, int w, int stride) -> Tensor");
-  m.def("bn_train_forward(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? acc, float eps) "
+  m.def("bn_train_forward(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? acc, float eps, "
+        "Tensor(b!)? running_mean=None, Tensor(c!)? running_var=None, "
+        "Tensor(d!)? num_batches_tracked=None, float momentum=0.0, bool relu=False) "
         "-> Tensor[]");
   m.def("bn_train_backward(Tensor dy, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) sums, "
-        "Tensor? gamma) -> Tensor[]");
+        "Tensor? gamma, Tensor? beta=None, bool relu=False) -> Tensor[]");
   m.def("dbn_commit64(Tensor(a!) acc, Tensor(b!) running_mean, Tensor(c!) running_var, "
         "float momentum) -> ()");
   m.def("convbn_forward(Tensor x, Tensor[] weights, int[] geo, bool relu, Tensor? gamma, "
         "Tensor? beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "Tensor(c!)? num_batches_tracked, float momentum, float eps, Tensor? add) -> Tensor[]");
+        "Tensor(c!)? num_batches_tracked, float momentum, float eps, Tensor? add, "
+        "bool relu_out=False) -> Tensor[]");
   m.def("convbn_backward(Tensor dy, Tensor x, Tensor z, Tensor mean, Tensor invstd, "
         "Tensor(a!) sums, Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx, "
-        "Tensor?[] accum, Tensor[] weights_t, bool defer_wgrad=False) -> Tensor[]");
+        "Tensor?[] accum, Tensor[] weights_t, bool defer_wgrad, Tensor?[] slabs, "
+        "int[] slab_first, Tensor? beta=None, bool relu_out=False) -> Tensor[]");
   m.def("convbn_wgrad(Tensor dz, Tensor x, Tensor[] weights, int[] geo, bool relu, "
-        "Tensor?[] accum) -> Tensor[]");
+        "Tensor?[] accum, Tensor?[] slabs, int[] slab_first) -> Tensor[]");
+  m.def("wgrad_slab_flush(Tensor[] slabs, Tensor(a!)[] grads, int[] accumulate) -> ()");
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
   m.def("conv_gemm_plans_export() -> str", &tgpipe::conv_gemm_plans_export);
   m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
@@ -871,13 +967,14 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "
         "Tensor? weight_t=None) -> Tensor");
   m.def("conv_gemm_backward_weight(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "
-        "Tensor? accum=None) -> Tensor");
+        "Tensor? accum=None, Tensor? slab=None, bool slab_first=False) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("convbn_forward", &tgpipe::convbn_forward);
   m.impl("convbn_backward", &tgpipe::convbn_backward);
   m.impl("convbn_wgrad", &tgpipe::convbn_wgrad);
+  m.impl("wgrad_slab_flush", &tgpipe::wgrad_slab_flush);
   m.impl("conv_gemm_forward", &tgpipe::conv_gemm_forward);
   m.impl("conv_gemm_sweep", &tgpipe::conv_gemm_sweep);
   m.impl("conv_gemm_backward_data", &tgpipe::conv_gemm_backward_data);

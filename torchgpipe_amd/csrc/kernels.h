@@ -153,9 +153,10 @@ struct ConvGemmGeo {
   bool a_t = false;      // backward-data: `a` is W transposed, [ci][co*kh*kw] row-major
 };
 // mode 0: forward  Z[:, co_off:co_off+co] = conv(relu(X)); a = W[co][ci*kh*kw], b = X;
-//         part_mean / part_m2 ([col_blocks][co_total]): per column block mean and centred
-//         second moment of each output channel (BatchNorm statistics) -- only when the
-//         plan does not split the reduction (splits > 1: statistics by launch_bn_stats).
+//         part_mean / part_m2 (may be null): BatchNorm statistics partials of each output
+//         channel, per column block ([col_blocks][co_total]) when the plan does not split
+//         the reduction, per image ([n][co_total], like launch_bn_stats) when it does (the
+//         split reduction computes them in the same pass).
 // mode 1: backward-data  dX (+)= relu'(X) * conv^T(dZ); a = W (untransposed), b = dZ,
 //         x_mask = X (relu mask); `accumulate` adds to dX (several convolutions of one X).
 //         dX must be zeroed when the plan scatters (stride holes).
@@ -178,6 +179,23 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
                       float* part_mean, float* part_m2, const ConvGemmGeo& g,
                       const ConvGemmPlan& plan, bool accumulate, float* ws, int64_t a_bytes,
                       int64_t b_bytes, hipStream_t stream);
+// Weight gradient of a split plan (splits > 1) into a per-parameter slab of `splits` weight-
+// sized slices that persists across the micro-batches of a step: split s stores
+// (accumulate = false) or adds (true) its partial into slice s, with no reduction pass;
+// launch_slab_flush sums the slices into the gradient once per step.
+void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
+                                 const ConvGemmGeo& g, const ConvGemmPlan& plan, bool accumulate,
+                                 int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
+constexpr int kSlabFlushMax = 24;  // table entries per flush launch (kernel argument bytes)
+struct SlabFlushEntry {
+  const float* slab;
+  float* grad;
+  int64_t numel;
+  int splits;
+  bool accumulate;
+};
+// grad (+)= sum_s slab[s] for every entry (ceil(count / kSlabFlushMax) launches).
+void launch_slab_flush(const SlabFlushEntry* entries, int count, hipStream_t stream);
 
 // (mean, M2) partials of z[n][c][s] per (image, channel): part_*[n][c] (width s).
 void launch_bn_stats(const float* z, float* part_mean, float* part_m2, int64_t n, int64_t c,
@@ -211,11 +229,14 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
                               double momentum, float* mean, float* invstd, float* running_mean,
                               float* running_var, int64_t* tracked, double* acc, float* zero2c,
                               const float* z, const float* gamma, const float* beta,
-                              const float* add, float* y, hipStream_t stream);
+                              const float* add, float* y, hipStream_t stream, bool relu = false);
+// relu_out: the forward applied a ReLU after the normalisation (launch_bn_finalize_apply's
+// `relu`); dy is that ReLU's output gradient and its mask is re-derived from z (needs beta).
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
                         bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
-                        int64_t dy_img, hipStream_t stream);  // dy_img: dy's image stride
+                        int64_t dy_img, hipStream_t stream,  // dy_img: dy's image stride
+                        bool relu_out = false, const float* beta = nullptr);
 
 // 3x3 average pool, padding 1, count_include_pad = False, stride 1 / 2 (pool.hip):
 // y = pool(x) (+ add) over `planes` = N*C planes of h x w; backward gathers dx.

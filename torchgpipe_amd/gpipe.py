@@ -27,6 +27,7 @@ from torch import Tensor, nn
 from torchgpipe_amd import microbatch
 from torchgpipe_amd.batchnorm import DeferredBatchNorm, set_micro_batches
 from torchgpipe_amd.ops.conv import new_step as wino_new_step
+from torchgpipe_amd.ops.fusion import relink
 from torchgpipe_amd.pipeline import Pipeline
 from torchgpipe_amd.skip.layout import inspect_skip_layout
 from torchgpipe_amd.skip.skippable import verify_skippables
@@ -118,6 +119,8 @@ def split_module(module: nn.Sequential, balance: Iterable[int], devices: List[to
             materialize(partition, device)
         else:
             partition.to(device)
+        # Conv-BN(-ReLU) runs fuse only inside one partition (ops/fusion.py)
+        relink(partition)
         partitions.append(partition)
     del devices[len(balance):]
     return cast(List[nn.Sequential], nn.ModuleList(partitions)), balance, devices

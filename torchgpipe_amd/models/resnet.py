@@ -5,6 +5,13 @@ Same structure as the reference benchmark model
 each bottleneck becomes a run of flat layers, with the residual carried by a
 ``@skippable`` ``Identity`` (stash) / ``Residual`` (pop) pair isolated in a
 per-block namespace.  ResNet-101 = 370 layers, 44.55 M parameters.
+
+``fused=True`` (default) keeps every layer, name and parameter but builds the convolution /
+BatchNorm / ReLU layers from :mod:`torchgpipe_amd.ops.fusion`: inside one partition each
+``conv, bn[, relu]`` run executes as one native op (implicit-GEMM MFMA convolution with the
+BatchNorm statistics in its epilogue, or Winograd F(4x4) for the 3x3 stride-1
+convolutions, then one normalise + ReLU pass), the BatchNorm and ReLU layers passing the
+result through.  ``fused=False`` is the plain ``nn`` model (the numerics oracle).
 """
 from collections import OrderedDict
 from typing import Any, Generator, List, Optional
@@ -12,6 +19,7 @@ from typing import Any, Generator, List, Optional
 from torch import Tensor, nn
 
 from torchgpipe_amd.models.flatten import flatten_sequential
+from torchgpipe_amd.ops.fusion import BatchNormAct2d, ConvBN2d, ReLU, relink
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
 __all__ = ['resnet50', 'resnet101', 'build_resnet']
@@ -37,44 +45,53 @@ class Residual(nn.Module):
         return x + identity
 
 
+def _layers(fused: bool):  # type: ignore[no-untyped-def]
+    if fused:
+        return ConvBN2d, BatchNormAct2d, ReLU
+    return nn.Conv2d, nn.BatchNorm2d, nn.ReLU
+
+
 def bottleneck(inplanes: int, planes: int, stride: int = 1,
-               downsample: Optional[nn.Module] = None, inplace: bool = False) -> nn.Sequential:
+               downsample: Optional[nn.Module] = None, inplace: bool = False,
+               fused: bool = False) -> nn.Sequential:
+    conv, bn, relu = _layers(fused)
     ns = Namespace()
     layers: 'OrderedDict[str, nn.Module]' = OrderedDict()
     layers['identity'] = Identity().isolate(ns)
-    layers['conv1'] = nn.Conv2d(inplanes, planes, 1, bias=False)
-    layers['bn1'] = nn.BatchNorm2d(planes)
-    layers['relu1'] = nn.ReLU(inplace=inplace)
-    layers['conv2'] = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
-    layers['bn2'] = nn.BatchNorm2d(planes)
-    layers['relu2'] = nn.ReLU(inplace=inplace)
-    layers['conv3'] = nn.Conv2d(planes, planes * 4, 1, bias=False)
-    layers['bn3'] = nn.BatchNorm2d(planes * 4)
+    layers['conv1'] = conv(inplanes, planes, 1, bias=False)
+    layers['bn1'] = bn(planes)
+    layers['relu1'] = relu(inplace=inplace)
+    layers['conv2'] = conv(planes, planes, 3, stride=stride, padding=1, bias=False)
+    layers['bn2'] = bn(planes)
+    layers['relu2'] = relu(inplace=inplace)
+    layers['conv3'] = conv(planes, planes * 4, 1, bias=False)
+    layers['bn3'] = bn(planes * 4)
     layers['residual'] = Residual(downsample).isolate(ns)
-    layers['relu3'] = nn.ReLU(inplace=inplace)
+    layers['relu3'] = relu(inplace=inplace)
     return nn.Sequential(layers)
 
 
-def build_resnet(layers: List[int], num_classes: int = 1000, inplace: bool = False
-                 ) -> nn.Sequential:
+def build_resnet(layers: List[int], num_classes: int = 1000, inplace: bool = False,
+                 fused: bool = True) -> nn.Sequential:
+    conv, bn, relu = _layers(fused)
     inplanes = 64
 
     def make_layer(planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
         nonlocal inplanes
         downsample = None
         if stride != 1 or inplanes != planes * 4:
-            downsample = nn.Sequential(nn.Conv2d(inplanes, planes * 4, 1, stride=stride,
-                                                 bias=False),
-                                       nn.BatchNorm2d(planes * 4))
-        seq = [bottleneck(inplanes, planes, stride, downsample, inplace)]
+            downsample = nn.Sequential(conv(inplanes, planes * 4, 1, stride=stride, bias=False),
+                                       bn(planes * 4))
+        seq = [bottleneck(inplanes, planes, stride, downsample, inplace, fused)]
         inplanes = planes * 4
-        seq += [bottleneck(inplanes, planes, inplace=inplace) for _ in range(1, blocks)]
+        seq += [bottleneck(inplanes, planes, inplace=inplace, fused=fused)
+                for _ in range(1, blocks)]
         return nn.Sequential(*seq)
 
     model = nn.Sequential(OrderedDict([
-        ('conv1', nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)),
-        ('bn1', nn.BatchNorm2d(64)),
-        ('relu', nn.ReLU()),
+        ('conv1', conv(3, 64, kernel_size=7, stride=2, padding=3, bias=False)),
+        ('bn1', bn(64)),
+        ('relu', relu()),
         ('maxpool', nn.MaxPool2d(kernel_size=3, stride=2, padding=1)),
         ('layer1', make_layer(64, layers[0])),
         ('layer2', make_layer(128, layers[1], stride=2)),
@@ -92,6 +109,8 @@ def build_resnet(layers: List[int], num_classes: int = 1000, inplace: bool = Fal
         elif isinstance(m, nn.BatchNorm2d):
             nn.init.constant_(m.weight, 1)
             nn.init.constant_(m.bias, 0)
+    if fused:
+        relink(model)
     return model
 
 

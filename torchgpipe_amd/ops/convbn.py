@@ -119,15 +119,19 @@ class _ConvBN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: Tensor, add: Optional[Tensor], gamma: Optional[Tensor],  # type: ignore[override]
                 beta: Optional[Tensor], bn: nn.BatchNorm2d, geo: List[int], relu: bool,
-                caches: List[_TransformCache], *weights: Tensor) -> Tensor:
+                relu_out: bool, caches: List[_TransformCache], *weights: Tensor) -> Tensor:
         ops = _ext.require(x)
         track = bn.track_running_stats and bn.running_mean is not None
         y, z, mean, invstd, sums = ops.convbn_forward(
             x, list(weights), geo, relu, gamma, beta,
             bn.running_mean if track else None, bn.running_var if track else None,
             bn.num_batches_tracked if track else None,
-            float(bn.momentum) if bn.momentum is not None else 0.0, float(bn.eps), add)
-        ctx.save_for_backward(x, z, mean, invstd, sums, gamma, *weights)
+            float(bn.momentum) if bn.momentum is not None else 0.0, float(bn.eps), add,
+            relu_out)
+        # (beta only for the ReLU mask of relu_out, re-derived from z in the backward)
+        ctx.save_for_backward(x, z, mean, invstd, sums, gamma, beta if relu_out else None,
+                              *weights)
+        ctx.relu_out = relu_out
         ctx.params = (gamma, beta) + weights  # gradient-accumulation fusion (ops/gradacc.py)
         ctx.caches = caches
         ctx.geo = geo
@@ -138,16 +142,26 @@ class _ConvBN(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy: Tensor):  # type: ignore[override]
-        x, z, mean, invstd, sums, gamma, *weights = ctx.saved_tensors
+        x, z, mean, invstd, sums, gamma, beta, *weights = ctx.saved_tensors
         need_dx = ctx.needs_input_grad[0]
         fused = [gradacc.target(p) for p in ctx.params]
         # the backward-data GEMM reads W^T: transposed once per step, not per micro-batch
         wts = [c.get_transposed(w) for c, w in zip(ctx.caches, weights)] if need_dx else []
         ops = _ext.require(dy)
         side = _wgrad_stream(dy.device) if all(f for f, _ in fused[2:]) else None
+        # deferred split weight gradients (ops/gradacc.py): per-parameter slabs
+        slabs: List[Optional[Tensor]] = []
+        firsts: List[int] = []
+        for (fuse, _), w in zip(fused[2:], ctx.params[2:]):
+            sb, first = gradacc.slab(w) if fuse else (None, False)
+            slabs.append(sb)
+            firsts.append(int(first))
+        if all(sb is None for sb in slabs):
+            slabs, firsts = [], []
         dx, dgamma, dbeta, *dws = ops.convbn_backward(
             dy, x, z, mean, invstd, sums, gamma, weights, ctx.geo, ctx.relu, need_dx,
-            [into for _, into in fused], wts, side is not None)
+            [into for _, into in fused], wts, side is not None, slabs, firsts, beta,
+            ctx.relu_out)
         if side is not None:
             # weight gradients on the side stream (written into .grad by the kernels)
             dz = dws[0]
@@ -156,23 +170,28 @@ class _ConvBN(torch.autograd.Function):
             x.record_stream(side)
             with torch.cuda.stream(side):
                 dws = ops.convbn_wgrad(dz, x, weights, ctx.geo, ctx.relu,
-                                       [into for _, into in fused[2:]])
+                                       [into for _, into in fused[2:]], slabs, firsts)
         grads = [dgamma, dbeta] + dws
         for k, ((fuse, into), p) in enumerate(zip(fused, ctx.params)):
-            if fuse:  # written into p.grad by the kernels
-                if into is None:
+            if fuse:  # written into p.grad (or its slab) by the kernels
+                if k >= 2 and slabs and gradacc.deferred(p, slabs[k - 2], grads[k]):
+                    pass
+                elif into is None:
                     gradacc.commit(p, grads[k])
                 grads[k] = None
         del ctx.params, ctx.caches
         dgamma, dbeta, *dws = grads
         return (dx if need_dx else None, dy if ctx.has_add else None,
                 dgamma if ctx.needs_input_grad[2] else None,
-                dbeta if ctx.needs_input_grad[3] else None, None, None, None, None, *dws)
+                dbeta if ctx.needs_input_grad[3] else None, None, None, None, None, None,
+                *dws)
 
 
 def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.BatchNorm2d,
-                 relu: bool = True, add: Optional[Tensor] = None) -> Tensor:
-    """``bn(cat([conv(relu(x) shifted by offset) for conv, offset in convs]))`` (+ ``add``).
+                 relu: bool = True, add: Optional[Tensor] = None,
+                 relu_out: bool = False) -> Tensor:
+    """``bn(cat([conv(relu(x) shifted by offset) for conv, offset in convs]))`` (+ ``add``),
+    followed by a ReLU when ``relu_out`` (ResNet's Conv-BN-ReLU; not with ``add``).
 
     ``convs`` are ``(conv, offset)`` pairs whose outputs are concatenated on channels
     (one pair for ReLU-Conv-BN, two for FactorizedReduce: offsets 0 and 1).  Runs the
@@ -182,7 +201,7 @@ def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.Batch
     for conv, offset in convs:
         geo += _geo(conv, offset)
     weights = [conv.weight for conv, _ in convs]
-    return _ConvBN.apply(x, add, bn.weight, bn.bias, bn, geo, relu,
+    return _ConvBN.apply(x, add, bn.weight, bn.bias, bn, geo, relu, relu_out,
                          [_weight_cache(conv) for conv, _ in convs], *weights)
 
 
@@ -286,9 +305,12 @@ class _GemmConv(torch.autograd.Function):
                                              ctx.cache.get_transposed(weight))
         if ctx.needs_input_grad[1]:
             fuse, into = gradacc.target(ctx.param)
-            dw = ops.conv_gemm_backward_weight(dz, x, weight, ctx.geo, False, into)
+            sb, first = gradacc.slab(ctx.param) if fuse else (None, False)
+            dw = ops.conv_gemm_backward_weight(dz, x, weight, ctx.geo, False, into, sb, first)
             if fuse:  # accumulated into / stored as weight.grad (ops/gradacc.py)
-                if into is None:
+                if sb is not None and gradacc.deferred(ctx.param, sb, dw):
+                    pass
+                elif into is None:
                     gradacc.commit(ctx.param, dw)
                 dw = None
         del ctx.param, ctx.cache

@@ -1,0 +1,162 @@
+"""Conv → BatchNorm (→ ReLU) fusion across the layers of a flat ``nn.Sequential``.
+
+The benchmark ResNet-101 (reference ``benchmarks/models/resnet/bottleneck.py:31-79``) is a
+flat sequence of 370 layers -- ``conv1, bn1, relu1, conv2, bn2, relu2, conv3, bn3, ...`` --
+because GPipe balances and checkpoints by layer.  Keeping that structure (the reference's
+balance tables and state-dict keys apply unchanged) while running each Conv-BN-ReLU run as
+one native op needs the layers to cooperate:
+
+* :class:`ConvBN2d` (an ``nn.Conv2d``): when :func:`relink` has linked it to the
+  :class:`BatchNormAct2d` right after it (and a :class:`ReLU` after that), its forward
+  runs the convolution, the BatchNorm and the ReLU:
+
+  - 1x1 / strided / 7x7 convolutions: the implicit-GEMM MFMA kernel with the BatchNorm
+    statistics in its epilogue, one finalize + normalise (+ ReLU) pass
+    (``ops.convbn.relu_conv_bn`` with ``relu_out``); the backward re-derives the ReLU
+    mask from the saved convolution output;
+  - 3x3 stride-1 convolutions: the Winograd F(4x4) / batched-GEMM kernels
+    (``ops.conv``), then the native BatchNorm(+ReLU) pass (:func:`bn_act`);
+
+  and marks its output as normalised (and rectified) by that BatchNorm;
+* :class:`BatchNormAct2d` passes a marked input through; otherwise it runs the native
+  BatchNorm (+ the linked ReLU) or ``nn.BatchNorm2d``;
+* :class:`ReLU` passes an input the BatchNorm already rectified through.
+
+Links are only made between consecutive layers of one ``nn.Sequential`` -- one pipeline
+partition -- so a balance that separates a convolution from its BatchNorm leaves both
+running on their own.  ``GPipe`` and ``PipelineStage`` call :func:`relink` on every
+partition after splitting (and after DeferredBatchNorm conversion, whose BatchNorms are
+not linked).  Outside training mode, on the CPU, or for non-fp32 tensors every layer runs
+its plain PyTorch forward.
+"""
+from typing import Optional
+
+import torch
+from torch import Tensor, nn
+import torch.nn.functional as F
+
+from torchgpipe_amd.ops import _ext
+from torchgpipe_amd.ops.conv import WinogradConv2d, wino_eligible
+from torchgpipe_amd.ops.convbn import (_bn_ok, fusable, gemm_conv2d, gemm_conv_eligible,
+                                       relu_conv_bn)
+
+__all__ = ['ConvBN2d', 'BatchNormAct2d', 'ReLU', 'relink', 'bn_act']
+
+_LINK = '_tgpipe_link'       # ConvBN2d -> (BatchNormAct2d, relu?)
+_RELU = '_tgpipe_relu_next'  # BatchNormAct2d -> a linked ReLU follows
+_DONE_BN = '_tgpipe_bn_done'    # tensor mark: id() of the BatchNorm already applied
+_DONE_RELU = '_tgpipe_relu_done'  # tensor mark: the ReLU after it too
+
+
+class _BNAct(torch.autograd.Function):
+    """Training-mode BatchNorm2d (batch statistics, running-stat EMA) + optional ReLU on the
+    native kernels (``csrc/batchnorm.hip``): statistics pass, finalize + normalise (+ ReLU)."""
+
+    @staticmethod
+    def forward(ctx, x: Tensor, gamma: Optional[Tensor], beta: Optional[Tensor],  # type: ignore[override]
+                bn: nn.BatchNorm2d, relu: bool) -> Tensor:
+        track = bn.track_running_stats and bn.running_mean is not None
+        y, mean, invstd, sums = _ext.require(x).bn_train_forward(
+            x, gamma, beta, None, float(bn.eps),
+            bn.running_mean if track else None, bn.running_var if track else None,
+            bn.num_batches_tracked if track else None,
+            float(bn.momentum) if track else 0.0, relu)
+        ctx.save_for_backward(x, mean, invstd, sums, gamma, beta)
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy: Tensor):  # type: ignore[override]
+        x, mean, invstd, sums, gamma, beta = ctx.saved_tensors
+        dx, dgamma, dbeta = _ext.require(dy).bn_train_backward(
+            dy.contiguous(), x, mean, invstd, sums, gamma, beta, ctx.relu)
+        return (dx, dgamma if ctx.needs_input_grad[1] else None,
+                dbeta if ctx.needs_input_grad[2] else None, None, None)
+
+
+def _native_bn_ok(bn: nn.BatchNorm2d, x: Tensor) -> bool:
+    return _bn_ok(bn, x) and x.numel() > 0 and _ext.available()
+
+
+def bn_act(x: Tensor, bn: nn.BatchNorm2d, relu: bool) -> Tensor:
+    """``relu(bn(x))`` (or ``bn(x)``) in training mode on the native kernels; callers check
+    :func:`_native_bn_ok` first."""
+    return _BNAct.apply(x.contiguous(), bn.weight, bn.bias, bn, relu)
+
+
+def _mark(y: Tensor, bn: nn.Module, relu: bool) -> Tensor:
+    setattr(y, _DONE_BN, id(bn))
+    if relu:
+        setattr(y, _DONE_RELU, True)
+    return y
+
+
+class ConvBN2d(WinogradConv2d):
+    """``nn.Conv2d`` (same parameters) that runs its linked BatchNorm (and ReLU) with it."""
+
+    def forward(self, input: Tensor) -> Tensor:
+        link = self.__dict__.get(_LINK)
+        if link is not None and self.padding_mode == 'zeros':
+            bn, relu = link
+            if self.bias is None and _native_bn_ok(bn, input):
+                if wino_eligible(input, self.weight, self.stride, self.padding, self.dilation,
+                                 self.groups) and self.bias is None:
+                    z = WinogradConv2d.forward(self, input)
+                    return _mark(bn_act(z, bn, relu), bn, relu)
+                if fusable(input, [self], bn):
+                    y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu)
+                    return _mark(y, bn, relu)
+        if self.padding_mode == 'zeros' and not wino_eligible(
+                input, self.weight, self.stride, self.padding, self.dilation, self.groups) \
+                and gemm_conv_eligible(input, self):
+            return gemm_conv2d(input, self)
+        return WinogradConv2d.forward(self, input)
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` (same parameters and buffers) that a linked :class:`ConvBN2d` may
+    have applied already, and that runs natively with a linked :class:`ReLU` fused."""
+
+    def forward(self, input: Tensor) -> Tensor:
+        if getattr(input, _DONE_BN, None) == id(self):
+            return input
+        relu = bool(self.__dict__.get(_RELU, False))
+        if input.dim() == 4 and _native_bn_ok(self, input):
+            y = bn_act(input, self, relu)
+            if relu:
+                setattr(y, _DONE_RELU, True)
+            return y
+        return super().forward(input)
+
+
+class ReLU(nn.ReLU):
+    """``nn.ReLU`` that passes through an input its linked BatchNorm already rectified."""
+
+    def forward(self, input: Tensor) -> Tensor:
+        if getattr(input, _DONE_RELU, False):
+            return input
+        return F.relu(input, inplace=self.inplace)
+
+
+def relink(module: nn.Module) -> int:
+    """(Re)link every ``ConvBN2d, BatchNormAct2d[, ReLU]`` run of consecutive children of
+    each ``nn.Sequential`` in ``module``; earlier links inside ``module`` are dropped first.
+    Returns the number of convolutions linked."""
+    for m in module.modules():
+        m.__dict__.pop(_LINK, None)
+        m.__dict__.pop(_RELU, None)
+    linked = 0
+    for seq in module.modules():
+        if not isinstance(seq, nn.Sequential):
+            continue
+        kids = list(seq.children())
+        for i, m in enumerate(kids):
+            if type(m) is BatchNormAct2d and i + 1 < len(kids) and type(kids[i + 1]) is ReLU:
+                m.__dict__[_RELU] = True
+            if not isinstance(m, ConvBN2d) or i + 1 >= len(kids) or \
+                    type(kids[i + 1]) is not BatchNormAct2d:
+                continue
+            relu = i + 2 < len(kids) and type(kids[i + 2]) is ReLU
+            m.__dict__[_LINK] = (kids[i + 1], relu)
+            linked += 1
+    return linked

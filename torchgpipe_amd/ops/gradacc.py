@@ -20,6 +20,18 @@ It only applies when the result is indistinguishable from autograd's:
 
 ``TGPIPE_FUSED_GRAD_ACCUM=0`` turns it off (plain autograd accumulation).
 
+Deferred weight gradients (:func:`deferred_wgrad`, used by ``PipelineStage.backward``):
+an implicit-GEMM weight gradient whose plan splits the reduction over workgroups (most of
+AmoebaNet's: few output tiles, a long images x pixels reduction) would reduce its split
+partials in a second launch every micro-batch.  Inside the scope each such parameter
+instead owns a *slab* of ``splits`` weight-sized slices that persists across the step's
+micro-batches: split ``s`` of every micro-batch adds its partial into slice ``s``
+(the first one stores), and one flush at the end of the scope sums the slices into
+``.grad`` for all parameters at once (a few launches per step instead of one reduction per
+parameter and micro-batch; ~9 k launches per AmoebaNet-D(18, 256) step).  The slices are
+summed in a fixed order, so the result is bitwise reproducible.  Slabs stay allocated
+(``TGPIPE_DEFERRED_WGRAD=0`` turns the deferral off).
+
 The parameter's ``AccumulateGrad`` node is looked up once per step and pinned on the
 parameter until :func:`release` (called when the next pipeline step starts,
 ``ops.conv.new_step``).  Pinning it longer would hand the next step's forward the old
@@ -27,16 +39,20 @@ node, which PyTorch bound to the stream it was created on: under forward / recom
 lanes that node's stream differs from the producer's, and the engine then warns ("The
 AccumulateGrad node's stream does not match ...") and inserts cross-stream syncs.
 """
+import contextlib
 import os
-from typing import Dict, Optional, Tuple
+from typing import Dict, Iterator, List, Optional, Tuple
 import weakref
 
 import torch
 from torch import Tensor
 
-__all__ = ['target', 'commit', 'enabled', 'release']
+__all__ = ['target', 'commit', 'enabled', 'release', 'deferred_wgrad', 'slab', 'deferred',
+           'flush_pending']
 
 _ENABLED = os.environ.get('TGPIPE_FUSED_GRAD_ACCUM', '1') != '0'
+_DEFER_ENABLED = os.environ.get('TGPIPE_DEFERRED_WGRAD', '1') != '0'
+_SLAB_ATTR = '_tgpipe_wgrad_slab'
 _ATTR = '_tgpipe_grad_accumulator'
 # id(param) -> weak reference (tensors compare elementwise, so no WeakSet)
 _PINNED: Dict[int, 'weakref.ref[Tensor]'] = {}
@@ -100,3 +116,118 @@ def commit(param: Tensor, grad: Tensor) -> None:
         param.grad = grad
     else:  # pragma: no cover - another op accumulated in between
         param.grad.add_(grad)
+
+
+# -- deferred weight gradients -------------------------------------------------------------
+
+class _Deferral:
+    """Per-device state of :func:`deferred_wgrad`: scope depth, step number, and the slabs
+    written in this step (``id(param)`` -> (weak parameter, slab))."""
+
+    __slots__ = ('depth', 'step', 'pending')
+
+    def __init__(self) -> None:
+        self.depth = 0
+        self.step = 0
+        self.pending: Dict[int, Tuple['weakref.ref[Tensor]', Tensor]] = {}
+
+
+_DEFER: Dict[torch.device, _Deferral] = {}
+
+
+def _device_key(device: torch.device) -> torch.device:
+    device = torch.device(device)
+    if device.type == 'cuda' and device.index is None:
+        device = torch.device('cuda', torch.cuda.current_device())
+    return device
+
+
+@contextlib.contextmanager
+def deferred_wgrad(device: torch.device, enabled: bool = True) -> Iterator[None]:
+    """Defer the split weight-gradient reductions of fused ops on ``device`` to the end of
+    this scope (one step's backward of every micro-batch).
+
+    On exit the calling thread's current stream on ``device`` sums every touched slab into
+    its parameter's ``.grad`` (accumulating into an existing gradient), so everything that
+    wrote a slab must be ordered before that stream by then -- as for the fused ops'
+    direct ``.grad`` writes.  Nested scopes flush at the outermost exit; a scope left by an
+    exception drops the pending partial sums (the step's gradients are incomplete anyway).
+    """
+    if not enabled or not _ENABLED or not _DEFER_ENABLED:
+        yield
+        return
+    device = _device_key(device)
+    if device.type != 'cuda':
+        yield
+        return
+    state = _DEFER.setdefault(device, _Deferral())
+    state.depth += 1
+    if state.depth == 1:
+        state.step += 1
+    ok = False
+    try:
+        yield
+        ok = True
+    finally:
+        state.depth -= 1
+        if state.depth == 0:
+            if ok:
+                flush_pending(device)
+            else:
+                state.pending.clear()
+
+
+def slab(param: Tensor) -> Tuple[Optional[Tensor], bool]:
+    """``(slab, first)`` for a fused weight-gradient kernel about to write ``param``'s
+    gradient: the parameter's persistent slab (``None`` outside a deferral scope) and
+    whether this is the step's first write into it (store rather than add)."""
+    state = _DEFER.get(param.device)
+    if state is None or state.depth == 0:
+        return None, False
+    entry: Optional[List] = getattr(param, _SLAB_ATTR, None)
+    if entry is None or entry[0].device != param.device:
+        entry = [torch.empty(0, device=param.device, dtype=torch.float32), -1]
+        setattr(param, _SLAB_ATTR, entry)
+    return entry[0], entry[1] != state.step
+
+
+def deferred(param: Tensor, slab: Tensor, result: Optional[Tensor]) -> bool:
+    """Whether the kernel deferred ``param``'s gradient into ``slab`` (it returned the slab
+    itself); if so, mark the slab as written in this step and pending its flush."""
+    if result is None or slab is None or slab.numel() == 0 or \
+            result.data_ptr() != slab.data_ptr():
+        return False
+    state = _DEFER[param.device]
+    entry = getattr(param, _SLAB_ATTR)
+    entry[1] = state.step
+    state.pending[id(param)] = (weakref.ref(param), slab)
+    return True
+
+
+def flush_pending(device: torch.device) -> None:
+    """Sum the slabs written in this step into ``.grad`` (one launch per 24 parameters)."""
+    device = _device_key(device)
+    state = _DEFER.get(device)
+    if state is None or not state.pending:
+        return
+    items = list(state.pending.values())
+    state.pending.clear()
+    slabs: List[Tensor] = []
+    grads: List[Tensor] = []
+    accumulate: List[int] = []
+    for ref, sb in items:
+        param = ref()
+        if param is None:
+            continue
+        grad = param.grad
+        if grad is None:
+            grad = torch.empty_like(param, memory_format=torch.contiguous_format)
+            param.grad = grad
+            accumulate.append(0)
+        else:
+            accumulate.append(1)
+        slabs.append(sb)
+        grads.append(grad)
+    if slabs:
+        from torchgpipe_amd.ops import _ext
+        _ext.require(grads[0]).wgrad_slab_flush(slabs, grads, accumulate)

@@ -43,6 +43,7 @@ from torchgpipe_amd.checkpoint import Checkpointing
 from torchgpipe_amd.gpipe import check_balance, partition_layers, verify_module
 from torchgpipe_amd.microbatch import Batch
 from torchgpipe_amd.ops.conv import new_step as wino_new_step
+from torchgpipe_amd.ops.fusion import relink
 from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P, _wait
 from torchgpipe_amd.skip.layout import SkipLayout, inspect_skip_layout
 from torchgpipe_amd.skip.namespace import Namespace
@@ -219,6 +220,8 @@ class PipelineStage:
             # Whole model built on the meta device: only this rank's layers get memory.
             meta_materialize(partition, device)
         self.partition = partition.to(device)
+        # Conv-BN(-ReLU) runs fuse only inside this partition (ops/fusion.py)
+        relink(self.partition)
         self._has_dbn = any(isinstance(m, DeferredBatchNorm) for m in partition.modules())
 
         # Cross-rank skip routes touching this rank, in a canonical order that every
@@ -530,12 +533,17 @@ class PipelineStage:
         ``None``.  With ``wgrad_stream`` the fused ops' weight-gradient GEMMs run on a side
         stream (``ops.convbn.wgrad_stream_scope``), joined before this returns.
         """
-        if self.wgrad_stream and self.device.type == 'cuda':
-            from torchgpipe_amd.ops.convbn import wgrad_stream_scope
-            with wgrad_stream_scope(self.device):
+        # split weight-gradient reductions of the fused ops are deferred to one flush after
+        # the last micro-batch (ops/gradacc.py deferred_wgrad), issued once every stream
+        # that wrote a slab has been joined to the current one
+        from torchgpipe_amd.ops.gradacc import deferred_wgrad
+        with deferred_wgrad(self.device, self.device.type == 'cuda'):
+            if self.wgrad_stream and self.device.type == 'cuda':
+                from torchgpipe_amd.ops.convbn import wgrad_stream_scope
+                with wgrad_stream_scope(self.device):
+                    self._backward(losses)
+            else:
                 self._backward(losses)
-        else:
-            self._backward(losses)
 
     def _backward(self, losses: Optional[Sequence[Tensor]] = None) -> None:
         if self.is_last and losses is None:
