@@ -197,3 +197,33 @@ def test_zoo_dropout2d_replays_from_tape_without_touching_global_rng():
         grads[mode] = [p.grad.clone() for p in gpipe.parameters()]
     for a, b in zip(grads['never'], grads['always']):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('where', ['gpipe', 'convert'])
+def test_user_dropout_on_the_philox_tape(where):
+    """GPipe(philox_dropout=True): the user's nn.Dropout / nn.Dropout2d layers draw Philox
+    pairs replayed from the checkpoint tape -- 'always' equals 'never' exactly and the
+    backward's recomputation leaves torch's generator alone."""
+    from torchgpipe_amd import GPipe
+    from torchgpipe_amd.ops.dropout import Dropout, Dropout2d, convert_dropout
+    grads = {}
+    for mode in ('never', 'always'):
+        torch.manual_seed(0)
+        model = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.Dropout2d(0.5),
+                              nn.Sequential(nn.Conv2d(8, 8, 3, padding=1), nn.Dropout(0.3)))
+        if where == 'convert':
+            convert_dropout(model)
+        assert isinstance(model[1], Dropout2d) == (where == 'convert')
+        gpipe = GPipe(model, [2, 1], devices=['cpu', 'cpu'], chunks=2, checkpoint=mode,
+                      philox_dropout=True)
+        assert isinstance(gpipe.partitions[0][1], Dropout2d)
+        assert isinstance(gpipe.partitions[1][0][1], Dropout)
+        x = torch.rand(4, 3, 8, 8)
+        torch.manual_seed(123)
+        out = gpipe(x)
+        state = torch.get_rng_state()
+        out.sum().backward()
+        assert torch.equal(state, torch.get_rng_state())
+        grads[mode] = [p.grad.clone() for p in gpipe.parameters()]
+    for a, b in zip(grads['never'], grads['always']):
+        assert torch.equal(a, b)

@@ -6,9 +6,13 @@
 // EMA (unbiased variance, like nn.BatchNorm) and writes mean / invstd for bn_apply and
 // the backward.  bn_apply normalises and optionally adds the other branch of an
 // AmoebaNet node (left + right) in the same pass.  The backward is two passes: per
-// channel sums of dy and dy*(z-mean), then dz and the affine gradients.
+// channel sums of dy and dy*(z-mean), then dz and the affine gradients -- one launch of
+// per-channel workgroups (bn_bwd_channel_kernel) when a channel is small enough.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <cstdlib>
+#include <string>
 
 #include "kernels.h"
 
@@ -324,6 +328,89 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
   }
 }
 
+// The whole BatchNorm backward of one channel in one workgroup: the (sum dy,
+// sum dy * (z - mean)) reduction, then dz and the affine gradients from the workgroup's own
+// sums -- one launch instead of bn_bwd_reduce + bn_bwd_dz, no atomics, for channels small
+// enough (n * s elements) that the second read of dy / z comes back from L2.  Same
+// arithmetic per element as the two-pass kernels.
+template <bool kVec>
+__global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
+    const float* __restrict__ dy, const float* __restrict__ z, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ dz, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, int acc_gamma, int acc_beta, int n, int c, int s, float inv_m,
+    int64_t dy_img, int relu_out) {
+  const int ch = blockIdx.x;
+  const float mu = mean[ch];
+  const float is = invstd[ch];
+  const float k1 = (gamma ? gamma[ch] : 1.f) * is;
+  const float rb = relu_out && beta ? beta[ch] : 0.f;
+  float sd = 0.f, sdz = 0.f;
+  const int per = kVec ? s / 4 : s;
+  const int total = n * per;
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const int img = e / per, q = e - img * per;
+    const int64_t zoff = (static_cast<int64_t>(img) * c + ch) * s;
+    const float* dyp = dy + img * dy_img + static_cast<int64_t>(ch) * s;
+    if constexpr (kVec) {
+      const floatx4 g = reinterpret_cast<const floatx4*>(dyp)[q];
+      const floatx4 v = reinterpret_cast<const floatx4*>(z + zoff)[q];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float ge = !relu_out || bn_relu_mask(v[k], mu, k1, rb) ? g[k] : 0.f;
+        sd += ge;
+        sdz += ge * (v[k] - mu);
+      }
+    } else {
+      const float v = z[zoff + q];
+      const float g = !relu_out || bn_relu_mask(v, mu, k1, rb) ? dyp[q] : 0.f;
+      sd += g;
+      sdz += g * (v - mu);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    sd += __shfl_xor(sd, off);
+    sdz += __shfl_xor(sdz, off);
+  }
+  __shared__ float red[2][4];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wave] = sd;
+    red[1][wave] = sdz;
+  }
+  __syncthreads();
+  sd = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  sdz = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[ch] = (acc_gamma ? dgamma[ch] : 0.f) + sdz * is;
+    if (dbeta) dbeta[ch] = (acc_beta ? dbeta[ch] : 0.f) + sd;
+  }
+  const float k2 = sd * inv_m;
+  const float k3 = is * is * sdz * inv_m;
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const int img = e / per, q = e - img * per;
+    const int64_t zoff = (static_cast<int64_t>(img) * c + ch) * s;
+    const float* dyp = dy + img * dy_img + static_cast<int64_t>(ch) * s;
+    if constexpr (kVec) {
+      floatx4 g = reinterpret_cast<const floatx4*>(dyp)[q];
+      const floatx4 v = reinterpret_cast<const floatx4*>(z + zoff)[q];
+      floatx4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (relu_out && !bn_relu_mask(v[k], mu, k1, rb)) g[k] = 0.f;
+        o[k] = k1 * (g[k] - k2 - (v[k] - mu) * k3);
+      }
+      reinterpret_cast<floatx4*>(dz + zoff)[q] = o;
+    } else {
+      const float v = z[zoff + q];
+      float g = dyp[q];
+      if (relu_out && !bn_relu_mask(v, mu, k1, rb)) g = 0.f;
+      dz[zoff + q] = k1 * (g - k2 - (v - mu) * k3);
+    }
+  }
+}
+
 // One wave per (image, channel) plane, four planes per workgroup: mean and centred M2
 // of the plane (two passes, the second from L1/L2), 16-byte loads when s % 4 == 0.
 // Wave-sized work keeps small planes (7^2..14^2) from leaving 3/4 of a workgroup idle.
@@ -488,6 +575,25 @@ void launch_bn_backward(const float* dy, const float* z, const float* mean, cons
   if (dy_img <= 0) dy_img = c * s;
   const int64_t total = n * c * s;
   if (total == 0) return;
+  // Channels of up to kBwdChannelMax elements: one workgroup per channel does both passes
+  // (its dy / z stay in L2 between them).  TGPIPE_BN_BWD_ONEPASS=0: always two passes.
+  static const int64_t one_pass_max = [] {
+    const char* v = std::getenv("TGPIPE_BN_BWD_ONEPASS");
+    return v != nullptr && std::string(v) == "0" ? int64_t{0} : int64_t{32768};
+  }();
+  if (n * s <= one_pass_max && c >= 64 && n * s * c < (int64_t{1} << 31) &&
+      dy_img < (int64_t{1} << 31)) {
+    const float inv_m1 = 1.f / static_cast<float>(n * s);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(c)), dim3(256), 0, stream, dy, z, mean,
+                         invstd, gamma, beta, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
+                         acc_beta ? 1 : 0, static_cast<int>(n), static_cast<int>(c),
+                         static_cast<int>(s), inv_m1, dy_img, relu_out ? 1 : 0);
+    };
+    if ((s & 3) == 0 && (dy_img & 3) == 0) go(bn_bwd_channel_kernel<true>);
+    else go(bn_bwd_channel_kernel<false>);
+    return;
+  }
   // enough (channel, image range) workgroups to cover the chip ~4x
   int64_t splits = (1024 + c - 1) / c;
   if (splits > n) splits = n;

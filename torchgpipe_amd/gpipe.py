@@ -27,6 +27,7 @@ from torch import Tensor, nn
 from torchgpipe_amd import microbatch
 from torchgpipe_amd.batchnorm import DeferredBatchNorm, set_micro_batches
 from torchgpipe_amd.ops.conv import new_step as wino_new_step
+from torchgpipe_amd.ops.dropout import convert_dropout
 from torchgpipe_amd.ops.fusion import relink
 from torchgpipe_amd.pipeline import Pipeline
 from torchgpipe_amd.skip.layout import inspect_skip_layout
@@ -166,6 +167,11 @@ class GPipe(nn.Module):
         deferred_batch_norm: accumulate BatchNorm running statistics over the
             whole mini-batch instead of per micro-batch (default ``False``).
         copy_streams_per_device: size of the per-device copy-stream ring.
+        philox_dropout: run the module's ``nn.Dropout`` / ``nn.Dropout2d`` layers on
+            explicit Philox pairs replayed from each checkpoint's RNG tape instead of
+            forking and restoring the global generators during recomputation
+            (``ops.dropout.convert_dropout``; default ``False``: the reference's
+            behaviour, bitwise equal to the plain model under the same seed).
     """
 
     balance: List[int] = []
@@ -176,7 +182,7 @@ class GPipe(nn.Module):
     def __init__(self, module: nn.Sequential, balance: Optional[Iterable[int]] = None, *,
                  devices: Optional[Devices] = None, chunks: int = chunks,
                  checkpoint: str = checkpoint, deferred_batch_norm: bool = False,
-                 copy_streams_per_device: int = 4) -> None:
+                 copy_streams_per_device: int = 4, philox_dropout: bool = False) -> None:
         super().__init__()
         chunks = int(chunks)
         checkpoint = str(checkpoint)
@@ -196,6 +202,8 @@ class GPipe(nn.Module):
 
         if deferred_batch_norm:
             module = DeferredBatchNorm.convert_deferred_batch_norm(module, chunks)
+        if philox_dropout:
+            convert_dropout(module)
 
         if devices is None:
             devices = range(torch.cuda.device_count())

@@ -18,7 +18,7 @@ from torchgpipe_amd.ops.fused import _signed64
 from torchgpipe_amd.ops.philox import uniform
 from torchgpipe_amd.utils.rng import philox_pair
 
-__all__ = ['dropout', 'Dropout', 'dropout2d', 'Dropout2d']
+__all__ = ['dropout', 'Dropout', 'dropout2d', 'Dropout2d', 'convert_dropout']
 
 
 def _reference(x: Tensor, p: float, seed: int, offset: int) -> Tensor:
@@ -106,3 +106,35 @@ class Dropout2d(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:  # type: ignore[override]
         return dropout2d(x, self.p, self.training)
+
+
+def convert_dropout(module: nn.Module) -> nn.Module:
+    """Replace every ``nn.Dropout`` / ``nn.Dropout2d`` in ``module`` (exact types, in place;
+    ``module`` itself too) by :class:`Dropout` / :class:`Dropout2d` with the same ``p`` and
+    training mode, and return the module.
+
+    ``GPipe(..., philox_dropout=True)`` / ``PipelineStage(..., philox_dropout=True)`` call
+    it: the user's dropout layers then draw explicit Philox pairs that a checkpointed
+    cell's RNG tape replays during recomputation, instead of the global-generator fork /
+    restore of the reference's checkpointing (``torchgpipe/checkpoint.py:191-231``), which
+    mutates process-global state from autograd threads.  The masks come from another
+    random stream than ``torch.nn.functional.dropout``'s, so the result is not bitwise the
+    plain model's under the same ``torch.manual_seed`` (the reason it is opt-in).
+    """
+    def swap(m: nn.Module) -> nn.Module:
+        if type(m) is nn.Dropout:
+            new: nn.Module = Dropout(m.p)
+        elif type(m) is nn.Dropout2d:
+            new = Dropout2d(m.p)
+        else:
+            return m
+        new.train(m.training)
+        return new
+
+    for name, child in list(module.named_children()):
+        swapped = swap(child)
+        if swapped is not child:
+            setattr(module, name, swapped)
+        else:
+            convert_dropout(child)
+    return swap(module)

@@ -43,6 +43,7 @@ from torchgpipe_amd.checkpoint import Checkpointing
 from torchgpipe_amd.gpipe import check_balance, partition_layers, verify_module
 from torchgpipe_amd.microbatch import Batch
 from torchgpipe_amd.ops.conv import new_step as wino_new_step
+from torchgpipe_amd.ops.dropout import convert_dropout
 from torchgpipe_amd.ops.fusion import relink
 from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P, _wait
 from torchgpipe_amd.skip.layout import SkipLayout, inspect_skip_layout
@@ -148,6 +149,8 @@ class PipelineStage:
         ctrl_group: ``gloo`` group for shape metadata (default: WORLD if it is
             gloo, otherwise a new gloo group over the same ranks).
         deferred_batch_norm: convert BatchNorm layers to DeferredBatchNorm.
+        philox_dropout: ``nn.Dropout`` / ``nn.Dropout2d`` on tape-replayed Philox pairs
+            (``ops.dropout.convert_dropout``), as for ``GPipe``.
         pack: pack multi-tensor messages into one transfer (HIP kernel).
         links: one 2-rank communicator per used link (default: on for RCCL,
             off for gloo).
@@ -172,7 +175,8 @@ class PipelineStage:
                  timeout: Optional[float] = None,
                  overlap_recompute: bool = False,
                  overlap_forward: bool = False,
-                 wgrad_stream: bool = False) -> None:
+                 wgrad_stream: bool = False,
+                 philox_dropout: bool = False) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
         if checkpoint not in ('always', 'except_last', 'never'):
@@ -214,6 +218,8 @@ class PipelineStage:
         partition = parts[self.rank]
         if deferred_batch_norm:
             partition = DeferredBatchNorm.convert_deferred_batch_norm(partition, chunks)
+        if philox_dropout:  # user dropout layers on the checkpoint's RNG tape
+            convert_dropout(partition)
         if materialize is not None:
             materialize(partition)
         if is_meta(partition):
