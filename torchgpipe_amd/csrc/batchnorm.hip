@@ -95,9 +95,26 @@ __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
     float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rm,
     float* __restrict__ rv, int64_t* __restrict__ tracked, double* __restrict__ acc,
     float* __restrict__ zero2c, const float* __restrict__ z, const float* __restrict__ gamma,
-    const float* __restrict__ beta, const float* __restrict__ add, float* __restrict__ y) {
+    const float* __restrict__ beta, const float* __restrict__ add, float* __restrict__ y,
+    BnParts parts) {
   const int ch = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // output channel ch of the statistics / z; with parts (a grouped convolution feeding
+  // several BatchNorms) its parameters, running statistics and output come from its part
+  int yc = c, ych = ch;
+  if (parts.count > 0) {
+    int pi = 0;
+    while (pi + 1 < parts.count && ch >= parts.c_end[pi]) ++pi;
+    const int begin = pi == 0 ? 0 : parts.c_end[pi - 1];
+    yc = parts.c_end[pi] - begin;
+    ych = ch - begin;
+    gamma = parts.gamma[pi] ? parts.gamma[pi] - begin : nullptr;
+    beta = parts.beta[pi] ? parts.beta[pi] - begin : nullptr;
+    rm = parts.rm[pi] ? parts.rm[pi] - begin : nullptr;
+    rv = parts.rv[pi] ? parts.rv[pi] - begin : nullptr;
+    tracked = ych == 0 ? parts.tracked[pi] : nullptr;
+    y = parts.y[pi];
+  }
   double na = 0.0, ma = 0.0, m2a = 0.0;
   for (int b = tid; b < blocks; b += 256) {
     const int left = cols - b * width;
@@ -131,7 +148,7 @@ __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
     kb[1] = is * (gamma ? gamma[ch] : 1.f);
     kb[2] = beta ? beta[ch] : 0.f;
     if (blockIdx.y == 0) {
-      if (tracked != nullptr && ch == 0) *tracked += 1;
+      if (tracked != nullptr && (ch == 0 || parts.count > 0)) *tracked += 1;
       if (zero2c != nullptr) {  // the backward's [2][C] reduction buffer
         zero2c[ch] = 0.f;
         zero2c[c + ch] = 0.f;
@@ -171,7 +188,8 @@ __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
       }
-      reinterpret_cast<floatx4*>(y)[off] = v;
+      reinterpret_cast<floatx4*>(y)[(static_cast<int64_t>(img) * yc + ych) * sq +
+                                    (q - (img - n0) * sq)] = v;
     }
   } else {
     const int elems = (n1 - n0) * s;
@@ -181,7 +199,7 @@ __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
       float v = __builtin_fmaf(z[off] - mu, k, bb);
       if constexpr (kAdd) v += add[off];
       if constexpr (kRelu) v = v > 0.f ? v : 0.f;
-      y[off] = v;
+      y[(static_cast<int64_t>(img) * yc + ych) * s + (e - (img - n0) * s)] = v;
     }
   }
 }
@@ -339,8 +357,23 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ dz, float* __restrict__ dgamma,
     float* __restrict__ dbeta, int acc_gamma, int acc_beta, int n, int c, int s, float inv_m,
-    int64_t dy_img, int relu_out) {
+    int64_t dy_img, int relu_out, BnParts parts) {
   const int ch = blockIdx.x;
+  int dyc = ch;  // dy's channel index (its own part's, with parts)
+  if (parts.count > 0) {
+    int pi = 0;
+    while (pi + 1 < parts.count && ch >= parts.c_end[pi]) ++pi;
+    const int begin = pi == 0 ? 0 : parts.c_end[pi - 1];
+    dyc = ch - begin;
+    dy = parts.dy[pi];
+    dy_img = parts.dy_img[pi];
+    gamma = parts.gamma[pi] ? parts.gamma[pi] - begin : nullptr;
+    beta = parts.beta[pi] ? parts.beta[pi] - begin : nullptr;
+    dgamma = parts.dgamma[pi] ? parts.dgamma[pi] - begin : nullptr;
+    dbeta = parts.dbeta[pi] ? parts.dbeta[pi] - begin : nullptr;
+    acc_gamma = parts.acc_gamma[pi];
+    acc_beta = parts.acc_beta[pi];
+  }
   const float mu = mean[ch];
   const float is = invstd[ch];
   const float k1 = (gamma ? gamma[ch] : 1.f) * is;
@@ -348,10 +381,21 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
   float sd = 0.f, sdz = 0.f;
   const int per = kVec ? s / 4 : s;
   const int total = n * per;
+  if (dy == nullptr) {  // a part without a gradient: dz = 0, no parameter gradient added
+    if (threadIdx.x == 0) {
+      if (dgamma && !acc_gamma) dgamma[ch] = 0.f;
+      if (dbeta && !acc_beta) dbeta[ch] = 0.f;
+    }
+    for (int e = threadIdx.x; e < n * s; e += 256) {
+      const int img = e / s;
+      dz[(static_cast<int64_t>(img) * c + ch) * s + (e - img * s)] = 0.f;
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < total; e += 256) {
     const int img = e / per, q = e - img * per;
     const int64_t zoff = (static_cast<int64_t>(img) * c + ch) * s;
-    const float* dyp = dy + img * dy_img + static_cast<int64_t>(ch) * s;
+    const float* dyp = dy + img * dy_img + static_cast<int64_t>(dyc) * s;
     if constexpr (kVec) {
       const floatx4 g = reinterpret_cast<const floatx4*>(dyp)[q];
       const floatx4 v = reinterpret_cast<const floatx4*>(z + zoff)[q];
@@ -391,7 +435,7 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
   for (int e = threadIdx.x; e < total; e += 256) {
     const int img = e / per, q = e - img * per;
     const int64_t zoff = (static_cast<int64_t>(img) * c + ch) * s;
-    const float* dyp = dy + img * dy_img + static_cast<int64_t>(ch) * s;
+    const float* dyp = dy + img * dy_img + static_cast<int64_t>(dyc) * s;
     if constexpr (kVec) {
       floatx4 g = reinterpret_cast<const floatx4*>(dyp)[q];
       const floatx4 v = reinterpret_cast<const floatx4*>(z + zoff)[q];
@@ -499,8 +543,11 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
                               double momentum, float* mean, float* invstd, float* running_mean,
                               float* running_var, int64_t* tracked, double* acc, float* zero2c,
                               const float* z, const float* gamma, const float* beta,
-                              const float* add, float* y, hipStream_t stream, bool relu) {
+                              const float* add, float* y, hipStream_t stream, bool relu,
+                              const BnParts* parts) {
   if (c == 0) return;
+  BnParts none{};
+  const BnParts& pt = parts != nullptr ? *parts : none;
   // enough (channel, image range) workgroups to cover the chip ~4x
   int64_t splits = (1024 + c - 1) / c;
   if (splits > n) splits = n;
@@ -513,7 +560,7 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, part_mean, part_m2, blocks, width, cols,
                        static_cast<int>(n), static_cast<int>(c), static_cast<int>(s),
                        static_cast<int>(n_per), eps, momentum, mean, invstd, running_mean,
-                       running_var, tracked, acc, zero2c, z, gamma, beta, add, y);
+                       running_var, tracked, acc, zero2c, z, gamma, beta, add, y, pt);
   };
   const bool vec = (s & 3) == 0;
   if (relu) {  // (ResNet's BatchNorm -> ReLU; never with a node sum)
@@ -568,6 +615,29 @@ void launch_bn_apply(const float* z, const float* mean, const float* invstd, con
   }
 }
 
+bool bn_backward_parts_ok(int64_t n, int64_t c, int64_t s) {
+  return n * s <= 32768 && n * s * c < (int64_t{1} << 31);
+}
+
+void launch_bn_backward_parts(const BnParts& parts, const float* z, const float* mean,
+                              const float* invstd, float* dz, int64_t n, int64_t c, int64_t s,
+                              hipStream_t stream) {
+  if (n * c * s == 0) return;
+  bool vec = (s & 3) == 0;
+  for (int p = 0; p < parts.count; ++p) vec = vec && (parts.dy_img[p] & 3) == 0;
+  const float inv_m1 = 1.f / static_cast<float>(n * s);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(c)), dim3(256), 0, stream,
+                       static_cast<const float*>(nullptr), z, mean, invstd,
+                       static_cast<const float*>(nullptr), static_cast<const float*>(nullptr),
+                       dz, static_cast<float*>(nullptr), static_cast<float*>(nullptr), 0, 0,
+                       static_cast<int>(n), static_cast<int>(c), static_cast<int>(s), inv_m1,
+                       int64_t{0}, 0, parts);
+  };
+  if (vec) go(bn_bwd_channel_kernel<true>);
+  else go(bn_bwd_channel_kernel<false>);
+}
+
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
                         bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
@@ -588,7 +658,7 @@ void launch_bn_backward(const float* dy, const float* z, const float* mean, cons
       hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(c)), dim3(256), 0, stream, dy, z, mean,
                          invstd, gamma, beta, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
                          acc_beta ? 1 : 0, static_cast<int>(n), static_cast<int>(c),
-                         static_cast<int>(s), inv_m1, dy_img, relu_out ? 1 : 0);
+                         static_cast<int>(s), inv_m1, dy_img, relu_out ? 1 : 0, BnParts{});
     };
     if ((s & 3) == 0 && (dy_img & 3) == 0) go(bn_bwd_channel_kernel<true>);
     else go(bn_bwd_channel_kernel<false>);

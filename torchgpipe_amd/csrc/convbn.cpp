@@ -546,6 +546,195 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   return out;
 }
 
+// ---- grouped convolutions (AmoebaNet normal cells) ----------------------------------------
+// Several ReLU -> 1x1 Conv -> BatchNorm operations reading the same input (a normal cell's
+// node 0 feeds three) as ONE implicit-GEMM convolution over their concatenated weights
+// (`w_cat` [sum co_p][ci], cached per step by the caller), one statistics + finalize +
+// normalise pass writing each operation's own output, and in the backward one BatchNorm
+// pass, one backward-data GEMM (`w_cat_t`) and one weight-gradient GEMM per operation.
+
+BnParts make_bn_parts(at::IntArrayRef channels, const c10::List<c10::optional<at::Tensor>>& gammas,
+                      const c10::List<c10::optional<at::Tensor>>& betas, const at::Tensor& like,
+                      int64_t c_total) {
+  TORCH_CHECK(channels.size() >= 1 && static_cast<int>(channels.size()) <= kBnPartsMax,
+              "1 to ", kBnPartsMax, " grouped operations");
+  TORCH_CHECK(gammas.size() == channels.size() && betas.size() == channels.size(),
+              "one gamma / beta per grouped operation");
+  BnParts pt{};
+  pt.count = static_cast<int>(channels.size());
+  int64_t end = 0;
+  for (size_t i = 0; i < channels.size(); ++i) {
+    end += channels[i];
+    pt.c_end[i] = static_cast<int>(end);
+    pt.gamma[i] = opt_ptr(gammas.get(i), "gamma", like, channels[i]);
+    pt.beta[i] = opt_ptr(betas.get(i), "beta", like, channels[i]);
+  }
+  TORCH_CHECK(end == c_total, "grouped channel counts must add up to the weight's rows");
+  return pt;
+}
+
+std::vector<at::Tensor> convbn_group_forward(
+    const at::Tensor& x_in, const at::Tensor& w_cat, at::IntArrayRef geo, bool relu,
+    at::IntArrayRef channels, const c10::List<c10::optional<at::Tensor>>& gammas,
+    const c10::List<c10::optional<at::Tensor>>& betas,
+    const c10::List<c10::optional<at::Tensor>>& running_means,
+    const c10::List<c10::optional<at::Tensor>>& running_vars,
+    const c10::List<c10::optional<at::Tensor>>& tracked, double momentum, double eps) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Parts p = make_parts(x, {w_cat}, geo, relu);
+  const int64_t n = x.size(0), c = p.co_total, s = p.ho * p.wo;
+  const auto stream = cur_stream(x);
+  BnParts pt = make_bn_parts(channels, gammas, betas, x, c);
+  TORCH_CHECK(running_means.size() == channels.size() && running_vars.size() == channels.size() &&
+                  tracked.size() == channels.size(),
+              "one running_mean / running_var / num_batches_tracked per grouped operation");
+  std::vector<at::Tensor> out;
+  for (size_t i = 0; i < channels.size(); ++i) {
+    pt.rm[i] = const_cast<float*>(opt_ptr(running_means.get(i), "running_mean", x, channels[i]));
+    pt.rv[i] = const_cast<float*>(opt_ptr(running_vars.get(i), "running_var", x, channels[i]));
+    TORCH_CHECK((pt.rm[i] == nullptr) == (pt.rv[i] == nullptr),
+                "running_mean and running_var go together");
+    const c10::optional<at::Tensor> t = tracked.get(i);
+    if (t.has_value() && t->defined()) {
+      TORCH_CHECK(t->device() == x.device() && t->scalar_type() == at::kLong && t->numel() == 1,
+                  "num_batches_tracked must be a 1-element int64 tensor on the input's device");
+      pt.tracked[i] = t->data_ptr<int64_t>();
+    }
+    out.push_back(at::empty({n, channels[i], p.ho, p.wo}, x.options()));
+    pt.y[i] = out.back().data_ptr<float>();
+  }
+  auto z = at::empty({n, c, p.ho, p.wo}, x.options());
+  const ConvGemmPlan plan =
+      tuned_plan(0, w_cat.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
+                 nullptr, nullptr, p.geo[0], false, w_cat.numel() * 4, x.numel() * 4, x,
+                 z.numel());
+  const bool split = plan.splits > 1;
+  const int width = split ? static_cast<int>(s) : plan.col_width;
+  const int blocks = split ? static_cast<int>(n) : plan.col_blocks;
+  auto part = at::empty({2, blocks, c}, x.options());
+  run_gemm(0, w_cat.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
+           part[0].data_ptr<float>(), part[1].data_ptr<float>(), p.geo[0], plan, false,
+           w_cat.numel() * 4, x.numel() * 4, x);
+  auto mean = at::empty({c}, x.options());
+  auto invstd = at::empty({c}, x.options());
+  launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, n,
+                           c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
+                           invstd.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr,
+                           z.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, stream, false,
+                           &pt);
+  out.push_back(z);
+  out.push_back(mean);
+  out.push_back(invstd);
+  return out;
+}
+
+bool convbn_group_backward_ok(int64_t n, int64_t c, int64_t hw) {
+  return bn_backward_parts_ok(n, c, hw);
+}
+
+// Returns {dx (undefined unless need_dx), dgamma_0, dbeta_0, ..., dw_0, ...}; `accum` holds
+// per operation {dgamma, dbeta, dw} (.grad to accumulate into, or none), `slabs` /
+// `slab_first` one entry per weight (ops/gradacc.py deferred weight gradients).
+std::vector<at::Tensor> convbn_group_backward(
+    const c10::List<c10::optional<at::Tensor>>& dys, const at::Tensor& x_in, const at::Tensor& z,
+    const at::Tensor& mean, const at::Tensor& invstd, at::TensorList weights,
+    const at::Tensor& w_cat_t, at::IntArrayRef geo, bool relu, bool need_dx,
+    at::IntArrayRef channels, const c10::List<c10::optional<at::Tensor>>& gammas,
+    const c10::List<c10::optional<at::Tensor>>& accum,
+    const c10::List<c10::optional<at::Tensor>>& slabs, at::IntArrayRef slab_first) {
+  auto x = x_in.contiguous();
+  check_f32(x, "x", x);
+  check_f32(z, "z", x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t n = x.size(0), c = z.size(1), s = z.size(2) * z.size(3);
+  TORCH_CHECK(bn_backward_parts_ok(n, c, s), "grouped backward: channels too large");
+  const size_t np = channels.size();
+  TORCH_CHECK(weights.size() == np && dys.size() == np, "one weight and dy per operation");
+  TORCH_CHECK(accum.size() == 3 * np, "accum must hold {dgamma, dbeta, dw} per operation");
+  c10::List<c10::optional<at::Tensor>> no_beta;
+  for (size_t i = 0; i < np; ++i) no_beta.push_back(c10::nullopt);
+  BnParts pt = make_bn_parts(channels, gammas, no_beta, x, c);
+  std::vector<at::Tensor> keep;  // contiguous dys, parameter gradients
+  std::vector<at::Tensor> dgb;
+  for (size_t i = 0; i < np; ++i) {
+    const c10::optional<at::Tensor> d = dys.get(i);
+    if (d.has_value() && d->defined()) {
+      int64_t img = image_stride_if_channel_slice(*d);
+      at::Tensor dd = img > 0 ? *d : d->contiguous();
+      if (img == 0) {
+        check_f32(dd, "dy", x);
+        img = channels[i] * s;
+      }
+      TORCH_CHECK(dd.dim() == 4 && dd.size(0) == n && dd.size(1) == channels[i] &&
+                      dd.size(2) * dd.size(3) == s,
+                  "dy of a grouped operation has the wrong shape");
+      keep.push_back(dd);
+      pt.dy[i] = dd.data_ptr<float>();
+      pt.dy_img[i] = img;
+    }
+    for (int k = 0; k < 2; ++k) {
+      const c10::optional<at::Tensor> a = accum.get(3 * i + k);
+      at::Tensor g;
+      if (a.has_value() && a->defined()) {
+        check_f32(*a, "accumulated gradient", x);
+        TORCH_CHECK(a->numel() == channels[i], "accumulated BatchNorm gradient size");
+        g = *a;
+        (k == 0 ? pt.acc_gamma : pt.acc_beta)[i] = 1;
+      } else {
+        g = at::empty({channels[i]}, x.options());
+      }
+      (k == 0 ? pt.dgamma : pt.dbeta)[i] = g.data_ptr<float>();
+      dgb.push_back(g);
+    }
+  }
+  auto dz = at::empty_like(z);
+  launch_bn_backward_parts(pt, z.data_ptr<float>(), mean.data_ptr<float>(),
+                           invstd.data_ptr<float>(), dz.data_ptr<float>(), n, c, s, cur_stream(x));
+  std::vector<at::Tensor> out;
+  Parts pc = make_parts(x, {weights[0]}, geo, relu);  // input geometry of the 1x1 convolutions
+  at::Tensor dx;
+  if (need_dx) {
+    check_f32(w_cat_t, "w_cat_t", x);
+    TORCH_CHECK(w_cat_t.size(0) == x.size(1) && w_cat_t.numel() == c * x.size(1),
+                "w_cat_t must be the concatenated weights transposed to [ci][sum co]");
+    ConvGemmGeo g = pc.geo[0];
+    g.co = static_cast<int>(c);
+    g.co_total = static_cast<int>(c);
+    g.co_off = 0;
+    g.a_t = true;
+    const bool zero = conv_gemm_plan(1, g).scatter;
+    dx = zero ? at::zeros_like(x) : at::empty_like(x);
+    const ConvGemmPlan plan =
+        tuned_plan(1, w_cat_t.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+                   dx.data_ptr<float>(), nullptr, nullptr, g, zero, w_cat_t.numel() * 4,
+                   dz.numel() * 4, x, x.numel());
+    run_gemm(1, w_cat_t.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+             dx.data_ptr<float>(), nullptr, nullptr, g, plan, zero, w_cat_t.numel() * 4,
+             dz.numel() * 4, x);
+  }
+  out.push_back(dx);
+  for (auto& g : dgb) out.push_back(g);
+  int64_t off = 0;
+  for (size_t i = 0; i < np; ++i) {
+    check_f32(weights[i], "weight", x);
+    TORCH_CHECK(weights[i].size(0) == channels[i] && weights[i].size(1) == x.size(1) &&
+                    weights[i].numel() == channels[i] * x.size(1),
+                "grouped operations must be 1x1 convolutions of the input");
+    ConvGemmGeo g = pc.geo[0];
+    g.co = static_cast<int>(channels[i]);
+    g.co_total = static_cast<int>(c);
+    g.co_off = static_cast<int>(off);
+    off += channels[i];
+    const c10::optional<at::Tensor> a = accum.get(3 * i + 2);
+    out.push_back(wgrad_part(dz, x, weights[i], g,
+                             a.has_value() && a->defined() ? *a : at::Tensor(), slab_of(slabs, i),
+                             first_of(slab_first, i)));
+  }
+  return out;
+}
+
 // Weight gradients of a fused op from its BatchNorm-backward output dz (convbn_backward
 // with defer_wgrad), on the current stream: dW_i (+)= dz[:, part i] x relu(X) taps.
 std::vector<at::Tensor> convbn_wgrad(const at::Tensor& dz, const at::Tensor& x_in,
@@ -956,6 +1145,14 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
         "Tensor(a!) sums, Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx, "
         "Tensor?[] accum, Tensor[] weights_t, bool defer_wgrad, Tensor?[] slabs, "
         "int[] slab_first, Tensor? beta=None, bool relu_out=False) -> Tensor[]");
+  m.def("convbn_group_forward(Tensor x, Tensor w_cat, int[] geo, bool relu, int[] channels, "
+        "Tensor?[] gammas, Tensor?[] betas, Tensor?[] running_means, Tensor?[] running_vars, "
+        "Tensor?[] tracked, float momentum, float eps) -> Tensor[]");
+  m.def("convbn_group_backward(Tensor?[] dys, Tensor x, Tensor z, Tensor mean, Tensor invstd, "
+        "Tensor[] weights, Tensor w_cat_t, int[] geo, bool relu, bool need_dx, int[] channels, "
+        "Tensor?[] gammas, Tensor?[] accum, Tensor?[] slabs, int[] slab_first) -> Tensor[]");
+  m.def("convbn_group_backward_ok(int n, int c, int hw) -> bool",
+        &tgpipe::convbn_group_backward_ok);
   m.def("convbn_wgrad(Tensor dz, Tensor x, Tensor[] weights, int[] geo, bool relu, "
         "Tensor?[] accum, Tensor?[] slabs, int[] slab_first) -> Tensor[]");
   m.def("wgrad_slab_flush(Tensor[] slabs, Tensor(a!)[] grads, int[] accumulate) -> ()");
@@ -974,6 +1171,8 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("convbn_forward", &tgpipe::convbn_forward);
   m.impl("convbn_backward", &tgpipe::convbn_backward);
   m.impl("convbn_wgrad", &tgpipe::convbn_wgrad);
+  m.impl("convbn_group_forward", &tgpipe::convbn_group_forward);
+  m.impl("convbn_group_backward", &tgpipe::convbn_group_backward);
   m.impl("wgrad_slab_flush", &tgpipe::wgrad_slab_flush);
   m.impl("conv_gemm_forward", &tgpipe::conv_gemm_forward);
   m.impl("conv_gemm_sweep", &tgpipe::conv_gemm_sweep);

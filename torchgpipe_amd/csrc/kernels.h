@@ -224,12 +224,40 @@ void launch_bn_apply(const float* z, const float* mean, const float* invstd, con
 // dz = gamma*invstd*(dy - sum_dy/M - (z-mean)*invstd^2*sum_dyz/M), dgamma, dbeta.
 // BatchNorm finalize (as launch_bn_finalize) fused with the normalising pass (as
 // launch_bn_apply): one launch of (channel, image range) workgroups.
+// A grouped convolution (one GEMM over the concatenated weights of several convolutions
+// reading the same input) feeding one BatchNorm per convolution: part p covers channels
+// [c_end[p-1], c_end[p]) of z / mean / invstd and has its own parameters, running
+// statistics and output y_p [n][c_p][s] (forward) / gradient dy_p (image stride dy_img[p];
+// null = no gradient) and parameter gradients (backward).  count = 0: not grouped.
+constexpr int kBnPartsMax = 3;
+struct BnParts {
+  int count;
+  int c_end[kBnPartsMax];
+  const float* gamma[kBnPartsMax];
+  const float* beta[kBnPartsMax];
+  float* rm[kBnPartsMax];
+  float* rv[kBnPartsMax];
+  int64_t* tracked[kBnPartsMax];
+  float* y[kBnPartsMax];
+  const float* dy[kBnPartsMax];
+  int64_t dy_img[kBnPartsMax];
+  float* dgamma[kBnPartsMax];
+  float* dbeta[kBnPartsMax];
+  int acc_gamma[kBnPartsMax];
+  int acc_beta[kBnPartsMax];
+};
 void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int blocks,
                               int width, int64_t n, int64_t c, int64_t s, float eps,
                               double momentum, float* mean, float* invstd, float* running_mean,
                               float* running_var, int64_t* tracked, double* acc, float* zero2c,
                               const float* z, const float* gamma, const float* beta,
-                              const float* add, float* y, hipStream_t stream, bool relu = false);
+                              const float* add, float* y, hipStream_t stream, bool relu = false,
+                              const BnParts* parts = nullptr);
+// Backward of a grouped BatchNorm (one workgroup per channel, both passes): dz [n][c][s].
+bool bn_backward_parts_ok(int64_t n, int64_t c, int64_t s);
+void launch_bn_backward_parts(const BnParts& parts, const float* z, const float* mean,
+                              const float* invstd, float* dz, int64_t n, int64_t c, int64_t s,
+                              hipStream_t stream);
 // relu_out: the forward applied a ReLU after the normalisation (launch_bn_finalize_apply's
 // `relu`); dy is that ReLU's output gradient and its mask is re-derived from z (needs beta).
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,

@@ -32,7 +32,8 @@ from torchgpipe_amd.ops import _ext, gradacc
 from torchgpipe_amd.ops.conv import _TransformCache
 
 __all__ = ['relu_conv_bn', 'ReLUConvBN', 'FusedChain', 'conv_supported', 'fused_triplets',
-           'fusable', 'disabled', 'GemmConv2d', 'gemm_conv2d', 'gemm_conv_eligible']
+           'fusable', 'disabled', 'GemmConv2d', 'gemm_conv2d', 'gemm_conv_eligible',
+           'group_relu_conv_bn', 'groupable']
 
 # TGPIPE_FUSED_CONVBN=0 runs the eager ReLU / Conv2d / BatchNorm2d modules instead.
 _ENABLED = os.environ.get('TGPIPE_FUSED_CONVBN', '1') != '0'
@@ -249,13 +250,19 @@ class FusedChain(nn.Sequential):
     triplet's normalisation pass.
     """
 
-    def forward(self, x: Tensor, add: Optional[Tensor] = None) -> Tensor:  # type: ignore[override]
+    def forward(self, x: Tensor, add: Optional[Tensor] = None,  # type: ignore[override]
+                start: int = 0) -> Tensor:
+        """The chain from triplet ``start`` on (``start`` > 0: ``x`` is the output of
+        triplet ``start - 1``, e.g. computed by :func:`group_relu_conv_bn`)."""
         triplets = fused_triplets(self)
         if triplets is None:
+            assert start == 0, 'start > 0 needs a chain of (ReLU, Conv2d, BatchNorm2d) triplets'
             out = super().forward(x)
             return out if add is None else out + add
         last = len(triplets) - 1
         for k, (relu, conv, bn) in enumerate(triplets):
+            if k < start:
+                continue
             extra = add if k == last else None
             if fusable(x, [conv], bn):
                 x = relu_conv_bn(x, [(conv, 0)], bn, relu=relu, add=extra)
@@ -268,6 +275,134 @@ class FusedChain(nn.Sequential):
 
 class ReLUConvBN(FusedChain):
     """``nn.Sequential(ReLU, Conv2d, BatchNorm2d)`` running as one fused op."""
+
+
+# -- grouped ReLU-Conv-BN operations reading one input ------------------------------------
+
+# TGPIPE_GROUP_CONVBN=0 runs grouped operations one by one.
+_GROUP_ENABLED = os.environ.get('TGPIPE_GROUP_CONVBN', '1') != '0'
+
+
+class _GroupCache:
+    """The concatenated weights of a group (and their transpose) for one pipeline step:
+    keyed like the Winograd transforms (storage, version, step of every weight)."""
+
+    __slots__ = ('key', 'cat', 'cat_t', '__weakref__')
+
+    def __init__(self) -> None:
+        self.key: Optional[Tuple] = None
+        self.cat: Optional[Tensor] = None
+        self.cat_t: Optional[Tensor] = None
+
+    def get(self, weights: Sequence[Tensor]) -> Tuple[Tensor, Tensor]:
+        from torchgpipe_amd.ops import conv as _conv
+        key = tuple((w.data_ptr(), w._version) for w in weights) + (_conv._STEP,)
+        if key != self.key or self.cat is None or self.cat_t is None:
+            with torch.no_grad():
+                cat = torch.cat([w.detach().reshape(w.shape[0], -1) for w in weights])
+                self.cat = cat.view(cat.shape[0], cat.shape[1], 1, 1)
+                self.cat_t = cat.t().contiguous().view(cat.shape[1], cat.shape[0], 1, 1)
+            self.key = key
+        return self.cat, self.cat_t
+
+
+class _GroupConvBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: Tensor, bns: List[nn.BatchNorm2d], cache: _GroupCache,  # type: ignore[override]
+                n_ops: int, *params: Tensor) -> Tuple[Tensor, ...]:
+        weights = list(params[:n_ops])
+        gammas, betas = list(params[n_ops:2 * n_ops]), list(params[2 * n_ops:])
+        w_cat, _ = cache.get(weights)
+        channels = [w.shape[0] for w in weights]
+        track = [bn.track_running_stats and bn.running_mean is not None for bn in bns]
+        outs = _ext.require(x).convbn_group_forward(
+            x, w_cat, [1, 1, 1, 1, 0, 0, 0, 0], True, channels, gammas, betas,
+            [bn.running_mean if t else None for bn, t in zip(bns, track)],
+            [bn.running_var if t else None for bn, t in zip(bns, track)],
+            [bn.num_batches_tracked if t else None for bn, t in zip(bns, track)],
+            float(bns[0].momentum), float(bns[0].eps))
+        ys, (z, mean, invstd) = outs[:n_ops], outs[n_ops:]
+        ctx.save_for_backward(x, z, mean, invstd, *weights, *gammas)
+        ctx.params = tuple(params)
+        ctx.cache = cache
+        ctx.channels = channels
+        ctx.n_ops = n_ops
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys: Tensor):  # type: ignore[override]
+        x, z, mean, invstd, *rest = ctx.saved_tensors
+        n = ctx.n_ops
+        weights, gammas = rest[:n], rest[n:]
+        params = ctx.params
+        # gradient-accumulation fusion per parameter (order: weights, gammas, betas)
+        fused = [gradacc.target(p) for p in params]
+        accum: List[Optional[Tensor]] = []
+        for i in range(n):
+            accum += [fused[n + i][1], fused[2 * n + i][1], fused[i][1]]
+        slabs: List[Optional[Tensor]] = []
+        firsts: List[int] = []
+        for i in range(n):
+            sb, first = gradacc.slab(params[i]) if fused[i][0] else (None, False)
+            slabs.append(sb)
+            firsts.append(int(first))
+        if all(sb is None for sb in slabs):
+            slabs, firsts = [], []
+        need_dx = ctx.needs_input_grad[0]
+        _, w_cat_t = ctx.cache.get(weights)
+        out = _ext.require(x).convbn_group_backward(
+            list(dys), x, z, mean, invstd, list(weights), w_cat_t, [1, 1, 1, 1, 0, 0, 0, 0],
+            True, need_dx, ctx.channels, list(gammas), accum, slabs, firsts)
+        dx = out[0]
+        dgb, dws = out[1:1 + 2 * n], out[1 + 2 * n:]
+        grads: List[Optional[Tensor]] = [None] * (3 * n)
+        for i in range(n):
+            grads[i] = dws[i]
+            grads[n + i] = dgb[2 * i]
+            grads[2 * n + i] = dgb[2 * i + 1]
+        for k, ((fuse, into), p) in enumerate(zip(fused, params)):
+            if fuse:  # written into p.grad (or its slab) by the kernels
+                if k < n and slabs and gradacc.deferred(p, slabs[k], grads[k]):
+                    pass
+                elif into is None:
+                    gradacc.commit(p, grads[k])  # type: ignore[arg-type]
+                grads[k] = None
+        del ctx.params, ctx.cache
+        return (dx if need_dx else None, None, None, None, *grads)
+
+
+def groupable(x: Tensor, triplets: Sequence[Tuple[bool, nn.Conv2d, nn.BatchNorm2d]]) -> bool:
+    """Whether :func:`group_relu_conv_bn` takes these (relu, conv, bn) triplets: ReLU ->
+    plain 1x1 convolutions of ``x`` -> BatchNorms with one momentum / eps, the grouped
+    BatchNorm backward's channel size limit, and the fused-op conditions."""
+    if not _GROUP_ENABLED or not 2 <= len(triplets) <= 3 or x.dim() != 4:
+        return False
+    bn0 = triplets[0][2]
+    for relu, conv, bn in triplets:
+        if not relu or tuple(conv.kernel_size) != (1, 1) or tuple(conv.stride) != (1, 1) or \
+                tuple(conv.padding) != (0, 0) or not fusable(x, [conv], bn) or \
+                bn.momentum != bn0.momentum or bn.eps != bn0.eps or \
+                (bn.weight is None) != (bn0.weight is None) or \
+                not bn.track_running_stats or bn.running_mean is None:
+            return False
+    if bn0.weight is None:
+        return False
+    co = sum(conv.out_channels for _, conv, _ in triplets)
+    hw = x.shape[2] * x.shape[3]
+    return bool(_ext.require(x).convbn_group_backward_ok(x.shape[0], co, hw)) and \
+        x.numel() // max(1, x.shape[1]) * co * 4 < (1 << 31) - 64
+
+
+def group_relu_conv_bn(x: Tensor, triplets: Sequence[Tuple[bool, nn.Conv2d, nn.BatchNorm2d]],
+                       cache: '_GroupCache') -> Tuple[Tensor, ...]:
+    """``[bn_i(conv_i(relu(x))) for each triplet]`` as one grouped op: one implicit-GEMM
+    launch over the concatenated weights, one statistics / normalise pass writing each
+    output, and one BatchNorm backward + one backward-data GEMM in the backward (callers
+    check :func:`groupable` first)."""
+    convs = [conv for _, conv, _ in triplets]
+    bns = [bn for _, _, bn in triplets]
+    params = ([c.weight for c in convs] + [b.weight for b in bns] + [b.bias for b in bns])
+    return _GroupConvBN.apply(x, bns, cache, len(convs), *params)
 
 
 # -- plain convolutions on the same implicit-GEMM kernels --------------------------------
