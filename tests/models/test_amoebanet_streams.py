@@ -31,3 +31,30 @@ def test_set_cell_streams_toggles_every_cell_and_cpu_runs_one_stream():
     assert torch.equal(model(x), ref)  # CPU tensors: the one-stream path
     set_cell_streams(model, False)
     assert not any(m.streams for m in model.modules() if isinstance(m, Cell))
+
+
+def test_shared_pools_compute_the_unshared_function():
+    """A cell's duplicate 3x3 average pools of one node run once (Cell._shared_plan): same
+    outputs and gradients as computing both (CPU)."""
+    import copy
+    import torch
+    from torchgpipe_amd.models import amoebanetd
+    from torchgpipe_amd.models.amoebanet import Cell
+    torch.manual_seed(0)
+    a = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
+    b = copy.deepcopy(a)
+    plans = [m._shared for m in a.modules() if isinstance(m, Cell)]
+    assert all(len(p) == 2 for p in plans)
+    for m in b.modules():
+        if isinstance(m, Cell):
+            m._shared = []
+    x = torch.randn(2, 3, 224, 224)
+    ya, yb = a(x), b(x)
+    torch.testing.assert_close(ya, yb, rtol=0, atol=0)
+    ya.square().sum().backward()
+    yb.square().sum().backward()
+    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        # (the shared pool's two gradients are summed before its backward instead of after:
+        # fp32 reassociation only)
+        rel = ((pa.grad - pb.grad).norm() / pb.grad.norm()).item()
+        assert rel < 1e-5, (name, rel)

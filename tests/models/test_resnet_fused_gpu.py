@@ -50,28 +50,27 @@ def test_conv_bn_relu_run_matches_fp64(case, relu):
         seq[1].bias.uniform_(-0.5, 0.5)
     assert relink(seq) == 1
     ref = nn.Sequential(nn.Conv2d(ci, co, k, stride=stride, padding=pad, bias=False),
-                        nn.BatchNorm2d(co), *([nn.ReLU()] if relu else [])).cuda().double()
-    ref.load_state_dict(seq.state_dict())
-    # the plain fp32 layers (MIOpen) set the bar: BatchNorm's backward makes dz zero-mean per
-    # channel, and the convolution's backward-data sums its per-channel rounding coherently
-    # over Ci x taps, so x.grad's relative error vs fp64 is ill-conditioned (grows with the
-    # channel count) for any fp32 implementation
-    plain = copy.deepcopy(ref).float()
+                        nn.BatchNorm2d(co)).cuda().double()
+    ref.load_state_dict(seq.state_dict(), strict=False)
     x = torch.randn(n, ci, hw, hw, device='cuda', requires_grad=True)
     x64 = x.detach().double().requires_grad_(True)
-    x32 = x.detach().clone().requires_grad_(True)
     y = seq(x)
-    y64 = ref(x64)
-    y32 = plain(x32)
     assert getattr(y, '_tgpipe_bn_done', None) == id(seq[1]), 'the fused path must run'
+    y64 = ref(x64)
+    if relu:
+        # The ReLU in fp64 with the fused forward's own decisions: a value within rounding
+        # of zero may fall on the other side in fp64, and each such flip moves a whole
+        # gradient element (benchmarks/diag/resnet_fused_diag2.py: 2.9e-6 on the
+        # convolution output becomes 6.8e-3 on dz through a handful of flips -- for any
+        # fp32 implementation, MIOpen's included).
+        y64 = y64 * (y > 0).double()
     assert rel_err(y, y64) < 1e-5
     g = torch.randn_like(y)
     y.backward(g)
     y64.backward(g.double())
-    y32.backward(g)
-    assert rel_err(x.grad, x64.grad) < max(1e-5, 4 * rel_err(x32.grad, x64.grad))
-    for (name, p), q, r in zip(seq.named_parameters(), ref.parameters(), plain.parameters()):
-        assert rel_err(p.grad, q.grad) < max(2e-5, 4 * rel_err(r.grad, q.grad)), name
+    assert rel_err(x.grad, x64.grad) < 2e-5
+    for (name, p), q in zip(seq.named_parameters(), ref.parameters()):
+        assert rel_err(p.grad, q.grad) < 2e-5, name
     # (the batch mean of a ~zero-mean output is ill-conditioned: the Winograd output's
     # ~1e-6 relative error shows up a few times larger in it)
     assert rel_err(seq[1].running_mean, ref[1].running_mean) < 2e-5
@@ -117,7 +116,7 @@ def test_fused_resnet50_matches_plain_model():
     t = torch.randint(10, (16,), device='cuda')
     res = []
     for model, dt in ((fused, torch.float32), (plain, torch.float32), (ref, torch.float64)):
-        xi = x.to(dt).requires_grad_(True)
+        xi = x.clone().to(dt).requires_grad_(True)
         loss = nn.functional.cross_entropy(model(xi), t)
         loss.backward()
         res.append((loss.detach(), xi.grad, [p.grad for p in model.parameters()],
@@ -127,6 +126,7 @@ def test_fused_resnet50_matches_plain_model():
     assert rel_err(xf, x64) < max(1e-4, 4 * rel_err(xp, x64))
     names = [n for n, _ in fused.named_parameters()]
     for name, a, b, r in zip(names, gf, gp, g64):
+        assert a is not None and b is not None and r is not None, name
         assert rel_err(a, r) < max(1e-4, 4 * rel_err(b, r)), name
     for a, b, r in zip(bf, bp, b64):
         assert rel_err(a, r) < max(1e-5, 4 * rel_err(b, r))

@@ -37,6 +37,8 @@ __all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS', 'set_cell_
 
 _SIDE_STREAMS: Dict[Tuple[torch.device, int], torch.cuda.Stream] = {}
 _CAPTURE_STREAMS = os.environ.get('TGPIPE_CAPTURE_STREAMS', '1') != '0'
+# TGPIPE_SHARE_POOLS=0 computes a cell's duplicate average pools twice (Cell._shared_plan)
+_SHARE_POOLS = os.environ.get('TGPIPE_SHARE_POOLS', '1') != '0'
 
 
 def _side_stream(device: torch.device, main: torch.cuda.Stream) -> torch.cuda.Stream:
@@ -261,6 +263,7 @@ class Cell(nn.Module):
         self._plan = self._stream_plan()
         self._group = self._group_plan()
         self._group_cache = _GroupCache()
+        self._shared = self._shared_plan()
 
     def _stream_plan(self) -> List[int]:
         """Stream (0 = current, 1 = side) of every node for the two-stream schedule.
@@ -299,6 +302,26 @@ class Cell(nn.Module):
             return -1, []
         return best[0], best[1][:3]
 
+    def _shared_plan(self) -> List[int]:
+        """Operations that compute the same function of the same node (the genotypes apply a
+        3x3 stride-1 average pool to one node twice: the reference's ``max_pool_3x3`` is an
+        average pool, ``operations.py:57-59``); the first of them is run once and its output
+        reused, its partners folding it in as their node sum."""
+        if not _SHARE_POOLS:
+            return []
+        seen: Dict[Tuple[int, int], List[int]] = {}
+        for k, op in enumerate(self.operations):
+            m = op.module
+            if type(m) is AvgPool3x3:
+                stride = m.stride if isinstance(m.stride, int) else m.stride[0]
+                seen.setdefault((self.indices[k], stride), []).append(k)
+        for ks in seen.values():
+            # each must pair with an operation that folds a sum (its node's other half)
+            if len(ks) >= 2 and all(self.operations[k ^ 1].takes_add and k ^ 1 not in ks
+                                    for k in ks):
+                return ks
+        return []
+
     def _grouped(self, nodes: List[Tensor]) -> Dict[int, Tensor]:
         """First-triplet outputs of the grouped operations (empty when not applicable)."""
         node, ops = self._group
@@ -314,12 +337,22 @@ class Cell(nn.Module):
     def extra_repr(self) -> str:
         return f'indices: {self.indices}'
 
-    def _node(self, k: int, nodes: List[Tensor], pre: Optional[Dict[int, Tensor]] = None
-              ) -> Tensor:
+    def _node(self, k: int, nodes: List[Tensor], pre: Optional[Dict[int, Tensor]] = None,
+              shared: Optional[Dict[int, Tensor]] = None) -> Tensor:
         # node = left + right: run the operation that cannot fold a sum first and hand
-        # its output to the other one's last pass
+        # its output to the other one's last pass (a shared operation's output, computed
+        # once per cell, is always the one handed over)
         ops = self.operations
         pre = pre or {}
+        if k in self._shared or k + 1 in self._shared:
+            a = k if k in self._shared else k + 1
+            b = a ^ 1
+            assert shared is not None
+            if a not in shared:
+                out = ops[a](nodes[self.indices[a]])
+                for j in self._shared:
+                    shared[j] = out
+            return ops[b](nodes[self.indices[b]], add=shared[a], first=pre.get(b))
         a, b = (k, k + 1) if ops[k + 1].takes_add or not ops[k].takes_add else (k + 1, k)
         first = ops[a](nodes[self.indices[a]], first=pre.get(a))
         return ops[b](nodes[self.indices[b]], add=first, first=pre.get(b))
@@ -337,8 +370,9 @@ class Cell(nn.Module):
             return self._forward_two_streams(s1, s2), skip
         nodes = [self.reduce1(s1), self.reduce2(s2)]
         pre = self._grouped(nodes)
+        shared: Dict[int, Tensor] = {}
         for k in range(0, len(self.operations), 2):
-            nodes.append(self._node(k, nodes, pre))
+            nodes.append(self._node(k, nodes, pre, shared))
         return torch.cat([nodes[i] for i in self.concat], dim=1), skip
 
     def _forward_two_streams(self, s1: Tensor, s2: Tensor) -> Tensor:
@@ -387,17 +421,25 @@ class Cell(nn.Module):
         run(1, lambda: self.reduce2(s2), [], [s2])
         # the grouped first triplets run with the first node that needs them; a later node
         # on the other stream waits for that node's event and records its group inputs
+        # (and a shared operation's output: computed with the first node that needs it)
         pre: Dict[int, Tensor] = {}
-        group_node = -1
+        shared: Dict[int, Tensor] = {}
+        group_node = shared_node = -1
         for k in range(0, len(self.operations), 2):
             ins = [self.indices[k], self.indices[k + 1]]
             mine = [o for o in (k, k + 1) if o in self._group[1]]
+            share = [o for o in (k, k + 1) if o in self._shared]
+            if share and shared_node >= 0 and self._plan[len(nodes)] != self._plan[shared_node]:
+                ins.append(shared_node)
+                shared[share[0]].record_stream(streams[self._plan[len(nodes)]])
+            elif share and shared_node < 0:
+                shared_node = len(nodes)
             if mine and group_node < 0:
                 group_node = len(nodes)
 
                 def fn(k: int = k) -> Tensor:
                     pre.update(self._grouped(nodes))
-                    return self._node(k, nodes, pre)
+                    return self._node(k, nodes, pre, shared)
                 run(len(nodes), fn, ins, [])
                 continue
             if mine and pre and self._plan[len(nodes)] != self._plan[group_node]:
@@ -405,7 +447,7 @@ class Cell(nn.Module):
                 stream = streams[self._plan[len(nodes)]]
                 for o in mine:
                     pre[o].record_stream(stream)
-            run(len(nodes), lambda k=k: self._node(k, nodes, pre), ins, [])
+            run(len(nodes), lambda k=k: self._node(k, nodes, pre, shared), ins, [])
         streams[0].wait_stream(streams[1])
         for i in self.concat:
             if self._plan[i] == 1:
