@@ -26,11 +26,11 @@ def rel_err(a, b):
 # (n, ci, hw, co, kernel, stride, padding)
 CASES = [
     (4, 64, 28, 96, 1, 1, 0),     # 1x1: implicit GEMM, statistics in the epilogue
-    (4, 64, 28, 128, 1, 2, 0),    # strided 1x1 (downsample)
+    (4, 64, 28, 128, 1, 2, 0),    # strided 1x1 (downsample): MIOpen + native BN
     (4, 64, 28, 64, 3, 1, 1),     # 3x3 stride 1: Winograd F(4x4) + native BN(+ReLU)
     (4, 256, 14, 256, 3, 1, 1),   # 3x3 stride 1, >= 256 channels: batched-GEMM Winograd
-    (4, 32, 28, 32, 3, 2, 1),     # 3x3 stride 2: implicit GEMM
-    (2, 3, 64, 64, 7, 2, 3),      # the stem's 7x7 stride 2
+    (4, 32, 28, 32, 3, 2, 1),     # 3x3 stride 2: MIOpen + native BN(+ReLU)
+    (2, 3, 64, 64, 7, 2, 3),      # the stem 7x7 stride 2: MIOpen + native BN(+ReLU)
     (4, 512, 7, 512, 1, 1, 0),    # 7x7 planes: split reduction, fused split statistics
 ]
 

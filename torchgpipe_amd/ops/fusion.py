@@ -10,12 +10,17 @@ one native op needs the layers to cooperate:
   :class:`BatchNormAct2d` right after it (and a :class:`ReLU` after that), its forward
   runs the convolution, the BatchNorm and the ReLU:
 
-  - 1x1 / strided / 7x7 convolutions: the implicit-GEMM MFMA kernel with the BatchNorm
+  - 1x1 stride-1 convolutions: the implicit-GEMM MFMA kernel with the BatchNorm
     statistics in its epilogue, one finalize + normalise (+ ReLU) pass
     (``ops.convbn.relu_conv_bn`` with ``relu_out``); the backward re-derives the ReLU
     mask from the saved convolution output;
   - 3x3 stride-1 convolutions: the Winograd F(4x4) / batched-GEMM kernels
     (``ops.conv``), then the native BatchNorm(+ReLU) pass (:func:`bn_act`);
+  - strided convolutions (the 7x7 stem, the stride-2 3x3 and 1x1 of each stage's first
+    block): MIOpen, then :func:`bn_act` -- the implicit-GEMM kernel's strided backward-data
+    walks every input pixel (stride holes included) and measured 6 ms per call at
+    ResNet-101's shapes (B 110), several times MIOpen's
+    (``benchmarks/diag/resnet_kernel_table.py``, ``profiles/r3/resnet_kernel_tables.md``);
 
   and marks its output as normalised (and rectified) by that BatchNorm;
 * :class:`BatchNormAct2d` passes a marked input through; otherwise it runs the native
@@ -91,26 +96,34 @@ def _mark(y: Tensor, bn: nn.Module, relu: bool) -> Tensor:
     return y
 
 
+def _pointwise(conv: nn.Conv2d) -> bool:
+    return (tuple(conv.kernel_size) == (1, 1) and tuple(conv.stride) == (1, 1)
+            and tuple(conv.padding) == (0, 0))  # type: ignore[arg-type]
+
+
 class ConvBN2d(WinogradConv2d):
     """``nn.Conv2d`` (same parameters) that runs its linked BatchNorm (and ReLU) with it."""
 
     def forward(self, input: Tensor) -> Tensor:
         link = self.__dict__.get(_LINK)
+        wino = self.padding_mode == 'zeros' and wino_eligible(
+            input, self.weight, self.stride, self.padding, self.dilation, self.groups)
         if link is not None and self.padding_mode == 'zeros':
             bn, relu = link
             if self.bias is None and _native_bn_ok(bn, input):
-                if wino_eligible(input, self.weight, self.stride, self.padding, self.dilation,
-                                 self.groups) and self.bias is None:
+                if wino:
                     z = WinogradConv2d.forward(self, input)
                     return _mark(bn_act(z, bn, relu), bn, relu)
-                if fusable(input, [self], bn):
+                if _pointwise(self) and fusable(input, [self], bn):
                     y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu)
                     return _mark(y, bn, relu)
-        if self.padding_mode == 'zeros' and not wino_eligible(
-                input, self.weight, self.stride, self.padding, self.dilation, self.groups) \
-                and gemm_conv_eligible(input, self):
+                z = nn.Conv2d.forward(self, input)  # strided: MIOpen
+                return _mark(bn_act(z, bn, relu), bn, relu)
+        if wino:
+            return WinogradConv2d.forward(self, input)
+        if _pointwise(self) and gemm_conv_eligible(input, self):
             return gemm_conv2d(input, self)
-        return WinogradConv2d.forward(self, input)
+        return nn.Conv2d.forward(self, input)
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
