@@ -128,8 +128,8 @@ def parse() -> argparse.Namespace:
                         'hipGraph after the warm-up and replay it (RNG-free models only: '
                         'AmoebaNet; parallel/graph.py; auto: on for one-GPU AmoebaNet)')
     p.add_argument('--cell-streams', choices=['auto', 'on', 'off'], default='auto',
-                   help="AmoebaNet: run each cell's independent nodes on two HIP streams "
-                        '(auto: on)')
+                   help="AmoebaNet: run each cell's independent nodes on several HIP streams "
+                        '(TGPIPE_CELL_STREAMS, default 3; auto: on)')
     p.add_argument('--overlap-recompute', choices=['auto', 'on', 'off'], default='auto',
                    help="recompute the next micro-batch on a second stream during this one's "
                         'backward (PipelineStage(overlap_recompute=True); auto: on for '
@@ -291,8 +291,9 @@ class Bench:
         if args.channels_last and not unet:
             stage.partition.to(memory_format=torch.channels_last)
         if cell_streams:
-            from torchgpipe_amd.models.amoebanet import set_cell_streams
+            from torchgpipe_amd.models.amoebanet import DEFAULT_CELL_STREAMS, set_cell_streams
             set_cell_streams(stage.partition, True)
+            cell_streams = DEFAULT_CELL_STREAMS  # streams per cell (TGPIPE_CELL_STREAMS)
         optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
         x, target, loss_fn, shape = self.data(kind, batch, stage.is_first, stage.is_last)
         signature = signature_of(torch.empty(batch, *shape, device='meta'))
@@ -321,7 +322,7 @@ class Bench:
             step, steps, args.warmup, tag,
             settle=(lambda: graph.captured) if graph is not None else None)
         res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
-                   steps=steps, cell_streams=cell_streams, overlap_recompute=overlap,
+                   steps=steps, cell_streams=int(cell_streams), overlap_recompute=overlap,
                    overlap_forward=overlap_fwd, wgrad_stream=wgrad_stream,
                    hipgraph=graph is not None)
         if probe and graph is None:

@@ -47,7 +47,8 @@ xw = x.clone().requires_grad_(True)
 zw = seq[0].__class__.__mro__[1].forward(seq[0], xw)
 zw.backward(dz64_32)
 print(f'dx   Winograd conv^T(fp64 dz) vs fp64 {rel(xw.grad, x64.grad):.2e}')
-print(f'|dx| {x64.grad.norm().item():.3e}  |W||dz| ~ {(ref[0].weight.norm() * z64.grad.norm()).item():.3e}')
+wdz = (ref[0].weight.norm() * z64.grad.norm()).item()
+print(f'|dx| {x64.grad.norm().item():.3e}  |W||dz| ~ {wdz:.3e}')
 
 from torchgpipe_amd.models.resnet import build_resnet  # noqa: E402
 torch.manual_seed(0)

@@ -10,15 +10,17 @@ def test_stream_plans_split_the_cell_and_respect_dependencies():
     cells = [m for m in model.modules() if isinstance(m, Cell)]
     assert cells
     for cell in cells:
-        plan = cell._plan
-        # the two input reductions on different streams, one stream per node
-        assert plan[:2] == [0, 1]
-        assert len(plan) == 2 + len(cell.operations) // 2
-        assert set(plan) == {0, 1}
-        # every node runs on the stream of one of its inputs
-        for k in range(0, len(cell.operations), 2):
-            node = 2 + k // 2
-            assert plan[node] in {plan[cell.indices[k]], plan[cell.indices[k + 1]]}
+        for count in (2, 3, 4):
+            plan = cell._stream_plan(count)
+            # the two input reductions on different streams, one stream per node
+            assert plan[:2] == [0, 1]
+            assert len(plan) == 2 + len(cell.operations) // 2
+            assert set(plan) <= set(range(count)) and len(set(plan)) >= 2
+        # normal cells: the two 1x7-7x1 chains after the grouped op (nodes 3 and 4) run on
+        # different streams once there are three
+        if cell._group[1]:
+            plan = cell._stream_plan(3)
+            assert plan[3] != plan[4]
 
 
 def test_set_cell_streams_toggles_every_cell_and_cpu_runs_one_stream():
@@ -27,7 +29,9 @@ def test_set_cell_streams_toggles_every_cell_and_cpu_runs_one_stream():
     x = torch.rand(2, 3, 224, 224)
     ref = model(x)
     set_cell_streams(model, True)
-    assert all(m.streams for m in model.modules() if isinstance(m, Cell))
+    assert all(m.streams == 3 for m in model.modules() if isinstance(m, Cell))
+    set_cell_streams(model, 2)
+    assert all(m.streams == 2 for m in model.modules() if isinstance(m, Cell))
     assert torch.equal(model(x), ref)  # CPU tensors: the one-stream path
     set_cell_streams(model, False)
     assert not any(m.streams for m in model.modules() if isinstance(m, Cell))

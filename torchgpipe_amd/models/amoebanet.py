@@ -35,17 +35,20 @@ from torchgpipe_amd.ops.unet_ops import MaxPool2x2
 
 __all__ = ['amoebanetd', 'NORMAL_OPERATIONS', 'REDUCTION_OPERATIONS', 'set_cell_streams']
 
-_SIDE_STREAMS: Dict[Tuple[torch.device, int], torch.cuda.Stream] = {}
+_SIDE_STREAMS: Dict[Tuple[torch.device, int, int], torch.cuda.Stream] = {}
 _CAPTURE_STREAMS = os.environ.get('TGPIPE_CAPTURE_STREAMS', '1') != '0'
 # TGPIPE_SHARE_POOLS=0 computes a cell's duplicate average pools twice (Cell._shared_plan)
 _SHARE_POOLS = os.environ.get('TGPIPE_SHARE_POOLS', '1') != '0'
+# streams per cell for set_cell_streams(model, True) (TGPIPE_CELL_STREAMS)
+DEFAULT_CELL_STREAMS = int(os.environ.get('TGPIPE_CELL_STREAMS', '3'))
 
 
-def _side_stream(device: torch.device, main: torch.cuda.Stream) -> torch.cuda.Stream:
-    """The side stream paired with ``main``: a cell recomputed on a pipeline's recompute
-    lane (``PipelineStage(overlap_recompute=True)``) gets its own, so its branch work does
-    not queue behind the backward of the micro-batch running beside it."""
-    key = (device, main.stream_id)
+def _side_stream(device: torch.device, main: torch.cuda.Stream, index: int = 1
+                 ) -> torch.cuda.Stream:
+    """Side stream ``index`` paired with ``main``: a cell recomputed on a pipeline's
+    recompute lane (``PipelineStage(overlap_recompute=True)``) gets its own, so its branch
+    work does not queue behind the backward of the micro-batch running beside it."""
+    key = (device, main.stream_id, index)
     stream = _SIDE_STREAMS.get(key)
     if stream is None:
         stream = _SIDE_STREAMS[key] = torch.cuda.Stream(device)
@@ -54,20 +57,30 @@ def _side_stream(device: torch.device, main: torch.cuda.Stream) -> torch.cuda.St
 
 class _JoinSideInBackward(torch.autograd.Function):
     """Identity on the cell inputs whose backward makes the current stream wait for the side
-    stream: the fused ops on the side stream write ``param.grad`` themselves (gradient-
+    streams: the fused ops on a side stream write ``param.grad`` themselves (gradient-
     accumulation fusion), which autograd's end-of-backward stream sync does not see.  Every
     op of the cell lies upstream of the inputs' gradients, so this backward runs after all
     of them have been issued."""
 
     @staticmethod
-    def forward(ctx, stream: torch.cuda.Stream, *xs: Tensor):  # type: ignore[override]
-        ctx.stream = stream
+    def forward(ctx, streams: List[torch.cuda.Stream], *xs: Tensor):  # type: ignore[override]
+        ctx.streams = streams
         return tuple(x.view_as(x) for x in xs)
 
     @staticmethod
     def backward(ctx, *grads: Tensor):  # type: ignore[override]
-        torch.cuda.current_stream().wait_stream(ctx.stream)
+        current = torch.cuda.current_stream()
+        for stream in ctx.streams:
+            current.wait_stream(stream)
         return (None,) + grads
+
+
+def _op_cost_module(m: nn.Module) -> float:
+    if isinstance(m, FusedChain):
+        return float(sum(isinstance(c, nn.Conv2d) for c in m.children()))
+    if isinstance(m, FactorizedReduce):
+        return 1.0
+    return 0.0
 
 
 def _op_cost(op: 'Operation') -> float:
@@ -259,26 +272,67 @@ class Cell(nn.Module):
         self.indices = [i for i, _ in genotype]
         self.operations = nn.ModuleList(
             factory(c, 2 if reduction and i < 2 else 1) for i, factory in genotype)
-        self.streams = False
-        self._plan = self._stream_plan()
+        self.streams = 0
         self._group = self._group_plan()
         self._group_cache = _GroupCache()
         self._shared = self._shared_plan()
+        self._plans: Dict[int, List[int]] = {}
 
-    def _stream_plan(self) -> List[int]:
-        """Stream (0 = current, 1 = side) of every node for the two-stream schedule.
+    @property
+    def _plan(self) -> List[int]:
+        """The stream plan for the current stream count (two streams when off)."""
+        return self._stream_plan(max(2, int(self.streams)))
 
-        The two input reductions go to different streams; every later node goes to the
-        less loaded of its inputs' streams (load = convolutions already placed there).
+    def _stream_plan(self, count: int = 2) -> List[int]:
+        """Stream (0 = current, 1.. = side streams) of every node.
+
+        List scheduling over ``count`` streams with a rough cost per node (convolutions):
+        the two input reductions go to streams 0 and 1; every later node goes to the
+        stream where it can start earliest after its inputs (ties: a stream one of its
+        inputs ran on, then the lower index).  A grouped first-triplet op counts at the
+        start of the node that runs it, and the nodes that consume its other outputs are
+        ready once it is done -- with three streams the two 1x7-7x1 chains after it run
+        side by side.
         """
-        plan, load = [0, 1], [1.0, 1.0]
+        plan = self._plans.get(count)
+        if plan is not None:
+            return plan
         ops = list(self.operations)
+        g_ops = self._group[1]
+        plan = [0, min(1, count - 1)]
+        finish = [_op_cost_module(self.reduce1), _op_cost_module(self.reduce2)]
+        free = [0.0] * count
+        free[plan[0]] = finish[0]
+        free[plan[1]] = max(free[plan[1]], finish[1])
+        group_done = shared_done = -1.0
         for k in range(0, len(ops), 2):
-            ia, ib = self.indices[k], self.indices[k + 1]
-            choices = {plan[ia], plan[ib]}
-            s = min(choices, key=lambda c: load[c])
-            load[s] += _op_cost(ops[k]) + _op_cost(ops[k + 1])
+            pair = (k, k + 1)
+            ins = [self.indices[k], self.indices[k + 1]]
+            ready = max(finish[i] for i in ins)
+            uses_group = any(o in g_ops for o in pair)
+            uses_shared = any(o in self._shared for o in pair)
+            if uses_group and group_done >= 0:
+                ready = max(ready, group_done)
+            if uses_shared and shared_done >= 0:
+                ready = max(ready, shared_done)
+            own = {plan[i] for i in ins}
+            s = min(range(count), key=lambda c: (max(ready, free[c]), c not in own, c))
+            t = max(ready, free[s])
+            if uses_group and group_done < 0:
+                t += 0.6 * len(g_ops)  # the grouped GEMM, run by this node
+                group_done = t
+            if uses_shared and shared_done < 0:
+                t += 0.5  # the shared pool, run by this node
+                shared_done = t
+            for o in pair:
+                if o in g_ops:
+                    t += _op_cost(ops[o]) - 1.0
+                elif o not in self._shared:
+                    t += _op_cost(ops[o])
             plan.append(s)
+            finish.append(t)
+            free[s] = t
+        self._plans[count] = plan
         return plan
 
     def _group_plan(self) -> Tuple[int, List[int]]:
@@ -367,7 +421,7 @@ class Cell(nn.Module):
         # one stream)
         if self.streams and s1.is_cuda and (_CAPTURE_STREAMS or
                                             not torch.cuda.is_current_stream_capturing()):
-            return self._forward_two_streams(s1, s2), skip
+            return self._forward_streams(s1, s2), skip
         nodes = [self.reduce1(s1), self.reduce2(s2)]
         pre = self._grouped(nodes)
         shared: Dict[int, Tensor] = {}
@@ -375,91 +429,117 @@ class Cell(nn.Module):
             nodes.append(self._node(k, nodes, pre, shared))
         return torch.cat([nodes[i] for i in self.concat], dim=1), skip
 
-    def _forward_two_streams(self, s1: Tensor, s2: Tensor) -> Tensor:
-        """The cell's independent nodes on two HIP streams (``set_cell_streams``).
+    def _forward_streams(self, s1: Tensor, s2: Tensor) -> Tensor:
+        """The cell's independent nodes on ``self.streams`` HIP streams
+        (``set_cell_streams``).
 
-        Node k runs on stream ``self._plan[k]`` after waiting on the events of inputs
-        produced on the other stream; tensors crossing streams are ``record_stream``-ed so
-        the caching allocator does not hand their memory out early.  Autograd runs each
+        Node k runs on stream ``plan[k]`` after waiting on the events of inputs produced on
+        another stream (the grouped first-triplet op and a shared pool have events of
+        their own, recorded right after them, so their consumers do not wait for the rest
+        of the node that ran them); tensors crossing streams are ``record_stream``-ed so the
+        caching allocator does not hand their memory out early.  Autograd runs each
         backward op on its forward op's stream.
         """
+        count = max(2, int(self.streams))
+        plan = self._stream_plan(count)
         current = torch.cuda.current_stream(s1.device)
-        streams = [current, _side_stream(s1.device, current)]
+        streams = [current] + [_side_stream(s1.device, current, i) for i in range(1, count)]
+        used = sorted(set(plan))
+        sides = [streams[i] for i in used if i != 0]
         if torch.is_grad_enabled() and (s1.requires_grad or s2.requires_grad):
             if s1 is s2:
-                s1 = s2 = _JoinSideInBackward.apply(streams[1], s1)[0]
+                s1 = s2 = _JoinSideInBackward.apply(sides, s1)[0]
             else:
-                s1, s2 = _JoinSideInBackward.apply(streams[1], s1, s2)
-        streams[1].wait_stream(streams[0])
+                s1, s2 = _JoinSideInBackward.apply(sides, s1, s2)
+        for side in sides:
+            side.wait_stream(current)
         events: List[Optional[torch.cuda.Event]] = []
         nodes: List[Tensor] = []
+        pre: Dict[int, Tensor] = {}
+        shared: Dict[int, Tensor] = {}
+        special: Dict[str, Tuple[int, torch.cuda.Event]] = {}  # 'group' / 'shared' -> (stream, ev)
+
+        def needs_event(k: int, s: int) -> bool:
+            return any(plan[j] != s for j in range(k + 1, len(plan))) or \
+                (s != 0 and k in self.concat)
 
         def run(k: int, fn: Callable[[], Tensor], inputs: List[int],
-                external: List[Tensor]) -> None:
-            s = self._plan[k]
+                external: List[Tensor], waits: List[str]) -> None:
+            s = plan[k]
             stream = streams[s]
             for i in inputs:
-                if self._plan[i] != s:
+                if plan[i] != s:
                     ev = events[i]
                     assert ev is not None
                     stream.wait_event(ev)
                     nodes[i].record_stream(stream)
-            if s == 1:
+            for name in waits:
+                src, ev = special[name]
+                if src != s:
+                    stream.wait_event(ev)
+                    for t in (pre.values() if name == 'group' else shared.values()):
+                        t.record_stream(stream)
+            if s != 0:
                 for t in external:
                     t.record_stream(stream)
             with torch.cuda.stream(stream):
                 out = fn()
             ev = None
-            if any(self._plan[j] != s for j in range(k + 1, len(self._plan))) or \
-                    (s == 1 and k in self.concat):
+            if needs_event(k, s):
                 ev = torch.cuda.Event()
                 ev.record(stream)
             nodes.append(out)
             events.append(ev)
 
-        run(0, lambda: self.reduce1(s1), [], [s1])
-        run(1, lambda: self.reduce2(s2), [], [s2])
-        # the grouped first triplets run with the first node that needs them; a later node
-        # on the other stream waits for that node's event and records its group inputs
-        # (and a shared operation's output: computed with the first node that needs it)
-        pre: Dict[int, Tensor] = {}
-        shared: Dict[int, Tensor] = {}
-        group_node = shared_node = -1
+        run(0, lambda: self.reduce1(s1), [], [s1], [])
+        run(1, lambda: self.reduce2(s2), [], [s2], [])
+        g_ops = self._group[1]
         for k in range(0, len(self.operations), 2):
+            node = len(nodes)
+            pair = (k, k + 1)
             ins = [self.indices[k], self.indices[k + 1]]
-            mine = [o for o in (k, k + 1) if o in self._group[1]]
-            share = [o for o in (k, k + 1) if o in self._shared]
-            if share and shared_node >= 0 and self._plan[len(nodes)] != self._plan[shared_node]:
-                ins.append(shared_node)
-                shared[share[0]].record_stream(streams[self._plan[len(nodes)]])
-            elif share and shared_node < 0:
-                shared_node = len(nodes)
-            if mine and group_node < 0:
-                group_node = len(nodes)
+            waits: List[str] = []
+            first_group = any(o in g_ops for o in pair) and 'group' not in special
+            first_shared = any(o in self._shared for o in pair) and 'shared' not in special
+            if any(o in g_ops for o in pair) and not first_group:
+                waits.append('group')
+            if any(o in self._shared for o in pair) and not first_shared:
+                waits.append('shared')
 
-                def fn(k: int = k) -> Tensor:
+            def fn(k: int = k, node: int = node, first_group: bool = first_group,
+                   first_shared: bool = first_shared) -> Tensor:
+                stream = streams[plan[node]]
+                if first_group:
                     pre.update(self._grouped(nodes))
-                    return self._node(k, nodes, pre, shared)
-                run(len(nodes), fn, ins, [])
-                continue
-            if mine and pre and self._plan[len(nodes)] != self._plan[group_node]:
-                ins.append(group_node)
-                stream = streams[self._plan[len(nodes)]]
-                for o in mine:
-                    pre[o].record_stream(stream)
-            run(len(nodes), lambda k=k: self._node(k, nodes, pre, shared), ins, [])
-        streams[0].wait_stream(streams[1])
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    special['group'] = (plan[node], ev)
+                if first_shared:
+                    a = next(o for o in (k, k + 1) if o in self._shared)
+                    out = self.operations[a](nodes[self.indices[a]])
+                    for j in self._shared:
+                        shared[j] = out
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    special['shared'] = (plan[node], ev)
+                return self._node(k, nodes, pre, shared)
+            run(node, fn, ins, [], waits)
+        for side in sides:
+            streams[0].wait_stream(side)
         for i in self.concat:
-            if self._plan[i] == 1:
+            if plan[i] != 0:
                 nodes[i].record_stream(streams[0])
         return torch.cat([nodes[i] for i in self.concat], dim=1)
 
 
-def set_cell_streams(model: nn.Module, enabled: bool = True) -> None:
-    """Run every AmoebaNet cell's independent nodes on two HIP streams (GPU inputs)."""
+def set_cell_streams(model: nn.Module, enabled: Union[bool, int] = True) -> None:
+    """Run every AmoebaNet cell's independent nodes on several HIP streams (GPU inputs):
+    ``True`` = ``DEFAULT_CELL_STREAMS`` (3, ``TGPIPE_CELL_STREAMS``), an int = that many
+    (2 or more), ``False`` / 0 / 1 = one stream."""
+    count = DEFAULT_CELL_STREAMS if enabled is True else int(enabled)
     for m in model.modules():
         if isinstance(m, Cell):
-            m.streams = enabled
+            m.streams = count if count >= 2 else 0
 
 
 def amoebanetd(num_classes: int = 10, num_layers: int = 4, num_filters: int = 512
