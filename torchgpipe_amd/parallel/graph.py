@@ -137,20 +137,22 @@ class StepGraph:
             return self._eager(input, target)
         if self._graph is None and self._warm < self.warmup:
             # Warm-up on a side stream, as graph capture requires of everything it will
-            # record (lazy initialisations must not happen inside the capture).
+            # record (lazy initialisations must not happen inside the capture) -- and on
+            # the big-stack thread that will capture and replay: its library handles
+            # (hipBLASLt, MIOpen) are created here, outside the capture.
             self._zero_grad()
             side = torch.cuda.Stream(device)
             side.wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(side):
-                loss = self._eager(input, target)
+                loss = call_with_big_stack(lambda: self._eager(input, target))
             torch.cuda.current_stream(device).wait_stream(side)
             self._warm += 1
             return loss
         if self._graph is None:
-            # captured on the calling thread, whose library handles (hipBLASLt, MIOpen) the
-            # warm-up steps created: a first library call inside a capture on a fresh thread
-            # would have to create them there
-            self._capture(input, target)
+            # captured on the big-stack thread too: ending the capture of a multi-stream
+            # step (three-stream AmoebaNet cells) walks the DAG recursively as well and
+            # overflowed the 8 MiB main-thread stack (utils/bigstack.py)
+            call_with_big_stack(lambda: self._capture(input, target))
         assert self._graph is not None and self._input is not None and self._target is not None
         if self._hyperparameters() != self._hyper:
             raise RuntimeError('StepGraph: optimizer hyperparameters changed since the capture '

@@ -14,12 +14,14 @@ recurse that deep, which is why the one-stream workaround of round 2 hid it.
 
 The fix here does not depend on the caller's ``ulimit``: graph launches run on one
 persistent worker thread whose stack is reserved at 1 GiB of address space (pages are
-committed only when touched).  Captures stay on the caller's thread: a library call
-(hipBLASLt for a Linear layer) made for the first time on a fresh thread inside a
-capture has to create its per-thread handle there, which crashed.  The caller's
-device and current stream are propagated, exceptions are re-raised in the caller, and
-the call is synchronous from the caller's point of view (the worker only *enqueues*
-GPU work, like the caller would have).
+committed only when touched).  ``StepGraph`` runs its warm-up steps and the capture on
+that thread as well: ending the capture of a three-stream AmoebaNet step overflowed the
+main thread's stack the same way (``hipStreamEndCapture`` / instantiation), and a library
+call (hipBLASLt for a Linear layer) made for the first time on a thread *inside* a
+capture has to create its per-thread handle there, which crashes -- the warm-up steps
+create those handles on the worker first.  The caller's device and current stream are
+propagated, exceptions are re-raised in the caller, and the call is synchronous from the
+caller's point of view (the worker only *enqueues* GPU work, like the caller would have).
 """
 import queue
 import threading
