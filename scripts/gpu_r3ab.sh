@@ -11,8 +11,8 @@ run() {
   e=$1; shift; env $e timeout -k 10 300 python bench.py --model amoebanet --steps 5 --warmup 2 --sections none "$@" > $out/amoeba_$tag.json 2> $out/amoeba_$tag.err || { tail -20 $out/amoeba_$tag.err; return 1; }
   echo "$tag $(cut -c1-150 $out/amoeba_$tag.json)"
 }
-run s3 TGPIPE_CELL_STREAMS=3 || exit 1
-run s2 TGPIPE_CELL_STREAMS=2 || exit 1
-run s3b TGPIPE_CELL_STREAMS=3 || exit 1
-run s4 TGPIPE_CELL_STREAMS=4 || exit 1
-run s3_eager TGPIPE_CELL_STREAMS=3 --graph off || exit 1
+run g2 TGPIPE_CELL_STREAMS=2 || exit 1
+run e3 TGPIPE_CELL_STREAMS=3 --graph off || exit 1
+run e2 TGPIPE_CELL_STREAMS=2 --graph off || exit 1
+run e3b TGPIPE_CELL_STREAMS=3 --graph off || exit 1
+run g2b TGPIPE_CELL_STREAMS=2 || exit 1

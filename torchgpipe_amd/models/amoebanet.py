@@ -41,6 +41,10 @@ _CAPTURE_STREAMS = os.environ.get('TGPIPE_CAPTURE_STREAMS', '1') != '0'
 _SHARE_POOLS = os.environ.get('TGPIPE_SHARE_POOLS', '1') != '0'
 # streams per cell for set_cell_streams(model, True) (TGPIPE_CELL_STREAMS)
 DEFAULT_CELL_STREAMS = int(os.environ.get('TGPIPE_CELL_STREAMS', '3'))
+# at most this many inside a hipGraph capture: the capture of a three-stream step ends in a
+# segfault inside the runtime (hipStreamEndCapture, also on the 1 GiB-stack thread;
+# scripts/gpu_r3ab.sh), two streams capture and replay correctly
+CAPTURE_CELL_STREAMS = int(os.environ.get('TGPIPE_CAPTURE_CELL_STREAMS', '2'))
 
 
 def _side_stream(device: torch.device, main: torch.cuda.Stream, index: int = 1
@@ -441,6 +445,8 @@ class Cell(nn.Module):
         backward op on its forward op's stream.
         """
         count = max(2, int(self.streams))
+        if torch.cuda.is_current_stream_capturing():
+            count = max(2, min(count, CAPTURE_CELL_STREAMS))
         plan = self._stream_plan(count)
         current = torch.cuda.current_stream(s1.device)
         streams = [current] + [_side_stream(s1.device, current, i) for i in range(1, count)]
