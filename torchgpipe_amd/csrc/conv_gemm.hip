@@ -27,6 +27,10 @@
 // its partial tile into a workspace slice and split_reduce sums them (no atomics); the
 // forward then leaves the BatchNorm statistics to a separate pass (bn_stats).
 //
+// Element-gathered N-major operands (planes whose pixel count is not a multiple of 4, e.g.
+// AmoebaNet's 7x7; every kernel with taps) give each lane columns BN/4 apart, so one load
+// instruction reads a contiguous run of pixels across the lanes (store_nmajor `spread`).
+//
 // LDS images:
 //   K-major operand (k contiguous in HBM: weights, dZ in weight-grad, X in weight-grad)
 //     [BK/4][2][rows][2]: k quad g split into the pairs (k0, k2) / (k1, k3) that lane half
@@ -46,6 +50,9 @@
 #include "kernels.h"
 
 namespace tgpipe {
+
+int env_int(const char* name, int fallback);
+
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -109,6 +116,7 @@ struct Geo {
   int relu;              // ReLU on the input (forward / weight-grad) / its mask (bwd-data)
   int scatter;           // bwd-data over output pixels, results scattered (strided 1x1)
   int a_t;               // bwd-data: A is the transposed weight [ci][co*T] (row-major)
+  int spread;            // element-gathered N-major columns spread over the lanes
   FastDiv fd_taps, fd_kw, fd_hwo, fd_wo, fd_hwi;  // / taps, / kw, / (ho*wo), / wo, / (h*w)
 };
 
@@ -178,15 +186,25 @@ __device__ __forceinline__ void store_kmajor(float* img, const floatx4 (&v)[Q], 
 }
 
 // N-major operand: quad index i of thread t -> row k = t / (BN/4) + (THREADS / (BN/4)) * i,
-// column quad t % (BN/4).
+// column quad t % (BN/4) -- or, when the operand is gathered element by element
+// (`spread`: columns whose pixels are not 16-byte quads), columns t % (BN/4) + (BN/4) e
+// for e = 0..3, so the lanes of one load instruction read consecutive pixels (one
+// contiguous run per row) instead of every fourth one.
 template <int BN, int Q, int THREADS>
-__device__ __forceinline__ void store_nmajor(float* img, const floatx4 (&v)[Q], int tid) {
+__device__ __forceinline__ void store_nmajor(float* img, const floatx4 (&v)[Q], int tid,
+                                             bool spread) {
   constexpr int QPR = BN / 4;
   constexpr int RPP = THREADS / QPR;
 #pragma unroll
   for (int i = 0; i < Q; ++i) {
     const int k = tid / QPR + RPP * i;
-    *reinterpret_cast<floatx4*>(img + k * (BN + 32) + (tid % QPR) * 4) = v[i];
+    float* row = img + k * (BN + 32);
+    if (spread) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) row[tid % QPR + QPR * e] = v[i][e];
+    } else {
+      *reinterpret_cast<floatx4*>(row + (tid % QPR) * 4) = v[i];
+    }
   }
 }
 
@@ -312,13 +330,19 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
   constexpr int kRB = kBK_major ? C::kBQuadsK : C::kBQuadsN;
   floatx4 ra[SUB][C::kAQuads], rb[SUB][kRB];
 
-  // N-major B columns of this thread (forward / bwd-data)
+  // N-major B columns of this thread (forward / bwd-data): a quad of adjacent columns when
+  // the operand is read as 16-byte quads (1x1, planes of 4k pixels), else columns BN/4
+  // apart (store_nmajor's `spread`)
   constexpr int QPR = C::BN / 4;
+  const bool spread = !kBK_major && g.spread &&
+                      !(((MODE == kFwd && kPlain) || (MODE == kBwdData && (kPlain || g.scatter)))
+                        && (hw_out & 3) == 0);
   Col col[4];
   if constexpr (!kBK_major) {
-    const int jq = n0 + (tid % QPR) * 4;
+    const int jq = n0 + (tid % QPR) * (spread ? 1 : 4);
+    const int cstep = spread ? QPR : 1;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) col[e] = make_col<MODE, kPlain>(g, jq + e, N);
+    for (int e = 0; e < 4; ++e) col[e] = make_col<MODE, kPlain>(g, jq + cstep * e, N);
   }
 
   // A: K-major rows (tid >> 3) + (threads / 8) i, k quad (tid & 7)
@@ -514,7 +538,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
       if constexpr (kBK_major)
         store_kmajor<C::BN, C::kBQuadsK, kThreads>(bimg(buf, u), rb[u], tid);
       else
-        store_nmajor<C::BN, C::kBQuadsN, kThreads>(bimg(buf, u), rb[u], tid);
+        store_nmajor<C::BN, C::kBQuadsN, kThreads>(bimg(buf, u), rb[u], tid, spread);
     }
   };
 
@@ -904,9 +928,11 @@ __global__ __launch_bounds__(256) void slab_flush_kernel(SlabTable t) {
 }
 
 Geo make_geo(const ConvGemmGeo& cg) {
+  // TGPIPE_CG_SPREAD=0: element-gathered columns as adjacent quads (the round-2 mapping)
+  static const int spread = env_int("TGPIPE_CG_SPREAD", 1) != 0 ? 1 : 0;
   Geo g{cg.n, cg.ci, cg.h, cg.w, cg.co, cg.ho, cg.wo, cg.co_total, cg.co_off, cg.kh, cg.kw,
         cg.kh * cg.kw, cg.sh, cg.sw, cg.ph, cg.pw, cg.oh, cg.ow, cg.relu ? 1 : 0, 0,
-        cg.a_t ? 1 : 0, {}, {}, {}, {}, {}};
+        cg.a_t ? 1 : 0, spread, {}, {}, {}, {}, {}};
   g.fd_taps = make_fastdiv(g.taps);
   g.fd_kw = make_fastdiv(g.kw);
   g.fd_hwo = make_fastdiv(g.ho * g.wo);

@@ -59,6 +59,14 @@ def _side_stream(device: torch.device, main: torch.cuda.Stream, index: int = 1
     return stream
 
 
+def prepare_side_streams(device: torch.device, main: torch.cuda.Stream,
+                         count: int = 4) -> None:
+    """Create the side streams paired with ``main`` ahead of time (``StepGraph`` calls it for
+    its capture stream, so no stream is created inside a capture)."""
+    for i in range(1, count):
+        _side_stream(torch.device(device), main, i)
+
+
 class _JoinSideInBackward(torch.autograd.Function):
     """Identity on the cell inputs whose backward makes the current stream wait for the side
     streams: the fused ops on a side stream write ``param.grad`` themselves (gradient-

@@ -181,10 +181,15 @@ class StepGraph:
         # Gradients are created inside the capture (from the graph's memory pool) and
         # rewritten by every replay.
         self._zero_grad()
+        # the capture stream and the side streams multi-stream cells pair with it exist
+        # before the capture starts (no stream creation inside it)
+        capture = torch.cuda.Stream(device)
+        from torchgpipe_amd.models.amoebanet import prepare_side_streams
+        prepare_side_streams(device, capture)
         torch.cuda.synchronize(device)
         graph = torch.cuda.CUDAGraph()
         self._hyper = self._hyperparameters()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, stream=capture):
             self._loss = self._eager(self._input, self._target)
         self._graph = graph
         self._grads = [(p, p.grad) for p in self.stage.parameters() if p.grad is not None]
