@@ -1038,6 +1038,19 @@ at::Tensor avgpool3_backward(const at::Tensor& dy_in, int64_t h, int64_t w, int6
 }
 
 // U-Net decoder: cat(upsample2x(x), skip) and its backward for x (unet_ops.hip).
+at::Tensor add_relu_forward(const at::Tensor& a_in, const at::Tensor& b_in) {
+  auto a = a_in.contiguous();
+  auto b = b_in.contiguous();
+  check_f32(a, "a", a);
+  check_f32(b, "b", a);
+  TORCH_CHECK(a.sizes() == b.sizes(), "a and b must have one shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  auto y = at::empty_like(a);
+  launch_add_relu(a.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>(), a.numel(),
+                  cur_stream(a));
+  return y;
+}
+
 at::Tensor up2x_cat_forward(const at::Tensor& x_in, const at::Tensor& skip_in) {
   auto x = x_in.contiguous();
   auto skip = skip_in.contiguous();
@@ -1124,6 +1137,7 @@ at::Tensor maxpool2x2_backward(const at::Tensor& x_in, const at::Tensor& dy_in) 
 
 TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("up2x_cat_forward(Tensor x, Tensor skip) -> Tensor");
+  m.def("add_relu_forward(Tensor a, Tensor b) -> Tensor");
   m.def("up2x_backward(Tensor dy, int c) -> Tensor");
   m.def("maxpool2x2_forward(Tensor x, Tensor? add=None) -> Tensor");
   m.def("maxpool2x2_backward(Tensor x, Tensor dy) -> Tensor");
@@ -1184,6 +1198,7 @@ TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
   m.impl("avgpool3_forward", &tgpipe::avgpool3_forward);
   m.impl("avgpool3_backward", &tgpipe::avgpool3_backward);
   m.impl("up2x_cat_forward", &tgpipe::up2x_cat_forward);
+  m.impl("add_relu_forward", &tgpipe::add_relu_forward);
   m.impl("up2x_backward", &tgpipe::up2x_backward);
   m.impl("maxpool2x2_forward", &tgpipe::maxpool2x2_forward);
   m.impl("maxpool2x2_backward", &tgpipe::maxpool2x2_backward);

@@ -285,6 +285,9 @@ void launch_up2x_cat(const float* x, const float* skip, float* out, int64_t n, i
                      int h, int w, hipStream_t stream);
 void launch_up2x_backward(const float* dy, float* dx, int64_t n, int c, int h, int w,
                           int64_t dy_img, hipStream_t stream);
+// y = relu(a + b) over `total` floats (ResNet's residual join; 16-byte aligned tensors).
+void launch_add_relu(const float* a, const float* b, float* y, int64_t total,
+                     hipStream_t stream);
 // add (nullable): y = maxpool(x) + add.  dy: image stride dy_img (channel slices).
 void launch_maxpool2x2_forward(const float* x, const float* add, float* y, int64_t planes, int h,
                                int w, hipStream_t stream);

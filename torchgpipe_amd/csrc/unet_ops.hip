@@ -134,7 +134,44 @@ __global__ __launch_bounds__(256) void maxpool2x2_bwd_kernel(const float* __rest
   }
 }
 
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// ResNet's residual join: y = relu(x + identity), one pass (the sum and the ReLU were two
+// ATen passes over the block output).
+__global__ __launch_bounds__(256) void add_relu_kernel(const float* __restrict__ a,
+                                                       const float* __restrict__ b,
+                                                       float* __restrict__ y, int64_t quads,
+                                                       int64_t total) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t q = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; q < quads; q += stride) {
+    const floatx4 v =
+        reinterpret_cast<const floatx4*>(a)[q] + reinterpret_cast<const floatx4*>(b)[q];
+    floatx4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = v[e] > 0.f ? v[e] : 0.f;
+    reinterpret_cast<floatx4*>(y)[q] = o;
+  }
+  // tail (total % 4), by the first workgroup
+  if (blockIdx.x == 0) {
+    const int64_t i = quads * 4 + threadIdx.x;
+    if (i < total) {
+      const float v = a[i] + b[i];
+      y[i] = v > 0.f ? v : 0.f;
+    }
+  }
+}
+
 }  // namespace
+
+void launch_add_relu(const float* a, const float* b, float* y, int64_t total,
+                     hipStream_t stream) {
+  if (total == 0) return;
+  const int64_t quads = total / 4;
+  int64_t blocks = (quads + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
+  hipLaunchKernelGGL(add_relu_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                     a, b, y, quads, total);
+}
 
 void launch_up2x_cat(const float* x, const float* skip, float* out, int64_t n, int c1, int c2,
                      int h, int w, hipStream_t stream) {

@@ -19,7 +19,8 @@ from typing import Any, Generator, List, Optional
 from torch import Tensor, nn
 
 from torchgpipe_amd.models.flatten import flatten_sequential
-from torchgpipe_amd.ops.fusion import BatchNormAct2d, ConvBN2d, ReLU, relink
+from torchgpipe_amd.ops.fusion import (BatchNormAct2d, ConvBN2d, ReLU, add_relu, relink,
+                                       relu_follows)
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
 __all__ = ['resnet50', 'resnet101', 'build_resnet']
@@ -34,6 +35,9 @@ class Identity(nn.Module):
 
 @skippable(pop=['identity'])
 class Residual(nn.Module):
+    # with a linked ReLU after it (ops/fusion.py relink): relu(x + identity) in one pass
+    fuses_relu = True
+
     def __init__(self, downsample: Optional[nn.Module] = None) -> None:
         super().__init__()
         self.downsample = downsample
@@ -42,6 +46,8 @@ class Residual(nn.Module):
         identity = yield pop('identity')
         if self.downsample is not None:
             identity = self.downsample(identity)
+        if relu_follows(self):
+            return add_relu(x, identity)
         return x + identity
 
 

@@ -45,7 +45,7 @@ from torchgpipe_amd.ops.conv import WinogradConv2d, wino_eligible
 from torchgpipe_amd.ops.convbn import (_bn_ok, fusable, gemm_conv2d, gemm_conv_eligible,
                                        relu_conv_bn)
 
-__all__ = ['ConvBN2d', 'BatchNormAct2d', 'ReLU', 'relink', 'bn_act']
+__all__ = ['ConvBN2d', 'BatchNormAct2d', 'ReLU', 'relink', 'bn_act', 'add_relu']
 
 _LINK = '_tgpipe_link'       # ConvBN2d -> (BatchNormAct2d, relu?)
 _RELU = '_tgpipe_relu_next'  # BatchNormAct2d -> a linked ReLU follows
@@ -94,6 +94,38 @@ def _mark(y: Tensor, bn: nn.Module, relu: bool) -> Tensor:
     if relu:
         setattr(y, _DONE_RELU, True)
     return y
+
+
+class _AddReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a: Tensor, b: Tensor) -> Tensor:  # type: ignore[override]
+        y = _ext.require(a).add_relu_forward(a, b)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy: Tensor):  # type: ignore[override]
+        (y,) = ctx.saved_tensors
+        g = torch.ops.aten.threshold_backward(dy, y, 0.0)
+        return g, g
+
+
+def add_relu(a: Tensor, b: Tensor) -> Tensor:
+    """``relu(a + b)`` in one pass on the GPU (fp32, same shape); marked for a following
+    :class:`ReLU` to pass through."""
+    if (a.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32
+            and a.shape == b.shape and a.device == b.device and _ext.available()):
+        y = _AddReLU.apply(a, b)
+    else:
+        y = F.relu(a + b)
+    setattr(y, _DONE_RELU, True)
+    return y
+
+
+def relu_follows(module: nn.Module) -> bool:
+    """Whether :func:`relink` linked a :class:`ReLU` after ``module`` (a layer that can apply
+    it itself, e.g. ResNet's residual join: ``fuses_relu = True``)."""
+    return bool(module.__dict__.get(_RELU, False))
 
 
 def _pointwise(conv: nn.Conv2d) -> bool:
@@ -164,8 +196,10 @@ def relink(module: nn.Module) -> int:
             continue
         kids = list(seq.children())
         for i, m in enumerate(kids):
-            if type(m) is BatchNormAct2d and i + 1 < len(kids) and type(kids[i + 1]) is ReLU:
-                m.__dict__[_RELU] = True
+            inner = getattr(m, 'module', m)  # (a @skippable layer wraps the real module)
+            if (type(m) is BatchNormAct2d or getattr(inner, 'fuses_relu', False)) and \
+                    i + 1 < len(kids) and type(kids[i + 1]) is ReLU:
+                inner.__dict__[_RELU] = True
             if not isinstance(m, ConvBN2d) or i + 1 >= len(kids) or \
                     type(kids[i + 1]) is not BatchNormAct2d:
                 continue
