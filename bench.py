@@ -150,6 +150,11 @@ def even_balance(layers: int, parts: int) -> list:
     return [base + (1 if i < extra else 0) for i in range(parts)]
 
 
+def _capture_streams() -> int:
+    from torchgpipe_amd.models.amoebanet import CAPTURE_CELL_STREAMS
+    return max(2, CAPTURE_CELL_STREAMS)
+
+
 def choice(value: str, auto: bool) -> bool:
     return {'on': True, 'off': False}.get(value, auto)
 
@@ -322,7 +327,10 @@ class Bench:
             step, steps, args.warmup, tag,
             settle=(lambda: graph.captured) if graph is not None else None)
         res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
-                   steps=steps, cell_streams=int(cell_streams), overlap_recompute=overlap,
+                   steps=steps, overlap_recompute=overlap,
+                   # (a captured step keeps at most CAPTURE_CELL_STREAMS per cell)
+                   cell_streams=min(int(cell_streams), _capture_streams())
+                   if graph is not None and cell_streams else int(cell_streams),
                    overlap_forward=overlap_fwd, wgrad_stream=wgrad_stream,
                    hipgraph=graph is not None)
         if probe and graph is None:

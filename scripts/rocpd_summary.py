@@ -43,6 +43,9 @@ def main() -> None:
     p.add_argument('--csv', default=None)
     p.add_argument('--md', default=None)
     p.add_argument('--title', default='rocprofv3 kernel trace')
+    p.add_argument('--whole', type=int, default=0,
+                   help='no optimizer bursts (e.g. benchmarks/stage_harness.py): the whole '
+                        'trace counts as this many steps')
     args = p.parse_args()
     con = sqlite3.connect(args.db)
     rows = con.execute('select name, start, end from kernels order by start').fetchall()
@@ -55,7 +58,9 @@ def main() -> None:
             else:
                 ends[-1] = end
             last = i
-    steps = len(ends) - args.skip
+    if args.whole:
+        ends, args.skip = [max(e for _, _, e in rows)], 0
+    steps = args.whole or len(ends) - args.skip
     t0 = ends[args.skip - 1] if args.skip > 0 else rows[0][1]
     timed = [(n, s, e) for n, s, e in rows if s >= t0 and e <= ends[-1]]
     per = collections.defaultdict(lambda: [0, 0])
