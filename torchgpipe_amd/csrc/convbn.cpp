@@ -439,6 +439,97 @@ void wgrad_slab_flush(at::TensorList slabs, at::TensorList grads, at::IntArrayRe
   launch_slab_flush(entries.data(), static_cast<int>(entries.size()), cur_stream(grads[0]));
 }
 
+// Backward-data of a single-part operation on the library convolution (MIOpen, through
+// ATen) + the ReLU mask, for the geometries where that measured faster than the implicit
+// GEMM: the strided convolutions of reduction cells (the GEMM walks every stride hole:
+// 206 vs 43 us for 32 ch 3x3 s2 at 112^2) and some deep 7x7 / 28x28 planes
+// (profiles/r3/convbn_bench_n20_spread.json).  Decided per geometry by timing both on the
+// first eager call, like the tile plans; a shape first met inside a stream capture, or
+// TGPIPE_LIB_DGRAD=0, keeps the implicit GEMM.
+std::mutex lib_mutex;
+std::map<PlanKey, bool> lib_dgrad_cache;
+std::atomic<int> forced_lib{-1};
+
+// Test hook: -1 = measured choice, 0 = always the implicit GEMM, 1 = always the library.
+void lib_dgrad_force(int64_t mode) { forced_lib.store(static_cast<int>(mode)); }
+
+bool lib_dgrad_eligible(const ConvGemmGeo& g) {
+  static const bool on = [] {
+    const char* v = std::getenv("TGPIPE_LIB_DGRAD");
+    return v == nullptr || std::string(v) != "0";
+  }();
+  const int forced = forced_lib.load();
+  if (forced == 0 || (forced < 0 && (!on || forced_cfg.load() >= 0))) return false;
+  if (g.oh != 0 || g.ow != 0 || g.co != g.co_total) return false;
+  // small operands stay native without a trial: the library's per-call overhead loses
+  // there, and a tiny 1x1 shape's library call faulted on the GPU box (miopenStatus-
+  // InternalError after an illegal address, r3ag)
+  const int64_t x_numel = static_cast<int64_t>(g.n) * g.ci * g.h * g.w;
+  return forced == 1 || (x_numel >= (int64_t{1} << 17) && g.ci >= 32 && g.co >= 32);
+}
+
+at::Tensor lib_dgrad(const at::Tensor& dz, const at::Tensor& x, const at::Tensor& w,
+                     const ConvGemmGeo& g) {
+  const int64_t stride[2] = {g.sh, g.sw}, pad[2] = {g.ph, g.pw}, one[2] = {1, 1},
+                zero[2] = {0, 0};
+  auto dxr = std::get<0>(at::convolution_backward(dz, x, w, c10::nullopt, stride, pad, one,
+                                                  false, zero, 1, {true, false, false}));
+  return g.relu ? at::threshold_backward(dxr, x, 0) : dxr;
+}
+
+template <typename Ours, typename Lib>
+bool lib_dgrad_chosen(const ConvGemmGeo& g, const at::Tensor& like, Ours&& ours, Lib&& lib) {
+  const PlanKey key{1, g.n, g.ci, g.h, g.w, g.co, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.oh,
+                    g.ow, g.co_total};
+  if (forced_lib.load() == 1) return true;
+  std::lock_guard<std::mutex> lock(lib_mutex);
+  auto hit = lib_dgrad_cache.find(key);
+  if (hit != lib_dgrad_cache.end()) return hit->second;
+  const hipStream_t stream = cur_stream(like);
+  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &capture) != hipSuccess ||
+      capture != hipStreamCaptureStatusNone)
+    return false;
+  hipEvent_t t0, t1;
+  hipEventCreate(&t0);
+  hipEventCreate(&t1);
+  auto time = [&](auto&& fn) {
+    float ms = 0.f, best = -1.f;
+    for (int rep = 0; rep < 3; ++rep) {  // first run: warm-up (plans, MIOpen's find step)
+      hipEventRecord(t0, stream);
+      fn();
+      hipEventRecord(t1, stream);
+      hipEventSynchronize(t1);
+      hipEventElapsedTime(&ms, t0, t1);
+      if (rep > 0 && (best < 0.f || ms < best)) best = ms;
+    }
+    return best;
+  };
+  const float ours_ms = time(ours);
+  const float lib_ms = time(lib);
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  const bool pick = lib_ms < 0.95f * ours_ms;  // ties stay on the native kernel
+  lib_dgrad_cache[key] = pick;
+  return pick;
+}
+
+// Geometries whose backward-data runs on the library convolution: "n ci h w co kh kw sh sw
+// ph pw" per line.
+std::string lib_dgrad_export() {
+  std::lock_guard<std::mutex> lock(lib_mutex);
+  std::ostringstream out;
+  for (const auto& kv : lib_dgrad_cache) {
+    if (!kv.second) continue;
+    const auto& k = kv.first;
+    out << std::get<1>(k) << ' ' << std::get<2>(k) << ' ' << std::get<3>(k) << ' '
+        << std::get<4>(k) << ' ' << std::get<5>(k) << ' ' << std::get<6>(k) << ' '
+        << std::get<7>(k) << ' ' << std::get<8>(k) << ' ' << std::get<9>(k) << ' '
+        << std::get<10>(k) << ' ' << std::get<11>(k) << '\n';
+  }
+  return out.str();
+}
+
 std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
                                         const at::Tensor& z, const at::Tensor& mean,
                                         const at::Tensor& invstd, at::Tensor& sums,
@@ -495,11 +586,11 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                      opt_ptr(beta, "beta", x, c));
   std::vector<at::Tensor> out;
   at::Tensor dx;
-  if (need_dx) {
+  auto ours = [&]() -> at::Tensor {
     std::vector<ConvGemmPlan> plans;
     bool zero = false;
     for (const auto& g : p.geo) zero = zero || conv_gemm_plan(1, g).scatter;
-    dx = zero ? at::zeros_like(x) : at::empty_like(x);  // stride holes receive nothing
+    at::Tensor d = zero ? at::zeros_like(x) : at::empty_like(x);  // stride holes receive nothing
     // the backward-data A operand is W^T: one small transpose per weight, then the
     // GEMM streams K-contiguous rows instead of gathering a column per element
     // (`weights_t`: the caller's per-step cached transposes, ops/conv.py _TransformCache)
@@ -521,15 +612,23 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
     }
     for (size_t i = 0; i < p.geo.size(); ++i)
       plans.push_back(tuned_plan(1, wts[i].data_ptr<float>(), dz.data_ptr<float>(),
-                                 x.data_ptr<float>(), dx.data_ptr<float>(), nullptr, nullptr,
+                                 x.data_ptr<float>(), d.data_ptr<float>(), nullptr, nullptr,
                                  p.geo[i], i > 0 || zero, wts[i].numel() * 4,
                                  dz.numel() * 4, x, x.numel()));
     for (size_t i = 0; i < p.geo.size(); ++i) {
       const auto& wt = wts[i];
       run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-               dx.data_ptr<float>(), nullptr, nullptr, p.geo[i], plans[i], i > 0 || zero,
+               d.data_ptr<float>(), nullptr, nullptr, p.geo[i], plans[i], i > 0 || zero,
                wt.numel() * 4, dz.numel() * 4, x);
     }
+    return d;
+  };
+  if (need_dx) {
+    const bool lib = p.geo.size() == 1 && lib_dgrad_eligible(p.geo[0]) &&
+                     lib_dgrad_chosen(p.geo[0], x, ours, [&] {
+                       return lib_dgrad(dz, x, weights[0], p.geo[0]);
+                     });
+    dx = lib ? lib_dgrad(dz, x, weights[0], p.geo[0]) : ours();
   }
   out.push_back(dx);
   out.push_back(dgamma);
@@ -1172,6 +1271,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("wgrad_slab_flush(Tensor[] slabs, Tensor(a!)[] grads, int[] accumulate) -> ()");
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
   m.def("conv_gemm_plans_export() -> str", &tgpipe::conv_gemm_plans_export);
+  m.def("lib_dgrad_export() -> str", &tgpipe::lib_dgrad_export);
+  m.def("lib_dgrad_force(int mode) -> ()", &tgpipe::lib_dgrad_force);
   m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
   m.def("conv_gemm_sweep(int mode, Tensor x, Tensor weight, int[] geo, int reps) -> float[]");
   m.def("conv_gemm_plans_import(str text) -> int", &tgpipe::conv_gemm_plans_import);
