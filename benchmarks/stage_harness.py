@@ -33,12 +33,17 @@ def main() -> None:
     p.add_argument('--stages', type=int, nargs='*', default=None)
     p.add_argument('--checkpoint', default='except_last')
     p.add_argument('--out', default=None)
+    p.add_argument('--cell-streams', type=int, default=0,
+                   help='AmoebaNet: streams per cell (0: one stream; bench.py uses 3 eager)')
     args = p.parse_args()
 
     dev = torch.device('cuda', 0)
     model = unet() if args.model == 'unet' else amoebanetd(1000, 18, 256)
     shape = (3, 192, 192) if args.model == 'unet' else (3, 224, 224)
     model.to(dev).train()
+    if args.cell_streams and args.model == 'amoebanet':
+        from torchgpipe_amd.models.amoebanet import set_cell_streams
+        set_cell_streams(model, args.cell_streams)
     layers = list(model)
     mb = args.batch // args.chunks
     m = args.chunks

@@ -133,3 +133,51 @@ def test_fused_resnet50_matches_plain_model():
         assert rel_err(a, r) < max(1e-3, 8 * rel_err(b, r)), name
     for a, b, r in zip(bf, bp, b64):
         assert rel_err(a, r) < max(1e-5, 4 * rel_err(b, r))
+
+
+@pytest.mark.parametrize('shape', [(4, 256, 14), (2, 1024, 7)], ids=['256@14', '1024@7'])
+def test_residual_join_runs_conv3_bn3_add_relu_as_one_op(shape):
+    """A bottleneck's conv3, bn3, residual, relu3 (ops/fusion.py pending_join): the join's
+    output and every gradient against the fp64 plain bottleneck (ReLU decisions of the
+    fused forward)."""
+    from torchgpipe_amd.models.resnet import bottleneck
+    from torchgpipe_amd.skip.tracker import SkipTracker, use_skip_tracker
+    n, c, hw = shape
+    torch.manual_seed(0)
+    fused = bottleneck(c, c // 4, fused=True).cuda()
+    plain = bottleneck(c, c // 4, fused=False).cuda().double()
+    plain.load_state_dict(fused.state_dict())
+    with torch.no_grad():
+        for m in fused.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.5, 0.5)
+    plain.load_state_dict(fused.state_dict())
+    assert relink(fused) == 3
+    conv3 = fused.conv3
+    assert conv3.__dict__['_tgpipe_link'][2] is not None
+    x = torch.randn(n, c, hw, hw, device='cuda').relu().requires_grad_(True)
+    x64 = x.detach().double().requires_grad_(True)
+    with use_skip_tracker(SkipTracker()):
+        y = fused(x)
+    with use_skip_tracker(SkipTracker()):
+        y64 = plain(x64)
+    assert getattr(y, '_tgpipe_relu_done', False)
+    y64 = y64 * (y > 0).double()
+    assert rel_err(y, y64) < 1e-5
+    g = torch.randn_like(y)
+    y.backward(g)
+    y64.backward(g.double())
+    # relu1 / relu2 decide in fp64 on their own: the plain fp32 bottleneck's error against
+    # the same reference sets the scale of what those flips may cost
+    plain32 = copy.deepcopy(plain).float()
+    x32 = x.detach().clone().requires_grad_(True)
+    with use_skip_tracker(SkipTracker()):
+        y32 = plain32(x32)
+    (y32 * (y > 0).float()).backward(g)
+    gate = max(5e-5, 8 * rel_err(x32.grad, x64.grad))
+    assert rel_err(x.grad, x64.grad) < gate
+    for (name, p), q, r in zip(fused.named_parameters(), plain.parameters(),
+                               plain32.parameters()):
+        assert rel_err(p.grad, q.grad) < max(5e-5, 8 * rel_err(r.grad, q.grad)), name
+    assert rel_err(fused.bn3.running_var, plain.bn3.running_var) < 2e-6

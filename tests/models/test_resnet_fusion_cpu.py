@@ -35,3 +35,18 @@ def test_fused_layers_are_nn_subclasses():
     assert issubclass(ConvBN2d, nn.Conv2d)
     assert issubclass(BatchNormAct2d, nn.BatchNorm2d)
     assert issubclass(ReLU, nn.ReLU)
+
+
+def test_conv3_is_linked_to_its_residual_join():
+    """conv3, bn3, residual, relu3: conv3's link names the residual join that runs it
+    (ops/fusion.py pending_join); conv1 / conv2 link to their BatchNorm + ReLU only."""
+    model = build_resnet([1, 1, 1, 1], num_classes=10)
+    layers = list(model.children())
+    conv1, conv3, residual = layers[5], layers[11], layers[13]
+    assert conv1.__dict__['_tgpipe_link'][1:] == (True, None)
+    bn, relu, join = conv3.__dict__['_tgpipe_link']
+    assert bn is layers[12] and relu is False
+    assert join is getattr(residual, 'module', residual)
+    # split after bn3: the join is in another partition, conv3 keeps a plain BN link
+    relink(nn.Sequential(*layers[:13]))
+    assert conv3.__dict__['_tgpipe_link'][2] is None

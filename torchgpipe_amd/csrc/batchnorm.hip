@@ -563,7 +563,10 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
                        running_var, tracked, acc, zero2c, z, gamma, beta, add, y, pt);
   };
   const bool vec = (s & 3) == 0;
-  if (relu) {  // (ResNet's BatchNorm -> ReLU; never with a node sum)
+  if (relu && add) {  // ResNet's residual join relu(bn(z) + identity)
+    if (vec) go(bn_finalize_apply_kernel<true, true, true>);
+    else go(bn_finalize_apply_kernel<false, true, true>);
+  } else if (relu) {  // (ResNet's BatchNorm -> ReLU)
     if (vec) go(bn_finalize_apply_kernel<true, false, true>);
     else go(bn_finalize_apply_kernel<false, false, true>);
   } else if (vec && add) go(bn_finalize_apply_kernel<true, true, false>);

@@ -351,7 +351,8 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     TORCH_CHECK(add_c.sizes() == z.sizes(), "add must have the output's shape");
     ad = add_c.data_ptr<float>();
   }
-  TORCH_CHECK(!(relu_out && ad != nullptr), "relu_out with a node sum is not supported");
+  // relu_out with a node sum: relu(bn(z) + add) (ResNet's residual join); the caller masks
+  // the gradient with the saved output (the backward's re-derived mask cannot see `add`)
   auto y = at::empty_like(z);
   launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, n,
                            c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),

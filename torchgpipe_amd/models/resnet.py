@@ -19,8 +19,8 @@ from typing import Any, Generator, List, Optional
 from torch import Tensor, nn
 
 from torchgpipe_amd.models.flatten import flatten_sequential
-from torchgpipe_amd.ops.fusion import (BatchNormAct2d, ConvBN2d, ReLU, add_relu, relink,
-                                       relu_follows)
+from torchgpipe_amd.ops.fusion import (BatchNormAct2d, ConvBN2d, ReLU, add_relu,
+                                       pending_join, relink, relu_follows)
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
 __all__ = ['resnet50', 'resnet101', 'build_resnet']
@@ -35,8 +35,10 @@ class Identity(nn.Module):
 
 @skippable(pop=['identity'])
 class Residual(nn.Module):
-    # with a linked ReLU after it (ops/fusion.py relink): relu(x + identity) in one pass
+    # with a linked ReLU after it (ops/fusion.py relink): relu(x + identity) in one pass; with
+    # conv3 / bn3 linked before it too, relu(bn3(conv3(x)) + identity) as one op
     fuses_relu = True
+    fuses_residual_bn = True
 
     def __init__(self, downsample: Optional[nn.Module] = None) -> None:
         super().__init__()
@@ -47,7 +49,8 @@ class Residual(nn.Module):
         if self.downsample is not None:
             identity = self.downsample(identity)
         if relu_follows(self):
-            return add_relu(x, identity)
+            y = pending_join(x, self, identity)
+            return y if y is not None else add_relu(x, identity)
         return x + identity
 
 

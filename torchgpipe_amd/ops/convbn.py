@@ -129,10 +129,13 @@ class _ConvBN(torch.autograd.Function):
             bn.num_batches_tracked if track else None,
             float(bn.momentum) if bn.momentum is not None else 0.0, float(bn.eps), add,
             relu_out)
-        # (beta only for the ReLU mask of relu_out, re-derived from z in the backward)
-        ctx.save_for_backward(x, z, mean, invstd, sums, gamma, beta if relu_out else None,
-                              *weights)
-        ctx.relu_out = relu_out
+        # (beta only for the ReLU mask of relu_out, re-derived from z in the backward; with a
+        # node sum the mask comes from the saved output instead: relu(bn(z) + add))
+        out_mask = relu_out and add is not None
+        ctx.save_for_backward(x, z, mean, invstd, sums, gamma,
+                              beta if relu_out and not out_mask else None,
+                              y if out_mask else None, *weights)
+        ctx.relu_out = relu_out and not out_mask
         ctx.params = (gamma, beta) + weights  # gradient-accumulation fusion (ops/gradacc.py)
         ctx.caches = caches
         ctx.geo = geo
@@ -143,7 +146,9 @@ class _ConvBN(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy: Tensor):  # type: ignore[override]
-        x, z, mean, invstd, sums, gamma, beta, *weights = ctx.saved_tensors
+        x, z, mean, invstd, sums, gamma, beta, y, *weights = ctx.saved_tensors
+        if y is not None:  # relu(bn(z) + add): the gradient of both terms, masked once
+            dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
         need_dx = ctx.needs_input_grad[0]
         fused = [gradacc.target(p) for p in ctx.params]
         # the backward-data GEMM reads W^T: transposed once per step, not per micro-batch
@@ -192,7 +197,8 @@ def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.Batch
                  relu: bool = True, add: Optional[Tensor] = None,
                  relu_out: bool = False) -> Tensor:
     """``bn(cat([conv(relu(x) shifted by offset) for conv, offset in convs]))`` (+ ``add``),
-    followed by a ReLU when ``relu_out`` (ResNet's Conv-BN-ReLU; not with ``add``).
+    followed by a ReLU when ``relu_out`` (ResNet's Conv-BN-ReLU, and with ``add`` its
+    residual join ``relu(bn(conv3(x)) + identity)`` in the same normalise pass).
 
     ``convs`` are ``(conv, offset)`` pairs whose outputs are concatenated on channels
     (one pair for ReLU-Conv-BN, two for FactorizedReduce: offsets 0 and 1).  Runs the

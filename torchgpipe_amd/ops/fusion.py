@@ -45,12 +45,14 @@ from torchgpipe_amd.ops.conv import WinogradConv2d, wino_eligible
 from torchgpipe_amd.ops.convbn import (_bn_ok, fusable, gemm_conv2d, gemm_conv_eligible,
                                        relu_conv_bn)
 
-__all__ = ['ConvBN2d', 'BatchNormAct2d', 'ReLU', 'relink', 'bn_act', 'add_relu']
+__all__ = ['ConvBN2d', 'BatchNormAct2d', 'ReLU', 'relink', 'bn_act', 'add_relu',
+           'pending_join']
 
 _LINK = '_tgpipe_link'       # ConvBN2d -> (BatchNormAct2d, relu?)
 _RELU = '_tgpipe_relu_next'  # BatchNormAct2d -> a linked ReLU follows
 _DONE_BN = '_tgpipe_bn_done'    # tensor mark: id() of the BatchNorm already applied
 _DONE_RELU = '_tgpipe_relu_done'  # tensor mark: the ReLU after it too
+_PENDING = '_tgpipe_pending'  # tensor mark: (conv, bn) left for the residual join to run
 
 
 class _BNAct(torch.autograd.Function):
@@ -122,6 +124,27 @@ def add_relu(a: Tensor, b: Tensor) -> Tensor:
     return y
 
 
+def pending_join(x: Tensor, join: nn.Module, identity: Tensor) -> Optional[Tensor]:
+    """``relu(bn(conv(x)) + identity)`` when ``x`` is the input a linked :class:`ConvBN2d`
+    left for the residual join ``join`` (ResNet's ``conv3, bn3, residual, relu3``): one
+    implicit-GEMM convolution with the BatchNorm statistics in its epilogue and one
+    normalise + add + ReLU pass, so the BatchNorm output never round-trips through memory.
+    ``None`` when ``x`` carries no such pending work."""
+    pend = getattr(x, _PENDING, None)
+    if pend is None or pend[2] is not join:
+        return None
+    conv, bn, _ = pend
+    n, _, h, w = x.shape
+    if identity.shape != (n, conv.out_channels, h, w) or identity.dtype != x.dtype:
+        y = relu_conv_bn(x, [(conv, 0)], bn, relu=False) + identity
+        y = F.relu(y)
+    else:
+        y = relu_conv_bn(x, [(conv, 0)], bn, relu=False, add=identity.contiguous(),
+                         relu_out=True)
+    setattr(y, _DONE_RELU, True)
+    return y
+
+
 def relu_follows(module: nn.Module) -> bool:
     """Whether :func:`relink` linked a :class:`ReLU` after ``module`` (a layer that can apply
     it itself, e.g. ResNet's residual join: ``fuses_relu = True``)."""
@@ -141,7 +164,15 @@ class ConvBN2d(WinogradConv2d):
         wino = self.padding_mode == 'zeros' and wino_eligible(
             input, self.weight, self.stride, self.padding, self.dilation, self.groups)
         if link is not None and self.padding_mode == 'zeros':
-            bn, relu = link
+            bn, relu, join = link
+            if (join is not None and self.bias is None and _pointwise(self)
+                    and _native_bn_ok(bn, input) and fusable(input, [self], bn)):
+                # the residual join right after the BatchNorm runs this convolution, the
+                # BatchNorm, the identity add and the ReLU as one op (pending_join)
+                out = input.view_as(input)
+                setattr(out, _PENDING, (self, bn, join))
+                setattr(out, _DONE_BN, id(bn))
+                return out
             if self.bias is None and _native_bn_ok(bn, input):
                 if wino:
                     z = WinogradConv2d.forward(self, input)
@@ -204,6 +235,11 @@ def relink(module: nn.Module) -> int:
                     type(kids[i + 1]) is not BatchNormAct2d:
                 continue
             relu = i + 2 < len(kids) and type(kids[i + 2]) is ReLU
-            m.__dict__[_LINK] = (kids[i + 1], relu)
+            join = None
+            if not relu and i + 3 < len(kids) and type(kids[i + 3]) is ReLU:
+                inner = getattr(kids[i + 2], 'module', kids[i + 2])
+                if getattr(inner, 'fuses_residual_bn', False):
+                    join = inner  # conv, bn, residual join, relu: see pending_join
+            m.__dict__[_LINK] = (kids[i + 1], relu, join)
             linked += 1
     return linked
