@@ -69,15 +69,17 @@ UNET_EXPERIMENTS = {
 }
 # the reference's speed-up denominator: U-Net without GPipe, one GPU
 UNET_BASELINE = dict(name='baseline', batch=40, ref=28.500)
-# AmoebaNet tuned balances: profiles/amoebanet_layer_profile.json (micro-batch 40) through
-# the same simulator (n2 535 vs 492, n4 851 vs 814, n8 1539 vs 1503 simulated samples/s).
+# AmoebaNet tuned balances: every layer timed as its own stage at micro-batch 40 (32
+# micro-batches, three-stream cells: profiles/r3/stage_harness_amoeba_layers_mb40.json),
+# min-max partitions by scripts/balance_from_layers.py: predicted n2 854 vs 735, n4 1353 vs
+# 1217, n8 2536 vs 2118 samples/s for the reference balances (profiles/r3/speedup_prediction.md).
 AMOEBA_EXPERIMENTS = {
     1: dict(name='n1m32', batch=640, chunks=32, balance=[24], tuned=[24], ref=None),
-    2: dict(name='n2m32', batch=1280, chunks=32, balance=[9, 15], tuned=[10, 14], ref=47.386),
-    4: dict(name='n4m32', batch=1152, chunks=32, balance=[3, 6, 7, 8], tuned=[5, 5, 6, 8],
+    2: dict(name='n2m32', batch=1280, chunks=32, balance=[9, 15], tuned=[11, 13], ref=47.386),
+    4: dict(name='n4m32', batch=1152, chunks=32, balance=[3, 6, 7, 8], tuned=[5, 6, 6, 7],
             ref=72.412),
     8: dict(name='n8m32', batch=1280, chunks=32, balance=[2, 2, 2, 3, 3, 4, 4, 4],
-            tuned=[2, 2, 3, 3, 3, 3, 4, 4], ref=132.413),
+            tuned=[2, 3, 3, 3, 3, 3, 3, 4], ref=132.413),
 }
 # the reference's AmoebaNet speed-up denominator (benchmarks/amoebanetd-speed/main.py:39-45)
 AMOEBA_N2M1 = dict(name='n2m1', batch=96, chunks=1, balance=[7, 17], ref=26.733)
