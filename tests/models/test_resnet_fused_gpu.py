@@ -163,6 +163,8 @@ def test_residual_join_runs_conv3_bn3_add_relu_as_one_op(shape):
     with use_skip_tracker(SkipTracker()):
         y64 = plain(x64)
     assert getattr(y, '_tgpipe_relu_done', False)
+    # the identity's gradient goes to conv1's backward-data GEMM (GradSink)
+    assert getattr(x, '_tgpipe_grad_sink').claimed
     y64 = y64 * (y > 0).double()
     assert rel_err(y, y64) < 1e-5
     g = torch.randn_like(y)

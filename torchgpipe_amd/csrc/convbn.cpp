@@ -541,7 +541,8 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                                         at::TensorList weights_t, bool defer_wgrad,
                                         const c10::List<c10::optional<at::Tensor>>& slabs,
                                         at::IntArrayRef slab_first,
-                                        const c10::optional<at::Tensor>& beta, bool relu_out) {
+                                        const c10::optional<at::Tensor>& beta, bool relu_out,
+                                        const c10::optional<at::Tensor>& dx_into) {
   auto x = x_in.contiguous();
   // dy is read in place when it is a channel slice (a concatenated cell output's gradient)
   int64_t dy_img = image_stride_if_channel_slice(dy_in);
@@ -587,11 +588,21 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                      opt_ptr(beta, "beta", x, c));
   std::vector<at::Tensor> out;
   at::Tensor dx;
-  auto ours = [&]() -> at::Tensor {
+  // `dx_into`: a gradient of the same input from another consumer (ResNet's identity path,
+  // ops/fusion.py): the backward-data GEMM accumulates onto it instead of autograd adding
+  // the two afterwards
+  const bool has_into = dx_into.has_value() && dx_into->defined();
+  if (has_into) {
+    check_f32(*dx_into, "dx_into", x);
+    TORCH_CHECK(dx_into->sizes() == x.sizes(), "dx_into must have the input's shape");
+  }
+  auto ours_into = [&](bool use_into) -> at::Tensor {
     std::vector<ConvGemmPlan> plans;
     bool zero = false;
     for (const auto& g : p.geo) zero = zero || conv_gemm_plan(1, g).scatter;
-    at::Tensor d = zero ? at::zeros_like(x) : at::empty_like(x);  // stride holes receive nothing
+    at::Tensor d = use_into ? *dx_into
+                            : (zero ? at::zeros_like(x) : at::empty_like(x));  // stride holes
+    zero = zero || use_into;  // (from here: accumulate onto d)
     // the backward-data A operand is W^T: one small transpose per weight, then the
     // GEMM streams K-contiguous rows instead of gathering a column per element
     // (`weights_t`: the caller's per-step cached transposes, ops/conv.py _TransformCache)
@@ -625,11 +636,17 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
     return d;
   };
   if (need_dx) {
+    auto ours = [&]() { return ours_into(false); };  // (timing trials never touch dx_into)
     const bool lib = p.geo.size() == 1 && lib_dgrad_eligible(p.geo[0]) &&
                      lib_dgrad_chosen(p.geo[0], x, ours, [&] {
                        return lib_dgrad(dz, x, weights[0], p.geo[0]);
                      });
-    dx = lib ? lib_dgrad(dz, x, weights[0], p.geo[0]) : ours();
+    if (lib) {
+      dx = lib_dgrad(dz, x, weights[0], p.geo[0]);
+      if (has_into) dx = dx_into->add_(dx);
+    } else {
+      dx = ours_into(has_into);
+    }
   }
   out.push_back(dx);
   out.push_back(dgamma);
@@ -1258,7 +1275,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("convbn_backward(Tensor dy, Tensor x, Tensor z, Tensor mean, Tensor invstd, "
         "Tensor(a!) sums, Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx, "
         "Tensor?[] accum, Tensor[] weights_t, bool defer_wgrad, Tensor?[] slabs, "
-        "int[] slab_first, Tensor? beta=None, bool relu_out=False) -> Tensor[]");
+        "int[] slab_first, Tensor? beta=None, bool relu_out=False, Tensor? dx_into=None) "
+        "-> Tensor[]");
   m.def("convbn_group_forward(Tensor x, Tensor w_cat, int[] geo, bool relu, int[] channels, "
         "Tensor?[] gammas, Tensor?[] betas, Tensor?[] running_means, Tensor?[] running_vars, "
         "Tensor?[] tracked, float momentum, float eps) -> Tensor[]");

@@ -116,11 +116,26 @@ def _wgrad_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     return stream
 
 
+class GradSink:
+    """A gradient handed from one fused op's backward to another's, outside autograd: ResNet's
+    residual join deposits the identity's gradient, the block's first convolution (which
+    reads the same tensor) accumulates it into its backward-data GEMM -- one pass instead of
+    autograd's separate sum of the two gradients (ops/fusion.py pending_join)."""
+
+    __slots__ = ('grad', 'claimed')
+
+    def __init__(self) -> None:
+        self.grad: Optional[Tensor] = None
+        self.claimed = False
+
+
 class _ConvBN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: Tensor, add: Optional[Tensor], gamma: Optional[Tensor],  # type: ignore[override]
                 beta: Optional[Tensor], bn: nn.BatchNorm2d, geo: List[int], relu: bool,
-                relu_out: bool, caches: List[_TransformCache], *weights: Tensor) -> Tensor:
+                relu_out: bool, caches: List[_TransformCache], sinks: Tuple[Optional[GradSink],
+                                                                            Optional[GradSink]],
+                *weights: Tensor) -> Tensor:
         ops = _ext.require(x)
         track = bn.track_running_stats and bn.running_mean is not None
         y, z, mean, invstd, sums = ops.convbn_forward(
@@ -142,6 +157,7 @@ class _ConvBN(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_add = add is not None
         ctx.n_weights = len(weights)
+        ctx.sink_in, ctx.sink_out = sinks  # (accumulate from / deposit the add's gradient)
         return y
 
     @staticmethod
@@ -164,10 +180,20 @@ class _ConvBN(torch.autograd.Function):
             firsts.append(int(first))
         if all(sb is None for sb in slabs):
             slabs, firsts = [], []
+        dx_into = None
+        if ctx.sink_in is not None and ctx.sink_in.grad is not None:
+            dx_into, ctx.sink_in.grad = ctx.sink_in.grad, None
+            if not need_dx:
+                dx_into = None
         dx, dgamma, dbeta, *dws = ops.convbn_backward(
             dy, x, z, mean, invstd, sums, gamma, weights, ctx.geo, ctx.relu, need_dx,
             [into for _, into in fused], wts, side is not None, slabs, firsts, beta,
-            ctx.relu_out)
+            ctx.relu_out, dx_into)
+        dadd = dy if ctx.has_add and ctx.needs_input_grad[1] else None
+        if dadd is not None and ctx.sink_out is not None:
+            ctx.sink_out.grad = dadd  # the reader's backward adds it (see GradSink)
+            dadd = None
+        ctx.sink_in = ctx.sink_out = None
         if side is not None:
             # weight gradients on the side stream (written into .grad by the kernels)
             dz = dws[0]
@@ -187,15 +213,16 @@ class _ConvBN(torch.autograd.Function):
                 grads[k] = None
         del ctx.params, ctx.caches
         dgamma, dbeta, *dws = grads
-        return (dx if need_dx else None, dy if ctx.has_add else None,
+        return (dx if need_dx else None, dadd,
                 dgamma if ctx.needs_input_grad[2] else None,
-                dbeta if ctx.needs_input_grad[3] else None, None, None, None, None, None,
+                dbeta if ctx.needs_input_grad[3] else None, None, None, None, None, None, None,
                 *dws)
 
 
 def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.BatchNorm2d,
                  relu: bool = True, add: Optional[Tensor] = None,
-                 relu_out: bool = False) -> Tensor:
+                 relu_out: bool = False, sink_in: Optional[GradSink] = None,
+                 sink_out: Optional[GradSink] = None) -> Tensor:
     """``bn(cat([conv(relu(x) shifted by offset) for conv, offset in convs]))`` (+ ``add``),
     followed by a ReLU when ``relu_out`` (ResNet's Conv-BN-ReLU, and with ``add`` its
     residual join ``relu(bn(conv3(x)) + identity)`` in the same normalise pass).
@@ -209,7 +236,8 @@ def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.Batch
         geo += _geo(conv, offset)
     weights = [conv.weight for conv, _ in convs]
     return _ConvBN.apply(x, add, bn.weight, bn.bias, bn, geo, relu, relu_out,
-                         [_weight_cache(conv) for conv, _ in convs], *weights)
+                         [_weight_cache(conv) for conv, _ in convs], (sink_in, sink_out),
+                         *weights)
 
 
 def _weight_cache(conv: nn.Module) -> _TransformCache:

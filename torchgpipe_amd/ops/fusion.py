@@ -42,8 +42,8 @@ import torch.nn.functional as F
 
 from torchgpipe_amd.ops import _ext
 from torchgpipe_amd.ops.conv import WinogradConv2d, wino_eligible
-from torchgpipe_amd.ops.convbn import (_bn_ok, fusable, gemm_conv2d, gemm_conv_eligible,
-                                       relu_conv_bn)
+from torchgpipe_amd.ops.convbn import (GradSink, _bn_ok, fusable, gemm_conv2d,
+                                       gemm_conv_eligible, relu_conv_bn)
 
 __all__ = ['ConvBN2d', 'BatchNormAct2d', 'ReLU', 'relink', 'bn_act', 'add_relu',
            'pending_join']
@@ -53,6 +53,7 @@ _RELU = '_tgpipe_relu_next'  # BatchNormAct2d -> a linked ReLU follows
 _DONE_BN = '_tgpipe_bn_done'    # tensor mark: id() of the BatchNorm already applied
 _DONE_RELU = '_tgpipe_relu_done'  # tensor mark: the ReLU after it too
 _PENDING = '_tgpipe_pending'  # tensor mark: (conv, bn) left for the residual join to run
+_SINK = '_tgpipe_grad_sink'  # tensor mark: a fused reader accepts this tensor's other gradient
 
 
 class _BNAct(torch.autograd.Function):
@@ -139,8 +140,15 @@ def pending_join(x: Tensor, join: nn.Module, identity: Tensor) -> Optional[Tenso
         y = relu_conv_bn(x, [(conv, 0)], bn, relu=False) + identity
         y = F.relu(y)
     else:
+        # identity is the block input that conv1 read: its gradient goes to conv1's
+        # backward-data GEMM (GradSink) instead of through autograd's sum
+        sink = getattr(identity, _SINK, None)
+        if sink is not None and (sink.claimed or not identity.is_contiguous()):
+            sink = None
+        if sink is not None:
+            sink.claimed = True
         y = relu_conv_bn(x, [(conv, 0)], bn, relu=False, add=identity.contiguous(),
-                         relu_out=True)
+                         relu_out=True, sink_out=sink)
     setattr(y, _DONE_RELU, True)
     return y
 
@@ -178,7 +186,14 @@ class ConvBN2d(WinogradConv2d):
                     z = WinogradConv2d.forward(self, input)
                     return _mark(bn_act(z, bn, relu), bn, relu)
                 if _pointwise(self) and fusable(input, [self], bn):
-                    y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu)
+                    sink = None
+                    if relu and input.requires_grad and input.is_contiguous():
+                        # (a residual join reading the same tensor may hand its gradient
+                        # over: accumulated by this op's backward-data GEMM)
+                        sink = GradSink()
+                        setattr(input, _SINK, sink)
+                    y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu,
+                                     sink_in=sink)
                     return _mark(y, bn, relu)
                 z = nn.Conv2d.forward(self, input)  # strided: MIOpen
                 return _mark(bn_act(z, bn, relu), bn, relu)
