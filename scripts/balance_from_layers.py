@@ -26,11 +26,13 @@ def main() -> None:
     p.add_argument('--batch', type=int, nargs='+', required=True,
                    help='global batch per depth (one value, or one per --parts entry)')
     p.add_argument('--chunks', type=int, required=True)
+    p.add_argument('--scale', type=float, default=1.0,
+                   help='multiply the profiled times (a profile taken with fewer micro-batches)')
     p.add_argument('--ref', type=str, nargs='*', default=[],
                    help="reference balances to price too, e.g. '2,2,2,3,3,4,4,4'")
     a = p.parse_args()
     stages = json.load(open(a.profile))['stages']
-    layers = [s['device_ms'] for s in sorted(stages, key=lambda s: s['layers'][0])]
+    layers = [s['device_ms'] * a.scale for s in sorted(stages, key=lambda s: s['layers'][0])]
     batches = a.batch if len(a.batch) == len(a.parts) else a.batch * len(a.parts)
     refs = {len(b.split(',')): [int(v) for v in b.split(',')] for b in a.ref}
     m = a.chunks
