@@ -164,7 +164,9 @@ def test_residual_join_runs_conv3_bn3_add_relu_as_one_op(shape):
         y64 = plain(x64)
     assert getattr(y, '_tgpipe_relu_done', False)
     # the identity's gradient goes to conv1's backward-data GEMM (GradSink)
-    assert getattr(x, '_tgpipe_grad_sink').claimed
+    from torchgpipe_amd.ops import fusion
+    sink = getattr(x, '_tgpipe_grad_sink', None)
+    assert (sink is not None and sink.claimed) or not fusion.GRAD_SINK
     y64 = y64 * (y > 0).double()
     assert rel_err(y, y64) < 1e-5
     g = torch.randn_like(y)

@@ -34,6 +34,7 @@ partition after splitting (and after DeferredBatchNorm conversion, whose BatchNo
 not linked).  Outside training mode, on the CPU, or for non-fp32 tensors every layer runs
 its plain PyTorch forward.
 """
+import os
 from typing import Optional
 
 import torch
@@ -54,6 +55,9 @@ _DONE_BN = '_tgpipe_bn_done'    # tensor mark: id() of the BatchNorm already app
 _DONE_RELU = '_tgpipe_relu_done'  # tensor mark: the ReLU after it too
 _PENDING = '_tgpipe_pending'  # tensor mark: (conv, bn) left for the residual join to run
 _SINK = '_tgpipe_grad_sink'  # tensor mark: a fused reader accepts this tensor's other gradient
+# TGPIPE_GRAD_SINK=0: the residual join returns the identity's gradient to autograd (which
+# sums it with conv1's) instead of handing it to conv1's backward-data GEMM
+GRAD_SINK = os.environ.get('TGPIPE_GRAD_SINK', '1') != '0'
 
 
 class _BNAct(torch.autograd.Function):
@@ -187,7 +191,7 @@ class ConvBN2d(WinogradConv2d):
                     return _mark(bn_act(z, bn, relu), bn, relu)
                 if _pointwise(self) and fusable(input, [self], bn):
                     sink = None
-                    if relu and input.requires_grad and input.is_contiguous():
+                    if GRAD_SINK and relu and input.requires_grad and input.is_contiguous():
                         # (a residual join reading the same tensor may hand its gradient
                         # over: accumulated by this op's backward-data GEMM)
                         sink = GradSink()
