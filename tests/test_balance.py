@@ -209,3 +209,30 @@ def test_balance_by_size_param_scale_tradeoff():
     sample = torch.rand(1, requires_grad=True)
     assert balance_by_size(2, model, sample, param_scale=0) == [2, 4]
     assert balance_by_size(2, model, sample, param_scale=100) == [4, 2]
+
+
+def test_balance_from_layers_script(tmp_path):
+    """scripts/balance_from_layers.py: min-max partition of a per-layer stage profile and
+    the GPipe-bubble throughput prediction, for the tuned and a reference balance."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    times = [4.0, 1.0, 1.0, 1.0, 1.0, 4.0]
+    prof = {'stages': [{'stage': i, 'layers': [i, i + 1], 'device_ms': t}
+                       for i, t in enumerate(times)]}
+    path = tmp_path / 'profile.json'
+    path.write_text(json.dumps(prof))
+    out = subprocess.run([sys.executable, os.path.join(root, 'scripts', 'balance_from_layers.py'),
+                          str(path), '--parts', '2', '3', '--batch', '64', '--chunks', '4',
+                          '--ref', '3,3', '--scale', '2'],
+                         check=True, capture_output=True, text=True).stdout
+    rows = [json.loads(line) for line in out.splitlines()]
+    tuned2 = next(r for r in rows if r['parts'] == 2 and r['balance_source'] == 'tuned')
+    assert tuned2['balance'] == [3, 3] and tuned2['max_stage_ms'] == 12.0
+    # bubble: max stage x (m + n - 1) / m = 12 ms x 5 / 4
+    assert tuned2['predicted_samples_per_sec'] == round(64 / 0.015, 1)
+    tuned3 = next(r for r in rows if r['parts'] == 3)
+    assert max(tuned3['stage_ms']) == 8.0
+    assert any(r['balance_source'] == 'ref' and r['balance'] == [3, 3] for r in rows)
