@@ -35,7 +35,7 @@ not linked).  Outside training mode, on the CPU, or for non-fp32 tensors every l
 its plain PyTorch forward.
 """
 import os
-from typing import Optional
+from typing import Callable, Dict, Optional
 
 import torch
 from torch import Tensor, nn
@@ -168,6 +168,61 @@ def _pointwise(conv: nn.Conv2d) -> bool:
             and tuple(conv.padding) == (0, 0))  # type: ignore[arg-type]
 
 
+# strided convolutions: geometry -> whether the fused implicit-GEMM op (its backward-data
+# on MIOpen where that timed faster) beat MIOpen + the native BatchNorm, forward + backward
+_STRIDED: Dict[tuple, bool] = {}
+STRIDED_CHOICE = os.environ.get('TGPIPE_STRIDED_CHOICE', '1') != '0'
+
+
+def _strided_fused(conv: nn.Conv2d, bn: nn.BatchNorm2d, x: Tensor, relu: bool) -> bool:
+    """Time both ways of one strided Conv-BN(-ReLU) on the first eager call of its geometry
+    (on copies of the layers: the real ones' parameters, gradients and running statistics
+    are untouched); inside a stream capture an undecided geometry stays on MIOpen.
+    ResNet-101 shapes split both ways (``profiles/r3/resnet_strided_probe.jsonl``)."""
+    if not STRIDED_CHOICE:
+        return False
+    key = (tuple(x.shape), conv.out_channels, tuple(conv.kernel_size), tuple(conv.stride),
+           tuple(conv.padding), relu, x.device)  # type: ignore[arg-type]
+    hit = _STRIDED.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    import copy
+    c2, b2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    for m in (c2, b2):
+        m.__dict__.pop(_LINK, None)
+        m.__dict__.pop('_wt_cache', None)
+    xg = x.detach().clone().requires_grad_(x.requires_grad)
+
+    def library() -> Tensor:
+        return bn_act(F.conv2d(xg, c2.weight, None, c2.stride, c2.padding), b2, relu)
+
+    def fused() -> Tensor:
+        return relu_conv_bn(xg, [(c2, 0)], b2, relu=False, relu_out=relu)
+
+    with torch.enable_grad():
+        dy = torch.randn_like(library())
+
+        def timed(fn: Callable[[], Tensor]) -> float:
+            best = float('inf')
+            for rep in range(3):  # first: warm-up (plans, MIOpen's find step)
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record()
+                fn().backward(dy)
+                b.record()
+                b.synchronize()
+                if rep:
+                    best = min(best, a.elapsed_time(b))
+            return best
+
+        lib_ms, fused_ms = timed(library), timed(fused)
+    pick = fused_ms < 0.97 * lib_ms
+    _STRIDED[key] = pick
+    return pick
+
+
 class ConvBN2d(WinogradConv2d):
     """``nn.Conv2d`` (same parameters) that runs its linked BatchNorm (and ReLU) with it."""
 
@@ -198,6 +253,9 @@ class ConvBN2d(WinogradConv2d):
                         setattr(input, _SINK, sink)
                     y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu,
                                      sink_in=sink)
+                    return _mark(y, bn, relu)
+                if fusable(input, [self], bn) and _strided_fused(self, bn, input, relu):
+                    y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu)
                     return _mark(y, bn, relu)
                 z = nn.Conv2d.forward(self, input)  # strided: MIOpen
                 return _mark(bn_act(z, bn, relu), bn, relu)
