@@ -171,7 +171,8 @@ def _pointwise(conv: nn.Conv2d) -> bool:
 # strided convolutions: geometry -> whether the fused implicit-GEMM op (its backward-data
 # on MIOpen where that timed faster) beat MIOpen + the native BatchNorm, forward + backward
 _STRIDED: Dict[tuple, bool] = {}
-STRIDED_CHOICE = os.environ.get('TGPIPE_STRIDED_CHOICE', '1') != '0'
+# (opt-in, TGPIPE_STRIDED_CHOICE=1: not yet measured on the GPU; default MIOpen + BN)
+STRIDED_CHOICE = os.environ.get('TGPIPE_STRIDED_CHOICE', '0') != '0'
 
 
 def _strided_fused(conv: nn.Conv2d, bn: nn.BatchNorm2d, x: Tensor, relu: bool) -> bool:
