@@ -5,7 +5,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from torchgpipe_amd.ops import _ext, dbn, fused, misc, philox
+from torchgpipe_amd.ops import _ext, fused, misc, philox
 from torchgpipe_amd.ops import dropout as dropout_ops
 
 pytestmark = pytest.mark.gpu
@@ -80,32 +80,6 @@ def test_drop_norm_act_module_replays_under_tape():
     c = fused.drop_norm_act(x, 0.5, training=True)
     assert torch.equal(a, b)
     assert not torch.equal(a, c)
-
-
-@pytest.mark.parametrize('shape', [(4, 16, 12, 12), (3, 7, 5, 5), (2, 64, 56, 56), (8, 3, 1),
-                                   (2, 3, 80, 80), (3, 5, 67, 67), (40, 1024, 14, 14)])
-def test_dbn_track_and_commit(shape):
-    x = torch.randn(shape, device=cuda) * 2 + 0.5
-    c = shape[1]
-    s = torch.zeros(c, device=cuda)
-    sq = torch.zeros(c, device=cuda)
-    dbn.track(x, s, sq)
-    dbn.track(x * 0.5, s, sq)
-    dims = [0] + list(range(2, x.dim()))
-    want_s = x.sum(dims) + (x * 0.5).sum(dims)
-    want_sq = (x * x).sum(dims) + (x * x * 0.25).sum(dims)
-    torch.testing.assert_close(s, want_s, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(sq, want_sq, rtol=1e-4, atol=1e-3)
-
-    rm = torch.zeros(c, device=cuda)
-    rv = torch.ones(c, device=cuda)
-    count = 2 * x.numel() // c
-    rm_ref, rv_ref, s_ref, sq_ref = rm.cpu(), rv.cpu(), s.cpu().clone(), sq.cpu().clone()
-    dbn.commit(s, sq, rm, rv, count, 0.1)
-    dbn.commit(s_ref, sq_ref, rm_ref, rv_ref, count, 0.1)
-    torch.testing.assert_close(rm.cpu(), rm_ref, rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(rv.cpu(), rv_ref, rtol=1e-5, atol=1e-6)
-    assert s.abs().sum().item() == 0 and sq.abs().sum().item() == 0
 
 
 @pytest.mark.parametrize('n', [1, 7, 4096, 100003])

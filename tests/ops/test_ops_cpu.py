@@ -2,7 +2,7 @@
 import torch
 import torch.nn.functional as F
 
-from torchgpipe_amd.ops import dbn, fused, misc, philox
+from torchgpipe_amd.ops import fused, misc, philox
 from torchgpipe_amd.ops.dropout import dropout
 from torchgpipe_amd.utils.rng import RngTape
 
@@ -65,18 +65,6 @@ def test_dropout_reference():
     assert abs(kept - 0.7) < 0.02
     torch.testing.assert_close(y[y != 0], torch.full_like(y[y != 0], 1 / 0.7))
     assert dropout(x, 0.3, training=False) is x
-
-
-def test_dbn_cpu_track_commit():
-    x = torch.randn(4, 3, 5, 5) * 3 + 1
-    s, sq = torch.zeros(3), torch.zeros(3)
-    dbn.track(x, s, sq)
-    torch.testing.assert_close(s, x.sum((0, 2, 3)))
-    rm, rv = torch.zeros(3), torch.ones(3)
-    dbn.commit(s, sq, rm, rv, x.numel() // 3, 1.0)
-    torch.testing.assert_close(rm, x.mean((0, 2, 3)))
-    torch.testing.assert_close(rv, x.transpose(0, 1).reshape(3, -1).var(1))
-    assert s.abs().sum() == 0
 
 
 def test_pack_unpack_cpu():

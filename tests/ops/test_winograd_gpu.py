@@ -261,3 +261,25 @@ def test_batched_gemm_tile_shapes_and_splits(waves, bn, sub, splits):
     want = _ref(x, wt)
     torch.testing.assert_close(got.double(), want, rtol=1e-4,
                                atol=2e-5 * (want.abs().max().item() + 1))
+
+
+@pytest.mark.parametrize('kind', ['winograd', 'gemm'])
+def test_retain_graph_second_backward_accumulates(kind):
+    """A second backward through the same graph (``retain_graph=True``) doubles every
+    gradient: the fused ``.grad`` accumulation of the first pass must not break the second
+    (it falls back to returning the weight gradient to autograd)."""
+    from torchgpipe_amd.ops.convbn import GemmConv2d
+    torch.manual_seed(0)
+    if kind == 'winograd':
+        conv = WinogradConv2d(32, 64, 3, padding=1, bias=False).to(cuda)
+        x = torch.randn(2, 32, 24, 24, device=cuda, requires_grad=True)
+    else:
+        conv = GemmConv2d(64, 8, kernel_size=1, bias=False).to(cuda)
+        x = torch.randn(2, 64, 24, 24, device=cuda, requires_grad=True)
+    y = conv(x)
+    dy = torch.randn_like(y)
+    y.backward(dy, retain_graph=True)
+    gw1, gx1 = conv.weight.grad.clone(), x.grad.clone()
+    y.backward(dy)
+    torch.testing.assert_close(conv.weight.grad, 2 * gw1, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad, 2 * gx1, rtol=1e-5, atol=1e-5)

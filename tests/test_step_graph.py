@@ -158,6 +158,26 @@ def test_big_stack_worker_runs_calls_and_reraises():
         call_with_big_stack(lambda: 1 / 0)
 
 
+def test_big_stack_worker_keeps_the_callers_autograd_state():
+    """Grad mode, inference mode and autocast follow the call to the worker thread, and a
+    call made from the worker itself runs in place instead of deadlocking."""
+    from torchgpipe_amd.utils.bigstack import call_with_big_stack
+
+    def state():
+        return (torch.is_grad_enabled(), torch.is_inference_mode_enabled(),
+                torch.is_autocast_enabled('cpu'), torch.get_autocast_dtype('cpu'))
+
+    assert call_with_big_stack(state)[:3] == (True, False, False)
+    with torch.no_grad():
+        assert call_with_big_stack(state)[0] is False
+    with torch.inference_mode():
+        assert call_with_big_stack(state)[1] is True
+    with torch.autocast('cpu', dtype=torch.bfloat16):
+        got = call_with_big_stack(state)
+        assert got[2] is True and got[3] == torch.bfloat16
+    assert call_with_big_stack(lambda: call_with_big_stack(lambda: 5)) == 5
+
+
 @pytest.mark.gpu
 def test_deep_two_stream_graph_replays_from_the_big_stack_thread():
     """A captured graph of ~40 k kernels forked and joined across two streams (the shape

@@ -22,34 +22,6 @@ void check_f32_gpu(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
-void dbn_track(const at::Tensor& x, at::Tensor& sum, at::Tensor& sumsq) {
-  check_f32_gpu(x, "x");
-  check_f32_gpu(sum, "sum");
-  check_f32_gpu(sumsq, "sumsq");
-  TORCH_CHECK(x.dim() >= 2, "x must be at least 2-D");
-  const int64_t n = x.size(0), c = x.size(1);
-  const int64_t s = c == 0 || n == 0 ? 0 : x.numel() / (n * c);
-  TORCH_CHECK(sum.numel() == c && sumsq.numel() == c, "stat buffers must have C elements");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  launch_dbn_track(x.data_ptr<float>(), sum.data_ptr<float>(), sumsq.data_ptr<float>(), n, c, s,
-                   stream_of(x));
-}
-
-void dbn_commit(at::Tensor& sum, at::Tensor& sumsq, at::Tensor& running_mean,
-                at::Tensor& running_var, double count, double momentum) {
-  check_f32_gpu(sum, "sum");
-  check_f32_gpu(sumsq, "sumsq");
-  check_f32_gpu(running_mean, "running_mean");
-  check_f32_gpu(running_var, "running_var");
-  const int64_t c = sum.numel();
-  TORCH_CHECK(sumsq.numel() == c && running_mean.numel() == c && running_var.numel() == c,
-              "all buffers must have C elements");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(sum.device());
-  launch_dbn_commit(sum.data_ptr<float>(), sumsq.data_ptr<float>(),
-                    running_mean.data_ptr<float>(), running_var.data_ptr<float>(), c, count,
-                    momentum, stream_of(sum));
-}
-
 std::vector<at::Tensor> dna_forward(const at::Tensor& x, double p, double eps, double slope,
                                     int64_t seed, int64_t offset, bool dropout) {
   check_f32_gpu(x, "x");
@@ -376,9 +348,6 @@ at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
 }  // namespace tgpipe
 
 TORCH_LIBRARY(tgpipe, m) {
-  m.def("dbn_track(Tensor x, Tensor(a!) sum, Tensor(b!) sumsq) -> ()");
-  m.def("dbn_commit(Tensor(a!) sum, Tensor(b!) sumsq, Tensor(c!) running_mean, "
-        "Tensor(d!) running_var, float count, float momentum) -> ()");
   m.def("dna_forward(Tensor x, float p, float eps, float slope, int seed, int offset, "
         "bool dropout) -> Tensor[]");
   m.def("dna_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor scale, "
@@ -401,8 +370,6 @@ TORCH_LIBRARY(tgpipe, m) {
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {
-  m.impl("dbn_track", &tgpipe::dbn_track);
-  m.impl("dbn_commit", &tgpipe::dbn_commit);
   m.impl("dna_forward", &tgpipe::dna_forward);
   m.impl("dna_backward", &tgpipe::dna_backward);
   m.impl("dropout", &tgpipe::dropout);

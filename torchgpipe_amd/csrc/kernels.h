@@ -9,14 +9,6 @@
 
 namespace tgpipe {
 
-// K1: per-channel sum / sum of squares of x[N, C, S] accumulated into sum[C], sumsq[C].
-void launch_dbn_track(const float* x, float* sum, float* sumsq, int64_t n, int64_t c, int64_t s,
-                      hipStream_t stream);
-
-// K2: running stats EMA from accumulated sums; zeroes the sums.
-void launch_dbn_commit(float* sum, float* sumsq, float* running_mean, float* running_var,
-                       int64_t c, double count, double momentum, hipStream_t stream);
-
 // Fused Dropout2d(p) -> InstanceNorm2d(eps, affine=False) -> LeakyReLU(slope) over
 // planes x[P, S] (P = N*C, S = H*W).  Saves per-plane mean (of x), rstd (of the
 // dropped-out input) and the dropout scale (0 or 1/(1-p)).

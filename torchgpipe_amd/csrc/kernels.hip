@@ -1,7 +1,5 @@
 // HIP kernels of torchgpipe_amd, written for gfx950 (CDNA4, wave64, 256 CUs).
 //
-//   K1  dbn_track        DeferredBatchNorm per-channel Σx, Σx² (one read pass)
-//   K2  dbn_commit       running-stat EMA + accumulator reset (one launch)
 //   K3  dna_forward      fused Dropout2d → InstanceNorm2d → LeakyReLU (U-Net cell)
 //   K3b dna_backward     its backward (mask regenerated from saved scale)
 //   K4  dropout          elementwise inverted dropout, explicit Philox (seed, offset)
@@ -11,7 +9,6 @@
 // Design notes (see /opt/skills guides, Appendix B "Reduction" / G13):
 // * every streaming access is a 16-byte float4 per lane when the layout allows;
 // * reductions: wave64 __shfl_xor tree, then LDS across the waves of a block,
-//   then (K1 only) one fp32 atomic per block and channel;
 // * K3 keeps the whole H*W plane of one (n, c) pair in VGPRs (up to 36 floats
 //   per lane for a 192x192 plane on a 1024-lane group), so the input is read
 //   from HBM exactly once in forward (stats + normalise from registers) and
@@ -44,137 +41,6 @@ __device__ __forceinline__ float group_sum_in_wave(float v) {
 }
 
 inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
-
-// ---------------------------------------------------------------------------------------------
-// K1: DeferredBatchNorm tracking.  Grid (nsplit, C); block 256.  Each block walks work items
-// (n, chunk of CH elements of the S-long slab of channel c) strided by nsplit.
-// ---------------------------------------------------------------------------------------------
-constexpr int kTrackThreads = 256;
-constexpr int kTrackUnroll = 4;
-constexpr int kTrackChunk = kTrackThreads * 4 * kTrackUnroll;  // 4096 elements
-
-template <bool VEC>
-__global__ __launch_bounds__(kTrackThreads) void dbn_track_kernel(
-    const float* __restrict__ x, float* __restrict__ sum, float* __restrict__ sumsq, int64_t n,
-    int64_t c, int64_t s, int64_t chunks_per_n, int nsplit) {
-  const int ch_idx = blockIdx.y;
-  const int tid = threadIdx.x;
-  float a = 0.f, b = 0.f;
-  const int64_t items = n * chunks_per_n;
-  for (int64_t it = blockIdx.x; it < items; it += nsplit) {
-    const int64_t ni = it / chunks_per_n;
-    const int64_t s0 = (it % chunks_per_n) * kTrackChunk;
-    const float* base = x + (ni * c + ch_idx) * s;
-    if (VEC) {
-      float4 v[kTrackUnroll];
-#pragma unroll
-      for (int k = 0; k < kTrackUnroll; ++k) {
-        const int64_t idx = s0 + static_cast<int64_t>(k * kTrackThreads + tid) * 4;
-        v[k] = idx < s ? *reinterpret_cast<const float4*>(base + idx) : make_float4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int k = 0; k < kTrackUnroll; ++k) {
-        a += (v[k].x + v[k].y) + (v[k].z + v[k].w);
-        b += (v[k].x * v[k].x + v[k].y * v[k].y) + (v[k].z * v[k].z + v[k].w * v[k].w);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4 * kTrackUnroll; ++k) {
-        const int64_t idx = s0 + k * kTrackThreads + tid;
-        const float v = idx < s ? base[idx] : 0.f;
-        a += v;
-        b += v * v;
-      }
-    }
-  }
-  __shared__ float red[2][kTrackThreads / kWave];
-  a = wave_sum(a);
-  b = wave_sum(b);
-  const int wave = tid / kWave;
-  if ((tid & (kWave - 1)) == 0) {
-    red[0][wave] = a;
-    red[1][wave] = b;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float ta = 0.f, tb = 0.f;
-#pragma unroll
-    for (int w = 0; w < kTrackThreads / kWave; ++w) {
-      ta += red[0][w];
-      tb += red[1][w];
-    }
-    atomicAdd(sum + ch_idx, ta);
-    atomicAdd(sumsq + ch_idx, tb);
-  }
-}
-
-// K1 for small spatial extents (S < one chunk): each block strides over the flattened
-// (n, s) index space of its channel so every lane has work even when S is 49 or 196.
-template <bool VEC>
-__global__ __launch_bounds__(kTrackThreads) void dbn_track_flat_kernel(
-    const float* __restrict__ x, float* __restrict__ sum, float* __restrict__ sumsq, int64_t n,
-    int64_t c, int64_t s, int nsplit) {
-  const int ch_idx = blockIdx.y;
-  const int tid = threadIdx.x;
-  float a = 0.f, b = 0.f;
-  if (VEC) {
-    const int64_t sv = s / 4;
-    const int64_t total = n * sv;
-    for (int64_t k = static_cast<int64_t>(blockIdx.x) * kTrackThreads + tid; k < total;
-         k += static_cast<int64_t>(nsplit) * kTrackThreads) {
-      const int64_t ni = k / sv;
-      const float4 v = reinterpret_cast<const float4*>(x + (ni * c + ch_idx) * s)[k - ni * sv];
-      a += (v.x + v.y) + (v.z + v.w);
-      b += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
-    }
-  } else {
-    const int64_t total = n * s;
-    for (int64_t k = static_cast<int64_t>(blockIdx.x) * kTrackThreads + tid; k < total;
-         k += static_cast<int64_t>(nsplit) * kTrackThreads) {
-      const int64_t ni = k / s;
-      const float v = x[(ni * c + ch_idx) * s + (k - ni * s)];
-      a += v;
-      b += v * v;
-    }
-  }
-  __shared__ float red[2][kTrackThreads / kWave];
-  a = wave_sum(a);
-  b = wave_sum(b);
-  const int wave = tid / kWave;
-  if ((tid & (kWave - 1)) == 0) {
-    red[0][wave] = a;
-    red[1][wave] = b;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float ta = 0.f, tb = 0.f;
-#pragma unroll
-    for (int w = 0; w < kTrackThreads / kWave; ++w) {
-      ta += red[0][w];
-      tb += red[1][w];
-    }
-    atomicAdd(sum + ch_idx, ta);
-    atomicAdd(sumsq + ch_idx, tb);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// K2: commit.  fp64 arithmetic for mean/variance (the sums are fp32).
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void dbn_commit_kernel(float* sum, float* sumsq, float* rmean,
-                                                          float* rvar, int64_t c, double count,
-                                                          double momentum) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= c) return;
-  const double mean = static_cast<double>(sum[i]) / count;
-  double var = static_cast<double>(sumsq[i]) / count - mean * mean;
-  var = var < 0.0 ? 0.0 : var;
-  const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
-  rmean[i] = static_cast<float>((1.0 - momentum) * rmean[i] + momentum * mean);
-  rvar[i] = static_cast<float>((1.0 - momentum) * rvar[i] + momentum * unbiased);
-  sum[i] = 0.f;
-  sumsq[i] = 0.f;
-}
 
 // ---------------------------------------------------------------------------------------------
 // K3: fused Dropout2d -> InstanceNorm2d -> LeakyReLU.
@@ -528,49 +394,6 @@ void dna_bwd_launch(const float* dy, const float* x, const float* mean, const fl
 }  // namespace
 
 constexpr int64_t kDnaMaxTile = 1024 * 9 * 4;
-
-void launch_dbn_track(const float* x, float* sum, float* sumsq, int64_t n, int64_t c, int64_t s,
-                      hipStream_t stream) {
-  if (n == 0 || c == 0 || s == 0) return;
-  const bool aligned = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  if (s < kTrackChunk) {
-    // Flattened (n, s) space per channel; >= 16 elements per lane, >= ~2048 blocks.
-    const bool vec_flat = (s % 4 == 0) && aligned;
-    const int64_t work = n * (vec_flat ? s / 4 : s);
-    int64_t nsplit = (work + kTrackThreads * 4 - 1) / (kTrackThreads * 4);
-    const int64_t want = (2048 + c - 1) / c;
-    if (nsplit > want) nsplit = want;
-    if (nsplit < 1) nsplit = 1;
-    const dim3 grid(static_cast<unsigned>(nsplit), static_cast<unsigned>(c));
-    if (vec_flat)
-      hipLaunchKernelGGL(dbn_track_flat_kernel<true>, grid, dim3(kTrackThreads), 0, stream, x,
-                         sum, sumsq, n, c, s, static_cast<int>(nsplit));
-    else
-      hipLaunchKernelGGL(dbn_track_flat_kernel<false>, grid, dim3(kTrackThreads), 0, stream, x,
-                         sum, sumsq, n, c, s, static_cast<int>(nsplit));
-    return;
-  }
-  const int64_t chunks_per_n = (s + kTrackChunk - 1) / kTrackChunk;
-  const int64_t items = n * chunks_per_n;
-  int64_t nsplit = (2048 + c - 1) / c;  // aim for >= 2048 blocks (8 per CU)
-  if (nsplit > items) nsplit = items;
-  if (nsplit < 1) nsplit = 1;
-  const bool vec = (s % 4 == 0) && aligned;
-  const dim3 grid(static_cast<unsigned>(nsplit), static_cast<unsigned>(c));
-  if (vec)
-    hipLaunchKernelGGL(dbn_track_kernel<true>, grid, dim3(kTrackThreads), 0, stream, x, sum,
-                       sumsq, n, c, s, chunks_per_n, static_cast<int>(nsplit));
-  else
-    hipLaunchKernelGGL(dbn_track_kernel<false>, grid, dim3(kTrackThreads), 0, stream, x, sum,
-                       sumsq, n, c, s, chunks_per_n, static_cast<int>(nsplit));
-}
-
-void launch_dbn_commit(float* sum, float* sumsq, float* running_mean, float* running_var,
-                       int64_t c, double count, double momentum, hipStream_t stream) {
-  if (c == 0) return;
-  hipLaunchKernelGGL(dbn_commit_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, stream, sum, sumsq,
-                     running_mean, running_var, c, count, momentum);
-}
 
 void launch_dna_forward(const float* x, float* y, float* mean, float* rstd, float* scale,
                         int64_t planes, int64_t s, float p, float eps, float slope,

@@ -261,7 +261,8 @@ class _WinogradConv(torch.autograd.Function):
         dy = dy.contiguous()
         dx, dw = _conv_grads(x, weight, dy, ctx.cache, ctx.needs_input_grad[0],
                              ctx.needs_input_grad[1], ctx.param)
-        del ctx.param
+        # a repeated backward (retain_graph=True) returns dw to autograd instead
+        ctx.param = None
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum((0, 2, 3))
@@ -287,8 +288,10 @@ def _conv_grads(x: Tensor, weight: Tensor, dy: Tensor, cache: _TransformCache, n
     if need_w:
         ops = _ext.require(dy)
         f4, mfma = _wgrad_f4(x, dy, weight), _wgrad_on_mfma(x, weight)
-        fuse, into = gradacc.target(param) if param is not None and (f4 or mfma) else \
-            (False, None)
+        # the MIOpen weight gradient is accumulated here as well (one add), so no
+        # AccumulateGrad node of these parameters runs: under forward / recompute lanes a
+        # node shared by micro-batches of different streams would otherwise sync them
+        fuse, into = gradacc.target(param) if param is not None else (False, None)
         if f4:
             # non-fused (transform passes + LDS-DMA GEMM) from 512 channels on both
             # sides: 11-23 % faster there, 1.2-3.6x slower on the wide shallow planes
@@ -305,6 +308,8 @@ def _conv_grads(x: Tensor, weight: Tensor, dy: Tensor, cache: _TransformCache, n
             assert param is not None
             if into is None:
                 gradacc.commit(param, dw)
+            elif not (f4 or mfma):  # the library result is a new tensor
+                into.add_(dw)
             dw = None
     return dx, dw
 

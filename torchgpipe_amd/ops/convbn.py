@@ -482,7 +482,8 @@ class _GemmConv(torch.autograd.Function):
                 elif into is None:
                     gradacc.commit(ctx.param, dw)
                 dw = None
-        del ctx.param, ctx.cache
+        # a repeated backward (retain_graph=True) returns dw to autograd instead
+        ctx.param = None
         return dx, dw, None, None
 
 

@@ -23,6 +23,7 @@ create those handles on the worker first.  The caller's device and current strea
 propagated, exceptions are re-raised in the caller, and the call is synchronous from the
 caller's point of view (the worker only *enqueues* GPU work, like the caller would have).
 """
+import contextlib
 import queue
 import threading
 from typing import Any, Callable, Optional, Tuple
@@ -59,19 +60,38 @@ class _Worker:
 
 
 def call_with_big_stack(fn: Callable[[], Any]) -> Any:
-    """``fn()`` on the big-stack worker, under the caller's CUDA device and stream."""
+    """``fn()`` on the big-stack worker, under the caller's CUDA device and stream.
+
+    The caller's thread-local autograd state follows the call: grad mode, inference mode
+    and autocast (enabled flag and dtype per device type), so a step captured or replayed
+    under ``torch.autocast`` or ``torch.no_grad`` runs exactly as it would have on the
+    caller's thread.  A call made from the worker itself runs in place (queueing it would
+    deadlock the worker on its own request).
+    """
     global _worker
     with _lock:
         if _worker is None:
             _worker = _Worker()
         worker = _worker
+    if threading.current_thread() is worker.thread:
+        return fn()
     device = torch.cuda.current_device() if torch.cuda.is_available() else None
     stream = torch.cuda.current_stream() if device is not None else None
+    grad = torch.is_grad_enabled()
+    inference = torch.is_inference_mode_enabled()
+    autocast = [(kind, torch.is_autocast_enabled(kind), torch.get_autocast_dtype(kind))
+                for kind in ('cuda', 'cpu')]
 
     def wrapped() -> Any:
-        if device is None:
-            return fn()
-        with torch.cuda.device(device), torch.cuda.stream(stream):
+        with contextlib.ExitStack() as stack:
+            stack.enter_context(torch.inference_mode(inference))
+            stack.enter_context(torch.set_grad_enabled(grad))
+            for kind, enabled, dtype in autocast:
+                if enabled:
+                    stack.enter_context(torch.autocast(kind, dtype=dtype))
+            if device is not None:
+                stack.enter_context(torch.cuda.device(device))
+                stack.enter_context(torch.cuda.stream(stream))
             return fn()
 
     reply: 'queue.Queue' = queue.Queue(maxsize=1)
