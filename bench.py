@@ -84,6 +84,15 @@ AMOEBA_EXPERIMENTS = {
 }
 # the reference's AmoebaNet speed-up denominator (benchmarks/amoebanetd-speed/main.py:39-45)
 AMOEBA_N2M1 = dict(name='n2m1', batch=96, chunks=1, balance=[7, 17], ref=26.733)
+# ResNet-101 (benchmarks/resnet101-speed/main.py:22-67): pipeline-1 as in
+# the reference; at N=2 BASELINE.json's config #2, pipeline-2 with chunks=32 and 'always',
+# at the reference's pipeline-2 micro-batch of 15 images (its table runs B=25000, m=1667).
+RESNET_EXPERIMENTS = {
+    1: dict(name='pipeline-1', batch=220, chunks=2, balance=[370], checkpoint='except_last',
+            ref=81.796),
+    2: dict(name='pipeline-2 (chunks=32, always)', batch=480, chunks=32, balance=[135, 235],
+            checkpoint='always', ref=135.539),
+}
 
 
 def parse() -> argparse.Namespace:
@@ -91,7 +100,7 @@ def parse() -> argparse.Namespace:
     p.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
     p.add_argument('--steps', type=int, default=5)
     p.add_argument('--warmup', type=int, default=2)
-    p.add_argument('--model', choices=['unet', 'amoebanet'], default='unet')
+    p.add_argument('--model', choices=['unet', 'amoebanet', 'resnet'], default='unet')
     p.add_argument('--checkpoint', choices=['always', 'except_last', 'never'], default=None,
                    help='override the experiment checkpoint mode (default: reference mode)')
     p.add_argument('--batch', type=int, default=None, help='override the global batch')
@@ -106,8 +115,9 @@ def parse() -> argparse.Namespace:
     p.add_argument('--sections', default='auto',
                    help="comma-separated extra timings after the headline: 'baseline' "
                         "(U-Net without GPipe, B=40, rank 0), 'amoebanet' (AmoebaNet-D n{N}m32 "
-                        "and, at N=2, n2m1); 'auto' = both when the headline is U-Net; "
-                        "'none'")
+                        "and, at N=2, n2m1), 'resnet' (ResNet-101 pipeline-1 at N=1, "
+                        "BASELINE config #2 at N=2); 'auto' = all of them when the headline is "
+                        "U-Net (resnet at N <= 2); 'none'")
     p.add_argument('--section-steps', type=int, default=None,
                    help='timed steps of each extra section (default: --steps)')
     p.add_argument('--probe', choices=['auto', 'on', 'off'], default='auto',
@@ -143,6 +153,10 @@ def parse() -> argparse.Namespace:
     p.add_argument('--wgrad-stream', choices=['auto', 'on', 'off'], default='auto',
                    help='run the fused ops\' weight-gradient GEMMs on a side stream '
                         '(PipelineStage(wgrad_stream=True); auto: off)')
+    p.add_argument('--graph-cells', choices=['auto', 'on', 'off'], default='auto',
+                   help='multi-GPU runs: replay each micro-batch of a stage as captured '
+                        'hipGraphs, transfers issued between them (PipelineStage('
+                        'graph_cells=True), parallel/segments.py; auto: off)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -210,7 +224,7 @@ class Bench:
     # -- models -----------------------------------------------------------------------------
 
     def build(self, kind: str, meta: bool = True) -> torch.nn.Sequential:
-        from torchgpipe_amd.models import amoebanetd, unet
+        from torchgpipe_amd.models import amoebanetd, resnet101, unet
         args = self.args
         ctx = torch.device('meta') if meta else torch.device(self.device)
         # Built on the meta device for pipelines: each rank materialises (random-initialises)
@@ -222,6 +236,11 @@ class Bench:
                                 output_channels=1, fused=not args.unfused)
                 return unet(depth=5, num_convs=5, base_channels=64, input_channels=3,
                             output_channels=1, fused=not args.unfused)
+            if kind == 'resnet':
+                if args.tiny:
+                    from torchgpipe_amd.models.resnet import build_resnet
+                    return build_resnet([1, 1, 1, 1], num_classes=10)
+                return resnet101(num_classes=1000)
             if args.tiny:
                 return amoebanetd(num_classes=10, num_layers=3, num_filters=8)
             return amoebanetd(num_classes=1000, num_layers=18, num_filters=256)
@@ -288,14 +307,17 @@ class Bench:
         # lanes (parallel/stage.py), parity-tested on shared-GPU gloo rehearsals.
         overlap = choice(args.overlap_recompute, self.gpu and unet)
         overlap_fwd = choice(args.overlap_forward, self.gpu and unet)
-        cell_streams = not unet and choice(args.cell_streams, self.gpu)
+        cell_streams = kind == 'amoebanet' and choice(args.cell_streams, self.gpu)
         # (auto: off -- with the two-stream cells it measured 280.3 vs 328.6 samples/s on one
         # box, profiles/r2/bench_amoeba_s13.md)
         wgrad_stream = choice(args.wgrad_stream, False)
+        # captured cells (parallel/segments.py): multi-rank stages replay each micro-batch's
+        # forward / recomputation / backward as hipGraphs, transfers in between
+        graph_cells = choice(args.graph_cells, False) and self.gpu and self.world > 1
         stage = PipelineStage(self.build(kind), balance, device=self.device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
                               overlap_recompute=overlap, overlap_forward=overlap_fwd,
-                              wgrad_stream=wgrad_stream)
+                              wgrad_stream=wgrad_stream, graph_cells=graph_cells)
         if args.channels_last and not unet:
             stage.partition.to(memory_format=torch.channels_last)
         if cell_streams:
@@ -309,7 +331,7 @@ class Bench:
         graph = None
         # whole-step hipGraph: AmoebaNet (no RNG) on one GPU (two-stream cells included,
         # launched from a big-stack thread: profiles/r3/capture_crash.md)
-        use_graph = choice(args.graph, self.world == 1 and self.gpu and not unet)
+        use_graph = choice(args.graph, self.world == 1 and self.gpu and kind == 'amoebanet')
         if use_graph:
             if self.world != 1:
                 raise SystemExit('--graph captures one-rank runs only')
@@ -326,16 +348,19 @@ class Bench:
 
         if self.gpu:
             torch.cuda.reset_peak_memory_stats(self.device)
-        res: Dict[str, Any] = self.timed(
-            step, steps, args.warmup, tag,
-            settle=(lambda: graph.captured) if graph is not None else None)
+        settle = None
+        if graph is not None:
+            settle = lambda: graph.captured  # noqa: E731
+        elif graph_cells:
+            settle = lambda: stage._segments is not None and stage._segments.captured  # noqa: E731
+        res: Dict[str, Any] = self.timed(step, steps, args.warmup, tag, settle=settle)
         res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
                    steps=steps, overlap_recompute=overlap,
                    # (a captured step keeps at most CAPTURE_CELL_STREAMS per cell)
                    cell_streams=min(int(cell_streams), _capture_streams())
                    if graph is not None and cell_streams else int(cell_streams),
                    overlap_forward=overlap_fwd, wgrad_stream=wgrad_stream,
-                   hipgraph=graph is not None)
+                   hipgraph=graph is not None, graph_cells=graph_cells)
         if probe and graph is None:
             # one untimed diagnostic step: per-rank receive waits and busy time
             mine = stage.probe_step(step)
@@ -458,7 +483,8 @@ def main() -> None:
                  'value': round(batch * args.steps / t['elapsed'], 3),
                  'ms_per_step': round(1000 * t['elapsed'] / args.steps, 3)}
 
-    sections = ({'baseline', 'amoebanet'} if kind == 'unet' else set()) \
+    sections = ({'baseline', 'amoebanet'} | ({'resnet'} if world in RESNET_EXPERIMENTS else set())
+                if kind == 'unet' else set()) \
         if args.sections == 'auto' else \
         (set() if args.sections == 'none' else set(args.sections.split(',')))
     sec_steps = args.section_steps or args.steps
@@ -493,6 +519,17 @@ def main() -> None:
             dr = b.pipeline('amoebanet', d, d['balance'], 'always', sec_steps, 'amoebanet-n2m1')
             amoeba['n2m1'] = summary(dr, None if args.tiny else d['ref'])
             amoeba['speedup_vs_n2m1'] = round(amoeba['value'] / amoeba['n2m1']['value'], 3)
+
+    resnet = None
+    if 'resnet' in sections and kind == 'unet' and world in RESNET_EXPERIMENTS:
+        rexp = dict(RESNET_EXPERIMENTS[world])
+        if args.tiny:
+            r_layers = len(b.build('resnet'))
+            rexp.update(batch=4, chunks=2, balance=even_balance(r_layers, world))
+        rr = b.pipeline('resnet', rexp, rexp['balance'], rexp['checkpoint'], sec_steps, 'resnet')
+        resnet = summary(rr, None if args.tiny else rexp['ref'])
+        resnet['experiment'] = rexp['name']
+        resnet['hipgraph'] = rr['hipgraph']
 
     if b.rank == 0:
         ref = None if args.tiny else exp.get('ref')
@@ -535,6 +572,7 @@ def main() -> None:
                 'overlap_recompute': main_run['overlap_recompute'],
                 'wgrad_stream': main_run['wgrad_stream'],
                 'overlap_forward': main_run['overlap_forward'],
+                'graph_cells': main_run['graph_cells'],
             },
             'tuned': tuned,
         }
@@ -545,6 +583,8 @@ def main() -> None:
             record['baseline'] = baseline
         if amoeba is not None:
             record['amoebanet'] = amoeba
+        if resnet is not None:
+            record['resnet101'] = resnet
         if 'per_rank' in main_run:
             record['per_rank'] = main_run['per_rank']
         print(json.dumps(record), file=result_out, flush=True)

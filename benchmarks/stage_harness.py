@@ -1,120 +1,163 @@
-"""Run ONE pipeline stage of a multi-GPU U-Net/AmoebaNet experiment on one GPU.
+"""Run ONE pipeline stage of a multi-GPU U-Net / AmoebaNet / ResNet-101 experiment on one GPU.
 
-Measures what a stage rank does per step — ``m`` checkpointed forwards, ``m``
-recomputes and backwards — with real inputs/skips of the right shapes, and
-reports device-busy time vs host wall time.  Host time ≫ device time means the
-stage is launch-bound (a hipGraph candidate); device time per stage validates
-the balance simulator (``torchgpipe_amd.balance.simulate``).
+The stage is the real engine -- :class:`~torchgpipe_amd.parallel.PipelineStage` as rank
+``k`` of ``len(balance)`` -- on a loopback transport
+(:class:`~torchgpipe_amd.parallel.loopback.LoopbackP2P`): its receives return, at once,
+the boundary activations and skips the preceding stages produce (computed here by running
+the model's prefix on one micro-batch) or random output gradients, and its sends are
+dropped.  Every step is what the rank does on a multi-GPU node (``m`` forwards, ``m``
+recomputations and backwards on the lanes, multi-stream cells, captured cells with
+``--graph-cells``, the SGD update) minus the waits on its neighbours, so
 
-    python benchmarks/stage_harness.py --balance 18 27 29 23 25 33 44 42 --chunks 40 --batch 640
+* ``device_ms`` is the stage's compute per step (GPU busy span, events on the main stream),
+* ``host_ms`` the host's enqueue time per step (Python, autograd, dispatcher, launches),
+* ``host_share`` = host / device: above 1 the stage is launch-bound; the pipeline needs it
+  well below 1 so that host hiccups stay off the critical path.
+
+The slowest stage's ``device_ms`` bounds the pipeline's step time (plus the fill/drain
+bubble, ``torchgpipe_amd.balance.simulate``).
+
+    python benchmarks/stage_harness.py --model amoebanet --balance 2 2 2 3 3 4 4 4 \\
+        --chunks 32 --batch 1280 --graph-cells
 """
 import argparse
 import json
 import os
 import sys
 import time
+from typing import Dict, List
 
 import torch
+import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from torchgpipe_amd.checkpoint import Checkpointing  # noqa: E402
 from torchgpipe_amd.microbatch import Batch  # noqa: E402
-from torchgpipe_amd.models import amoebanetd, unet  # noqa: E402
+from torchgpipe_amd.parallel import PipelineStage  # noqa: E402
+from torchgpipe_amd.parallel.loopback import LoopbackP2P  # noqa: E402
+from torchgpipe_amd.parallel.stage import signature_of  # noqa: E402
 from torchgpipe_amd.skip.tracker import SkipTracker, use_skip_tracker  # noqa: E402
+
+SHAPES = {'unet': (3, 192, 192), 'amoebanet': (3, 224, 224), 'resnet101': (3, 224, 224)}
+
+
+def build(kind: str, dev: torch.device) -> torch.nn.Sequential:
+    from torchgpipe_amd.models import amoebanetd, resnet101, unet
+    with dev:
+        if kind == 'unet':
+            return unet(depth=5, num_convs=5, base_channels=64)
+        if kind == 'amoebanet':
+            return amoebanetd(num_classes=1000, num_layers=18, num_filters=256)
+        return resnet101(num_classes=1000)
+
+
+def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, object]:
+    torch.manual_seed(0)
+    model = build(args.model, dev).train()
+    shape = SHAPES[args.model]
+    layers = list(model)
+    bounds = [0]
+    for b in args.balance:
+        bounds.append(bounds[-1] + b)
+    lo, hi = bounds[k], bounds[k + 1]
+    mb = -(-args.batch // args.chunks)
+
+    # the boundary tensors of this stage: the prefix's output and the skips still in flight
+    tracker = SkipTracker()
+    with torch.no_grad(), use_skip_tracker(tracker):
+        batch = Batch(torch.rand(mb, *shape, device=dev))
+        for layer in layers[:lo]:
+            batch = batch.call(layer)
+    acts, atomic = [t.detach() for t in batch], batch.atomic
+    pending = dict(tracker.tensors)
+    del batch, tracker
+
+    lanes = {'auto': args.model == 'unet', 'on': True, 'off': False}[args.lanes]
+    # placeholder transport until the stage knows its skip routes
+    transport = LoopbackP2P(dev, acts, atomic, {})
+    stage = PipelineStage(model, args.balance, rank=k, device=dev, chunks=args.chunks,
+                          checkpoint=args.checkpoint, transport=transport,
+                          overlap_recompute=lanes, overlap_forward=lanes,
+                          graph_cells=args.graph_cells)
+    skips: Dict[int, List[torch.Tensor]] = {}
+    for src, key in stage.in_skips:
+        skips.setdefault(src, []).append(pending[key])
+    transport.skips = skips
+    del pending
+    if args.cell_streams and args.model == 'amoebanet':
+        from torchgpipe_amd.models.amoebanet import set_cell_streams
+        set_cell_streams(stage.partition, args.cell_streams)
+
+    x = torch.rand(args.batch, *shape, device=dev) if stage.is_first else None
+    if args.model == 'unet':
+        target = torch.ones(args.batch, 1, 192, 192, device=dev) if stage.is_last else None
+        loss_fn = F.binary_cross_entropy_with_logits
+    else:
+        target = torch.randint(1000, (args.batch,), device=dev) if stage.is_last else None
+        loss_fn = F.cross_entropy
+    signature = signature_of(torch.empty(args.batch, *shape, device='meta'))
+    optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
+
+    def step() -> None:
+        stage.train_step(x, target, loss_fn, signature=signature)
+        optimizer.step()
+        optimizer.zero_grad(set_to_none=True)
+
+    t0 = time.perf_counter()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    warm_s = time.perf_counter() - t0
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    host_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    e1.record()
+    e1.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    dev_ms = e0.elapsed_time(e1) / args.steps
+    row = {'stage': k, 'layers': [lo, hi], 'graph_cells': args.graph_cells,
+           'graph_phase': stage.graph_phase, 'lanes': lanes,
+           'host_ms': round(host_ms, 2), 'wall_ms': round(wall_ms, 2),
+           'device_ms': round(dev_ms, 2), 'host_share': round(host_ms / dev_ms, 3),
+           'warmup_s': round(warm_s, 1),
+           'peak_mem_gib': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)}
+    del stage, optimizer, model, x, target, acts, skips, transport
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)
+    return row
 
 
 def main() -> None:
-    p = argparse.ArgumentParser()
-    p.add_argument('--model', choices=['unet', 'amoebanet'], default='unet')
+    p = argparse.ArgumentParser(description=__doc__,
+                                formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument('--model', choices=sorted(SHAPES), default='unet')
     p.add_argument('--balance', type=int, nargs='+', required=True)
     p.add_argument('--chunks', type=int, required=True)
     p.add_argument('--batch', type=int, required=True)
     p.add_argument('--stages', type=int, nargs='*', default=None)
     p.add_argument('--checkpoint', default='except_last')
+    p.add_argument('--graph-cells', action='store_true',
+                   help='captured cells (PipelineStage(graph_cells=True))')
+    p.add_argument('--lanes', choices=['auto', 'on', 'off'], default='auto',
+                   help='forward / recompute lanes (auto: on for U-Net, as bench.py)')
+    p.add_argument('--cell-streams', type=int, default=3,
+                   help='AmoebaNet: streams per cell (0: one stream; bench.py: 3)')
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--steps', type=int, default=2)
     p.add_argument('--out', default=None)
-    p.add_argument('--cell-streams', type=int, default=0,
-                   help='AmoebaNet: streams per cell (0: one stream; bench.py uses 3 eager)')
     args = p.parse_args()
-
+    if args.graph_cells and args.warmup < 3:
+        args.warmup = 3  # eager, capture, first replay
     dev = torch.device('cuda', 0)
-    model = unet() if args.model == 'unet' else amoebanetd(1000, 18, 256)
-    shape = (3, 192, 192) if args.model == 'unet' else (3, 224, 224)
-    model.to(dev).train()
-    if args.cell_streams and args.model == 'amoebanet':
-        from torchgpipe_amd.models.amoebanet import set_cell_streams
-        set_cell_streams(model, args.cell_streams)
-    layers = list(model)
-    mb = args.batch // args.chunks
-    m = args.chunks
-    stop = {'always': m, 'except_last': m - 1, 'never': 0}[args.checkpoint]
-
-    bounds = [0]
-    for b in args.balance:
-        bounds.append(bounds[-1] + b)
     results = []
-    stages = args.stages if args.stages else list(range(len(args.balance)))
-
-    for k in stages:
-        lo, hi = bounds[k], bounds[k + 1]
-        # Produce this stage's input (and the skips stashed before it) once.
-        tracker = SkipTracker()
-        with torch.no_grad(), use_skip_tracker(tracker):
-            x = torch.rand(mb, *shape, device=dev)
-            batch = Batch(x)
-            for layer in layers[:lo]:
-                batch = batch.call(layer)
-        saved_skips = dict(tracker.tensors)
-        part = torch.nn.Sequential(*layers[lo:hi])
-        inputs = [t.detach() for t in batch]
-        atomic = batch.atomic
-
-        def fn(flat, part=part):
-            tr = SkipTracker()
-            tr.tensors = dict(saved_skips)
-            with use_skip_tracker(tr):
-                out = part(flat[0] if atomic else tuple(flat))
-            b = Batch(out)
-            return tuple(b)
-
-        def step():
-            cells = []
-            for i in range(m):
-                leaves = [t.detach().requires_grad_(k > 0 and t.is_floating_point())
-                          for t in inputs]
-                if i < stop:
-                    chk = Checkpointing(fn, Batch(tuple(leaves)))
-                    out = list(chk.checkpoint())
-                else:
-                    chk = None
-                    out = list(fn(tuple(leaves)))
-                cells.append((chk, out))
-            for chk, out in reversed(cells):
-                if chk is not None:
-                    chk.recompute_now()
-                ys = [y for y in out if y.requires_grad]
-                torch.autograd.backward(ys, [torch.ones_like(y) for y in ys])
-            part.zero_grad(set_to_none=True)
-
-        step()
-        torch.cuda.synchronize()
-        reps = 2
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        e0.record()
-        for _ in range(reps):
-            step()
-        host_ms = (time.perf_counter() - t0) * 1e3 / reps
-        e1.record()
-        e1.synchronize()
-        wall_ms = (time.perf_counter() - t0) * 1e3 / reps
-        dev_ms = e0.elapsed_time(e1) / reps
-        row = {'stage': k, 'layers': [lo, hi], 'host_enqueue_ms': round(host_ms, 2),
-               'wall_ms': round(wall_ms, 2), 'device_ms': round(dev_ms, 2),
-               'per_cell_ms': round(wall_ms / m, 3)}
+    for k in (args.stages if args.stages else range(len(args.balance))):
+        row = run_stage(args, k, dev)
         results.append(row)
         print(json.dumps(row), flush=True)
-
     if args.out:
         with open(args.out, 'w') as f:
             json.dump({'args': vars(args), 'stages': results}, f, indent=1)

@@ -77,16 +77,20 @@ def reference(kind: str, device: torch.device, chunks: int):
 
 def stage_worker(rank: int, world: int, kind: str, chunks: int, checkpoint: str,
                  device_type: str, options: dict = None):
-    """One rank: two training steps (the second on cached message metadata).
+    """One rank: two training steps (the second on cached message metadata), or
+    ``options['steps']`` (captured cells: warm-up, capture, replays).
 
     ``device_type``: 'cpu', 'cuda' (rank r on cuda:r) or 'cuda-shared' (every rank on
     cuda:0, host-staged gloo transport: the one-GPU rehearsal of a multi-rank run, which
     exercises the stage's stream logic -- lanes, two-stream cells -- for real).
-    ``options``: extra PipelineStage keywords, plus ``cell_streams`` (AmoebaNet).
+    ``options``: extra PipelineStage keywords, plus ``cell_streams`` (AmoebaNet) and
+    ``steps``.  Every step computes the same gradients (same data, no optimizer step), so
+    the last step's are compared with the oracle.
     """
     from torchgpipe_amd.parallel import PipelineStage
     options = dict(options or {})
     cell_streams = options.pop('cell_streams', False)
+    steps = options.pop('steps', 2)
     if device_type == 'cuda':
         device = torch.device('cuda', rank)
     elif device_type == 'cuda-shared':
@@ -100,16 +104,19 @@ def stage_worker(rank: int, world: int, kind: str, chunks: int, checkpoint: str,
         set_cell_streams(stage.partition, True)
     x, t = data(kind, device)
     loss = None
-    for _ in range(2):
+    phases = []
+    for _ in range(steps):
         for p in stage.parameters():
             p.grad = None
         loss = stage.train_step(x if stage.is_first else None, t if stage.is_last else None,
                                 loss_fn(kind))
+        phases.append(stage.graph_phase)
     if device.type == 'cuda':
         torch.cuda.synchronize(device)
     return {'grads': [p.grad.detach().cpu().clone() for p in stage.parameters()],
             'loss': None if loss is None else loss.item(),
-            'skip_peers': sorted({d for d, _ in stage.out_skips} | {s for s, _ in stage.in_skips})}
+            'skip_peers': sorted({d for d, _ in stage.out_skips} | {s for s, _ in stage.in_skips}),
+            'phases': phases}
 
 
 def assert_parity(results, want_grads, want_loss, rel: float) -> None:

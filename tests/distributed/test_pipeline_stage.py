@@ -273,3 +273,17 @@ def test_misordered_exchange_raises_pipeline_timeout(tmp_path):
         assert r['raised'] == 'PipelineTimeout', r
         assert r["elapsed"] < 10.0, r
         assert "'act'" in r['msg']
+
+
+@pytest.mark.parametrize('kind,options', [
+    ('unet', dict(overlap_recompute=True, overlap_forward=True, graph_cells=True, steps=3)),
+    ('amoebanet', dict(cell_streams=True, graph_cells=True, steps=3)),
+])
+def test_bench_options_cpu_twin(tmp_path, kind, options):
+    """CPU/gloo twin of tests/distributed/test_rccl_multigpu.py::
+    test_rccl_bench_options_match_single_gpu: the GPU-only options are accepted and the
+    stage runs its eager schedule."""
+    results = run(parity.stage_worker, 2, tmp_path, kind, 3, 'except_last', 'cpu', options)
+    grads, loss = parity.reference(kind, torch.device('cpu'), 3)
+    parity.assert_parity(results, grads, loss, rel=1e-5)
+    assert all(r['phases'] == ['eager'] * 3 for r in results)

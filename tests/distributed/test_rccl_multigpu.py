@@ -31,6 +31,35 @@ def test_rccl_pipeline_matches_single_gpu(tmp_path, kind, world, checkpoint):
     parity.assert_parity(results, grads, loss, rel=1e-4)
 
 
+# The stream options bench.py turns on at N > 1 (U-Net: forward and recompute lanes;
+# AmoebaNet: multi-stream cells), alone and with captured cells: the first RCCL run of a
+# multi-GPU node checks the stream-ordered receive waits against every lane layout.
+BENCH_OPTIONS = {
+    'unet': [dict(overlap_recompute=True, overlap_forward=True),
+             dict(overlap_recompute=True, overlap_forward=True, graph_cells=True, steps=4)],
+    'amoebanet': [dict(cell_streams=True),
+                  dict(cell_streams=True, graph_cells=True, steps=4)],
+}
+BENCH_CASES = [(kind, world, opts) for kind in parity.MODELS for world in (2, 4)
+               for opts in BENCH_OPTIONS[kind]]
+
+
+@pytest.mark.parametrize('kind,world,options', BENCH_CASES,
+                         ids=[f'{k}-{w}-{"+".join(x for x in o if x != "steps")}'
+                              for k, w, o in BENCH_CASES])
+def test_rccl_bench_options_match_single_gpu(tmp_path, kind, world, options):
+    """bench.py's N > 1 stage options over RCCL, lazily created per-link communicators."""
+    if torch.cuda.device_count() < world:
+        pytest.skip(f'needs {world} GPUs')
+    chunks = 3
+    results = run(parity.stage_worker, world, tmp_path, kind, chunks, 'except_last', 'cuda',
+                  options, backend='nccl-lazy', timeout=120)
+    grads, loss = parity.reference(kind, torch.device('cuda', 0), chunks)
+    parity.assert_parity(results, grads, loss, rel=1e-4)
+    if options.get('graph_cells'):
+        assert all(r['phases'][-1] == 'replay' for r in results)
+
+
 @pytest.mark.parametrize('kind', parity.MODELS)
 def test_rccl_eager_communicator_with_link_groups(tmp_path, kind):
     """Eager init (``device_id``): one 2-rank group per pipeline link."""

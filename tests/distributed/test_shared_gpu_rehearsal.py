@@ -25,11 +25,19 @@ CASES = [
     ('unet', 'always', dict(overlap_recompute=True)),
     ('amoebanet', 'except_last', dict(cell_streams=True)),
     ('amoebanet', 'except_last', dict(cell_streams=True, overlap_recompute=True)),
+    # captured cells (parallel/segments.py): warm-up, capture and two replayed steps with
+    # the persistent receive buffers, the transfers between graph launches
+    ('unet', 'except_last', dict(overlap_recompute=True, overlap_forward=True,
+                                 graph_cells=True, steps=4)),
+    ('unet', 'always', dict(graph_cells=True, steps=4)),
+    ('amoebanet', 'except_last', dict(cell_streams=True, graph_cells=True, steps=4)),
+    ('amoebanet', 'always', dict(overlap_recompute=True, graph_cells=True, steps=4)),
 ]
 
 
 @pytest.mark.parametrize('kind,checkpoint,options', CASES,
-                         ids=[f'{k}-{c}-{"+".join(o)}' for k, c, o in CASES])
+                         ids=[f'{k}-{c}-{"+".join(x for x in o if x != "steps")}'
+                              for k, c, o in CASES])
 def test_overlapped_stage_matches_one_gpu(tmp_path, kind, checkpoint, options):
     if not torch.cuda.is_available():
         pytest.skip('needs a GPU')
@@ -38,3 +46,6 @@ def test_overlapped_stage_matches_one_gpu(tmp_path, kind, checkpoint, options):
                   options, backend='gloo', timeout=120)
     grads, loss = parity.reference(kind, torch.device('cuda', 0), chunks)
     parity.assert_parity(results, grads, loss, rel=1e-4)
+    if options.get('graph_cells'):
+        assert all(r['phases'] == ['eager', 'capture', 'replay', 'replay'] for r in results), \
+            [r['phases'] for r in results]

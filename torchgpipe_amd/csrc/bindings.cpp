@@ -16,6 +16,15 @@ hipStream_t stream_of(const at::Tensor& t) {
   return at::hip::getCurrentHIPStream(t.device().index()).stream();
 }
 
+// Optional device-resident Philox state: int64 [2] (seed, base offset) on the op's device.
+const int64_t* rng_state(const c10::optional<at::Tensor>& rng, const at::Device& device) {
+  if (!rng.has_value() || !rng->defined()) return nullptr;
+  TORCH_CHECK(rng->is_cuda() && rng->device() == device && rng->scalar_type() == at::kLong &&
+                  rng->is_contiguous() && rng->numel() == 2,
+              "rng must be a contiguous int64 [2] (seed, offset) tensor on the op's device");
+  return rng->data_ptr<int64_t>();
+}
+
 void check_f32_gpu(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
@@ -23,7 +32,8 @@ void check_f32_gpu(const at::Tensor& t, const char* name) {
 }
 
 std::vector<at::Tensor> dna_forward(const at::Tensor& x, double p, double eps, double slope,
-                                    int64_t seed, int64_t offset, bool dropout) {
+                                    int64_t seed, int64_t offset, bool dropout,
+                                    const c10::optional<at::Tensor>& rng) {
   check_f32_gpu(x, "x");
   TORCH_CHECK(x.dim() >= 3, "expected (N, C, *spatial) input");
   TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout probability must be in [0, 1)");
@@ -39,7 +49,7 @@ std::vector<at::Tensor> dna_forward(const at::Tensor& x, double p, double eps, d
                      rstd.data_ptr<float>(), scale.data_ptr<float>(), planes, s,
                      static_cast<float>(p), static_cast<float>(eps), static_cast<float>(slope),
                      static_cast<uint64_t>(seed), static_cast<uint64_t>(offset), dropout,
-                     stream_of(x));
+                     rng_state(rng, x.device()), stream_of(x));
   return {y, mean, rstd, scale};
 }
 
@@ -61,23 +71,27 @@ at::Tensor dna_backward(const at::Tensor& dy_in, const at::Tensor& x, const at::
   return dx;
 }
 
-at::Tensor dropout(const at::Tensor& x_in, double p, int64_t seed, int64_t offset) {
+at::Tensor dropout(const at::Tensor& x_in, double p, int64_t seed, int64_t offset,
+                   const c10::optional<at::Tensor>& rng) {
   auto x = x_in.contiguous();
   check_f32_gpu(x, "x");
   TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout probability must be in [0, 1)");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto y = at::empty_like(x);
   launch_dropout(x.data_ptr<float>(), y.data_ptr<float>(), x.numel(), static_cast<float>(p),
-                 static_cast<uint64_t>(seed), static_cast<uint64_t>(offset), stream_of(x));
+                 static_cast<uint64_t>(seed), static_cast<uint64_t>(offset),
+                 rng_state(rng, x.device()), stream_of(x));
   return y;
 }
 
-at::Tensor philox_uniform(int64_t n, int64_t seed, int64_t offset, at::Device device) {
+at::Tensor philox_uniform(int64_t n, int64_t seed, int64_t offset, at::Device device,
+                          const c10::optional<at::Tensor>& rng) {
   TORCH_CHECK(device.is_cuda(), "philox_uniform runs on the GPU");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(device);
   auto out = at::empty({n}, at::TensorOptions().dtype(at::kFloat).device(device));
   launch_philox_uniform(out.data_ptr<float>(), n, static_cast<uint64_t>(seed),
-                        static_cast<uint64_t>(offset), stream_of(out));
+                        static_cast<uint64_t>(offset), rng_state(rng, out.device()),
+                        stream_of(out));
   return out;
 }
 
@@ -349,11 +363,11 @@ at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
 
 TORCH_LIBRARY(tgpipe, m) {
   m.def("dna_forward(Tensor x, float p, float eps, float slope, int seed, int offset, "
-        "bool dropout) -> Tensor[]");
+        "bool dropout, Tensor? rng=None) -> Tensor[]");
   m.def("dna_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor scale, "
         "float slope) -> Tensor");
-  m.def("dropout(Tensor x, float p, int seed, int offset) -> Tensor");
-  m.def("philox_uniform(int n, int seed, int offset, Device device) -> Tensor");
+  m.def("dropout(Tensor x, float p, int seed, int offset, Tensor? rng=None) -> Tensor");
+  m.def("philox_uniform(int n, int seed, int offset, Device device, Tensor? rng=None) -> Tensor");
   m.def("spin(int ns, Device device) -> ()");
   m.def("copy_segments(Tensor[] srcs, Tensor(a!)[] dsts) -> ()");
   m.def("wino_weight(Tensor w, bool flip) -> Tensor");

@@ -9,12 +9,17 @@
 
 namespace tgpipe {
 
+// RNG ops take an optional device-resident Philox state ``rng`` (int64 [2]: seed, base
+// offset; nullptr = use ``seed`` / ``offset``): with it the seed is rng[0] and the offset
+// rng[1] + offset, read by the kernel when it runs (graph replays, parallel/segments.py).
+//
 // Fused Dropout2d(p) -> InstanceNorm2d(eps, affine=False) -> LeakyReLU(slope) over
 // planes x[P, S] (P = N*C, S = H*W).  Saves per-plane mean (of x), rstd (of the
 // dropped-out input) and the dropout scale (0 or 1/(1-p)).
 void launch_dna_forward(const float* x, float* y, float* mean, float* rstd, float* scale,
                         int64_t planes, int64_t s, float p, float eps, float slope,
-                        uint64_t seed, uint64_t offset, bool dropout, hipStream_t stream);
+                        uint64_t seed, uint64_t offset, bool dropout, const int64_t* rng,
+                        hipStream_t stream);
 
 void launch_dna_backward(const float* dy, const float* x, const float* mean, const float* rstd,
                          const float* scale, float* dx, int64_t planes, int64_t s, float slope,
@@ -23,11 +28,11 @@ void launch_dna_backward(const float* dy, const float* x, const float* mean, con
 // Elementwise inverted dropout with explicit Philox (seed, offset); the mask is
 // regenerated in backward instead of stored.
 void launch_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, uint64_t offset,
-                    hipStream_t stream);
+                    const int64_t* rng, hipStream_t stream);
 
 // Uniform [0,1) Philox draws (tests / reference checks).
 void launch_philox_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
-                           hipStream_t stream);
+                           const int64_t* rng, hipStream_t stream);
 
 // Spin for `ns` nanoseconds of wall time (s_memrealtime, 100 MHz) — race tests.
 void launch_spin(uint64_t ns, hipStream_t stream);

@@ -124,6 +124,18 @@ struct PlaneTile {
   }
 };
 
+// Device-resident Philox state (captured graphs, parallel/segments.py): when ``rng`` is
+// given, the seed is rng[0] and the call's offset is rng[1] + offset (``offset`` is then the
+// call's delta inside its cell), so a replayed graph draws a fresh mask every step from
+// the values the host wrote into rng before the replay.
+__device__ __forceinline__ void philox_resolve(const int64_t* __restrict__ rng, uint64_t& seed,
+                                               uint64_t& offset) {
+  if (rng != nullptr) {
+    seed = static_cast<uint64_t>(rng[0]);
+    offset += static_cast<uint64_t>(rng[1]);
+  }
+}
+
 __device__ __forceinline__ float plane_dropout_scale(int64_t plane, float p, uint64_t seed,
                                                      uint64_t offset, bool dropout) {
   if (!dropout) return 1.f;
@@ -135,8 +147,10 @@ template <int GROUP, int V, bool VEC>
 __global__ __launch_bounds__(kPlaneBlock<GROUP>) void dna_forward_kernel(
     const float* __restrict__ x, float* __restrict__ y, float* __restrict__ mean_out,
     float* __restrict__ rstd_out, float* __restrict__ scale_out, int64_t planes, int64_t s,
-    float p, float eps, float slope, uint64_t seed, uint64_t offset, bool dropout) {
+    float p, float eps, float slope, uint64_t seed, uint64_t offset, bool dropout,
+    const int64_t* __restrict__ rng) {
   using T = PlaneTile<GROUP, V, VEC>;
+  philox_resolve(rng, seed, offset);
   __shared__ float lds[T::kBlock / kWave];
   const int t = threadIdx.x % GROUP;
   const int64_t plane = static_cast<int64_t>(blockIdx.x) * T::kPlanesPerBlock + threadIdx.x / GROUP;
@@ -222,8 +236,9 @@ constexpr int kBigGroup = 1024;
 __global__ __launch_bounds__(kBigGroup) void dna_forward_big_kernel(
     const float* __restrict__ x, float* __restrict__ y, float* __restrict__ mean_out,
     float* __restrict__ rstd_out, float* __restrict__ scale_out, int64_t s, float p, float eps,
-    float slope, uint64_t seed, uint64_t offset, bool dropout) {
+    float slope, uint64_t seed, uint64_t offset, bool dropout, const int64_t* __restrict__ rng) {
   __shared__ float lds[kBigGroup / kWave];
+  philox_resolve(rng, seed, offset);
   using T = PlaneTile<kBigGroup, 1, false>;
   const int64_t plane = blockIdx.x;
   const float* xp = x + plane * s;
@@ -286,7 +301,9 @@ __global__ __launch_bounds__(kBigGroup) void dna_backward_big_kernel(
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ x,
                                                       float* __restrict__ y, int64_t n, float p,
-                                                      uint64_t seed, uint64_t offset, bool vec) {
+                                                      uint64_t seed, uint64_t offset, bool vec,
+                                                      const int64_t* __restrict__ rng) {
+  philox_resolve(rng, seed, offset);
   const float scale = 1.f / (1.f - p);
   const int64_t quads = (n + 3) / 4;
   for (int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; q < quads;
@@ -308,7 +325,9 @@ __global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void philox_uniform_kernel(float* __restrict__ out, int64_t n,
-                                                             uint64_t seed, uint64_t offset) {
+                                                             uint64_t seed, uint64_t offset,
+                                                             const int64_t* __restrict__ rng) {
+  philox_resolve(rng, seed, offset);
   const int64_t quads = (n + 3) / 4;
   for (int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; q < quads;
        q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -357,11 +376,12 @@ __global__ __launch_bounds__(256) void segments_copy_kernel(SegmentTable table) 
 template <int GROUP, int V, bool VEC>
 void dna_fwd_launch(const float* x, float* y, float* mean, float* rstd, float* scale,
                     int64_t planes, int64_t s, float p, float eps, float slope, uint64_t seed,
-                    uint64_t offset, bool dropout, hipStream_t stream) {
+                    uint64_t offset, bool dropout, const int64_t* rng, hipStream_t stream) {
   using T = PlaneTile<GROUP, V, VEC>;
   const int grid = ceil_div(planes, T::kPlanesPerBlock);
   hipLaunchKernelGGL((dna_forward_kernel<GROUP, V, VEC>), dim3(grid), dim3(T::kBlock), 0, stream,
-                     x, y, mean, rstd, scale, planes, s, p, eps, slope, seed, offset, dropout);
+                     x, y, mean, rstd, scale, planes, s, p, eps, slope, seed, offset, dropout,
+                     rng);
 }
 
 template <int GROUP, int V, bool VEC>
@@ -397,22 +417,23 @@ constexpr int64_t kDnaMaxTile = 1024 * 9 * 4;
 
 void launch_dna_forward(const float* x, float* y, float* mean, float* rstd, float* scale,
                         int64_t planes, int64_t s, float p, float eps, float slope,
-                        uint64_t seed, uint64_t offset, bool dropout, hipStream_t stream) {
+                        uint64_t seed, uint64_t offset, bool dropout, const int64_t* rng,
+                        hipStream_t stream) {
   if (planes == 0 || s == 0) return;
   if (s > kDnaMaxTile) {
     hipLaunchKernelGGL(dna_forward_big_kernel, dim3(static_cast<unsigned>(planes)),
                        dim3(kBigGroup), 0, stream, x, y, mean, rstd, scale, s, p, eps, slope,
-                       seed, offset, dropout);
+                       seed, offset, dropout, rng);
     return;
   }
   const bool vec = (s % 4 == 0) && (((reinterpret_cast<uintptr_t>(x) |
                                       reinterpret_cast<uintptr_t>(y)) & 15) == 0);
   if (vec) {
     TGPIPE_DNA_DISPATCH(dna_fwd_launch, true, x, y, mean, rstd, scale, planes, s, p, eps, slope,
-                        seed, offset, dropout, stream)
+                        seed, offset, dropout, rng, stream)
   } else {
     TGPIPE_DNA_DISPATCH(dna_fwd_launch, false, x, y, mean, rstd, scale, planes, s, p, eps,
-                        slope, seed, offset, dropout, stream)
+                        slope, seed, offset, dropout, rng, stream)
   }
 }
 
@@ -438,23 +459,23 @@ void launch_dna_backward(const float* dy, const float* x, const float* mean, con
 }
 
 void launch_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, uint64_t offset,
-                    hipStream_t stream) {
+                    const int64_t* rng, hipStream_t stream) {
   if (n == 0) return;
   const int64_t quads = (n + 3) / 4;
   int64_t grid = (quads + 255) / 256;
   if (grid > 2048) grid = 2048;
   const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
   hipLaunchKernelGGL(dropout_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0, stream, x,
-                     y, n, p, seed, offset, vec);
+                     y, n, p, seed, offset, vec, rng);
 }
 
 void launch_philox_uniform(float* out, int64_t n, uint64_t seed, uint64_t offset,
-                           hipStream_t stream) {
+                           const int64_t* rng, hipStream_t stream) {
   if (n == 0) return;
   int64_t grid = ((n + 3) / 4 + 255) / 256;
   if (grid > 2048) grid = 2048;
   hipLaunchKernelGGL(philox_uniform_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0,
-                     stream, out, n, seed, offset);
+                     stream, out, n, seed, offset, rng);
 }
 
 void launch_spin(uint64_t ns, hipStream_t stream) {

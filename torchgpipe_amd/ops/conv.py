@@ -18,6 +18,13 @@ the transform runs once per optimizer step instead of once per call.
   between steps through ``param.data`` (which does not bump ``_version``), EMA
   swaps or manual surgery are always re-transformed; :func:`clear_winograd_caches`
   drops a module's caches explicitly.
+* Refresh in place: :func:`refresh_step_caches` (``PipelineStage.forward``, once per step,
+  on the stage's main stream) recomputes every existing entry *into its own buffer*, so a
+  cached transform keeps its address across steps -- which captured cell graphs
+  (``parallel/segments.py``) rely on -- and is ordered before every lane that later reads
+  it.  An entry created lazily inside a step records an event, and a reader on another
+  stream waits for it (forward lanes: micro-batch 1 may reach a layer before micro-batch 0
+  has transformed its weights).
 * Memory: every cached byte counts against one process-wide budget
   (``TGPIPE_WINOGRAD_CACHE_MB``, default 5 % of the device's memory).  A
   transform that would exceed it is used for the call and then dropped, so giant
@@ -25,7 +32,7 @@ the transform runs once per optimizer step instead of once per call.
   the uncached path.
 """
 import os
-from typing import Dict, Optional, Sequence, Tuple
+from typing import Any, Dict, Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -34,7 +41,7 @@ import torch.nn.functional as F
 from torchgpipe_amd.ops import _ext, gradacc
 
 __all__ = ['WinogradConv2d', 'winograd_conv2d', 'wino_eligible', 'new_step',
-           'clear_winograd_caches', 'cache_bytes']
+           'clear_winograd_caches', 'cache_bytes', 'refresh_step_caches']
 
 _STEP = 0
 _CACHE_BYTES = 0
@@ -67,74 +74,118 @@ def _budget(device: torch.device) -> int:
     return _BUDGET
 
 
-class _TransformCache:
-    """Winograd-domain weights keyed by (storage, version, device, step) of the parameter.
+def _derive(weight: Tensor, slot: Tuple) -> Tensor:
+    """The derived weight of one cache slot: ``(flip, f4, bg)`` Winograd transforms, or
+    ``(True, True, 'T')`` the ``[ci][co][kh][kw]`` transpose."""
+    with torch.no_grad():
+        w = weight.detach()
+        if slot[2] == 'T':
+            return w.transpose(0, 1).contiguous()
+        ops = _ext.require(weight)
+        flip, f4, bg = slot
+        w = w.contiguous()
+        if bg:
+            return ops.bg_weight(w, flip, bg)
+        return ops.wino4_weight(w, flip) if f4 else ops.wino_weight(w, flip)
 
-    Entries per (flip, f4): F(2x2) ``U[Rp][Op][16]`` and F(4x4) ``U4[Rp/4][Op/16][4][16][36]``.
+
+def _ready_event(t: Tensor) -> Optional[Any]:
+    """An event after the work that produced ``t`` on the current stream (``None`` on CPU or
+    inside a capture, where every reader is ordered by the capture itself)."""
+    if not t.is_cuda or torch.cuda.is_current_stream_capturing():
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+    return ev
+
+
+def _await(t: Tensor, ready: Optional[Any]) -> None:
+    if ready is not None and not torch.cuda.is_current_stream_capturing():
+        torch.cuda.current_stream(t.device).wait_event(ready)
+
+
+class _TransformCache:
+    """Derived weights keyed by (storage, version, device, step) of the parameter.
+
+    Entries per slot ``(flip, f4, bg)``: F(2x2) ``U[Rp][Op][16]``, F(4x4)
+    ``U4[Rp/4][Op/16][4][16][36]``, the batched-GEMM layouts, or the transpose (slot
+    ``(True, True, 'T')``).  Each entry is ``(key, tensor, ready event)``.
     """
 
-    __slots__ = ('_entries', '__weakref__')
+    __slots__ = ('_entries', '_weight', '__weakref__')
 
     def __init__(self) -> None:
-        self._entries: Dict[Tuple, Tuple[Tuple[int, int, torch.device, int], Tensor]] = {}
+        self._entries: Dict[Tuple, Tuple[Tuple[int, int, torch.device, int], Tensor,
+                                         Optional[Any]]] = {}
+        # a detached alias of the weight (same storage and version counter): the caller may
+        # pass a saved-tensor object rather than the parameter, which a weak reference
+        # would not keep
+        self._weight: Optional[Tensor] = None
+
+    def _lookup(self, weight: Tensor, slot: Tuple) -> Tensor:
+        global _CACHE_BYTES
+        key = (weight.data_ptr(), weight._version, weight.device, _STEP)
+        hit = self._entries.get(slot)
+        if hit is not None and hit[0] == key:
+            _await(hit[1], hit[2])
+            return hit[1]
+        if hit is not None:  # stale: release before transforming again
+            _CACHE_BYTES -= hit[1].numel() * hit[1].element_size()
+            del self._entries[slot]
+        u = _derive(weight, slot)
+        size = u.numel() * u.element_size()
+        if _CACHE_BYTES + size <= _budget(weight.device):
+            self._entries[slot] = (key, u, _ready_event(u))
+            self._weight = weight.detach()
+            _CACHE_BYTES += size
+        return u
 
     def get(self, weight: Tensor, flip: bool, f4: bool = False, bg: int = 0) -> Tensor:
         """The transformed weight for ``flip`` (backward-data) and the kernel family:
         F(2x2) (default), F(4x4) fused (``f4``) or the batched-GEMM layout of F(4x4) /
         F(2x2) (``bg`` = 4 / 2)."""
-        global _CACHE_BYTES
-        key = (weight.data_ptr(), weight._version, weight.device, _STEP)
-        slot = (flip, f4, bg)
-        hit = self._entries.get(slot)
-        if hit is not None and hit[0] == key:
-            return hit[1]
-        if hit is not None:  # stale: release before transforming again
-            _CACHE_BYTES -= hit[1].numel() * hit[1].element_size()
-            del self._entries[slot]
-        ops = _ext.require(weight)
-        with torch.no_grad():
-            w = weight.detach().contiguous()
-            if bg:
-                u = ops.bg_weight(w, flip, bg)
-            else:
-                u = ops.wino4_weight(w, flip) if f4 else ops.wino_weight(w, flip)
-        size = u.numel() * u.element_size()
-        if _CACHE_BYTES + size <= _budget(weight.device):
-            self._entries[slot] = (key, u)
-            _CACHE_BYTES += size
-        return u
+        return self._lookup(weight, (flip, f4, bg))
 
     def get_transposed(self, weight: Tensor) -> Tensor:
         """``weight`` as ``[ci][co][kh][kw]`` (contiguous): the backward-data GEMM operand
         of the implicit-GEMM convolutions, transposed once per step instead of per call."""
-        global _CACHE_BYTES
+        return self._lookup(weight, (True, True, 'T'))
+
+    def refresh(self) -> None:
+        """Recompute every entry in place for the weight's current value and this step."""
+        weight = self._weight
+        if weight is None:
+            return
         key = (weight.data_ptr(), weight._version, weight.device, _STEP)
-        slot = (True, True, 'T')
-        hit = self._entries.get(slot)
-        if hit is not None and hit[0] == key:
-            return hit[1]
-        if hit is not None:
-            _CACHE_BYTES -= hit[1].numel() * hit[1].element_size()
-            del self._entries[slot]
-        with torch.no_grad():
-            t = weight.detach().transpose(0, 1).contiguous()
-        size = t.numel() * t.element_size()
-        if _CACHE_BYTES + size <= _budget(weight.device):
-            self._entries[slot] = (key, t)
-            _CACHE_BYTES += size
-        return t
+        for slot, (old, u, _) in list(self._entries.items()):
+            if old[0] != key[0] or old[2] != key[2]:
+                continue  # another weight storage (module surgery): left to the lazy path
+            if old != key:
+                u.copy_(_derive(weight, slot))
+            self._entries[slot] = (key, u, None)
 
     def clear(self) -> None:
         global _CACHE_BYTES
-        for _, u in self._entries.values():
+        for _, u, _ in self._entries.values():
             _CACHE_BYTES -= u.numel() * u.element_size()
         self._entries.clear()
+        self._weight = None
 
     def __del__(self) -> None:
         try:
             self.clear()
         except Exception:  # interpreter shutdown
             pass
+
+
+def refresh_step_caches(module: nn.Module) -> None:
+    """Refresh every step-scoped derived-weight cache in ``module`` in place (current
+    stream): Winograd transforms, transposed weights and grouped-GEMM concatenations."""
+    from torchgpipe_amd.ops.convbn import _GroupCache
+    for m in module.modules():
+        for v in list(vars(m).values()):
+            if isinstance(v, (_TransformCache, _GroupCache)):
+                v.refresh()
 
 
 def clear_winograd_caches(module: torch.nn.Module) -> None:

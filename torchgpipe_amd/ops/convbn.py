@@ -321,23 +321,48 @@ class _GroupCache:
     """The concatenated weights of a group (and their transpose) for one pipeline step:
     keyed like the Winograd transforms (storage, version, step of every weight)."""
 
-    __slots__ = ('key', 'cat', 'cat_t', '__weakref__')
+    __slots__ = ('key', 'cat', 'cat_t', 'weights', 'ready', '__weakref__')
 
     def __init__(self) -> None:
         self.key: Optional[Tuple] = None
         self.cat: Optional[Tensor] = None
         self.cat_t: Optional[Tensor] = None
+        self.weights: List[Tensor] = []  # detached aliases (see _TransformCache)
+        self.ready: Optional[object] = None
+
+    @staticmethod
+    def _key(weights: Sequence[Tensor]) -> Tuple:
+        from torchgpipe_amd.ops import conv as _conv
+        return tuple((w.data_ptr(), w._version) for w in weights) + (_conv._STEP,)
 
     def get(self, weights: Sequence[Tensor]) -> Tuple[Tensor, Tensor]:
-        from torchgpipe_amd.ops import conv as _conv
-        key = tuple((w.data_ptr(), w._version) for w in weights) + (_conv._STEP,)
+        from torchgpipe_amd.ops.conv import _await, _ready_event
+        key = self._key(weights)
         if key != self.key or self.cat is None or self.cat_t is None:
             with torch.no_grad():
                 cat = torch.cat([w.detach().reshape(w.shape[0], -1) for w in weights])
                 self.cat = cat.view(cat.shape[0], cat.shape[1], 1, 1)
                 self.cat_t = cat.t().contiguous().view(cat.shape[1], cat.shape[0], 1, 1)
             self.key = key
+            self.weights = [w.detach() for w in weights]
+            self.ready = _ready_event(self.cat_t)
+        else:
+            _await(self.cat, self.ready)
         return self.cat, self.cat_t
+
+    def refresh(self) -> None:
+        """Recompute the concatenations in place (same buffers) for this step."""
+        weights = self.weights
+        if not weights or self.cat is None or self.cat_t is None:
+            return
+        key = self._key(weights)
+        if key != self.key:
+            with torch.no_grad():
+                flat = self.cat.view(self.cat.shape[0], self.cat.shape[1])
+                torch.cat([w.reshape(w.shape[0], -1) for w in weights], out=flat)
+                self.cat_t.view(flat.shape[1], flat.shape[0]).copy_(flat.t())
+            self.key = key
+        self.ready = None
 
 
 class _GroupConvBN(torch.autograd.Function):

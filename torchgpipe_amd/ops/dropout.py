@@ -8,7 +8,7 @@ pairs from its RNG tape instead of restoring global generator state from an
 autograd thread (the reference's ``fork_rng``, ``torchgpipe/checkpoint.py:191-231``).
 The elementwise kernel stores no mask: backward regenerates it from the pair.
 """
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -16,7 +16,7 @@ from torch import Tensor, nn
 from torchgpipe_amd.ops import _ext
 from torchgpipe_amd.ops.fused import _signed64
 from torchgpipe_amd.ops.philox import uniform
-from torchgpipe_amd.utils.rng import philox_pair
+from torchgpipe_amd.utils.rng import philox_draw
 
 __all__ = ['dropout', 'Dropout', 'dropout2d', 'Dropout2d', 'convert_dropout']
 
@@ -28,15 +28,16 @@ def _reference(x: Tensor, p: float, seed: int, offset: int) -> Tensor:
 
 class _Dropout(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x: Tensor, p: float, seed: int, offset: int) -> Tensor:  # type: ignore[override]
-        ctx.p, ctx.seed, ctx.offset = p, seed, offset
-        return _ext.require(x).dropout(x, p, seed, offset)
+    def forward(ctx, x: Tensor, p: float, seed: int, offset: int,  # type: ignore[override]
+                rng: Optional[Tensor] = None) -> Tensor:
+        ctx.p, ctx.seed, ctx.offset, ctx.rng = p, seed, offset, rng
+        return _ext.require(x).dropout(x, p, seed, offset, rng)
 
     @staticmethod
     def backward(ctx, dy: Tensor) -> Tuple:  # type: ignore[override]
         # The same mask and scale apply to the gradient.
-        return _ext.require(dy).dropout(dy.contiguous(), ctx.p, ctx.seed, ctx.offset), \
-            None, None, None
+        return _ext.require(dy).dropout(dy.contiguous(), ctx.p, ctx.seed, ctx.offset,
+                                        ctx.rng), None, None, None, None
 
 
 def dropout(x: Tensor, p: float = 0.5, training: bool = True) -> Tensor:
@@ -44,9 +45,11 @@ def dropout(x: Tensor, p: float = 0.5, training: bool = True) -> Tensor:
         return x
     if p >= 1.0:
         return x * 0.0
-    seed, offset = philox_pair(x.device, x.numel())
+    seed, offset, rng = philox_draw(x.device, x.numel())
     if x.is_cuda and x.dtype == torch.float32:
-        return _Dropout.apply(x.contiguous(), float(p), _signed64(seed), _signed64(offset))
+        return _Dropout.apply(x.contiguous(), float(p), _signed64(seed), _signed64(offset), rng)
+    if rng is not None:
+        raise RuntimeError('dropout: a device Philox slot needs the fp32 GPU kernel')
     return _reference(x, p, seed, offset)
 
 
@@ -83,9 +86,10 @@ def dropout2d(x: Tensor, p: float = 0.5, training: bool = True) -> Tensor:
     if p >= 1.0:
         return x * 0.0
     planes = x.shape[0] * x.shape[1]
-    seed, offset = philox_pair(x.device, planes)
+    seed, offset, rng = philox_draw(x.device, planes)
     if x.is_cuda:
-        u = _ext.require(x).philox_uniform(planes, _signed64(seed), _signed64(offset), x.device)
+        u = _ext.require(x).philox_uniform(planes, _signed64(seed), _signed64(offset), x.device,
+                                           rng)
     else:
         u = uniform(planes, seed, offset)
     keep = (u >= p).to(x.dtype).view(x.shape[0], x.shape[1], *([1] * (x.dim() - 2)))

@@ -16,7 +16,7 @@ checkpoint recomputation through the cell's RNG tape.
 CPU tensors (and non-fp32 dtypes) use a PyTorch composite with the same
 Philox mask — the oracle of the kernel tests.
 """
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -24,7 +24,7 @@ import torch.nn.functional as F
 
 from torchgpipe_amd.ops import _ext
 from torchgpipe_amd.ops.philox import philox4x32_10, to_uniform
-from torchgpipe_amd.utils.rng import philox_pair
+from torchgpipe_amd.utils.rng import philox_draw
 
 __all__ = ['drop_norm_act', 'DropNormAct', 'plane_scale_reference']
 
@@ -55,9 +55,9 @@ def _composite(x: Tensor, p: float, eps: float, slope: float, seed: int, offset:
 class _DropNormAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: Tensor, p: float, eps: float, slope: float,  # type: ignore[override]
-                seed: int, offset: int, dropout: bool) -> Tensor:
+                seed: int, offset: int, dropout: bool, rng: Optional[Tensor] = None) -> Tensor:
         ops = _ext.require(x)
-        y, mean, rstd, scale = ops.dna_forward(x, p, eps, slope, seed, offset, dropout)
+        y, mean, rstd, scale = ops.dna_forward(x, p, eps, slope, seed, offset, dropout, rng)
         ctx.save_for_backward(x, mean, rstd, scale)
         ctx.slope = slope
         return y
@@ -66,7 +66,7 @@ class _DropNormAct(torch.autograd.Function):
     def backward(ctx, dy: Tensor) -> Tuple:  # type: ignore[override]
         x, mean, rstd, scale = ctx.saved_tensors
         dx = _ext.require(dy).dna_backward(dy, x, mean, rstd, scale, ctx.slope)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
 def drop_norm_act(x: Tensor, p: float = 0.1, training: bool = True, eps: float = 1e-5,
@@ -74,10 +74,12 @@ def drop_norm_act(x: Tensor, p: float = 0.1, training: bool = True, eps: float =
     """``leaky_relu(instance_norm(dropout2d(x, p)), slope)`` in one HIP kernel."""
     dropout = training and p > 0.0
     n, c = x.shape[:2]
-    seed, offset = philox_pair(x.device, n * c) if dropout else (0, 0)
+    seed, offset, rng = philox_draw(x.device, n * c) if dropout else (0, 0, None)
     if x.is_cuda and x.dtype == torch.float32:
         return _DropNormAct.apply(x.contiguous(), float(p), float(eps), float(slope),
-                                  _signed64(seed), _signed64(offset), dropout)
+                                  _signed64(seed), _signed64(offset), dropout, rng)
+    if rng is not None:
+        raise RuntimeError('drop_norm_act: a device Philox slot needs the fp32 GPU kernel')
     return _composite(x, p, eps, slope, seed, offset, dropout)
 
 

@@ -48,7 +48,7 @@ import torch
 from torch import Tensor
 
 __all__ = ['target', 'commit', 'enabled', 'release', 'deferred_wgrad', 'slab', 'deferred',
-           'flush_pending']
+           'flush_pending', 'pending_snapshot', 'register_pending']
 
 _ENABLED = os.environ.get('TGPIPE_FUSED_GRAD_ACCUM', '1') != '0'
 _DEFER_ENABLED = os.environ.get('TGPIPE_DEFERRED_WGRAD', '1') != '0'
@@ -231,3 +231,29 @@ def flush_pending(device: torch.device) -> None:
     if slabs:
         from torchgpipe_amd.ops import _ext
         _ext.require(grads[0]).wgrad_slab_flush(slabs, grads, accumulate)
+
+
+def pending_snapshot(device: torch.device) -> List[Tuple['weakref.ref[Tensor]', Tensor]]:
+    """The slabs written so far in the current deferral scope on ``device`` (before its
+    flush).  Captured cell graphs (``parallel/segments.py``) write these slabs again on
+    every replay without running the Python that registers them; the pipeline re-registers
+    this snapshot in each replayed step (:func:`register_pending`)."""
+    state = _DEFER.get(_device_key(device))
+    return list(state.pending.values()) if state is not None else []
+
+
+def register_pending(device: torch.device,
+                     items: List[Tuple['weakref.ref[Tensor]', Tensor]]) -> None:
+    """Mark ``items`` (from :func:`pending_snapshot`) as written in the current scope, so the
+    scope's flush sums them into ``.grad``."""
+    state = _DEFER.get(_device_key(device))
+    if state is None or state.depth == 0:
+        return
+    for ref, sb in items:
+        param = ref()
+        if param is None:
+            continue
+        entry = getattr(param, _SLAB_ATTR, None)
+        if entry is not None:
+            entry[1] = state.step
+        state.pending.setdefault(id(param), (ref, sb))

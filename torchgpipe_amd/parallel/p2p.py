@@ -117,12 +117,13 @@ class Message:
     """Handle of a posted receive: ``wait()`` returns the received tensors."""
 
     __slots__ = ('_works', '_tensors', '_buffer', '_metas', 'atomic', '_device', '_timeout',
-                 '_what')
+                 '_what', '_dest')
 
     def __init__(self, works: List[object], tensors: Optional[List[Tensor]],
                  buffer: Optional[Tensor], metas: List[TensorMeta], atomic: bool,
                  device: Optional[torch.device] = None,
-                 timeout: Optional[datetime.timedelta] = None, what: str = '') -> None:
+                 timeout: Optional[datetime.timedelta] = None, what: str = '',
+                 dest: Optional[List[Tensor]] = None) -> None:
         self._works = works
         self._timeout = timeout
         self._what = what
@@ -131,8 +132,10 @@ class Message:
         self._metas = metas
         self.atomic = atomic
         # Host-staged receive (gloo transport for device tensors): move the
-        # received host buffers onto this device after the wait.
+        # received host buffers onto this device after the wait -- into ``dest``
+        # (persistent device buffers, same layout as the host ones) when given.
         self._device = device
+        self._dest = dest
 
     def wait(self) -> List[Tensor]:
         """Wait (stream-ordered on GPUs) and return detached leaf tensors.
@@ -144,10 +147,20 @@ class Message:
             _wait(w, self._timeout, self._what)
         self._works = []
         if self._device is not None:
-            if self._tensors is not None:
-                self._tensors = [t.to(self._device, non_blocking=True) for t in self._tensors]
-            if self._buffer is not None:
-                self._buffer = self._buffer.to(self._device, non_blocking=True)
+            if self._dest is not None:
+                host = self._tensors if self._tensors is not None else [self._buffer]
+                for d, h in zip(self._dest, host):  # type: ignore[arg-type]
+                    d.copy_(h, non_blocking=True)
+                if self._tensors is not None:
+                    self._tensors = list(self._dest)
+                else:
+                    self._buffer = self._dest[0]
+            else:
+                if self._tensors is not None:
+                    self._tensors = [t.to(self._device, non_blocking=True)
+                                     for t in self._tensors]
+                if self._buffer is not None:
+                    self._buffer = self._buffer.to(self._device, non_blocking=True)
             self._device = None
         if self._tensors is None:
             assert self._buffer is not None
@@ -202,6 +215,8 @@ class P2P:
         self._host_waits = not dist.is_initialized() or dist.get_backend(group) == 'gloo' \
             or device.type != 'cuda'
         self._meta: Dict[Hashable, Tuple[List[TensorMeta], bool]] = {}
+        # persistent receive buffers (recv(..., persistent=True)), per message key
+        self._bufs: Dict[Hashable, List[Tensor]] = {}
         self._pending_sends: List[object] = []
         self._pending_meta: List[object] = []
 
@@ -233,6 +248,7 @@ class P2P:
 
     def forget(self) -> None:
         self._meta.clear()
+        self._bufs.clear()
 
     # -- tensors ----------------------------------------------------------------------------
 
@@ -269,8 +285,16 @@ class P2P:
             buf = buf.cpu()
         self._pending_sends.append(dist.isend(buf, dst, group=self._link(dst)))
 
-    def recv(self, src: int, key: Hashable, cache: bool = True) -> Message:
-        """Post a receive from ``src``; the returned handle's ``wait()`` yields tensors."""
+    def recv(self, src: int, key: Hashable, cache: bool = True,
+             persistent: bool = False) -> Message:
+        """Post a receive from ``src``; the returned handle's ``wait()`` yields tensors.
+
+        ``persistent``: receive into buffers kept per ``key`` and reused by every later
+        receive of that key, so the tensors of a message sit at the same addresses each
+        step (captured cell graphs read them in place, ``parallel/segments.py``).  The
+        caller orders a new receive after the last reader of the previous one (the
+        pipeline posts receives from its main stream, which has joined every lane by then).
+        """
         cached = self._meta.get(key)
         if cached is None:
             cached = self._recv_meta(src, key)
@@ -283,13 +307,31 @@ class P2P:
         late = self.device if self.stage_host else None
         timeout = self.timeout if self._host_waits else None
         what = f'message {key!r} from rank {src}'
-        if len(metas) == 1 or not self.pack:
-            out = [torch.empty(m.shape, dtype=m.dtype, device=where) for m in metas]
+        split = len(metas) == 1 or not self.pack
+        keep = self._persistent(key, metas, split) if persistent else None
+        if split:
+            out = ([torch.empty(m.shape, dtype=m.dtype, device=where) for m in metas]
+                   if keep is None or self.stage_host else list(keep))
             works = [dist.irecv(t, src, group=self._link(src)) for t in out]
-            return Message(works, out, None, metas, atomic, late, timeout, what)
-        buf = torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=where)
+            return Message(works, out, None, metas, atomic, late, timeout, what,
+                           keep if self.stage_host else None)
+        buf = (torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=where)
+               if keep is None or self.stage_host else keep[0])
         return Message([dist.irecv(buf, src, group=self._link(src))], None, buf, metas, atomic,
-                       late, timeout, what)
+                       late, timeout, what, keep if self.stage_host else None)
+
+    def _persistent(self, key: Hashable, metas: Sequence[TensorMeta],
+                    split: bool) -> List[Tensor]:
+        """The device buffers of ``key``'s persistent receives (allocated on first use)."""
+        bufs = self._bufs.get(key)
+        if bufs is None:
+            if split:
+                bufs = [torch.empty(m.shape, dtype=m.dtype, device=self.device) for m in metas]
+            else:
+                bufs = [torch.empty(self._packed_nbytes(metas), dtype=torch.uint8,
+                                    device=self.device)]
+            self._bufs[key] = bufs
+        return bufs
 
     def _link(self, peer: int) -> Optional[dist.ProcessGroup]:
         return self.link_groups.get(peer, self.group)

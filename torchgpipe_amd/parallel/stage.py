@@ -43,6 +43,7 @@ from torchgpipe_amd.checkpoint import Checkpointing
 from torchgpipe_amd.gpipe import check_balance, partition_layers, verify_module
 from torchgpipe_amd.microbatch import Batch
 from torchgpipe_amd.ops.conv import new_step as wino_new_step
+from torchgpipe_amd.ops.conv import refresh_step_caches
 from torchgpipe_amd.ops.dropout import convert_dropout
 from torchgpipe_amd.ops.fusion import relink
 from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P, _wait
@@ -94,6 +95,25 @@ def _micro_batch_count(sig: Signature, chunks: int) -> int:
     return len(torch.empty(batch, 0).chunk(chunks)) if batch > 0 else 0
 
 
+@contextlib.contextmanager
+def _shared_accumulators() -> Any:
+    """Backward passes of micro-batches that ran on different lanes.
+
+    A parameter whose gradient autograd accumulates (one the fused ops do not write into
+    ``.grad`` themselves: MIOpen strided convolutions, Linear layers) has one
+    ``AccumulateGrad`` node per step, shared by the graphs of every micro-batch alive at
+    once and bound to the stream of the micro-batch that created it.  Lanes put those
+    micro-batches on different streams by design, so the engine orders each accumulation
+    after the producing lane (the ordering the lanes need) and warns about the mismatch;
+    here it is intentional, and the warning is off for the duration of the backward.
+    """
+    torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
+    try:
+        yield
+    finally:
+        torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(True)
+
+
 class _RemoteSkipTracker(SkipTracker):
     """Skip tracker of one cell: local skips in a dict, cross-rank ones captured."""
 
@@ -121,10 +141,13 @@ class _RemoteSkipTracker(SkipTracker):
 class _Cell:
     """Bookkeeping of one micro-batch on this rank."""
 
-    __slots__ = ('index', 'inputs', 'outputs', 'out_atomic', 'chk', 'n_act_out', 'lane')
+    __slots__ = ('index', 'inputs', 'outputs', 'out_atomic', 'chk', 'n_act_out', 'lane', 'fn',
+                 'seg')
 
     def __init__(self, index: int) -> None:
         self.index = index
+        self.fn: Optional[Callable[[Tensors], Tensors]] = None  # (segments: for the capture)
+        self.seg = False  # a captured cell (parallel/segments.py)
         self.inputs: List[Tensor] = []      # leaves: activations + popped remote skips
         self.outputs: List[Tensor] = []     # outputs + stashed remote skips
         self.out_atomic = True
@@ -156,6 +179,17 @@ class PipelineStage:
             off for gloo).
         materialize: called on this rank's partition before it is moved to
             ``device`` (e.g. to initialise layers built on the ``meta`` device).
+        graph_cells: replay every checkpointed micro-batch's forward, recomputation and
+            backward as captured hipGraphs, with the transfers issued eagerly in between
+            (``parallel/segments.py``): after ``graph_warmup`` eager steps and one capture
+            step, the host launches three graphs per cell instead of every kernel.  GPU
+            stages only; gradients are zeroed at the start of each step (each step computes
+            them from scratch, like ``StepGraph``).
+        graph_warmup: eager steps before the capture step.
+        transport: a stand-in for the point-to-point layer (``P2P`` interface), e.g.
+            :class:`~torchgpipe_amd.parallel.loopback.LoopbackP2P` to run this stage as
+            ``rank`` of a ``len(balance)``-stage pipeline in one process without
+            ``torch.distributed`` (single-device stage emulation); ``rank`` is required.
         timeout: seconds any host-blocking wait of this stage (shape metadata,
             control messages, gloo tensors) may take before raising
             :class:`~torchgpipe_amd.parallel.p2p.PipelineTimeout`; also the
@@ -176,7 +210,10 @@ class PipelineStage:
                  overlap_recompute: bool = False,
                  overlap_forward: bool = False,
                  wgrad_stream: bool = False,
-                 philox_dropout: bool = False) -> None:
+                 philox_dropout: bool = False,
+                 graph_cells: bool = False,
+                 graph_warmup: int = 1,
+                 transport: Optional[Any] = None) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
         if checkpoint not in ('always', 'except_last', 'never'):
@@ -187,16 +224,22 @@ class PipelineStage:
         check_balance(module, balance)
 
         self.group = group
-        distributed = dist.is_available() and dist.is_initialized()
-        if not distributed and len(balance) != 1:
-            raise RuntimeError('a multi-stage pipeline needs torch.distributed to be initialized')
-        self.world = dist.get_world_size(group) if distributed else 1
-        self.rank = (dist.get_rank(group) if distributed else 0) if rank is None else rank
+        distributed = dist.is_available() and dist.is_initialized() and transport is None
+        if transport is not None:
+            if rank is None:
+                raise ValueError('a stage on a stand-in transport needs its rank')
+            self.world, self.rank = len(balance), rank
+        else:
+            if not distributed and len(balance) != 1:
+                raise RuntimeError('a multi-stage pipeline needs torch.distributed to be '
+                                   'initialized')
+            self.world = dist.get_world_size(group) if distributed else 1
+            self.rank = (dist.get_rank(group) if distributed else 0) if rank is None else rank
         if self.world != len(balance):
             raise ValueError(f'pipeline group has {self.world} ranks but balance has '
                              f'{len(balance)} partitions')
-        self.ranks = [dist.get_global_rank(group, r) if group is not None else r
-                      for r in range(self.world)]
+        self.ranks = [dist.get_global_rank(group, r) if group is not None and distributed
+                      else r for r in range(self.world)]
         self.n = len(balance)
         self.balance = balance
         self.chunks = chunks
@@ -252,9 +295,10 @@ class PipelineStage:
             else:
                 ctrl_group = dist.new_group(ranks=self.ranks, backend='gloo', **group_kwargs)
         self.ctrl_group = ctrl_group
-        self.p2p = P2P(device, group=group, ctrl_group=ctrl_group, pack=pack,
-                       link_groups=self._make_links(links, group_kwargs) if distributed else None,
-                       timeout=timeout)
+        self.p2p = transport if transport is not None else \
+            P2P(device, group=group, ctrl_group=ctrl_group, pack=pack,
+                link_groups=self._make_links(links, group_kwargs) if distributed else None,
+                timeout=timeout)
 
         self._cells: List[_Cell] = []
         self.overlap_recompute = overlap_recompute
@@ -269,8 +313,37 @@ class PipelineStage:
         self._sig: Optional[Signature] = None
         self._m = 0
         self._probe: Optional[List[Tuple[str, Any, Any]]] = None
+        if graph_cells and wgrad_stream:
+            raise ValueError('graph_cells does not combine with wgrad_stream')
+        if graph_warmup < 1:
+            raise ValueError('graph_cells needs at least one eager warm-up step')
+        self.graph_cells = graph_cells and device.type == 'cuda'
+        self.graph_warmup = graph_warmup
+        self._segments: Optional[Any] = None
+        self._seg_key: Optional[Tuple[Any, ...]] = None
+        self._seg_phase = 'eager'
+        self._persistent = False  # this step receives into persistent buffers
         if distributed and self.n > 1:
             self.connect()
+
+    def _segments_for(self, sig: Signature, stop: int) -> Optional[Any]:
+        """The captured cells for this step's signature (``None``: eager step)."""
+        if not self.graph_cells or not self.training or \
+                not torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing():
+            return None
+        key = (sig, stop)
+        if self._segments is None or self._seg_key != key:
+            from torchgpipe_amd.parallel.segments import Segments
+            self._segments = Segments(self.partition, self.device,
+                                      _micro_batch_count(sig, self.chunks), stop,
+                                      self.graph_warmup)
+            self._seg_key = key
+        return self._segments
+
+    @property
+    def graph_phase(self) -> str:
+        """Phase of the last step with ``graph_cells``: 'eager', 'capture' or 'replay'."""
+        return self._seg_phase
 
     def _link_pairs(self) -> List[Tuple[int, int]]:
         """Stage pairs that exchange messages: neighbours plus cross-rank skip routes."""
@@ -442,6 +515,14 @@ class PipelineStage:
         if self._has_dbn:
             set_micro_batches(self.partition, m)
         stop = self.checkpoint_stop(m)
+        if self.device.type == 'cuda':
+            # derived weights recomputed in place, on this stream, before any lane reads them
+            refresh_step_caches(self.partition)
+        seg = self._segments_for(sig, stop)
+        phase = seg.begin_step() if seg is not None else 'eager'
+        self._seg_phase = phase
+        graphed = phase in ('capture', 'replay')
+        persistent = self._persistent = seg is not None
 
         batches: Optional[List[Batch]] = None
         if self.is_first:
@@ -466,9 +547,11 @@ class PipelineStage:
                 in_atomic = b.atomic
                 act_msg = None
             else:
-                act_msg = self.p2p.recv(prev, self._key('act', i, prev, me))  # type: ignore[arg-type]
+                act_msg = self.p2p.recv(prev, self._key('act', i, prev, me),  # type: ignore[arg-type]
+                                        persistent=persistent)
                 in_atomic = True
-            skip_msgs = [self.p2p.recv(self.ranks[src], self._key('skip', i, self.ranks[src], me))
+            skip_msgs = [self.p2p.recv(self.ranks[src], self._key('skip', i, self.ranks[src], me),
+                                       persistent=persistent)
                          for src in sorted({s for s, _ in self.in_skips})]
             mark = self._probe_begin() if act_msg is not None or skip_msgs else None
             if act_msg is not None:
@@ -485,19 +568,42 @@ class PipelineStage:
             #    alternate between two forward lanes)
             fn = self._make_fn(cell, len(acts), in_atomic)
             lane = None
-            if flanes is not None:
+            if graphed:
+                # a captured cell: its graphs read the persistent inputs in place
+                assert seg is not None
+                sc = seg.cells[i]
+                fresh = sc.fwd is None
+                if fresh:
+                    flat = seg.adopt_inputs(i, flat, owned=self.is_first)
+                else:
+                    flat = seg.static_inputs(i, flat)
+                cell.inputs = flat
+                cell.seg = True
+                cell.fn = fn if sc.rec is None else None
+                if flanes is not None:
+                    lane = flanes[i % 2]
+                run = lane if lane is not None else torch.cuda.current_stream(self.device)
+                with trace.range(f'fwd graph mb{i} stage{self.rank}'):
+                    seg.forward(i, fn, run)
+                if fresh:  # the capture ran fn: it described the outputs
+                    sc.out_atomic, sc.n_act_out = cell.out_atomic, cell.n_act_out
+                else:
+                    cell.out_atomic, cell.n_act_out = sc.out_atomic, sc.n_act_out
+                out = seg.user_outputs(i)
+            elif flanes is not None:
                 assert main is not None
                 lane = flanes[i % 2]
                 lane.wait_stream(main)
                 for t in flat:
                     t.record_stream(lane)
-            with torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext():
-                if i < stop:
-                    cell.chk = Checkpointing(fn, Batch(tuple(flat)))
-                    out = list(cell.chk.checkpoint())
-                else:
-                    out = list(fn(tuple(flat)))
-            if lane is not None:
+            if not cell.seg:
+                with torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext():
+                    if i < stop:
+                        cell.chk = Checkpointing(fn, Batch(tuple(flat)))
+                        out = list(cell.chk.checkpoint())
+                    else:
+                        out = list(fn(tuple(flat)))
+            if lane is not None and not cell.seg:
                 assert main is not None
                 for t in out:
                     t.record_stream(main)
@@ -552,6 +658,13 @@ class PipelineStage:
                 self._backward(losses)
 
     def _backward(self, losses: Optional[Sequence[Tensor]] = None) -> None:
+        if self._recompute_lanes() is not None or self._fwd_lanes is not None:
+            with _shared_accumulators():
+                self._backward_cells(losses)
+        else:
+            self._backward_cells(losses)
+
+    def _backward_cells(self, losses: Optional[Sequence[Tensor]] = None) -> None:
         if self.is_last and losses is None:
             raise ValueError('the last stage must pass the per-micro-batch losses')
         nxt = self.ranks[self.rank + 1] if not self.is_last else None
@@ -562,6 +675,11 @@ class PipelineStage:
         lanes = self._recompute_lanes()
         on_gpu = self.device.type == 'cuda'
         main = torch.cuda.current_stream(self.device) if on_gpu else None
+        seg = self._segments if self._seg_phase in ('capture', 'replay') else None
+        # the capture step recomputes no cell ahead: a graph captured while another cell's
+        # autograd graph is alive would share its AccumulateGrad nodes (and their streams)
+        ahead = seg is None or self._seg_phase == 'replay'
+        persistent = self._persistent
         # stream that ran the previous micro-batch's backward (None: main / CPU)
         prev_run: Optional[torch.cuda.Stream] = None
         for j, cell in enumerate(cells):
@@ -569,21 +687,27 @@ class PipelineStage:
             # 1. post the gradient receives first ...
             grad_msg = None
             if nxt is not None and any(t.requires_grad for t in cell.outputs[:cell.n_act_out]):
-                grad_msg = self.p2p.recv(nxt, self._key('gact', i, nxt, me))
+                grad_msg = self.p2p.recv(nxt, self._key('gact', i, nxt, me),
+                                         persistent=persistent)
             skip_grad_msgs = []
             for dst in sorted({d for d, _ in self.out_skips}):
                 peer = self.ranks[dst]
                 skip_grad_msgs.append(
-                    (dst, self.p2p.recv(peer, self._key('gskip', i, peer, me))))
+                    (dst, self.p2p.recv(peer, self._key('gskip', i, peer, me),
+                                        persistent=persistent)))
             # 2. ... then recompute while they are in flight
             if lanes is None:
-                if cell.chk is not None:
+                if cell.seg:
+                    assert seg is not None and main is not None
+                    with trace.range(f'recompute graph mb{i} stage{self.rank}'):
+                        seg.recompute(i, cell.fn, main)
+                elif cell.chk is not None:
                     with trace.range(f'recompute mb{i} stage{self.rank}'):
                         cell.chk.recompute_now()
             else:
                 assert main is not None
                 self._recompute_on_lane(cell, lanes[j % 2], main)
-                if j + 1 < len(cells):
+                if j + 1 < len(cells) and ahead:
                     # the next micro-batch's recomputation (which touches no gradient) runs
                     # on the other lane while this backward runs; issued before this
                     # cell's gradient wait so it never queues behind the transfer
@@ -592,28 +716,40 @@ class PipelineStage:
             # 3. backward through this cell
             tensors: List[Tensor] = []
             grads: List[Tensor] = []
+            # captured cells: the gradient of each output (None: none), and whether it sits
+            # in a persistent receive buffer
+            seg_grads: List[Optional[Tensor]] = [None] * len(cell.outputs)
+            seg_kept = [False] * len(cell.outputs)
             act_out = cell.outputs[:cell.n_act_out]
             mark = self._probe_begin() if grad_msg is not None or skip_grad_msgs else None
             if self.is_last:
                 assert losses is not None
-                tensors.append(losses[i])
-                grads.append(torch.ones_like(losses[i]))
+                if cell.seg:  # the loss gradient w.r.t. the cell's output leaves
+                    torch.autograd.backward([losses[i]], [torch.ones_like(losses[i])])
+                    for k, t in enumerate(act_out):
+                        seg_grads[k] = t.grad
+                else:
+                    tensors.append(losses[i])
+                    grads.append(torch.ones_like(losses[i]))
             elif grad_msg is not None:
                 received = iter(grad_msg.wait())
-                for t in act_out:
+                for k, t in enumerate(act_out):
                     if t.requires_grad:
                         tensors.append(t)
                         grads.append(next(received))
+                        seg_grads[k], seg_kept[k] = grads[-1], persistent
             skip_out = cell.outputs[cell.n_act_out:]
             dst_of = [d for d, _ in self.out_skips]
             for dst, msg in skip_grad_msgs:
                 received = iter(msg.wait())
-                for d, t in zip(dst_of, skip_out):
+                for k, (d, t) in enumerate(zip(dst_of, skip_out)):
                     if d == dst:
                         g = next(received)
                         if t.requires_grad:
                             tensors.append(t)
                             grads.append(g)
+                            seg_grads[cell.n_act_out + k] = g
+                            seg_kept[cell.n_act_out + k] = persistent
             self._probe_end('bwd', mark)
             # A cell computed or recomputed on a lane runs its backward there (autograd
             # replays each op on its forward stream).  Order it after main (received
@@ -626,32 +762,46 @@ class PipelineStage:
                 cell.lane.wait_stream(main)
             if run is not None and prev_run is not None and prev_run is not run:
                 run.wait_stream(prev_run)
-            with trace.range(f'bwd mb{i} stage{self.rank}'):
-                if tensors:
-                    torch.autograd.backward(tensors, grads)
+            gins: Optional[List[Tensor]] = None
+            if cell.seg:
+                assert seg is not None and run is not None
+                with trace.range(f'bwd graph mb{i} stage{self.rank}'):
+                    gins = seg.backward(i, seg_grads, seg_kept, run)
+            else:
+                with trace.range(f'bwd mb{i} stage{self.rank}'):
+                    if tensors:
+                        torch.autograd.backward(tensors, grads)
             prev_run = run
 
-            # 4. ship input gradients upstream
+            # 4. ship input gradients upstream (a replayed backward ran no autograd, so its
+            #    sends leave from the stream that ran it)
             n_in_act = len(cell.inputs) - len(self.in_skips)
-            if prev is not None:
-                gin = [self._grad_of(t) for t in cell.inputs[:n_in_act] if t.requires_grad]
-                self.p2p.send(gin, prev, self._key('gact', i, me, prev))
-            skip_in = cell.inputs[n_in_act:]
-            by_src: Dict[int, List[Tensor]] = {}
-            for (src, _), t in zip(self.in_skips, skip_in):
-                by_src.setdefault(src, []).append(self._grad_of(t))
-            for src in sorted(by_src):
-                peer = self.ranks[src]
-                self.p2p.send(by_src[src], peer, self._key('gskip', i, me, peer))
+
+            def grad_in(k: int) -> Tensor:
+                return gins[k] if gins is not None else self._grad_of(cell.inputs[k])
+
+            with torch.cuda.stream(run) if gins is not None else contextlib.nullcontext():
+                if prev is not None:
+                    gin = [grad_in(k) for k in range(n_in_act) if cell.inputs[k].requires_grad]
+                    self.p2p.send(gin, prev, self._key('gact', i, me, prev))
+                by_src: Dict[int, List[Tensor]] = {}
+                for k, (src, _) in enumerate(self.in_skips):
+                    by_src.setdefault(src, []).append(grad_in(n_in_act + k))
+                for src in sorted(by_src):
+                    peer = self.ranks[src]
+                    self.p2p.send(by_src[src], peer, self._key('gskip', i, me, peer))
             cell.inputs = []
             cell.outputs = []
             cell.chk = None
             cell.lane = None
+            cell.fn = None
         if on_gpu:
             # fused kernels on the lanes wrote .grad without autograd knowing
             cur = torch.cuda.current_stream(self.device)
             for lane in (lanes or []) + (self._fwd_lanes or []):
                 cur.wait_stream(lane)
+        if seg is not None:
+            seg.end_backward()
         self._cells = []
         self.p2p.flush()
 
@@ -687,6 +837,13 @@ class PipelineStage:
     def _recompute_on_lane(self, cell: _Cell, lane: torch.cuda.Stream,
                            main: torch.cuda.Stream) -> None:
         """Issue ``cell``'s recomputation on ``lane`` (once); its backward then runs there."""
+        if cell.seg:
+            if cell.lane is None:
+                assert self._segments is not None
+                with trace.range(f'recompute graph mb{cell.index} stage{self.rank}'):
+                    self._segments.recompute(cell.index, cell.fn, lane)
+                cell.lane = lane
+            return
         if cell.chk is None or cell.lane is not None:
             return
         lane.wait_stream(main)

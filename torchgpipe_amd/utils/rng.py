@@ -14,6 +14,15 @@ generator at all and is bit-exact by construction.
 
 Because the pair is explicit, backward kernels regenerate the dropout mask
 from ``(seed, offset)`` instead of storing it — no mask tensor is kept alive.
+
+Captured cells (:mod:`torchgpipe_amd.parallel.segments`) cannot use host-side pairs: a
+graph replay would re-issue the captured constants and draw the same mask every step.
+Inside a :func:`slot_scope` the RNG ops instead read a *device-resident* state
+(:class:`PhiloxSlot`, int64 ``[seed, base offset]``) when their kernel runs, and the
+host-side offset they pass is the counter position *within the cell*.  The pipeline
+writes fresh ``(seed, base offset)`` values (reserved from the device generator) into the
+slot before each replay; the forward and the recomputation of a cell read the same slot,
+so their masks agree bit for bit.
 """
 from contextlib import contextmanager
 import threading
@@ -21,7 +30,8 @@ from typing import Generator, List, Optional, Tuple
 
 import torch
 
-__all__ = ['RngTape', 'philox_pair', 'current_tape']
+__all__ = ['RngTape', 'philox_pair', 'current_tape', 'PhiloxSlot', 'slot_scope', 'philox_draw',
+           'reserve']
 
 SeedOffset = Tuple[int, int]
 
@@ -29,6 +39,7 @@ SeedOffset = Tuple[int, int]
 class _TapeState(threading.local):
     def __init__(self) -> None:
         self.tape: Optional['RngTape'] = None
+        self.slot: Optional['PhiloxSlot'] = None
 
 
 _state = _TapeState()
@@ -69,6 +80,11 @@ class RngTape:
 
 def current_tape() -> Optional[RngTape]:
     return _state.tape
+
+
+def reserve(device: torch.device, increment: int) -> SeedOffset:
+    """Reserve ``increment`` Philox counters from ``device``'s generator: ``(seed, offset)``."""
+    return _reserve(device, (int(increment) + 3) // 4 * 4)
 
 
 def _reserve(device: torch.device, increment: int) -> SeedOffset:
@@ -112,3 +128,49 @@ def philox_pair(device: torch.device, increment: int) -> SeedOffset:
     if tape is not None and tape.mode == 'record':
         tape.entries.append(pair)
     return pair
+
+
+class PhiloxSlot:
+    """Device-resident Philox state of one captured cell.
+
+    ``state`` is an int64 ``[2]`` GPU tensor ``(seed, base offset)`` that the host fills
+    before each replay; ``delta`` counts the counters drawn so far in the current
+    :func:`slot_scope` (the per-call offsets relative to the base).
+    """
+
+    __slots__ = ('state', 'delta')
+
+    def __init__(self, state: torch.Tensor) -> None:
+        if state.dtype != torch.int64 or state.numel() != 2 or not state.is_cuda:
+            raise ValueError('a Philox slot is an int64 [2] GPU tensor')
+        self.state = state
+        self.delta = 0
+
+
+@contextmanager
+def slot_scope(slot: PhiloxSlot) -> Generator[None, None, None]:
+    """RNG ops of this thread draw from ``slot`` (counters from 0) until the scope ends."""
+    prev = _state.slot
+    slot.delta = 0
+    _state.slot = slot
+    try:
+        yield
+    finally:
+        _state.slot = prev
+
+
+def philox_draw(device: torch.device,
+                increment: int) -> Tuple[int, int, Optional[torch.Tensor]]:
+    """``(seed, offset, rng)`` for one RNG op consuming ``increment`` counters.
+
+    Inside a :func:`slot_scope` on a GPU: ``rng`` is the slot's device state and
+    ``offset`` the op's position in the cell (``seed`` unused).  Otherwise ``rng`` is
+    ``None`` and ``(seed, offset)`` is :func:`philox_pair`'s.
+    """
+    slot = _state.slot
+    if slot is not None and device.type == 'cuda':
+        delta = slot.delta
+        slot.delta += (int(increment) + 3) // 4 * 4
+        return 0, delta, slot.state
+    seed, offset = philox_pair(device, increment)
+    return seed, offset, None
