@@ -47,11 +47,15 @@ def main() -> None:
     p = argparse.ArgumentParser()
     p.add_argument('--iters', type=int, default=15)
     p.add_argument('--out', default=None)
+    p.add_argument('--shapes', default=None,
+                   help="'N,C,K,H;...' instead of the built-in U-Net shapes")
     a = p.parse_args()
+    shapes = SHAPES if a.shapes is None else \
+        [tuple(int(v) for v in part.split(',')) for part in a.shapes.split(';')]
     dev = torch.device('cuda', 0)
     ops = _ext.require(torch.empty(0, device=dev))
     rows = []
-    for n, c, k, h in SHAPES:
+    for n, c, k, h in shapes:
         torch.manual_seed(0)
         x = torch.randn(n, c, h, h, device=dev)
         w = torch.randn(k, c, 3, 3, device=dev) / (3 * c ** 0.5)

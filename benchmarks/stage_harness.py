@@ -150,8 +150,8 @@ def main() -> None:
     p.add_argument('--steps', type=int, default=2)
     p.add_argument('--out', default=None)
     args = p.parse_args()
-    if args.graph_cells and args.warmup < 3:
-        args.warmup = 3  # eager, capture, first replay
+    if args.graph_cells and args.warmup < 4:
+        args.warmup = 4  # two eager steps, the capture, a first replay
     dev = torch.device('cuda', 0)
     results = []
     for k in (args.stages if args.stages else range(len(args.balance))):

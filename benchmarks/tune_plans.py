@@ -1,14 +1,16 @@
 """Measure the implicit-GEMM convolution plans of the benchmark models and save them.
 
-Runs one training forward + backward of U-Net(5,64) and AmoebaNet-D(18,256) on one GPU at
-every micro-batch size the speed benchmarks use (``bench.py``'s experiment tables: the
-micro-batch is global batch / chunks), so the autotuner in ``csrc/convbn.cpp`` measures
-every convolution shape those runs meet, then writes the plan table.  The package loads
-``torchgpipe_amd/tuned/conv_gemm_mi355x.txt`` at start-up, so benchmark processes on a
-fresh machine skip the per-shape find (AmoebaNet's first step: seconds of candidate
-timing per rank).
+Runs one training forward + backward of U-Net(5,64), AmoebaNet-D(18,256) and ResNet-101
+on one GPU at every micro-batch size the speed benchmarks use (``bench.py``'s experiment
+tables: the micro-batch is global batch / chunks) with the autotuner of
+``csrc/convbn.cpp`` switched on (``TGPIPE_CG_TUNE=1``), so it times every candidate plan
+of every convolution shape those runs meet -- and, for backward-data, the library
+convolution against the implicit GEMM -- then writes both tables.  Training processes
+only *read* them (``torchgpipe_amd/tuned/``): no training step ever synchronises the host
+to time kernels, and every rank of a pipeline runs the same plan for a shape.
 
-    python benchmarks/tune_plans.py --out torchgpipe_amd/tuned/conv_gemm_mi355x.txt
+    python benchmarks/tune_plans.py --out torchgpipe_amd/tuned/conv_gemm_mi355x.txt \
+        --lib-out torchgpipe_amd/tuned/lib_dgrad_mi355x.txt
 """
 import argparse
 import os
@@ -21,7 +23,8 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 UNET_MICRO = (40, 16, 32)       # pipeline-1 80/2, -2 512/32 and -8 640/40, -4 512/16
-AMOEBA_MICRO = (20, 40, 36)     # n1m32 640/32, n2/n8 1280/32, n4 1152/32
+AMOEBA_MICRO = (20, 40, 36, 96)  # n1m32 640/32, n2/n8 1280/32, n4 1152/32, n2m1 96/1
+RESNET_MICRO = (110, 15)        # pipeline-1 220/2, pipeline-2 480/32 (bench.py)
 
 
 def run(model: torch.nn.Module, micro: int, shape, target_fn) -> None:
@@ -34,13 +37,16 @@ def run(model: torch.nn.Module, micro: int, shape, target_fn) -> None:
 def main() -> None:
     p = argparse.ArgumentParser(description=__doc__)
     p.add_argument('--out', required=True)
-    p.add_argument('--models', default='amoebanet,unet')
+    p.add_argument('--lib-out', default=None, help='backward-data library-choice table')
+    p.add_argument('--models', default='amoebanet,unet,resnet')
     p.add_argument('--merge', action='store_true',
                    help='seed from the shipped table and measure only the shapes it lacks')
     args = p.parse_args()
+    os.environ['TGPIPE_CG_TUNE'] = '1'  # time candidates on first use (this script only)
     if not args.merge:
-        os.environ['TGPIPE_CG_DB'] = '0'  # measure, do not seed from the shipped table
-    from torchgpipe_amd.models import amoebanetd, unet
+        os.environ['TGPIPE_CG_DB'] = '0'  # measure, do not seed from the shipped tables
+        os.environ['TGPIPE_LIB_DGRAD_DB'] = '0'
+    from torchgpipe_amd.models import amoebanetd, resnet101, unet
     from torchgpipe_amd.ops import _ext
     _ext.require()
     t0 = time.time()
@@ -59,9 +65,20 @@ def main() -> None:
             run(model, micro, (3, 192, 192), lambda o: o.float().square().mean())
             print(f'unet micro-batch {micro}: {time.time() - t0:.1f}s', flush=True)
         del model
+    if 'resnet' in args.models:
+        model = resnet101(num_classes=1000).cuda().train()
+        for micro in RESNET_MICRO:
+            run(model, micro, (3, 224, 224),
+                lambda o: F.cross_entropy(o, torch.zeros(o.shape[0], dtype=torch.long,
+                                                         device=o.device)))
+            print(f'resnet101 micro-batch {micro}: {time.time() - t0:.1f}s', flush=True)
+        del model
     torch.cuda.synchronize()
     n = _ext.save_plans(args.out)
     print(f'{n} plans -> {args.out}', flush=True)
+    if args.lib_out:
+        n = _ext.save_lib_dgrad(args.lib_out)
+        print(f'{n} library backward-data geometries -> {args.lib_out}', flush=True)
 
 
 if __name__ == '__main__':

@@ -36,9 +36,9 @@ def test_rccl_pipeline_matches_single_gpu(tmp_path, kind, world, checkpoint):
 # multi-GPU node checks the stream-ordered receive waits against every lane layout.
 BENCH_OPTIONS = {
     'unet': [dict(overlap_recompute=True, overlap_forward=True),
-             dict(overlap_recompute=True, overlap_forward=True, graph_cells=True, steps=4)],
+             dict(overlap_recompute=True, overlap_forward=True, graph_cells=True, steps=5)],
     'amoebanet': [dict(cell_streams=True),
-                  dict(cell_streams=True, graph_cells=True, steps=4)],
+                  dict(cell_streams=True, graph_cells=True, steps=5)],
 }
 BENCH_CASES = [(kind, world, opts) for kind in parity.MODELS for world in (2, 4)
                for opts in BENCH_OPTIONS[kind]]

@@ -28,10 +28,10 @@ CASES = [
     # captured cells (parallel/segments.py): warm-up, capture and two replayed steps with
     # the persistent receive buffers, the transfers between graph launches
     ('unet', 'except_last', dict(overlap_recompute=True, overlap_forward=True,
-                                 graph_cells=True, steps=4)),
-    ('unet', 'always', dict(graph_cells=True, steps=4)),
-    ('amoebanet', 'except_last', dict(cell_streams=True, graph_cells=True, steps=4)),
-    ('amoebanet', 'always', dict(overlap_recompute=True, graph_cells=True, steps=4)),
+                                 graph_cells=True, steps=5)),
+    ('unet', 'always', dict(graph_cells=True, steps=5)),
+    ('amoebanet', 'except_last', dict(cell_streams=True, graph_cells=True, steps=5)),
+    ('amoebanet', 'always', dict(overlap_recompute=True, graph_cells=True, steps=5)),
 ]
 
 
@@ -47,5 +47,5 @@ def test_overlapped_stage_matches_one_gpu(tmp_path, kind, checkpoint, options):
     grads, loss = parity.reference(kind, torch.device('cuda', 0), chunks)
     parity.assert_parity(results, grads, loss, rel=1e-4)
     if options.get('graph_cells'):
-        assert all(r['phases'] == ['eager', 'capture', 'replay', 'replay'] for r in results), \
-            [r['phases'] for r in results]
+        want = ['eager', 'eager', 'capture', 'replay', 'replay']
+        assert all(r['phases'] == want for r in results), [r['phases'] for r in results]

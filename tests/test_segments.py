@@ -82,7 +82,7 @@ def test_graph_cells_train_like_eager(kind, checkpoint, lanes):
     ob = torch.optim.SGD(sb.parameters(), lr=0.05)
     gen = torch.Generator(device=dev).manual_seed(5)
     phases = []
-    for _ in range(4):
+    for step in range(5):
         x, y, loss_fn = _batch(kind, shape, classes, gen, dev)
         la = sa.train_step(x, y, loss_fn)
         lb = sb.train_step(x, y, loss_fn)
@@ -92,14 +92,20 @@ def test_graph_cells_train_like_eager(kind, checkpoint, lanes):
         for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
             scale = pa.grad.abs().max().item() + 1e-12
             torch.testing.assert_close(pb.grad, pa.grad, rtol=1e-4, atol=1e-5 * scale,
-                                       msg=name)
+                                       msg=lambda m: f'step {step} {name}: {m}')
+        # Both models continue from the same SGD-updated weights (new values every step:
+        # the captured graphs must see them through the in-place refreshed weight
+        # transforms).  Stepping each model on its own would let fp32 rounding noise grow
+        # chaotically through a few updates of this tiny U-Net (eager with and without
+        # lanes drift apart by percents too).
         oa.step()
         ob.step()
+        with torch.no_grad():
+            for pa, pb in zip(a.parameters(), b.parameters()):
+                pb.copy_(pa)
         oa.zero_grad(set_to_none=True)
         ob.zero_grad(set_to_none=True)
-    assert phases == ['eager', 'capture', 'replay', 'replay']
-    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
-        torch.testing.assert_close(pb, pa, rtol=1e-5, atol=1e-6, msg=name)
+    assert phases == ['eager', 'eager', 'capture', 'replay', 'replay']
     # running statistics (AmoebaNet BatchNorm) follow the same updates
     for (name, ba), bb in zip(a.named_buffers(), b.buffers()):
         if ba.is_floating_point():
@@ -123,12 +129,12 @@ def test_graph_cells_dropout_masks_fresh_and_replayed():
     x = torch.rand(4, 3, 32, 32, device=dev)
     y = torch.rand(4, 1, 32, 32, device=dev)
     losses = []
-    for step in range(4):
+    for step in range(5):
         for p in stage.parameters():
             p.grad = None
         losses.append(stage.train_step(x, y, F.binary_cross_entropy_with_logits).item())
     assert stage.graph_phase == 'replay'
-    assert len(set(losses[1:])) == 3, losses  # fresh masks every step
+    assert len(set(losses[2:])) == 3, losses  # fresh masks every step
     # oracle: each micro-batch once, with grad, under the slot values of the last step
     slots = stage._segments.slots.clone()
     for p in oracle.parameters():
@@ -157,7 +163,7 @@ def test_graph_cells_deferred_batch_norm_commits():
     sb = PipelineStage(b, [len(b)], device=dev, chunks=4, deferred_batch_norm=True,
                        graph_cells=True)
     gen = torch.Generator(device=dev).manual_seed(3)
-    for _ in range(4):
+    for _ in range(5):
         x = torch.randn(8, 3, 8, 8, device=dev, generator=gen) * 2 + 1
         y = torch.randint(3, (8,), device=dev, generator=gen)
         sa.train_step(x, y, F.cross_entropy)

@@ -66,9 +66,13 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
                         float* pm, float* pm2, const ConvGemmGeo& g, bool accumulate,
                         int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
                         int64_t out_numel) {
+  // Timing trials only when asked for (TGPIPE_CG_TUNE=1: benchmarks/tune_plans.py, the
+  // offline tuner): a training step never synchronises the host to time candidates, and
+  // every rank of a pipeline picks the same plan for the same shape.  A shape missing from
+  // the shipped table (torchgpipe_amd/tuned/conv_gemm_mi355x.txt) runs the heuristic.
   static const bool tune = [] {
     const char* v = std::getenv("TGPIPE_CG_TUNE");
-    return v == nullptr || std::string(v) != "0";
+    return v != nullptr && std::string(v) == "1";
   }();
   const ConvGemmPlan heuristic = conv_gemm_plan(mode, g);
   const int forced = forced_cfg.load();
@@ -83,13 +87,13 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
       }
     return pick;
   }
-  if (!tune) return heuristic;
   const hipStream_t stream = cur_stream(like);
   const PlanKey key{mode, g.n, g.ci, g.h, g.w, g.co, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.oh,
                     g.ow, g.co_total};
   std::lock_guard<std::mutex> lock(plan_mutex);
   auto hit = plan_cache.find(key);
   if (hit != plan_cache.end()) return hit->second;
+  if (!tune) return heuristic;
   // A stream capture (hipGraph) records launches, it cannot time them: a shape first met
   // inside a capture runs the heuristic plan (warm-up steps before capturing tune it).
   hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
@@ -444,9 +448,10 @@ void wgrad_slab_flush(at::TensorList slabs, at::TensorList grads, at::IntArrayRe
 // ATen) + the ReLU mask, for the geometries where that measured faster than the implicit
 // GEMM: the strided convolutions of reduction cells (the GEMM walks every stride hole:
 // 206 vs 43 us for 32 ch 3x3 s2 at 112^2) and some deep 7x7 / 28x28 planes
-// (profiles/r3/convbn_bench_n20_spread.json).  Decided per geometry by timing both on the
-// first eager call, like the tile plans; a shape first met inside a stream capture, or
-// TGPIPE_LIB_DGRAD=0, keeps the implicit GEMM.
+// (profiles/r3/convbn_bench_n20_spread.json).  Decided per geometry by the shipped table
+// (torchgpipe_amd/tuned/lib_dgrad_mi355x.txt, measured by benchmarks/tune_plans.py); with
+// TGPIPE_CG_TUNE=1 a geometry missing from it is timed both ways on its first eager call.
+// Otherwise (and inside a stream capture, or with TGPIPE_LIB_DGRAD=0) the implicit GEMM.
 std::mutex lib_mutex;
 std::map<PlanKey, bool> lib_dgrad_cache;
 std::atomic<int> forced_lib{-1};
@@ -483,9 +488,14 @@ bool lib_dgrad_chosen(const ConvGemmGeo& g, const at::Tensor& like, Ours&& ours,
   const PlanKey key{1, g.n, g.ci, g.h, g.w, g.co, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.oh,
                     g.ow, g.co_total};
   if (forced_lib.load() == 1) return true;
+  static const bool tune = [] {
+    const char* v = std::getenv("TGPIPE_CG_TUNE");
+    return v != nullptr && std::string(v) == "1";
+  }();
   std::lock_guard<std::mutex> lock(lib_mutex);
   auto hit = lib_dgrad_cache.find(key);
   if (hit != lib_dgrad_cache.end()) return hit->second;
+  if (!tune) return false;
   const hipStream_t stream = cur_stream(like);
   hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &capture) != hipSuccess ||
@@ -513,6 +523,29 @@ bool lib_dgrad_chosen(const ConvGemmGeo& g, const at::Tensor& like, Ours&& ours,
   const bool pick = lib_ms < 0.95f * ours_ms;  // ties stay on the native kernel
   lib_dgrad_cache[key] = pick;
   return pick;
+}
+
+// Seed the backward-data choice with a saved table (lib_dgrad_export's format); entries
+// already decided in this process are kept.  Returns the lines taken.
+int64_t lib_dgrad_import(const std::string& text) {
+  std::istringstream in(text);
+  std::string line;
+  int64_t taken = 0;
+  std::lock_guard<std::mutex> lock(lib_mutex);
+  while (std::getline(in, line)) {
+    std::istringstream ls(line);
+    int v[11];
+    int got = 0;
+    while (got < 11 && (ls >> v[got])) ++got;
+    if (got != 11) continue;
+    bool ok = true;
+    for (int i = 0; i < 11; ++i) ok = ok && v[i] >= (i >= 9 ? 0 : 1);
+    if (!ok) continue;
+    const PlanKey key{1, v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], 0,
+                      0, v[4]};
+    if (lib_dgrad_cache.emplace(key, true).second) ++taken;
+  }
+  return taken;
 }
 
 // Geometries whose backward-data runs on the library convolution: "n ci h w co kh kw sh sw
@@ -1291,6 +1324,7 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("conv_gemm_forward(Tensor x, Tensor weight, int[] geo, bool relu) -> Tensor");
   m.def("conv_gemm_plans_export() -> str", &tgpipe::conv_gemm_plans_export);
   m.def("lib_dgrad_export() -> str", &tgpipe::lib_dgrad_export);
+  m.def("lib_dgrad_import(str text) -> int", &tgpipe::lib_dgrad_import);
   m.def("lib_dgrad_force(int mode) -> ()", &tgpipe::lib_dgrad_force);
   m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
   m.def("conv_gemm_sweep(int mode, Tensor x, Tensor weight, int[] geo, int reps) -> float[]");

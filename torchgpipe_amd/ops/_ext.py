@@ -11,12 +11,18 @@ from typing import Any, Optional
 
 import torch
 
-__all__ = ['available', 'ops', 'require', 'load_error', 'load_plans', 'save_plans']
+__all__ = ['available', 'ops', 'require', 'load_error', 'load_plans', 'save_plans',
+           'load_lib_dgrad', 'save_lib_dgrad']
 
 # Implicit-GEMM launch plans measured on an MI355X for the benchmark models (written by
-# benchmarks/tune_plans.py).  TGPIPE_CG_DB=<file> loads another table, =0 none.
-SHIPPED_PLANS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                             'tuned', 'conv_gemm_mi355x.txt')
+# benchmarks/tune_plans.py).  TGPIPE_CG_DB=<file> loads another table, =0 none.  Training
+# never times candidates itself (csrc/convbn.cpp tuned_plan): a shape missing from the
+# table runs the heuristic plan unless TGPIPE_CG_TUNE=1.
+_TUNED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tuned')
+SHIPPED_PLANS = os.path.join(_TUNED, 'conv_gemm_mi355x.txt')
+# Geometries whose backward-data measured faster on MIOpen (same tuner): "n ci h w co kh kw
+# sh sw ph pw" per line.  TGPIPE_LIB_DGRAD_DB=<file> / =0 as above.
+SHIPPED_LIB_DGRAD = os.path.join(_TUNED, 'lib_dgrad_mi355x.txt')
 
 _loaded = False
 _error: Optional[BaseException] = None
@@ -32,6 +38,9 @@ def _load() -> None:
         db = os.environ.get('TGPIPE_CG_DB', SHIPPED_PLANS)
         if db != '0' and os.path.exists(db):
             load_plans(db)
+        db = os.environ.get('TGPIPE_LIB_DGRAD_DB', SHIPPED_LIB_DGRAD)
+        if db != '0' and os.path.exists(db):
+            load_lib_dgrad(db)
     except Exception as exc:  # pragma: no cover - depends on the build
         _error = exc
         if os.environ.get('TGPIPE_AUTOBUILD', '0') == '1':
@@ -80,6 +89,20 @@ def load_plans(path: str) -> int:
 def save_plans(path: str) -> int:
     """Write every plan measured (or loaded) in this process; returns the line count."""
     text = require().conv_gemm_plans_export()
+    with open(path, 'w') as f:
+        f.write(text)
+    return text.count('\n')
+
+
+def load_lib_dgrad(path: str) -> int:
+    """Seed the backward-data library choice with a saved table; returns lines taken."""
+    with open(path) as f:
+        return int(torch.ops.tgpipe.lib_dgrad_import(f.read()))
+
+
+def save_lib_dgrad(path: str) -> int:
+    """Write the geometries whose backward-data runs on the library; returns the count."""
+    text = require().lib_dgrad_export()
     with open(path, 'w') as f:
         f.write(text)
     return text.count('\n')

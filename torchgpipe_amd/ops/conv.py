@@ -25,11 +25,14 @@ the transform runs once per optimizer step instead of once per call.
   it.  An entry created lazily inside a step records an event, and a reader on another
   stream waits for it (forward lanes: micro-batch 1 may reach a layer before micro-batch 0
   has transformed its weights).
-* Memory: every cached byte counts against one process-wide budget
-  (``TGPIPE_WINOGRAD_CACHE_MB``, default 5 % of the device's memory).  A
-  transform that would exceed it is used for the call and then dropped, so giant
-  models (U-Net(48, 576)'s 18432-channel layers) keep the memory footprint of
-  the uncached path.
+* Memory: every cached byte counts against a per-device budget.  A pipeline stage sizes it
+  from its own footprint (:func:`size_cache_budget`, ``PipelineStage``): the first step
+  runs uncached, and afterwards the cache may hold ``TGPIPE_WINOGRAD_CACHE_FRACTION``
+  (default 0.15) of that step's peak, capped at 5 % of the device -- so a stage's memory
+  grows by at most that fraction, however large the model (U-Net(48, 160)'s transforms
+  alone would double it).  Before a stage has sized it (or outside a stage) the budget
+  is 5 % of the device; ``TGPIPE_WINOGRAD_CACHE_MB`` overrides both.  A transform that
+  would exceed the budget is used for the call and then dropped.
 """
 import os
 from typing import Any, Dict, Optional, Sequence, Tuple
@@ -41,11 +44,15 @@ import torch.nn.functional as F
 from torchgpipe_amd.ops import _ext, gradacc
 
 __all__ = ['WinogradConv2d', 'winograd_conv2d', 'wino_eligible', 'new_step',
-           'clear_winograd_caches', 'cache_bytes', 'refresh_step_caches']
+           'clear_winograd_caches', 'cache_bytes', 'refresh_step_caches', 'hold_cache',
+           'size_cache_budget']
 
 _STEP = 0
-_CACHE_BYTES = 0
+_CACHE_BYTES: Dict[torch.device, int] = {}  # cached bytes per device
 _BUDGET: Optional[int] = None
+# per-device budgets set by size_cache_budget / hold_cache (bytes)
+_DEVICE_BUDGET: Dict[torch.device, int] = {}
+CACHE_PEAK_FRACTION = float(os.environ.get('TGPIPE_WINOGRAD_CACHE_FRACTION', '0.15'))
 
 
 def new_step() -> None:
@@ -60,18 +67,35 @@ def new_step() -> None:
 
 def cache_bytes() -> int:
     """Bytes currently held by Winograd weight-transform caches (this process)."""
-    return _CACHE_BYTES
+    return sum(_CACHE_BYTES.values())
+
+
+def _device_cap(device: torch.device) -> int:
+    return torch.cuda.get_device_properties(device).total_memory // 20
 
 
 def _budget(device: torch.device) -> int:
     global _BUDGET
-    if _BUDGET is None:
-        mb = os.environ.get('TGPIPE_WINOGRAD_CACHE_MB')
-        if mb is not None:
+    mb = os.environ.get('TGPIPE_WINOGRAD_CACHE_MB')
+    if mb is not None:
+        if _BUDGET is None:
             _BUDGET = int(float(mb) * (1 << 20))
-        else:
-            _BUDGET = torch.cuda.get_device_properties(device).total_memory // 20
-    return _BUDGET
+        return _BUDGET
+    sized = _DEVICE_BUDGET.get(device)
+    return sized if sized is not None else _device_cap(device)
+
+
+def hold_cache(device: torch.device) -> None:
+    """Cache nothing on ``device`` (a stage's first step, which measures its footprint)."""
+    _DEVICE_BUDGET[device] = 0
+
+
+def size_cache_budget(device: torch.device, peak_bytes: int) -> int:
+    """Let the caches on ``device`` hold ``CACHE_PEAK_FRACTION`` of ``peak_bytes`` (a
+    stage's uncached step peak), at most 5 % of the device; returns the budget."""
+    budget = min(_device_cap(device), int(CACHE_PEAK_FRACTION * peak_bytes))
+    _DEVICE_BUDGET[device] = budget
+    return budget
 
 
 def _derive(weight: Tensor, slot: Tuple) -> Tensor:
@@ -123,21 +147,21 @@ class _TransformCache:
         self._weight: Optional[Tensor] = None
 
     def _lookup(self, weight: Tensor, slot: Tuple) -> Tensor:
-        global _CACHE_BYTES
-        key = (weight.data_ptr(), weight._version, weight.device, _STEP)
+        dev = weight.device
+        key = (weight.data_ptr(), weight._version, dev, _STEP)
         hit = self._entries.get(slot)
         if hit is not None and hit[0] == key:
             _await(hit[1], hit[2])
             return hit[1]
         if hit is not None:  # stale: release before transforming again
-            _CACHE_BYTES -= hit[1].numel() * hit[1].element_size()
+            _CACHE_BYTES[dev] -= hit[1].numel() * hit[1].element_size()
             del self._entries[slot]
         u = _derive(weight, slot)
         size = u.numel() * u.element_size()
-        if _CACHE_BYTES + size <= _budget(weight.device):
+        if _CACHE_BYTES.get(dev, 0) + size <= _budget(dev):
             self._entries[slot] = (key, u, _ready_event(u))
             self._weight = weight.detach()
-            _CACHE_BYTES += size
+            _CACHE_BYTES[dev] = _CACHE_BYTES.get(dev, 0) + size
         return u
 
     def get(self, weight: Tensor, flip: bool, f4: bool = False, bg: int = 0) -> Tensor:
@@ -165,9 +189,8 @@ class _TransformCache:
             self._entries[slot] = (key, u, None)
 
     def clear(self) -> None:
-        global _CACHE_BYTES
         for _, u, _ in self._entries.values():
-            _CACHE_BYTES -= u.numel() * u.element_size()
+            _CACHE_BYTES[u.device] -= u.numel() * u.element_size()
         self._entries.clear()
         self._weight = None
 

@@ -43,7 +43,7 @@ from torchgpipe_amd.checkpoint import Checkpointing
 from torchgpipe_amd.gpipe import check_balance, partition_layers, verify_module
 from torchgpipe_amd.microbatch import Batch
 from torchgpipe_amd.ops.conv import new_step as wino_new_step
-from torchgpipe_amd.ops.conv import refresh_step_caches
+from torchgpipe_amd.ops.conv import hold_cache, refresh_step_caches, size_cache_budget
 from torchgpipe_amd.ops.dropout import convert_dropout
 from torchgpipe_amd.ops.fusion import relink
 from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P, _wait
@@ -185,7 +185,9 @@ class PipelineStage:
             step, the host launches three graphs per cell instead of every kernel.  GPU
             stages only; gradients are zeroed at the start of each step (each step computes
             them from scratch, like ``StepGraph``).
-        graph_warmup: eager steps before the capture step.
+        graph_warmup: eager steps before the capture step (the first runs without cached
+            weight transforms and sizes their budget, the second fills the caches, so the
+            capture reads them instead of recomputing transforms in its graphs).
         transport: a stand-in for the point-to-point layer (``P2P`` interface), e.g.
             :class:`~torchgpipe_amd.parallel.loopback.LoopbackP2P` to run this stage as
             ``rank`` of a ``len(balance)``-stage pipeline in one process without
@@ -212,7 +214,7 @@ class PipelineStage:
                  wgrad_stream: bool = False,
                  philox_dropout: bool = False,
                  graph_cells: bool = False,
-                 graph_warmup: int = 1,
+                 graph_warmup: int = 2,
                  transport: Optional[Any] = None) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
@@ -323,6 +325,9 @@ class PipelineStage:
         self._seg_key: Optional[Tuple[Any, ...]] = None
         self._seg_phase = 'eager'
         self._persistent = False  # this step receives into persistent buffers
+        # derived-weight cache budget: None = not sized yet, 'measuring' = first step ran
+        # uncached (ops/conv.py size_cache_budget), 'sized'
+        self._cache_state: Optional[str] = None
         if distributed and self.n > 1:
             self.connect()
 
@@ -516,6 +521,11 @@ class PipelineStage:
             set_micro_batches(self.partition, m)
         stop = self.checkpoint_stop(m)
         if self.device.type == 'cuda':
+            if self._cache_state is None and self.training and torch.is_grad_enabled():
+                # the first training step runs without cached weight transforms: its peak
+                # sizes the cache (at most a fraction of the stage's own footprint)
+                hold_cache(self.device)
+                self._cache_state = 'measuring'
             # derived weights recomputed in place, on this stream, before any lane reads them
             refresh_step_caches(self.partition)
         seg = self._segments_for(sig, stop)
@@ -802,6 +812,9 @@ class PipelineStage:
                 cur.wait_stream(lane)
         if seg is not None:
             seg.end_backward()
+        if self._cache_state == 'measuring':
+            size_cache_budget(self.device, torch.cuda.max_memory_allocated(self.device))
+            self._cache_state = 'sized'
         self._cells = []
         self.p2p.flush()
 
