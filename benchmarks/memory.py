@@ -31,6 +31,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from torchgpipe_amd.checkpoint import Checkpointing  # noqa: E402
 from torchgpipe_amd.microbatch import Batch  # noqa: E402
 from torchgpipe_amd.models import amoebanetd, unet  # noqa: E402
+from torchgpipe_amd.ops import conv as wino  # noqa: E402
 from torchgpipe_amd.skip.tracker import SkipTracker, use_skip_tracker  # noqa: E402
 from torchgpipe_amd.utils.meta import materialize  # noqa: E402
 
@@ -91,7 +92,14 @@ def measure_stage(kind, layers, lo, hi, batch_size, chunks, shape, checkpoint, d
     stop = {'always': m, 'except_last': m - 1, 'never': 0}[checkpoint]
     last = hi == len(layers)
     torch.cuda.reset_peak_memory_stats(device)
-    for _ in range(2):
+    # as PipelineStage does: the first step runs without cached weight transforms, and its
+    # peak sizes the cache for the second (ops/conv.py size_cache_budget)
+    wino.hold_cache(device)
+    cache_budget = 0
+    for step in range(2):
+        wino.new_step()
+        if step == 1:
+            cache_budget = wino.size_cache_budget(device, torch.cuda.max_memory_allocated(device))
         cells = []
         for i in range(m):
             acts = [real(t).requires_grad_(lo > 0) for t in meta_in]
@@ -128,11 +136,13 @@ def measure_stage(kind, layers, lo, hi, batch_size, chunks, shape, checkpoint, d
         opt.zero_grad(set_to_none=True)
     torch.cuda.synchronize(device)
     peak = torch.cuda.max_memory_reserved(device)
+    cached = wino.cache_bytes()
     del opt
+    wino.clear_winograd_caches(part)
     part.to_empty(device='meta')  # release this stage before measuring the next one
     del part
     torch.cuda.empty_cache()
-    return params, peak
+    return params, peak, cache_budget, cached
 
 
 def main() -> None:
@@ -180,10 +190,13 @@ def main() -> None:
     rows = []
     t0 = time.time()
     for k in stages:
-        params, peak = measure_stage(args.model, layers, bounds[k], bounds[k + 1], batch, chunks,
-                                     shape, args.checkpoint, device)
+        params, peak, budget, cached = measure_stage(args.model, layers, bounds[k], bounds[k + 1],
+                                                     batch, chunks, shape, args.checkpoint,
+                                                     device)
         row = {'stage': k, 'layers': [bounds[k], bounds[k + 1]], 'params': params,
-               'peak_reserved_gib': round(peak / 2 ** 30, 2)}
+               'peak_reserved_gib': round(peak / 2 ** 30, 2),
+               'transform_cache_budget_gib': round(budget / 2 ** 30, 2),
+               'transform_cache_gib': round(cached / 2 ** 30, 2)}
         rows.append(row)
         print(json.dumps(row), f'({time.time() - t0:.0f}s)', flush=True)
     summary = {'model': args.model, 'depth': depth, 'channels': channels, 'balance': balance,

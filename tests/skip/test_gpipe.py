@@ -151,3 +151,50 @@ def test_same_route_skips_travel_as_one_hop(balance):
     assert portal.portal_hops - before == groups * chunks
     out.mean().backward()
     assert all(p.grad is not None for p in gpipe.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('base_channels,hw', [(4, 64), (32, 128)])
+def test_unet_p2_skips_packed_peer_copies_match_one_gpu(base_channels, hw):
+    """K5-K7 across two GPUs: U-Net pipeline-2 at the reference balance [104, 137] (all
+    four long skips cross from GPU 0 to GPU 1 on one route).  Every micro-batch's skips
+    make one PortalCopy hop; skips under ``copy.SKIP_PACK_MAX_BYTES`` travel as one packed
+    peer copy (base 4: all of them; base 32 at 128^2: the 4.2 MB top-level skip one by
+    one, the three others packed), and gradients
+    match the whole model on one GPU with the same micro-batching."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip('needs 2 GPUs')
+    import torch.nn.functional as F
+
+    from torchgpipe_amd import copy as copymod
+    from torchgpipe_amd.models import unet
+    from torchgpipe_amd.skip import portal
+
+    torch.manual_seed(0)
+    model = unet(depth=5, num_convs=5, base_channels=base_channels)
+    for m in model.modules():  # no dropout: deterministic comparison
+        if isinstance(getattr(m, 'p', None), float):
+            m.p = 0.0
+    plain = copy.deepcopy(model).cuda(0)
+    chunks = 2
+    gpipe = GPipe(model, [104, 137], devices=[0, 1], chunks=chunks)
+    x = torch.rand(4, 3, hw, hw, device='cuda:0')
+    t = torch.rand(4, 1, hw, hw)
+    hops, packed = portal.portal_hops, copymod.packed_hops
+    out = gpipe(x)
+    assert portal.portal_hops - hops == chunks  # one skip hop per micro-batch
+    # bytes of level k's skip per micro-batch (2 images, base_channels * 2^k channels)
+    sizes = [base_channels * 2 ** k * (hw >> k) ** 2 * 2 * 4 for k in range(5)]
+    small = sum(s < copymod.SKIP_PACK_MAX_BYTES for s in sizes[:4])
+    assert copymod.packed_hops - packed == (chunks if small >= 2 else 0)
+    F.binary_cross_entropy_with_logits(out, t.to(out.device)).backward()
+
+    total = 0.0
+    for xc, tc in zip(x.chunk(chunks), t.cuda(0).chunk(chunks)):
+        loss = F.binary_cross_entropy_with_logits(plain(xc), tc) * (tc.size(0) / 4)
+        loss.backward()
+        total += loss.item()
+    for (name, pa), pb in zip(plain.named_parameters(), gpipe.parameters()):
+        scale = pa.grad.abs().max().item() + 1e-12
+        torch.testing.assert_close(pb.grad.to(pa.device), pa.grad, rtol=1e-4,
+                                   atol=1e-5 * scale, msg=name)

@@ -59,12 +59,17 @@ def test_bench_json_contract(nproc, model):
         assert amoeba['value'] > 0 and amoeba['steps'] == 1
         if nproc == 2:
             assert amoeba['n2m1']['chunks'] == 1 and amoeba['speedup_vs_n2m1'] > 0
+        # ResNet-101 section (tiny stand-in): pipeline-1 at N=1, config #2's shape at N=2
+        res = rec['resnet101']
+        assert res['value'] > 0 and res['checkpoint'] == ('except_last' if nproc == 1
+                                                           else 'always')
     if nproc > 1:
         ranks = rec['per_rank']
         assert [r['rank'] for r in ranks] == list(range(nproc))
         for r in ranks:
             assert r['step_ms'] > 0 and r['busy_ms'] <= r['step_ms'] + 1e-6
             assert min(r['fwd_wait_ms'], r['bwd_wait_ms'], r['fill_ms'], r['drain_ms']) >= 0
+            assert r['host_enqueue_ms'] > 0
         # rank 1 waits for rank 0's activations, rank 0 for rank 1's gradients
         assert ranks[1]['fwd_wait_ms'] > 0 and ranks[0]['bwd_wait_ms'] > 0
 

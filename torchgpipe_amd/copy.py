@@ -35,6 +35,13 @@ Tensors = Tuple[Tensor, ...]
 # counters of packed hops (tests / diagnostics)
 packed_hops = 0
 
+# Skip hops (PortalCopy) pack only tensors below this size: every packed tensor is a view
+# of one received buffer, so the buffer -- all of the route's skips -- would stay alive
+# until the last of them is popped, while a separately copied skip is freed as soon as its
+# pop partition is done with it (tensor-life accounting, skip/portal.py).  Above a few MiB
+# a copy's launch cost is noise next to its transfer, so packing them saves nothing.
+SKIP_PACK_MAX_BYTES = 4 << 20
+
 
 def _packable(tensors: Tensors, device: torch.device) -> bool:
     if len(tensors) < 2 or device.type != 'cuda':
@@ -68,7 +75,23 @@ def _transfer(tensors: Tensors,
               src_stream: AbstractStream,
               dst_stream: AbstractStream,
               device: torch.device,
-              consumer_stream: AbstractStream) -> List[Tensor]:
+              consumer_stream: AbstractStream,
+              pack_max: Optional[int] = None) -> List[Tensor]:
+    """Move ``tensors`` to ``device``; several GPU tensors go as one packed hop (only those
+    below ``pack_max`` bytes when given, the others one by one)."""
+    if pack_max is not None:
+        small = [k for k, t in enumerate(tensors) if t.numel() * t.element_size() < pack_max]
+        if len(small) < len(tensors):
+            moved: List[Optional[Tensor]] = [None] * len(tensors)
+            if len(small) >= 2:
+                for k, y in zip(small, _transfer(tuple(tensors[k] for k in small), src_stream,
+                                                 dst_stream, device, consumer_stream)):
+                    moved[k] = y
+            rest = [k for k in range(len(tensors)) if moved[k] is None]
+            for k in rest:
+                moved[k] = _transfer((tensors[k],), src_stream, dst_stream, device,
+                                     consumer_stream)[0]
+            return [t for t in moved if t is not None]
     out: List[Tensor] = []
     with use_stream(src_stream), use_stream(dst_stream):
         if _packable(tensors, device):
@@ -99,14 +122,16 @@ class Copy(torch.autograd.Function):
         ctx.prev_stream = prev_stream
         ctx.next_stream = next_stream
         dst = get_device(next_stream)
-        return tuple(_transfer(input, prev_stream, next_stream, dst, current_stream(dst)))
+        return tuple(_transfer(input, prev_stream, next_stream, dst, current_stream(dst),
+                               getattr(ctx, 'pack_max', None)))
 
     @staticmethod
     def backward(ctx, *grad_output: Tensor) -> Tuple[Optional[Tensor], ...]:  # type: ignore[override]
         prev_stream = ctx.prev_stream
         next_stream = ctx.next_stream
         src = get_device(prev_stream)
-        grads = _transfer(grad_output, next_stream, prev_stream, src, current_stream(src))
+        grads = _transfer(grad_output, next_stream, prev_stream, src, current_stream(src),
+                          getattr(ctx, 'pack_max', None))
         return (None, None) + tuple(grads)
 
 

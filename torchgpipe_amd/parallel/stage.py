@@ -904,9 +904,11 @@ class PipelineStage:
         sat idle waiting for activations / gradients to arrive: each wait is measured from
         the moment the last of main and the lanes reached it, so lane compute is not
         counted), ``fill_ms`` / ``drain_ms`` (the first forward and first backward wait:
-        the pipeline fill and drain bubbles this rank sees) and ``busy_ms`` (``step_ms``
-        minus the waits).  Meant for one diagnostic step outside the timed ones: the
-        events add a little host work per micro-batch.
+        the pipeline fill and drain bubbles this rank sees), ``busy_ms`` (``step_ms``
+        minus the waits) and ``host_enqueue_ms`` (host time until ``step()`` returned:
+        Python, autograd and launches -- above ``busy_ms`` the rank is launch-bound).
+        Meant for one diagnostic step outside the timed ones: the events add a little host
+        work per micro-batch.
         """
         gpu = self.device.type == 'cuda'
         self._probe = []
@@ -915,7 +917,9 @@ class PipelineStage:
                 torch.cuda.synchronize(self.device)
                 start = torch.cuda.Event(enable_timing=True)
                 start.record(torch.cuda.current_stream(self.device))
+                h0 = time.perf_counter()
                 step()
+                host = 1000 * (time.perf_counter() - h0)
                 end = torch.cuda.Event(enable_timing=True)
                 end.record(torch.cuda.current_stream(self.device))
                 for s in self._streams():
@@ -929,7 +933,7 @@ class PipelineStage:
             else:
                 t0 = time.perf_counter()
                 step()
-                total = 1000 * (time.perf_counter() - t0)
+                total = host = 1000 * (time.perf_counter() - t0)
 
                 def wait_of(mark: Any, stop: Any) -> float:
                     return 1000 * (stop - mark)
@@ -942,7 +946,8 @@ class PipelineStage:
                 'fwd_wait_ms': round(sum(fwd), 3), 'bwd_wait_ms': round(sum(bwd), 3),
                 'fill_ms': round(fwd[0], 3) if fwd else 0.0,
                 'drain_ms': round(bwd[0], 3) if bwd else 0.0,
-                'busy_ms': round(total - sum(fwd) - sum(bwd), 3)}
+                'busy_ms': round(total - sum(fwd) - sum(bwd), 3),
+                'host_enqueue_ms': round(host, 3)}
 
     @staticmethod
     def _grad_of(t: Tensor) -> Tensor:

@@ -38,7 +38,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 from torch import Tensor
 
-from torchgpipe_amd.copy import Copy
+from torchgpipe_amd.copy import SKIP_PACK_MAX_BYTES, Copy
 from torchgpipe_amd.phony import get_phony
 from torchgpipe_amd.stream import AbstractStream, get_device
 
@@ -159,6 +159,8 @@ class PortalCopy(torch.autograd.Function):
     def forward(ctx, portals: Tuple[Portal, ...], prev_stream: AbstractStream,  # type: ignore[override]
                 next_stream: AbstractStream, phony: Tensor) -> Tensor:
         ctx.portals = portals
+        # large skips travel (and are freed) one by one, small ones packed (copy.py)
+        ctx.pack_max = SKIP_PACK_MAX_BYTES
         moved = Copy.forward(ctx, prev_stream, next_stream,
                              *[p.tensor for p in portals])  # type: ignore[misc]
         for portal, tensor in zip(portals, moved):
