@@ -154,9 +154,10 @@ def parse() -> argparse.Namespace:
                    help='run the fused ops\' weight-gradient GEMMs on a side stream '
                         '(PipelineStage(wgrad_stream=True); auto: off)')
     p.add_argument('--graph-cells', choices=['auto', 'on', 'off'], default='auto',
-                   help='multi-GPU runs: replay each micro-batch of a stage as captured '
-                        'hipGraphs, transfers issued between them (PipelineStage('
-                        'graph_cells=True), parallel/segments.py; auto: off)')
+                   help='replay each micro-batch of a stage as captured hipGraphs, transfers '
+                        'issued between them (PipelineStage(graph_cells=True), '
+                        'parallel/segments.py; instead of the one-GPU whole-step graph; '
+                        'auto: off)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -313,7 +314,7 @@ class Bench:
         wgrad_stream = choice(args.wgrad_stream, False)
         # captured cells (parallel/segments.py): multi-rank stages replay each micro-batch's
         # forward / recomputation / backward as hipGraphs, transfers in between
-        graph_cells = choice(args.graph_cells, False) and self.gpu and self.world > 1
+        graph_cells = choice(args.graph_cells, False) and self.gpu
         stage = PipelineStage(self.build(kind), balance, device=self.device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
                               overlap_recompute=overlap, overlap_forward=overlap_fwd,
@@ -331,7 +332,8 @@ class Bench:
         graph = None
         # whole-step hipGraph: AmoebaNet (no RNG) on one GPU (two-stream cells included,
         # launched from a big-stack thread: profiles/r3/capture_crash.md)
-        use_graph = choice(args.graph, self.world == 1 and self.gpu and kind == 'amoebanet')
+        use_graph = choice(args.graph, self.world == 1 and self.gpu and kind == 'amoebanet'
+                           and not graph_cells)
         if use_graph:
             if self.world != 1:
                 raise SystemExit('--graph captures one-rank runs only')

@@ -206,10 +206,11 @@ class Segments:
         """Fix cell ``i``'s input buffers at capture: ``flat`` itself when it is persistent
         (``owned`` False: received buffers), else copies the cell keeps."""
         cell = self.cells[i]
+        # (requires_grad as received: it decides which input gradients the cell returns)
         if owned:
-            cell.inputs = [t.detach().clone() for t in flat]
+            cell.inputs = [t.detach().clone().requires_grad_(t.requires_grad) for t in flat]
         else:
-            cell.inputs = [t.detach() for t in flat]
+            cell.inputs = [t.detach().requires_grad_(t.requires_grad) for t in flat]
         return cell.inputs
 
     def pool_index(self, i: int) -> int:
