@@ -110,19 +110,37 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
     warm_s = time.perf_counter() - t0
 
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    seg = stage._segments
+    launch0 = seg.launch_s if seg is not None else 0.0
     e0.record()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     host_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    launch_ms = ((seg.launch_s - launch0) * 1e3 / args.steps) if seg is not None else None
     e1.record()
     e1.synchronize()
     wall_ms = (time.perf_counter() - t0) * 1e3 / args.steps
     dev_ms = e0.elapsed_time(e1) / args.steps
+    idle_launch_ms = None
+    if seg is not None and seg.cells and seg.cells[0].fwd is not None:
+        # one forward graph launched on an idle GPU: the launch's own host cost
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        seg.cells[0].fwd.replay()
+        idle_launch_ms = (time.perf_counter() - t1) * 1e3
+        torch.cuda.synchronize(dev)
     row = {'stage': k, 'layers': [lo, hi], 'graph_cells': args.graph_cells,
            'graph_phase': stage.graph_phase, 'lanes': lanes,
            'host_ms': round(host_ms, 2), 'wall_ms': round(wall_ms, 2),
            'device_ms': round(dev_ms, 2), 'host_share': round(host_ms / dev_ms, 3),
+           # captured cells: host time inside graph launches (enqueueing each graph's nodes,
+           # and waiting whenever the GPU's queue is full) vs the rest (Python, transfers)
+           'graph_launch_ms': None if launch_ms is None else round(launch_ms, 2),
+           'host_outside_launch_share': None if launch_ms is None
+           else round((host_ms - launch_ms) / dev_ms, 3),
+           'idle_fwd_graph_launch_ms': None if idle_launch_ms is None
+           else round(idle_launch_ms, 3),
            'warmup_s': round(warm_s, 1),
            'peak_mem_gib': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)}
     del stage, optimizer, model, x, target, acts, skips, transport

@@ -15,3 +15,6 @@ for gc in "" "--graph-cells"; do
   timeout -k 10 300 python -u benchmarks/stage_harness.py --model unet --balance 16 27 31 44 22 57 27 17 --chunks 40 --batch 640 --stages 0 3 5 $gc > $out/harness_unet$gc.log 2>&1 || { echo "harness unet $gc failed"; tail -20 $out/harness_unet$gc.log; exit 1; }
   cat $out/harness_unet$gc.log
 done
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/ops/test_winograd_gpu.py -k "split_patch" > $out/v20_tests.log 2>&1; rc=$?; tail -3 $out/v20_tests.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -u benchmarks/wino_variants.py --variants 6 20 --shape 32 128 128 96 --shape 40 128 128 96 --shape 16 128 128 96 --shape 40 64 64 192 --shape 16 64 64 192 --shape 32 64 64 192 --shape 16 128 64 192 --out $out/wino_v20.json > $out/wino_v20.log 2>&1; echo "v20 rc=$?"; cat $out/wino_v20.log

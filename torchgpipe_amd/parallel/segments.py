@@ -50,6 +50,7 @@ pools, and the graphs of one pool replay in their capture order (forward phase, 
 backward phase), so no graph ever reads scratch another one is writing.
 """
 import contextlib
+import time
 from typing import Any, Callable, Iterator, List, Optional, Sequence, Tuple
 
 import torch
@@ -140,6 +141,9 @@ class Segments:
         self.grads: List[Tuple[Tensor, Tensor]] = []
         self.pending: List[Any] = []
         self._zeros: List[Tensor] = []
+        # host seconds spent inside graph launches (hipGraphLaunch enqueues every node;
+        # it blocks when the hardware queue is full, i.e. when the GPU is the bottleneck)
+        self.launch_s = 0.0
 
     # -- step ---------------------------------------------------------------------------------
 
@@ -244,8 +248,7 @@ class Segments:
             cell.fwd = graph
             self._fill_slots([cell])
         lane.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(lane):
-            cell.fwd.replay()
+        self._replay(cell.fwd, lane)
         return cell.outputs
 
     def user_outputs(self, i: int) -> List[Tensor]:
@@ -279,8 +282,7 @@ class Segments:
                                    f'counters, the forward {cell.increment}')
             cell.rec = graph
         lane.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(lane):
-            cell.rec.replay()
+        self._replay(cell.rec, lane)
         cell.recomputed = True
 
     def backward(self, i: int, grads: Sequence[Optional[Tensor]], persistent: Sequence[bool],
@@ -320,10 +322,15 @@ class Segments:
                 if dst is not None and g is not None and dst.data_ptr() != g.data_ptr():
                     dst.copy_(g)
         lane.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(lane):
-            cell.bwd.replay()
+        self._replay(cell.bwd, lane)
         cell.recomputed = False
         return cell.gins
+
+    def _replay(self, graph: 'torch.cuda.CUDAGraph', lane: 'torch.cuda.Stream') -> None:
+        t0 = time.perf_counter()
+        with torch.cuda.stream(lane):
+            graph.replay()
+        self.launch_s += time.perf_counter() - t0
 
     def end_backward(self) -> None:
         """End of the step's backward (inside the deferral scope): the capture step records
