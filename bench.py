@@ -157,7 +157,7 @@ def parse() -> argparse.Namespace:
                    help='replay each micro-batch of a stage as captured hipGraphs, transfers '
                         'issued between them (PipelineStage(graph_cells=True), '
                         'parallel/segments.py; instead of the one-GPU whole-step graph; '
-                        'auto: off)')
+                        'auto: on for N > 1)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -313,8 +313,11 @@ class Bench:
         # box, profiles/r2/bench_amoeba_s13.md)
         wgrad_stream = choice(args.wgrad_stream, False)
         # captured cells (parallel/segments.py): multi-rank stages replay each micro-batch's
-        # forward / recomputation / backward as hipGraphs, transfers in between
-        graph_cells = choice(args.graph_cells, False) and self.gpu
+        # forward / recomputation / backward as hipGraphs, transfers in between -- host
+        # enqueue 4-5 % of device time on the U-Net p8 stages instead of 28-46 %
+        # (profiles/r4/stage_harness_unet_p8_ref_*.jsonl), so no rank's host sits on the
+        # pipeline's critical path
+        graph_cells = choice(args.graph_cells, self.world > 1) and self.gpu
         stage = PipelineStage(self.build(kind), balance, device=self.device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
                               overlap_recompute=overlap, overlap_forward=overlap_fwd,

@@ -53,6 +53,10 @@ AMOEBA_TABLE = {  # reference: benchmarks/amoebanetd-memory/main.py (128x3x224x2
 }
 
 
+# transform-cache budget of the measured stages: a fraction of their uncached first-step peak
+CACHE_FRACTION = float(os.environ.get('TGPIPE_WINOGRAD_CACHE_FRACTION', '0.15'))
+
+
 def build(kind: str, b: int, c: int) -> nn.Sequential:
     """U-Net(B, C) = unet(depth=5, num_convs=B, base_channels=C); AmoebaNet-D(L, D)."""
     with torch.device('meta'):
@@ -93,13 +97,15 @@ def measure_stage(kind, layers, lo, hi, batch_size, chunks, shape, checkpoint, d
     last = hi == len(layers)
     torch.cuda.reset_peak_memory_stats(device)
     # as PipelineStage does: the first step runs without cached weight transforms, and its
-    # peak sizes the cache for the second (ops/conv.py size_cache_budget)
+    # peak sizes the cache for the second (ops/conv.py size_cache_budget) -- here in the
+    # memory-lean mode, at most CACHE_FRACTION of that peak
     wino.hold_cache(device)
     cache_budget = 0
     for step in range(2):
         wino.new_step()
         if step == 1:
-            cache_budget = wino.size_cache_budget(device, torch.cuda.max_memory_allocated(device))
+            cache_budget = wino.size_cache_budget(device, torch.cuda.max_memory_allocated(device),
+                                                  CACHE_FRACTION)
         cells = []
         for i in range(m):
             acts = [real(t).requires_grad_(lo > 0) for t in meta_in]

@@ -283,20 +283,3 @@ def test_retain_graph_second_backward_accumulates(kind):
     y.backward(dy)
     torch.testing.assert_close(conv.weight.grad, 2 * gw1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(x.grad, 2 * gx1, rtol=1e-5, atol=1e-5)
-
-
-@pytest.mark.parametrize('shape,splits', [
-    ((2, 128, 128, 24), 0), ((3, 20, 64, 17), 0), ((2, 128, 64, 40), 3), ((1, 8, 64, 8), 0),
-    ((4, 64, 128, 96), 0)])
-def test_f4_split_patch_waves_variant(shape, splits):
-    """Variant 20 (four alternating patch waves): the fused F(4x4) forward against an fp64
-    convolution, odd and even step counts, split-K, ragged tiles."""
-    n, c, k, h = shape
-    torch.manual_seed(0)
-    ops = _ext.require()
-    x = torch.randn(n, c, h, h, device=cuda)
-    w = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
-    y = ops.wino4_conv(x, ops.wino4_weight(w, False), None, k, 20, splits)
-    ref = _ref(x, w)
-    scale = ref.abs().max().item() + 1
-    torch.testing.assert_close(y.double(), ref, rtol=1e-4, atol=2e-5 * scale)

@@ -211,8 +211,8 @@ at::Tensor wino4_conv(const at::Tensor& x_in, const at::Tensor& u,
   auto y = at::empty({n, out_channels, h, w}, x.options());
   if (y.numel() == 0) return y;
   TORCH_CHECK(variant == -1 || (variant >= 4 && variant <= 15 && variant != 11 && variant != 13) ||
-                  variant == 18 || variant == 20,
-              "variant must be -1, 4-10, 12, 14, 15, 18 or 20");
+                  variant == 18,
+              "variant must be -1, 4-10, 12, 14, 15 or 18");
   const WinoPlan plan = wino4_plan(n, r, h, w, out_channels, static_cast<int>(variant),
                                    static_cast<int>(splits));
   at::Tensor ws;

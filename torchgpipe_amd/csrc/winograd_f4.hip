@@ -545,106 +545,6 @@ __global__ __launch_bounds__(F4Cfg<OG>::kThreads, 4 / OG) void f4_conv_kernel(
                       H, W, O, o0 + wo * 16 + 4 * (lane >> 4));
 }
 
-// Variant 20: variant 6 with the input-patch work spread over four waves.  In variant 6
-// waves 0-1 load and transform every step's 128 patches, so two of the four SIMDs carry
-// a whole transform stream next to their MFMAs while the other two carry none, and every
-// step waits for the slower pair at its barrier (0.40 MFMA busy, profiles/r3/pmc).  Here
-// waves 0-3 (one per SIMD) are patch waves in two groups that take turns: group g
-// transforms the patches of every other step (g = step parity) into the idle buffer and
-// issues the loads of its next step two steps ahead; waves 4-7 copy the weight slab by
-// LDS-DMA (9 pieces each).  Per SIMD and step: half a transform stream instead of 0 or 1.
-__global__ __launch_bounds__(512, 1) void f4_conv_split_kernel(
-    const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ bias,
-    float* __restrict__ y, int R, int H, int W, int O, int Rp, int Op, int TH, int TW, int P,
-    int tblocks, int oblocks, int splits, uint32_t x_bytes) {
-  using Cfg = F4Cfg<4>;
-  constexpr int kO = Cfg::kO;
-  constexpr int kBuf = Cfg::kBuf;
-  __shared__ float lds[2 * kBuf];  // 108 KiB
-
-  const int nwg = tblocks * oblocks * splits;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int qq = nwg >> 3, rr = nwg & 7;
-  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  const int ob = wgid % oblocks;
-  const int tb = (wgid / oblocks) % tblocks;
-  const int z = wgid / (oblocks * tblocks);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wo = wave % 4;
-  const int wt = wave / 4;
-  const int t0 = tb * kT;
-  const int o0 = ob * kO;
-  const int HW = H * W;
-  const int tpi = TH * TW;
-
-  const int nsteps = Rp / kC;
-  const int s_begin = z * nsteps / splits;
-  const int s_end = (z + 1) * nsteps / splits;
-  floatx4 acc[kP];
-#pragma unroll
-  for (int i = 0; i < kP; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  if (wave < 4) {
-    // -- patch waves: tile t0 + 16*(wave & 1) + (lane & 15), channel (lane >> 4); group
-    //    wave >> 1 owns the steps s with (s - s_begin) & 1 == group --
-    const int half = wave & 1;
-    const int grp = wave >> 1;
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
-                                          static_cast<int>(x_bytes), 0x00020000);
-    F4Patch p;
-    f4_fwd_offsets(p, t0 + half * 16 + (lane & 15), lane >> 4, P, tpi, TW, R, H, W);
-    float* vmine = lds + Cfg::kUImg + ((lane >> 4) * kT + half * 16 + (lane & 15)) * kP;
-    const uint32_t step_bytes = static_cast<uint32_t>(kC) * HW * 4;
-    if (grp == 0) {
-      f4_load_patch<false>(p, xr, s_begin * step_bytes);
-      f4_transform_store(p, vmine);
-      f4_load_patch<false>(p, xr, min(s_begin + 2, s_end - 1) * step_bytes);
-    } else {
-      f4_load_patch<false>(p, xr, min(s_begin + 1, s_end - 1) * step_bytes);
-    }
-    __syncthreads();
-    for (int s = s_begin; s < s_end; ++s) {
-      const int rel = s - s_begin;
-      const int buf = rel & 1;
-      if (((rel + 1) & 1) == grp && s + 1 < s_end) {
-        // the patch of step s + 1 (loaded two steps ago) into the idle buffer, then the
-        // loads of this group's next step, s + 3
-        f4_transform_store(p, vmine + (buf ^ 1) * kBuf);
-        __builtin_amdgcn_sched_barrier(0);
-        f4_load_patch<false>(p, xr, min(s + 3, s_end - 1) * step_bytes);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
-      __syncthreads();
-    }
-  } else {
-    // -- slab waves 4-7: the step's [4 o-groups][4 c][16 o][36] weight slab by LDS-DMA --
-    const int sw = wave - 4;
-    const int64_t slab_stride = static_cast<int64_t>(Op / 16) * (kC * 16 * kP);
-    const float* ubase = u + static_cast<int64_t>(o0 / 16) * (kC * 16 * kP);
-    f4_glds_slab<Cfg, 4>(ubase + s_begin * slab_stride, lds, sw, lane);
-    __syncthreads();
-    for (int s = s_begin; s < s_end; ++s) {
-      const int buf = (s - s_begin) & 1;
-      if (s + 1 < s_end)
-        f4_glds_slab<Cfg, 4>(ubase + (s + 1) * slab_stride, lds + (buf ^ 1) * kBuf, sw, lane);
-      f4_mfma<Cfg>(acc, lds + buf * kBuf, lane, wo, wt);
-      __syncthreads();
-    }
-  }
-
-  const int tp = t0 + wt * 16 + (lane & 15);
-  if (tp >= P) return;
-  float* ydst = y + static_cast<int64_t>(z) * (P / tpi) * O * HW;
-  f4_output_transform(acc, ydst, bias != nullptr && splits == 1 ? bias : nullptr, tp, tpi, TW,
-                      H, W, O, o0 + wo * 16 + 4 * (lane >> 4));
-}
-
 // Variant 18: variant 6 with the weight slab two steps ahead.  Variant 6 waits at every
 // step's barrier for the slab LDS-DMA issued at the start of that step (__syncthreads
 // drains vmcnt to 0; one step of MFMAs, ~0.5 us, does not cover an L2/HBM fetch).  Here
@@ -1837,7 +1737,7 @@ WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64
                     int variant, int splits) {
   WinoPlan plan;
   plan.variant = (variant >= 4 && variant <= 12 && variant != 11) || variant == 14 ||
-                         variant == 15 || variant == 18 || variant == 20 ? variant : 5;
+                         variant == 15 || variant == 18 ? variant : 5;
   const int og = plan.variant == 5 || plan.variant == 7 || plan.variant == 15 ? 2 : 4;
   const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
   const int64_t blocks = ((P + kT - 1) / kT) * ((out_channels + 16 * og - 1) / (16 * og));
@@ -1918,7 +1818,6 @@ void launch_wino4_conv(const float* x, const float* u, const float* bias, float*
   if (plan.variant == 10) kernel = f4_conv_kernel<4, false, true, 3>;
   if (plan.variant == 12) kernel = vec ? f4_conv_kernel<4, true, true> : f4_conv_kernel<4, false, true>;
   if (plan.variant == 7) kernel = vec ? f4_conv_kernel<2, true, true> : f4_conv_kernel<2, false, true>;
-  if (plan.variant == 20) kernel = f4_conv_split_kernel;
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(nwg)), dim3(128 * og), 0, stream,
                      x, u, bias, splits > 1 ? ws : y, static_cast<int>(red_channels),
                      static_cast<int>(h), static_cast<int>(w), static_cast<int>(out_channels),

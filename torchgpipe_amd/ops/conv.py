@@ -26,13 +26,16 @@ the transform runs once per optimizer step instead of once per call.
   stream waits for it (forward lanes: micro-batch 1 may reach a layer before micro-batch 0
   has transformed its weights).
 * Memory: every cached byte counts against a per-device budget.  A pipeline stage sizes it
-  from its own footprint (:func:`size_cache_budget`, ``PipelineStage``): the first step
-  runs uncached, and afterwards the cache may hold ``TGPIPE_WINOGRAD_CACHE_FRACTION``
-  (default 0.15) of that step's peak, capped at 5 % of the device -- so a stage's memory
-  grows by at most that fraction, however large the model (U-Net(48, 160)'s transforms
-  alone would double it).  Before a stage has sized it (or outside a stage) the budget
-  is 5 % of the device; ``TGPIPE_WINOGRAD_CACHE_MB`` overrides both.  A transform that
-  would exceed the budget is used for the call and then dropped.
+  from its own first step, which runs uncached (:func:`size_cache_budget`,
+  ``PipelineStage``): afterwards the cache may use half of the device memory that step
+  left free, capped at 5 % of the device -- it only ever takes memory the stage does not
+  need, so it cannot make a model that fits uncached run out of memory (the largest
+  trainable model is the cache-free one).  ``TGPIPE_WINOGRAD_CACHE_FRACTION=f`` is the
+  memory-lean mode: at most ``f`` times the first step's peak (``benchmarks/memory.py``
+  uses 0.15, so a stage grows by at most 15 %; the speed benchmarks' stages would then
+  recompute part of their transforms per call).  Before a stage has sized it (or outside
+  a stage) the budget is 5 % of the device; ``TGPIPE_WINOGRAD_CACHE_MB`` overrides all of
+  these.  A transform that would exceed the budget is used for the call and dropped.
 """
 import os
 from typing import Any, Dict, Optional, Sequence, Tuple
@@ -52,7 +55,8 @@ _CACHE_BYTES: Dict[torch.device, int] = {}  # cached bytes per device
 _BUDGET: Optional[int] = None
 # per-device budgets set by size_cache_budget / hold_cache (bytes)
 _DEVICE_BUDGET: Dict[torch.device, int] = {}
-CACHE_PEAK_FRACTION = float(os.environ.get('TGPIPE_WINOGRAD_CACHE_FRACTION', '0.15'))
+_FRACTION = os.environ.get('TGPIPE_WINOGRAD_CACHE_FRACTION')
+CACHE_PEAK_FRACTION: Optional[float] = float(_FRACTION) if _FRACTION else None
 
 
 def new_step() -> None:
@@ -90,10 +94,18 @@ def hold_cache(device: torch.device) -> None:
     _DEVICE_BUDGET[device] = 0
 
 
-def size_cache_budget(device: torch.device, peak_bytes: int) -> int:
-    """Let the caches on ``device`` hold ``CACHE_PEAK_FRACTION`` of ``peak_bytes`` (a
-    stage's uncached step peak), at most 5 % of the device; returns the budget."""
-    budget = min(_device_cap(device), int(CACHE_PEAK_FRACTION * peak_bytes))
+def size_cache_budget(device: torch.device, peak_bytes: int,
+                      fraction: Optional[float] = None) -> int:
+    """Size the caches on ``device`` from a stage's uncached step peak ``peak_bytes``: half
+    the memory that leaves free, or (``fraction`` / ``TGPIPE_WINOGRAD_CACHE_FRACTION``)
+    that fraction of the peak; at most 5 % of the device.  Returns the budget."""
+    fraction = CACHE_PEAK_FRACTION if fraction is None else fraction
+    if fraction is not None:
+        budget = int(fraction * peak_bytes)
+    else:
+        total = torch.cuda.get_device_properties(device).total_memory
+        budget = max(0, total - peak_bytes) // 2
+    budget = min(_device_cap(device), budget)
     _DEVICE_BUDGET[device] = budget
     return budget
 
