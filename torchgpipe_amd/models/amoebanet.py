@@ -21,7 +21,9 @@ keep the reference's children, so parameters and state-dict keys are the same
 as the plain model (``fused=False``), which also serves as the numerics oracle.
 """
 from collections import OrderedDict
+import contextlib
 import os
+import threading
 from typing import Callable, Dict, Iterator, List, Optional, Tuple, Union
 
 import torch
@@ -41,10 +43,24 @@ _CAPTURE_STREAMS = os.environ.get('TGPIPE_CAPTURE_STREAMS', '1') != '0'
 _SHARE_POOLS = os.environ.get('TGPIPE_SHARE_POOLS', '1') != '0'
 # streams per cell for set_cell_streams(model, True) (TGPIPE_CELL_STREAMS)
 DEFAULT_CELL_STREAMS = int(os.environ.get('TGPIPE_CELL_STREAMS', '3'))
-# at most this many inside a hipGraph capture: the capture of a three-stream step ends in a
-# segfault inside the runtime (hipStreamEndCapture, also on the 1 GiB-stack thread;
-# scripts/gpu_r3ab.sh), two streams capture and replay correctly
+# at most this many inside a whole-step hipGraph capture (StepGraph): a capture holding a
+# three-stream forward and its backward segfaults inside the runtime, even for one
+# micro-batch; per-pass captures (PipelineStage(graph_cells=True)) keep the eager stream
+# count (profiles/r3/capture_crash.md, round-4 section)
 CAPTURE_CELL_STREAMS = int(os.environ.get('TGPIPE_CAPTURE_CELL_STREAMS', '2'))
+_WHOLE_STEP = threading.local()
+
+
+@contextlib.contextmanager
+def whole_step_capture() -> Iterator[None]:
+    """Mark a capture that records forward and backward in one graph (StepGraph): cells
+    then use at most ``CAPTURE_CELL_STREAMS`` streams."""
+    prev = getattr(_WHOLE_STEP, 'on', False)
+    _WHOLE_STEP.on = True
+    try:
+        yield
+    finally:
+        _WHOLE_STEP.on = prev
 
 
 def _side_stream(device: torch.device, main: torch.cuda.Stream, index: int = 1
@@ -453,7 +469,7 @@ class Cell(nn.Module):
         backward op on its forward op's stream.
         """
         count = max(2, int(self.streams))
-        if torch.cuda.is_current_stream_capturing():
+        if getattr(_WHOLE_STEP, 'on', False) and torch.cuda.is_current_stream_capturing():
             count = max(2, min(count, CAPTURE_CELL_STREAMS))
         plan = self._stream_plan(count)
         current = torch.cuda.current_stream(s1.device)

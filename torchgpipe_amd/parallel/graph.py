@@ -189,7 +189,8 @@ class StepGraph:
         torch.cuda.synchronize(device)
         graph = torch.cuda.CUDAGraph()
         self._hyper = self._hyperparameters()
-        with torch.cuda.graph(graph, stream=capture):
+        from torchgpipe_amd.models.amoebanet import whole_step_capture
+        with torch.cuda.graph(graph, stream=capture), whole_step_capture():
             self._loss = self._eager(self._input, self._target)
         self._graph = graph
         self._grads = [(p, p.grad) for p in self.stage.parameters() if p.grad is not None]
