@@ -212,6 +212,14 @@ class _TransformCache:
         except Exception:  # interpreter shutdown
             pass
 
+    # derived data: a copied or pickled module starts with an empty cache (the entries hold
+    # device tensors and HIP events of this process)
+    def __deepcopy__(self, memo: Dict[int, Any]) -> '_TransformCache':
+        return type(self)()
+
+    def __reduce__(self) -> Tuple[Any, ...]:
+        return (type(self), ())
+
 
 def refresh_step_caches(module: nn.Module) -> None:
     """Refresh every step-scoped derived-weight cache in ``module`` in place (current

@@ -364,6 +364,12 @@ class _GroupCache:
             self.key = key
         self.ready = None
 
+    def __deepcopy__(self, memo: Dict[int, object]) -> '_GroupCache':
+        return type(self)()  # derived data (see _TransformCache)
+
+    def __reduce__(self) -> Tuple[object, ...]:
+        return (type(self), ())
+
 
 class _GroupConvBN(torch.autograd.Function):
     @staticmethod
