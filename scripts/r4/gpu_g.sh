@@ -11,3 +11,5 @@ timeout -k 10 600 python -u bench.py --gpus 1 --steps 10 --warmup 3 > $out/bench
 cat $out/bench.json
 timeout -k 10 300 python -u benchmarks/stage_harness.py --model amoebanet --balance 2 2 2 3 3 4 4 4 --chunks 32 --batch 1280 --stages 5 6 --graph-cells > $out/harness_amoeba_gc3.log 2>&1 || { tail -20 $out/harness_amoeba_gc3.log; exit 1; }
 grep stage $out/harness_amoeba_gc3.log
+timeout -k 10 300 python -u bench.py --gpus 1 --steps 10 --warmup 4 --graph-cells on --sections none > $out/bench_unet_gc.json 2> $out/bench_unet_gc.err || { tail -20 $out/bench_unet_gc.err; exit 1; }
+cat $out/bench_unet_gc.json

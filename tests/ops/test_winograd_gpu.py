@@ -200,7 +200,8 @@ def test_weight_update_through_data_is_seen_by_the_next_pipeline_step():
 
 def test_cache_budget_zero_keeps_no_transforms(monkeypatch):
     from torchgpipe_amd.ops import conv as convmod
-    monkeypatch.setattr(convmod, '_BUDGET', 0)
+    monkeypatch.delenv('TGPIPE_WINOGRAD_CACHE_MB', raising=False)
+    monkeypatch.setitem(convmod._DEVICE_BUDGET, torch.device('cuda', 0), 0)  # hold_cache
     torch.manual_seed(1)
     layer = convmod.WinogradConv2d(16, 16, 3, padding=1, bias=False).cuda()
     x = torch.randn(2, 16, 12, 12, device='cuda', requires_grad=True)
@@ -283,3 +284,17 @@ def test_retain_graph_second_backward_accumulates(kind):
     y.backward(dy)
     torch.testing.assert_close(conv.weight.grad, 2 * gw1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(x.grad, 2 * gx1, rtol=1e-5, atol=1e-5)
+
+
+def test_cache_budget_sizing_modes(monkeypatch):
+    """size_cache_budget: half of what the uncached step left free (default), or a
+    fraction of its peak (the memory-lean mode), never above 5 % of the device."""
+    from torchgpipe_amd.ops import conv as convmod
+    dev = torch.device('cuda', 0)
+    monkeypatch.setitem(convmod._DEVICE_BUDGET, dev, 0)
+    total = torch.cuda.get_device_properties(dev).total_memory
+    cap = total // 20
+    assert convmod.size_cache_budget(dev, total - (1 << 30), fraction=None) == \
+        min(cap, (1 << 30) // 2)
+    assert convmod.size_cache_budget(dev, 1 << 30, fraction=0.15) == int(0.15 * (1 << 30))
+    assert convmod.size_cache_budget(dev, total // 2, fraction=None) == cap
