@@ -19,6 +19,9 @@ The top-level ``value`` is the U-Net headline.  After it, every run also times
   is measured on the same box as the headline;
 * ``amoebanet``: AmoebaNet-D(18,256), n{N}m32 at the reference balance (n1m32, B=640
   at N=1), and at N=2 the reference's own denominator n2m1 (B=96, ``always``);
+* ``resnet`` (N <= 2): ResNet-101 pipeline-1 (B=220, m=2) at N=1, BASELINE.json's config
+  #2 (pipeline-2, chunks=32, ``always``) at N=2, and the reference's ResNet denominator
+  (no GPipe, B=118) on rank 0's GPU;
 * for N > 1, one extra *diagnostic* step (not timed) in which every rank measures
   how long its streams waited for activations / gradients (``per_rank``).
 
@@ -85,14 +88,19 @@ AMOEBA_EXPERIMENTS = {
 # the reference's AmoebaNet speed-up denominator (benchmarks/amoebanetd-speed/main.py:39-45)
 AMOEBA_N2M1 = dict(name='n2m1', batch=96, chunks=1, balance=[7, 17], ref=26.733)
 # ResNet-101 (benchmarks/resnet101-speed/main.py:22-67): pipeline-1 as in
-# the reference; at N=2 BASELINE.json's config #2, pipeline-2 with chunks=32 and 'always',
-# at the reference's pipeline-2 micro-batch of 15 images (its table runs B=25000, m=1667).
+# the reference; at N=2 BASELINE.json's config #2, pipeline-2 at the reference balance with
+# chunks=32 and 'always'.  The reference ran B=25000 as m=1667 micro-batches of 15 images,
+# a P40 sizing: 15-image micro-batches leave an MI355X's GEMMs underfed (the stages run at
+# half of pipeline-1's per-image speed, profiles/r4/speedup_prediction.md), so the 32
+# micro-batches here hold pipeline-1's 110 images each (B = 3520).
 RESNET_EXPERIMENTS = {
     1: dict(name='pipeline-1', batch=220, chunks=2, balance=[370], checkpoint='except_last',
             ref=81.796),
-    2: dict(name='pipeline-2 (chunks=32, always)', batch=480, chunks=32, balance=[135, 235],
+    2: dict(name='pipeline-2 (chunks=32, always)', batch=3520, chunks=32, balance=[135, 235],
             checkpoint='always', ref=135.539),
 }
+# the reference's ResNet speed-up denominator: ResNet-101 without GPipe, one GPU
+RESNET_BASELINE = dict(name='baseline', batch=118, ref=95.862)
 
 
 def parse() -> argparse.Namespace:
@@ -455,6 +463,13 @@ def main() -> None:
         checkpoint = 'except_last'
         model_name = 'U-Net(5,64)'
         in_shape = '3x192x192'
+    elif kind == 'resnet':
+        exp = dict(RESNET_EXPERIMENTS.get(world) or dict(
+            name=f'pipeline-{world}', batch=240 * world, chunks=32,
+            balance=even_balance(n_layers, world), checkpoint='always', ref=None))
+        checkpoint = exp['checkpoint']
+        model_name = 'ResNet-101'
+        in_shape = '3x224x224'
     else:
         exp = dict(table.get(world) or dict(name=f'n{world}m32', batch=160 * world, chunks=32,
                                             balance=even_balance(n_layers, world), ref=None))
@@ -463,6 +478,8 @@ def main() -> None:
         in_shape = '3x224x224'
     if args.tiny:
         exp['balance'] = exp['tuned'] = even_balance(n_layers, world)
+        if kind == 'resnet':
+            exp.update(batch=4, chunks=2)
     if args.checkpoint:
         checkpoint = args.checkpoint
     if args.batch:
@@ -535,6 +552,13 @@ def main() -> None:
         resnet = summary(rr, None if args.tiny else rexp['ref'])
         resnet['experiment'] = rexp['name']
         resnet['hipgraph'] = rr['hipgraph']
+        resnet['graph_cells'] = rr['graph_cells']
+        rb = b.plain('resnet', 4 if args.tiny else RESNET_BASELINE['batch'], sec_steps,
+                     'resnet-baseline')
+        if rb is not None:
+            resnet['baseline'] = summary(rb, None if args.tiny else RESNET_BASELINE['ref'])
+            resnet['speedup_vs_baseline'] = round(resnet['value'] / resnet['baseline']['value'],
+                                                  3)
 
     if b.rank == 0:
         ref = None if args.tiny else exp.get('ref')

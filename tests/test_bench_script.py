@@ -39,7 +39,8 @@ def _run(nproc: int, *extra: str) -> dict:
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize('nproc,model', [(1, 'unet'), (2, 'unet'), (2, 'amoebanet')])
+@pytest.mark.parametrize('nproc,model', [(1, 'unet'), (2, 'unet'), (2, 'amoebanet'),
+                                         (1, 'resnet')])
 def test_bench_json_contract(nproc, model):
     rec = _run(nproc, '--model', model)
     assert KEYS <= set(rec)
@@ -48,6 +49,9 @@ def test_bench_json_contract(nproc, model):
     assert rec['config']['global_batch'] == 4
     assert rec['config']['parallelism'] == f'pp{nproc}'
     assert 'TINY' in rec['metric'] and rec['vs_baseline'] is None
+    if model == 'resnet':
+        assert rec['metric'].startswith('ResNet-101')
+        assert rec['config']['checkpoint'] == 'except_last'
     # value is the whole-job aggregate: batch * steps / elapsed
     assert rec['value'] == pytest.approx(4 * 1000 / rec['ms_per_step'], rel=1e-2)
     if model == 'unet':
@@ -63,6 +67,10 @@ def test_bench_json_contract(nproc, model):
         res = rec['resnet101']
         assert res['value'] > 0 and res['checkpoint'] == ('except_last' if nproc == 1
                                                            else 'always')
+        # with its own no-GPipe denominator (the reference's ResNet baseline, B=118)
+        assert res['baseline']['value'] > 0
+        assert res['speedup_vs_baseline'] == pytest.approx(
+            res['value'] / res['baseline']['value'], rel=1e-2)
     if nproc > 1:
         ranks = rec['per_rank']
         assert [r['rank'] for r in ranks] == list(range(nproc))
