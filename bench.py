@@ -34,6 +34,7 @@ stages; fp32 like the reference.  Rank 0 prints one JSON line.
 """
 import argparse
 import datetime
+import gc
 import json
 import os
 import sys
@@ -314,7 +315,9 @@ class Bench:
         # on one GPU: profiles/r2/bench_amoeba_s13.md).  Multi-rank runs keep them: sends
         # leave from the lane that computed them and backward passes are ordered across
         # lanes (parallel/stage.py), parity-tested on shared-GPU gloo rehearsals.
-        overlap = choice(args.overlap_recompute, self.gpu and unet)
+        # (ResNet-101 p1: 1459 vs 1411 samples/s with the recompute lane,
+        # profiles/r4/resnet_p1_engine.md)
+        overlap = choice(args.overlap_recompute, self.gpu and kind in ('unet', 'resnet'))
         overlap_fwd = choice(args.overlap_forward, self.gpu and unet)
         cell_streams = kind == 'amoebanet' and choice(args.cell_streams, self.gpu)
         # (auto: off -- with the two-stream cells it measured 280.3 vs 328.6 samples/s on one
@@ -395,10 +398,22 @@ class Bench:
                 sort_by='cuda_time_total' if self.gpu else 'cpu_time_total', row_limit=30),
                 file=sys.stderr)
         res['mem'] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30 if self.gpu else 0.0
-        del stage, optimizer, x, target, graph
-        if self.gpu:
-            torch.cuda.empty_cache()
+        del stage, optimizer, x, target, graph, step, settle
+        self.release()
         return res
+
+    def release(self) -> None:
+        """Free what a finished timing held before the next one is built: autograd graphs
+        and captured graphs in reference cycles, and with them their Winograd transform
+        caches, which would otherwise still count against the next stage's cache budget."""
+        gc.collect()
+        if self.gpu:
+            from torchgpipe_amd.ops.conv import cache_bytes
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()
+            held = cache_bytes()
+            if held:
+                self.log(f'{held / 2 ** 20:.0f} MiB of transform caches still held')
 
     def plain(self, kind: str, batch: int, steps: int, tag: str) -> Optional[Dict[str, Any]]:
         """The model without GPipe (no micro-batches, no checkpointing) on rank 0's GPU,
@@ -424,9 +439,8 @@ class Bench:
             finally:
                 self.world = world
             res.update(batch=batch, steps=steps)
-            del model, optimizer, x, target
-            if self.gpu:
-                torch.cuda.empty_cache()
+            del model, optimizer, x, target, step
+            self.release()
         self.ctrl_barrier()
         return res
 

@@ -3,6 +3,7 @@ time of the fused model (ops/fusion.py) or the plain nn model (--plain).  A rocp
 kernel trace of this benchmark loses its buffers: the process aborts at interpreter exit
 in a library's static teardown (plain and fused alike)."""
 import argparse
+import os
 import sys
 import time
 
@@ -10,8 +11,10 @@ import torch
 import torch.nn.functional as F
 from torch.profiler import ProfilerActivity, profile
 
-from torchgpipe_amd import GPipe
-from torchgpipe_amd.models.resnet import build_resnet
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+from torchgpipe_amd import GPipe  # noqa: E402
+from torchgpipe_amd.models.resnet import build_resnet  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument('--plain', action='store_true')
