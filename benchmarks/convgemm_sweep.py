@@ -1,5 +1,6 @@
 """Device time of every implicit-GEMM launch plan (tile config x reduction splits) for a
-few AmoebaNet-D convolution shapes at micro-batch 20 -- what the autotuner chooses from.
+few AmoebaNet-D convolution shapes (micro-batch 20: ``--micro-batch``) -- what the
+autotuner chooses from.
 
     python benchmarks/convgemm_sweep.py --out profiles/convgemm_sweep.json
 """
@@ -24,12 +25,14 @@ CFG = {0: '64x64/4w', 1: '128x128/8w', 2: '128x128/4w', 3: '64x64/4w/sub4',
 def main() -> None:
     p = argparse.ArgumentParser(description=__doc__)
     p.add_argument('--reps', type=int, default=20)
+    p.add_argument('--micro-batch', type=int, default=20, help='images per shape')
     p.add_argument('--out', default='')
     a = p.parse_args()
     from torchgpipe_amd.ops import _ext
     ops = _ext.require()
     out = []
-    for n, ci, h, co, kh, kw in SHAPES:
+    for _, ci, h, co, kh, kw in SHAPES:
+        n = a.micro_batch
         x = torch.randn(n, ci, h, h, device='cuda')
         w = torch.randn(co, ci, kh, kw, device='cuda') * 0.05
         geo = [kh, kw, 1, 1, (kh - 1) // 2, (kw - 1) // 2, 0, 0]

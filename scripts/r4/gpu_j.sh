@@ -4,6 +4,8 @@
 set -o pipefail
 out=gpurun_out/r4j
 mkdir -p $out
+timeout -k 10 300 python -u -m pytest tests/ops/test_convbn_gpu.py -q -x --timeout 120 --timeout-method thread -k "conv_gemm_matches or phases" > $out/conv_tests.log 2>&1 || { tail -30 $out/conv_tests.log; exit 1; }
+tail -2 $out/conv_tests.log
 timeout -k 10 600 python -u bench.py --gpus 1 --steps 10 --warmup 3 > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
 python -c "import json;d=json.load(open('$out/bench.json'));print('unet', d['value'], 'base', d['baseline']['value'], 'amoeba', d['amoebanet']['value'], 'resnet', d['resnet101']['value'], d['resnet101'].get('baseline',{}).get('value'))"
 grep -i "still held" $out/bench.err || true

@@ -45,6 +45,12 @@ CASES = [
     (3, 16, 15, 15, 24, 3, 3, 2, 1, 0),      # 3x3 stride 2, odd plane
     (2, 3, 32, 32, 16, 3, 3, 2, 1, 0),       # AmoebaNet stem (3 channels, stride 2)
     (2, 16, 14, 14, 16, 1, 7, 2, 3, 0),      # 1x7 at stride 2
+    # strided k x k backward-data: one GEMM per stride phase (conv_gemm_phases)
+    (2, 3, 33, 33, 16, 7, 7, 2, 3, 0),       # ResNet stem 7x7 s2 p3, odd plane
+    (3, 20, 16, 16, 24, 5, 5, 2, 2, 0),      # 5x5 s2
+    (2, 16, 13, 13, 16, 3, 3, 3, 1, 0),      # stride 3: one tap per phase
+    (2, 16, 14, 14, 16, 2, 2, 3, 0, 0),      # kernel < stride: phases without taps (zeros)
+    (8, 128, 28, 28, 128, 3, 3, 2, 1, 0),    # reduction-cell 3x3 s2 at AmoebaNet width
 ]
 
 
@@ -91,6 +97,23 @@ def test_conv_gemm_matches_fp64(case, relu, tile_cfg):
     dw = ops().conv_gemm_backward_weight(dz, x, wt, geo, relu)
     assert rel_err(dx, x64.grad) < 2e-6
     assert rel_err(dw, w64.grad) < 5e-6
+
+
+@pytest.mark.parametrize('kernel,stride,pad', [((1, 7), (1, 2), (0, 3)), ((7, 1), (2, 1), (3, 0)),
+                                               ((3, 5), (2, 3), (1, 2))])
+def test_strided_backward_data_phases_anisotropic(kernel, stride, pad):
+    """AmoebaNet's reduction 1x7 / 7x1 (stride along one axis) and a mixed-stride kernel:
+    the phase decomposition per axis matches fp64."""
+    torch.manual_seed(0)
+    x = torch.randn(3, 16, 14, 15, device='cuda')
+    wt = torch.randn(24, 16, *kernel, device='cuda') / (16 * kernel[0] * kernel[1]) ** 0.5
+    geo = [kernel[0], kernel[1], stride[0], stride[1], pad[0], pad[1], 0, 0]
+    x64 = x.double().requires_grad_(True)
+    want = F.conv2d(F.relu(x64), wt.double(), stride=stride, padding=pad)
+    dz = torch.randn(want.shape, device='cuda')
+    want.backward(dz.double())
+    dx = ops().conv_gemm_backward_data(dz, x, wt, geo, True)
+    assert rel_err(dx, x64.grad) < 2e-6
 
 
 def _block(kind, ci, co):

@@ -15,6 +15,9 @@
 //                strided 1x1 ("scatter"): N = output pixels, each result scattered to
 //                its input pixel (the stride holes are zero; 4x less work than a
 //                dense pass that reads zeros for them)
+//                strided k x k ("phase", conv_gemm_phases): one GEMM per residue of the
+//                input pixel modulo the stride, over exactly the taps that reach it --
+//                N = that phase's pixels, K = Co x its taps, results scattered likewise
 //   weight-grad  dW[co][ci][t]  = sum_{n,p} dZ[n][co][p] * relu(X[n][ci][tap(p,t)])
 //                M = Co, N = Ci x taps, K = images x output pixels
 //
@@ -118,6 +121,9 @@ struct Geo {
   int a_t;               // bwd-data: A is the transposed weight [ci][co*T] (row-major)
   int spread;            // element-gathered N-major columns spread over the lanes
   FastDiv fd_taps, fd_kw, fd_hwo, fd_wo, fd_hwi;  // / taps, / kw, / (ho*wo), / wo, / (h*w)
+  // bwd-data of one stride phase (scatter set too): ho x wo = the phase grid, zh x zw =
+  // the dZ plane, tap (th, tw) of column (y, x) reads dZ[y + dy0 - th][x + dx0 - tw]
+  int phase, zh, zw, dy0, dx0;
 };
 
 // Tile configurations.  CFG 0: 64 x 64 block, 4 waves (2 x 2) of one 32 x 32 MFMA tile;
@@ -273,7 +279,12 @@ __device__ __forceinline__ Col make_col(const Geo& g, int j, int N) {
       c.x = (p - y * wdt) * g.sw - g.pw + g.ow;
     }
   } else {  // bwd-data: dZ source
-    if (kPlain || g.scatter) {
+    if (g.phase) {
+      const int y = p / wdt;
+      c.base = (n * g.co_total + g.co_off) * g.zh * g.zw;
+      c.y = y + g.dy0;
+      c.x = (p - y * wdt) + g.dx0;
+    } else if (kPlain || g.scatter) {
       c.base = (n * g.co_total + g.co_off) * g.ho * g.wo + p;
       c.y = c.x = 0;
       if (g.scatter) {  // destination input pixel, for the epilogue
@@ -335,8 +346,9 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
   // apart (store_nmajor's `spread`)
   constexpr int QPR = C::BN / 4;
   const bool spread = !kBK_major && g.spread &&
-                      !(((MODE == kFwd && kPlain) || (MODE == kBwdData && (kPlain || g.scatter)))
-                        && (hw_out & 3) == 0);
+                      !(((MODE == kFwd && kPlain) ||
+                         (MODE == kBwdData && (kPlain || (g.scatter && !g.phase)))) &&
+                        (hw_out & 3) == 0);
   Col col[4];
   if constexpr (!kBK_major) {
     const int jq = n0 + (tid % QPR) * (spread ? 1 : 4);
@@ -444,7 +456,18 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
         const int k = k0 + tid / QPR + (kThreads / QPR) * i;
         const bool kin = k < k_end;
         floatx4 v;
-        if (kPlain || g.scatter) {
+        if (g.phase) {
+          // dZ taps of this phase: dense, stride 1 (the decomposition removed the holes)
+          const int co = g.fd_taps.div(k), t = k - co * g.taps;
+          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int y = col[e].y - th, x = col[e].x - tw;
+            const bool ok = col[e].ok && kin && y >= 0 && y < g.zh && x >= 0 && x < g.zw;
+            v[e] = bload(br, ok ? static_cast<uint32_t>(
+                                      (col[e].base + (co * g.zh + y) * g.zw + x) * 4) : kOOB);
+          }
+        } else if (kPlain || g.scatter) {
           const int coff = k * hw_out;
           if (((hw_out & 3) == 0) && col[3].ok && kin) {
             v = bload4(br, static_cast<uint32_t>((col[0].base + coff) * 4));
@@ -932,7 +955,8 @@ Geo make_geo(const ConvGemmGeo& cg) {
   static const int spread = env_int("TGPIPE_CG_SPREAD", 1) != 0 ? 1 : 0;
   Geo g{cg.n, cg.ci, cg.h, cg.w, cg.co, cg.ho, cg.wo, cg.co_total, cg.co_off, cg.kh, cg.kw,
         cg.kh * cg.kw, cg.sh, cg.sw, cg.ph, cg.pw, cg.oh, cg.ow, cg.relu ? 1 : 0, 0,
-        cg.a_t ? 1 : 0, spread, {}, {}, {}, {}, {}};
+        cg.a_t ? 1 : 0, spread, {}, {}, {}, {}, {},
+        cg.phase ? 1 : 0, cg.zh, cg.zw, cg.dy0, cg.dx0};
   g.fd_taps = make_fastdiv(g.taps);
   g.fd_kw = make_fastdiv(g.kw);
   g.fd_hwo = make_fastdiv(g.ho * g.wo);
@@ -952,7 +976,7 @@ void gemm_dims(int mode, const Geo& g, int& M, int& N, int& K) {
 }
 
 bool scatter_bwd(const ConvGemmGeo& cg) {
-  return cg.kh == 1 && cg.kw == 1 && (cg.sh > 1 || cg.sw > 1);
+  return cg.phase || (cg.kh == 1 && cg.kw == 1 && (cg.sh > 1 || cg.sw > 1));
 }
 
 }  // namespace
@@ -960,6 +984,43 @@ bool scatter_bwd(const ConvGemmGeo& cg) {
 int env_int(const char* name, int fallback) {
   const char* v = std::getenv(name);
   return v != nullptr && *v != 0 ? std::atoi(v) : fallback;
+}
+
+bool conv_gemm_phased(const ConvGemmGeo& g) {
+  return !g.phase && (g.kh > 1 || g.kw > 1) && (g.sh > 1 || g.sw > 1) && g.oh == 0 &&
+         g.ow == 0;
+}
+
+// Residue (a, b) of the input pixel modulo the stride: the taps th = th0 + sh*i with
+// th0 = (a + ph) mod sh meet it (y + ph - th divisible by sh), reading dZ row
+// (y + ph - th) / sh = yy + dy0 - i for y = sh*yy + a, dy0 = (a + ph - th0) / sh.
+std::vector<ConvGemmPhase> conv_gemm_phases(const ConvGemmGeo& g) {
+  std::vector<ConvGemmPhase> out;
+  for (int a = 0; a < g.sh && a < g.h; ++a) {
+    const int th0 = (a + g.ph) % g.sh;
+    if (th0 >= g.kh) continue;
+    for (int b = 0; b < g.sw && b < g.w; ++b) {
+      const int tw0 = (b + g.pw) % g.sw;
+      if (tw0 >= g.kw) continue;
+      ConvGemmPhase p{g, th0, tw0};
+      ConvGemmGeo& q = p.geo;
+      q.phase = true;
+      q.kh = (g.kh - th0 + g.sh - 1) / g.sh;
+      q.kw = (g.kw - tw0 + g.sw - 1) / g.sw;
+      q.ho = (g.h - a + g.sh - 1) / g.sh;  // this phase's pixel grid
+      q.wo = (g.w - b + g.sw - 1) / g.sw;
+      q.zh = g.ho;
+      q.zw = g.wo;
+      q.dy0 = (a + g.ph - th0) / g.sh;
+      q.dx0 = (b + g.pw - tw0) / g.sw;
+      q.ph = q.pw = 0;  // destination pixel (sh*y + oh, sw*x + ow) in the epilogue
+      q.oh = a;
+      q.ow = b;
+      q.a_t = true;
+      out.push_back(p);
+    }
+  }
+  return out;
 }
 
 ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
@@ -1055,7 +1116,7 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
                       const ConvGemmPlan& plan, bool accumulate, float* ws, int64_t a_bytes,
                       int64_t b_bytes, hipStream_t stream) {
   Geo g = make_geo(cg);
-  g.scatter = plan.scatter ? 1 : 0;
+  g.scatter = plan.scatter || cg.phase ? 1 : 0;
   int M, N, K;
   gemm_dims(mode, g, M, N, K);
   if (M == 0 || N == 0) return;

@@ -92,7 +92,15 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
                     g.ow, g.co_total};
   std::lock_guard<std::mutex> lock(plan_mutex);
   auto hit = plan_cache.find(key);
-  if (hit != plan_cache.end()) return hit->second;
+  if (hit != plan_cache.end()) {
+    // (a stride phase's key could name a plain strided geometry too: its plan must
+    // scatter and cannot split)
+    if (!g.phase) return hit->second;
+    ConvGemmPlan p = hit->second;
+    p.scatter = true;
+    p.splits = 1;
+    return p;
+  }
   if (!tune) return heuristic;
   // A stream capture (hipGraph) records launches, it cannot time them: a shape first met
   // inside a capture runs the heuristic plan (warm-up steps before capturing tune it).
@@ -201,6 +209,46 @@ void run_gemm(int mode, const float* a, const float* b, const float* mask, float
               float* pm, float* pm2, const ConvGemmGeo& g, const ConvGemmPlan& plan,
               bool accumulate, int64_t a_bytes, int64_t b_bytes, const at::Tensor& like) {
   launch_one(mode, a, b, mask, out, pm, pm2, g, plan, accumulate, a_bytes, b_bytes, like);
+}
+
+// Whether a backward-data into `dx` leaves pixels unwritten (stride holes of a strided 1x1,
+// or stride phases no tap reaches): such a dx starts zeroed.
+bool dx_needs_zero(const ConvGemmGeo& g) {
+  if (conv_gemm_phased(g))
+    return conv_gemm_phases(g).size() <
+           static_cast<size_t>(std::min(g.sh, g.h) * std::min(g.sw, g.w));
+  return conv_gemm_plan(1, g).scatter;
+}
+
+// Backward-data of one convolution into `dx` (accumulating onto it when asked) with the
+// transposed weight `wt` ([ci][co][kh][kw]) as the A operand.  A strided k x k convolution
+// runs as one GEMM per stride phase (conv_gemm_phases: the sub-pixel decomposition, no
+// stride holes walked) on that phase's slice of the weight's taps.
+void backward_data_into(const at::Tensor& wt, const at::Tensor& dz, const at::Tensor& x,
+                        at::Tensor& dx, ConvGemmGeo g, bool accumulate) {
+  g.a_t = true;
+  if (conv_gemm_phased(g)) {
+    for (const auto& ph : conv_gemm_phases(g)) {
+      const at::Tensor wp = wt.slice(2, ph.th0, c10::nullopt, g.sh)
+                                .slice(3, ph.tw0, c10::nullopt, g.sw)
+                                .contiguous();
+      const ConvGemmPlan plan =
+          tuned_plan(1, wp.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+                     dx.data_ptr<float>(), nullptr, nullptr, ph.geo, accumulate,
+                     wp.numel() * 4, dz.numel() * 4, x, x.numel());
+      run_gemm(1, wp.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+               dx.data_ptr<float>(), nullptr, nullptr, ph.geo, plan, accumulate,
+               wp.numel() * 4, dz.numel() * 4, x);
+    }
+    return;
+  }
+  const ConvGemmPlan plan =
+      tuned_plan(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+                 dx.data_ptr<float>(), nullptr, nullptr, g, accumulate, wt.numel() * 4,
+                 dz.numel() * 4, x, x.numel());
+  run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
+           dx.data_ptr<float>(), nullptr, nullptr, g, plan, accumulate, wt.numel() * 4,
+           dz.numel() * 4, x);
 }
 
 // A channel slice of a dense NCHW tensor (e.g. the gradient of one input of a
@@ -630,9 +678,8 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
     TORCH_CHECK(dx_into->sizes() == x.sizes(), "dx_into must have the input's shape");
   }
   auto ours_into = [&](bool use_into) -> at::Tensor {
-    std::vector<ConvGemmPlan> plans;
     bool zero = false;
-    for (const auto& g : p.geo) zero = zero || conv_gemm_plan(1, g).scatter;
+    for (const auto& g : p.geo) zero = zero || dx_needs_zero(g);
     at::Tensor d = use_into ? *dx_into
                             : (zero ? at::zeros_like(x) : at::empty_like(x));  // stride holes
     zero = zero || use_into;  // (from here: accumulate onto d)
@@ -653,19 +700,9 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                     "weights_t[i] must be weights[i] transposed to [ci][co][kh][kw]");
         wts.push_back(weights_t[i]);
       }
-      p.geo[i].a_t = true;
     }
     for (size_t i = 0; i < p.geo.size(); ++i)
-      plans.push_back(tuned_plan(1, wts[i].data_ptr<float>(), dz.data_ptr<float>(),
-                                 x.data_ptr<float>(), d.data_ptr<float>(), nullptr, nullptr,
-                                 p.geo[i], i > 0 || zero, wts[i].numel() * 4,
-                                 dz.numel() * 4, x, x.numel()));
-    for (size_t i = 0; i < p.geo.size(); ++i) {
-      const auto& wt = wts[i];
-      run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-               d.data_ptr<float>(), nullptr, nullptr, p.geo[i], plans[i], i > 0 || zero,
-               wt.numel() * 4, dz.numel() * 4, x);
-    }
+      backward_data_into(wts[i], dz, x, d, p.geo[i], i > 0 || zero);
     return d;
   };
   if (need_dx) {
@@ -853,16 +890,9 @@ std::vector<at::Tensor> convbn_group_backward(
     g.co = static_cast<int>(c);
     g.co_total = static_cast<int>(c);
     g.co_off = 0;
-    g.a_t = true;
-    const bool zero = conv_gemm_plan(1, g).scatter;
+    const bool zero = dx_needs_zero(g);
     dx = zero ? at::zeros_like(x) : at::empty_like(x);
-    const ConvGemmPlan plan =
-        tuned_plan(1, w_cat_t.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-                   dx.data_ptr<float>(), nullptr, nullptr, g, zero, w_cat_t.numel() * 4,
-                   dz.numel() * 4, x, x.numel());
-    run_gemm(1, w_cat_t.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-             dx.data_ptr<float>(), nullptr, nullptr, g, plan, zero, w_cat_t.numel() * 4,
-             dz.numel() * 4, x);
+    backward_data_into(w_cat_t, dz, x, dx, g, zero);
   }
   out.push_back(dx);
   for (auto& g : dgb) out.push_back(g);
@@ -1002,8 +1032,8 @@ at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_
   Parts p = make_parts(x, {weight}, geo, relu);
   TORCH_CHECK(dz.size(1) == p.co_total && dz.size(2) == p.ho && dz.size(3) == p.wo,
               "dz does not match the convolution's output");
-  const bool scatter = conv_gemm_plan(1, p.geo[0]).scatter;
-  auto dx = scatter ? at::zeros_like(x) : at::empty_like(x);
+  const bool zero = dx_needs_zero(p.geo[0]);
+  auto dx = zero ? at::zeros_like(x) : at::empty_like(x);
   at::Tensor wt;  // A = W^T (see convbn_backward)
   if (weight_t.has_value() && weight_t->defined()) {
     check_f32(*weight_t, "weight_t", x);
@@ -1014,14 +1044,7 @@ at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_
   } else {
     wt = weight.transpose(0, 1).contiguous();
   }
-  p.geo[0].a_t = true;
-  const ConvGemmPlan plan =
-      tuned_plan(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-                 dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], scatter, wt.numel() * 4,
-                 dz.numel() * 4, x, x.numel());
-  run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
-           dx.data_ptr<float>(), nullptr, nullptr, p.geo[0], plan, plan.scatter,
-           wt.numel() * 4, dz.numel() * 4, x);
+  backward_data_into(wt, dz, x, dx, p.geo[0], zero);
   return dx;
 }
 

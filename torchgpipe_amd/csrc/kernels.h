@@ -148,7 +148,22 @@ struct ConvGemmGeo {
   int oh, ow;            // extra input offset (FactorizedReduce's shifted branch)
   bool relu;             // ReLU on the input (its mask in backward-data)
   bool a_t = false;      // backward-data: `a` is W transposed, [ci][co*kh*kw] row-major
+  // backward-data of one stride phase of a strided k x k convolution (conv_gemm_phases):
+  // ho x wo = the phase's pixel grid (input pixels (sh*y + oh, sw*x + ow)), kh x kw its
+  // taps, zh x zw the dZ plane, tap (i, j) reading dZ[y + dy0 - i][x + dx0 - j]
+  bool phase = false;
+  int zh = 0, zw = 0, dy0 = 0, dx0 = 0;
 };
+// Sub-pixel decomposition of a strided convolution's backward-data: input pixels of one
+// residue (a, b) modulo the stride receive exactly the taps th = th0 + sh*i, tw = tw0 + sw*j,
+// so each phase is a dense stride-1 GEMM (no stride holes), its results scattered back.
+// Phases without taps (kernel smaller than the stride) are left out: their pixels are 0.
+struct ConvGemmPhase {
+  ConvGemmGeo geo;  // a = the weight transposed [ci][co][kh][kw] sliced to [:, :, th0::sh, tw0::sw]
+  int th0, tw0;
+};
+bool conv_gemm_phased(const ConvGemmGeo& g);
+std::vector<ConvGemmPhase> conv_gemm_phases(const ConvGemmGeo& g);
 // mode 0: forward  Z[:, co_off:co_off+co] = conv(relu(X)); a = W[co][ci*kh*kw], b = X;
 //         part_mean / part_m2 (may be null): BatchNorm statistics partials of each output
 //         channel, per column block ([col_blocks][co_total]) when the plan does not split
@@ -166,7 +181,7 @@ struct ConvGemmPlan {
   int splits = 1;        // reduction splits (grid.y), > 1: workspace slices + split_reduce
   int col_width = 128;   // forward: columns per statistics block
   int col_blocks = 0;    // forward: statistics blocks
-  bool scatter = false;  // backward-data of a strided 1x1 over output pixels
+  bool scatter = false;  // backward-data over output / phase pixels, results scattered
 };
 ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& g);
 // Every launch shape worth timing (tile size x reduction splits) for the autotuner.
