@@ -6,9 +6,13 @@ downsample as subsample + pointwise implicit GEMM (ops.convbn.gemm_conv2d).
 """
 import argparse
 import json
+import os
+import sys
 
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 SHAPES = [  # name, cin, cout, k, stride, pad, h
     ('stem 7x7', 3, 64, 7, 2, 3, 224),
@@ -74,6 +78,17 @@ def main() -> None:
         row['fusable'] = fusable(xg, [conv], bn)
         if row['fusable']:
             row['fused_fwd_bwd_us'] = timed(fused)
+            # the native backward-data (stride phases: conv_gemm_phases), no library choice
+            ops = torch.ops.tgpipe
+            geo = [k, k, s, s, pad, pad, 0, 0]
+            row['native_bwd_data_us'] = timed(
+                lambda: ops.conv_gemm_backward_data(dy, x, w, geo, False))
+            row['native_fwd_us'] = timed(lambda: ops.conv_gemm_forward(x, w, geo, False))
+            ops.lib_dgrad_force(0)
+            try:
+                row['fused_native_fwd_bwd_us'] = timed(fused)
+            finally:
+                ops.lib_dgrad_force(-1)
         if k == 1:
             from torchgpipe_amd.ops.convbn import gemm_conv2d
             conv = torch.nn.Conv2d(cin, cout, 1, bias=False).to(dev)

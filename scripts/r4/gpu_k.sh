@@ -3,6 +3,11 @@
 set -o pipefail
 out=gpurun_out/r4k
 mkdir -p $out
+timeout -k 10 300 python -u benchmarks/diag/resnet_strided_probe.py > $out/resnet_strided_probe.jsonl 2> $out/resnet_strided_probe.err || { tail -20 $out/resnet_strided_probe.err; exit 1; }
+python -c "
+import json
+for l in open('$out/resnet_strided_probe.jsonl'):
+    r=json.loads(l); print(r['name'], 'miopen dgrad', r['bwd_data_us'], 'native', r.get('native_bwd_data_us'), '| conv+bn miopen', r['miopen_bn_fwd_bwd_us'], 'fused', r.get('fused_fwd_bwd_us'), 'fused native', r.get('fused_native_fwd_bwd_us'))"
 timeout -k 10 300 python -u benchmarks/convbn_bench.py --micro-batch 40 --out $out/convbn_bench_n40.json > $out/convbn_bench.log 2>&1 || { tail -20 $out/convbn_bench.log; exit 1; }
 tail -1 $out/convbn_bench.log
 timeout -k 10 300 python -u benchmarks/convgemm_sweep.py --micro-batch 40 --out $out/convgemm_sweep_n40.json > $out/sweep.log 2>&1 || { tail -20 $out/sweep.log; exit 1; }

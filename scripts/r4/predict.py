@@ -53,7 +53,7 @@ def main():
         sp = f'{sps / d:.3f}' if d else 'n/a'
         print(f"| {name} B {a['batch']} m {m} {a['balance']} | "
               f"{' / '.join(f'{s:.1f}' for s in st)} | {st[k]:.1f} | {sps:.1f} | {sp} | "
-              f"{REF.get(name, '')} | {host[k] / st[k]:.2f} |")
+              f"{REF.get(name, REF.get(name[:9], ''))} | {host[k] / st[k]:.2f} |")
 
 
 if __name__ == '__main__':

@@ -455,6 +455,22 @@ MAX_TRANSFORM_BYTES = int(float(os.environ.get('TGPIPE_WINOGRAD_MAX_TRANSFORM_MB
                           * (1 << 20))
 
 
+# A convolution whose weight transform dwarfs its input -- a few images through thousands
+# of channels, e.g. benchmarks/memory.py's U-Net(48,160) at micro-batch 1 (2560 channels at
+# 12^2: 943 MB of F(4x4) transform for a 1.5 MB input, ratio 640) -- stays on MIOpen: the
+# transform would move far more bytes than the convolution reads, and when it is not
+# cached it is a transient the size of the transform (U-Net(48,160) p8's fullest stage 33.6
+# vs 22.4 GiB).  U-Net(5,64)'s deepest layers at 16 images per micro-batch reach 57.
+WEIGHT_DOMINATED_RATIO = float(os.environ.get('TGPIPE_WINOGRAD_WEIGHT_RATIO', '256'))
+
+
+def _transform_ratio(x: Tensor, weight: Tensor) -> float:
+    """Weight-transform floats (16 / 36 per channel pair at F(2x2) / F(4x4) planes) per
+    input float."""
+    positions = 16 if min(x.shape[2], x.shape[3]) < F4_MIN_PLANE else 36
+    return weight.shape[0] * weight.shape[1] * positions / max(1, x.numel())
+
+
 def wino_eligible(x: Tensor, weight: Tensor, stride: Sequence[int] = (1, 1),
                   padding: Sequence[int] = (1, 1), dilation: Sequence[int] = (1, 1),
                   groups: int = 1) -> bool:
@@ -464,7 +480,8 @@ def wino_eligible(x: Tensor, weight: Tensor, stride: Sequence[int] = (1, 1),
             and weight.shape[0] * weight.shape[1] * 16 * 4 <= MAX_TRANSFORM_BYTES
             and weight.dtype == torch.float32 and tuple(weight.shape[2:]) == (3, 3)
             and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
-            and tuple(dilation) == (1, 1) and groups == 1)
+            and tuple(dilation) == (1, 1) and groups == 1
+            and _transform_ratio(x, weight) <= WEIGHT_DOMINATED_RATIO)
 
 
 def winograd_conv2d(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None,
