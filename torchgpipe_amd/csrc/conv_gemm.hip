@@ -63,6 +63,8 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kBK = 32;
+// mfma_stage: all of a stage's LDS fragment reads ahead of its MFMAs (see there)
+constexpr bool kMfmaReadsFirst = true;
 constexpr uint32_t kOOB = 0x7ffffff0u;  // buffer offset past every tensor (< 2 GiB)
 
 enum Mode : int { kFwd = 0, kBwdData = 1, kWgrad = 2 };
@@ -221,33 +223,66 @@ __device__ __forceinline__ void mfma_stage(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG
                                            const float* aimg, const float* bimg, int lane, int wm,
                                            int wn) {
   using C = Cfg<CFG>;
-  constexpr int WM = C::TM, WN = C::TN;
+  constexpr int WM = C::TM, WN = C::TN, G = kBK / 4;
   const int h = lane >> 5, l32 = lane & 31;
-#pragma unroll
-  for (int g = 0; g < kBK / 4; ++g) {
-    floatx2 a[WM], b[WN];
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-      a[i] = *reinterpret_cast<const floatx2*>(
-          aimg + ((2 * g + h) * C::BM + kswz(wm * 32 * WM + i * 32 + l32, g)) * 2);
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      if constexpr (kBKMajor) {
-        b[j] = *reinterpret_cast<const floatx2*>(
-            bimg + ((2 * g + h) * C::BN + kswz(wn * 32 * WN + j * 32 + l32, g)) * 2);
-      } else {
-        const int col = wn * 32 * WN + j * 32 + l32;
-        b[j] = floatx2{bimg[(4 * g + h) * C::kBStrideN + col],
-                       bimg[(4 * g + 2 + h) * C::kBStrideN + col]};
-      }
+  auto read_a = [&](int g, int i) {
+    return *reinterpret_cast<const floatx2*>(
+        aimg + ((2 * g + h) * C::BM + kswz(wm * 32 * WM + i * 32 + l32, g)) * 2);
+  };
+  auto read_b = [&](int g, int j) -> floatx2 {
+    if constexpr (kBKMajor) {
+      return *reinterpret_cast<const floatx2*>(
+          bimg + ((2 * g + h) * C::BN + kswz(wn * 32 * WN + j * 32 + l32, g)) * 2);
+    } else {
+      const int col = wn * 32 * WN + j * 32 + l32;
+      return floatx2{bimg[(4 * g + h) * C::kBStrideN + col],
+                     bimg[(4 * g + 2 + h) * C::kBStrideN + col]};
     }
+  };
+  // Every fragment of the stage read before the first MFMA: read next to its MFMA pair (as
+  // the compiler schedules a per-group loop), each group's LDS latency sat exposed in front
+  // of the dependent accumulator chain -- 6 waits per 16 MFMAs in the ISA, 0.41 MFMA busy
+  // on 1024 x 7^2 x 1024 at micro-batch 40 (profiles/r4/pmc).  One wait per stage instead.
+  // (Not for the 8-wave 128 x 128 tile: the extra fragment registers would pass the 128
+  // that its two workgroups per CU allow.)
+  constexpr bool kFirst = kMfmaReadsFirst && CFG != 1;
+  if constexpr (kFirst) {
+    floatx2 a[G][WM], b[G][WN];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int g = 0; g < G; ++g) {
 #pragma unroll
-      for (int i = 0; i < WM; ++i)
+      for (int i = 0; i < WM; ++i) a[g][i] = read_a(g, i);
 #pragma unroll
-        for (int j = 0; j < WN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < WN; ++j) b[g][j] = read_b(g, j);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i][s], b[g][j][s], acc[i][j],
+                                                             0, 0, 0);
+  } else {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      floatx2 a[WM], b[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) a[i] = read_a(g, i);
+#pragma unroll
+      for (int j = 0; j < WN; ++j) b[j] = read_b(g, j);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+    }
   }
 }
 
