@@ -145,6 +145,9 @@ struct Cfg {
   static constexpr int TM = TILE == 0 ? 1 : 2;   // 32 x 32 MFMA tiles per wave (rows)
   static constexpr int TN = TILE == 2 ? 2 : 1;   // (columns)
   static constexpr int kThreads = 64 * WVM * WVN;
+  // waves per SIMD when the LDS footprint's workgroups per CU are resident (4 x 40 KiB /
+  // 2 x 72 KiB / 1 x 147-160 KiB): the register budget __launch_bounds__ holds them to
+  static constexpr int kWavesPerSimd = CFG == 0 || CFG == 1 ? 4 : (CFG == 2 || CFG == 4 ? 2 : 1);
   static constexpr int BM = WVM * 32 * TM;
   static constexpr int BN = WVN * 32 * TN;
   static constexpr int kAImg = kBK * BM;          // K-major image (one sub-stage)
@@ -218,10 +221,12 @@ __device__ __forceinline__ void store_nmajor(float* img, const floatx4 (&v)[Q], 
 
 // ---- the GEMM core ------------------------------------------------------------------------
 
-template <int CFG, bool kBKMajor>
+// `between(g)` runs after MFMA group g (the two k-steps of k quad g): the main loop issues the
+// next stage's loads from it, pinned there by scheduling barriers.
+template <int CFG, bool kBKMajor, typename Between>
 __device__ __forceinline__ void mfma_stage(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG>::TN],
                                            const float* aimg, const float* bimg, int lane, int wm,
-                                           int wn) {
+                                           int wn, Between&& between) {
   using C = Cfg<CFG>;
   constexpr int WM = C::TM, WN = C::TN, G = kBK / 4;
   const int h = lane >> 5, l32 = lane & 31;
@@ -257,7 +262,7 @@ __device__ __forceinline__ void mfma_stage(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g) {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -266,6 +271,8 @@ __device__ __forceinline__ void mfma_stage(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG
           for (int j = 0; j < WN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][i][s], b[g][j][s], acc[i][j],
                                                              0, 0, 0);
+      between(g);
+    }
   } else {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -282,6 +289,7 @@ __device__ __forceinline__ void mfma_stage(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG
           for (int j = 0; j < WN; ++j)
             acc[i][j] =
                 __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+      between(g);
     }
   }
 }
@@ -338,7 +346,7 @@ __device__ __forceinline__ Col make_col(const Geo& g, int j, int N) {
 }
 
 template <int MODE, int CFG, bool kPlain>
-__global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
+__global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void conv_gemm_kernel(
     const float* __restrict__ a_src, const float* __restrict__ b_src,
     const float* __restrict__ x_mask, float* __restrict__ out, float* __restrict__ part_mean,
     float* __restrict__ part_m2, Geo g, int M, int N, int K, int k_chunk, int64_t split_stride,
@@ -392,189 +400,182 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
     for (int e = 0; e < 4; ++e) col[e] = make_col<MODE, kPlain>(g, jq + cstep * e, N);
   }
 
+  // Operand loads, one 16-byte quad per call (unit i of this thread's kAQuads / kRB), so the
+  // main loop can spread a stage's loads between the MFMAs of the previous stage.  Tail
+  // handling is by buffer offsets past the end (kOOB reads 0) selected per quad wherever the
+  // quad layout allows it (K a multiple of 4; planes of 4k pixels), not by divergent
+  // branches: those split the unit into basic blocks with exec-mask juggling around every
+  // quad.
+  const bool k4 = (K & 3) == 0;  // (then k_end is too: k quads never straddle it)
   // A: K-major rows (tid >> 3) + (threads / 8) i, k quad (tid & 7)
-  auto load_a = [&](int k0, floatx4 (&ra)[C::kAQuads]) {
+  auto load_a = [&](int k0, int i) -> floatx4 {
     const int k = k0 + 4 * (tid & 7);
-#pragma unroll
-    for (int i = 0; i < C::kAQuads; ++i) {
-      const int row = m0 + (tid >> 3) + (kThreads / 8) * i;
-      if constexpr (MODE == kFwd) {
-        // W[co][ci*T + t], row-major
-        if (row < M && k + 3 < k_end && (K & 3) == 0) {
-          ra[i] = bload4(ar, static_cast<uint32_t>((row * K + k) * 4));
+    const int row = m0 + (tid >> 3) + (kThreads / 8) * i;
+    floatx4 v;
+    if constexpr (MODE == kFwd || MODE == kBwdData) {
+      // forward W[co][ci*T + t] / transposed weight [ci][co*T]: K-contiguous rows
+      if (MODE == kFwd || g.a_t) {
+        if (k4) {
+          v = bload4(ar, row < M && k < k_end ? static_cast<uint32_t>((row * K + k) * 4)
+                                              : kOOB);
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            ra[i][e] = bload(ar, row < M && k + e < k_end
-                                     ? static_cast<uint32_t>((row * K + k + e) * 4) : kOOB);
+            v[e] = bload(ar, row < M && k + e < k_end
+                                 ? static_cast<uint32_t>((row * K + k + e) * 4) : kOOB);
         }
-      } else if constexpr (MODE == kBwdData) {
-        if (g.a_t) {  // transposed weight [ci][co*T]: K-contiguous rows, like the forward
-          if (row < M && k + 3 < k_end && (K & 3) == 0) {
-            ra[i] = bload4(ar, static_cast<uint32_t>((row * K + k) * 4));
-          } else {
+        return v;
+      }
+      // A[ci][co*T + t] = W[co][ci][t]: gathered from the untransposed weight (L2)
+      const int T = g.taps;
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              ra[i][e] = bload(ar, row < M && k + e < k_end
-                                       ? static_cast<uint32_t>((row * K + k + e) * 4) : kOOB);
-          }
-          continue;
+      for (int e = 0; e < 4; ++e) {
+        uint32_t off = kOOB;
+        if (row < M && k + e < k_end) {
+          const int co = T == 1 ? k + e : (k + e) / T;
+          const int t = k + e - co * T;
+          off = static_cast<uint32_t>(((co * g.ci + row) * T + t) * 4);
         }
-        // A[ci][co*T + t] = W[co][ci][t]: gathered from the untransposed weight (L2)
-        const int T = g.taps;
+        v[e] = bload(ar, off);
+      }
+      return v;
+    } else {
+      // dZ rows: A[co][k = (n, p)]
+      if (quads) {  // K = n * hw_out, 4 | hw_out: a k quad is one image's 4 pixels
+        const int n = g.fd_hwo.div(k), p = k - n * hw_out;
+        v = bload4(ar, row < M && k < k_end
+                           ? static_cast<uint32_t>(
+                                 ((n * g.co_total + g.co_off + row) * hw_out + p) * 4)
+                           : kOOB);
+      } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           uint32_t off = kOOB;
           if (row < M && k + e < k_end) {
-            const int co = T == 1 ? k + e : (k + e) / T;
-            const int t = k + e - co * T;
-            off = static_cast<uint32_t>(((co * g.ci + row) * T + t) * 4);
+            const int n = g.fd_hwo.div(k + e), p = k + e - n * hw_out;
+            off = static_cast<uint32_t>(((n * g.co_total + g.co_off + row) * hw_out + p) * 4);
           }
-          ra[i][e] = bload(ar, off);
-        }
-      } else {
-        // dZ rows: A[co][k = (n, p)]
-        if (quads && row < M && k + 3 < k_end) {
-          const int n = g.fd_hwo.div(k), p = k - n * hw_out;
-          ra[i] = bload4(ar, static_cast<uint32_t>(
-                                 ((n * g.co_total + g.co_off + row) * hw_out + p) * 4));
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            uint32_t off = kOOB;
-            if (row < M && k + e < k_end) {
-              const int n = g.fd_hwo.div(k + e), p = k + e - n * hw_out;
-              off = static_cast<uint32_t>(((n * g.co_total + g.co_off + row) * hw_out + p) * 4);
-            }
-            ra[i][e] = bload(ar, off);
-          }
+          v[e] = bload(ar, off);
         }
       }
+      return v;
     }
   };
 
-  auto load_b = [&](int k0, floatx4 (&rb)[kRB]) {
+  auto load_b = [&](int k0, int i) -> floatx4 {
+    floatx4 v;
     if constexpr (MODE == kFwd) {
-      // relu(X) taps: B[k = (ci, t)][j = output pixel]
-#pragma unroll
-      for (int i = 0; i < C::kBQuadsN; ++i) {
-        const int k = k0 + tid / QPR + (kThreads / QPR) * i;
-        const bool kin = k < k_end;
-        floatx4 v;
-        if constexpr (kPlain) {
-          const int coff = k * hw_in;
-          if (quads && col[3].ok && kin) {
-            v = bload4(br, static_cast<uint32_t>((col[0].base + coff) * 4));
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              v[e] = bload(br, col[e].ok && kin
-                                   ? static_cast<uint32_t>((col[e].base + coff) * 4) : kOOB);
-          }
+      // relu(X) taps: B[k = (ci, t)][j = output pixel]  (ReLU at store time: using the value
+      // here would wait for the load)
+      const int k = k0 + tid / QPR + (kThreads / QPR) * i;
+      const bool kin = k < k_end;
+      if constexpr (kPlain) {
+        const int coff = k * hw_in;
+        if (quads) {  // 4 | N: a column quad is valid or not as a whole
+          v = bload4(br, col[0].ok && kin ? static_cast<uint32_t>((col[0].base + coff) * 4)
+                                          : kOOB);
         } else {
-          const int ci = g.fd_taps.div(k), t = k - ci * g.taps;
-          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int yi = col[e].y + th, xi = col[e].x + tw;
-            const bool ok = col[e].ok && kin && yi >= 0 && yi < g.h && xi >= 0 && xi < g.w;
-            v[e] = bload(br, ok ? static_cast<uint32_t>(
-                                      (col[e].base + (ci * g.h + yi) * g.w + xi) * 4) : kOOB);
-          }
+          for (int e = 0; e < 4; ++e)
+            v[e] = bload(br, col[e].ok && kin
+                                 ? static_cast<uint32_t>((col[e].base + coff) * 4) : kOOB);
         }
-        rb[i] = v;  // (ReLU at store time: using the value here would wait for the load)
+      } else {
+        const int ci = g.fd_taps.div(k), t = k - ci * g.taps;
+        const int th = g.fd_kw.div(t), tw = t - th * g.kw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int yi = col[e].y + th, xi = col[e].x + tw;
+          const bool ok = col[e].ok && kin && yi >= 0 && yi < g.h && xi >= 0 && xi < g.w;
+          v[e] = bload(br, ok ? static_cast<uint32_t>(
+                                    (col[e].base + (ci * g.h + yi) * g.w + xi) * 4) : kOOB);
+        }
       }
     } else if constexpr (MODE == kBwdData) {
       // dZ taps: B[k = (co, t)][j = pixel]
+      const int k = k0 + tid / QPR + (kThreads / QPR) * i;
+      const bool kin = k < k_end;
+      if (g.phase) {
+        // dZ taps of this phase: dense, stride 1 (the decomposition removed the holes)
+        const int co = g.fd_taps.div(k), t = k - co * g.taps;
+        const int th = g.fd_kw.div(t), tw = t - th * g.kw;
 #pragma unroll
-      for (int i = 0; i < C::kBQuadsN; ++i) {
-        const int k = k0 + tid / QPR + (kThreads / QPR) * i;
-        const bool kin = k < k_end;
-        floatx4 v;
-        if (g.phase) {
-          // dZ taps of this phase: dense, stride 1 (the decomposition removed the holes)
-          const int co = g.fd_taps.div(k), t = k - co * g.taps;
-          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
+        for (int e = 0; e < 4; ++e) {
+          const int y = col[e].y - th, x = col[e].x - tw;
+          const bool ok = col[e].ok && kin && y >= 0 && y < g.zh && x >= 0 && x < g.zw;
+          v[e] = bload(br, ok ? static_cast<uint32_t>(
+                                    (col[e].base + (co * g.zh + y) * g.zw + x) * 4) : kOOB);
+        }
+      } else if (kPlain || g.scatter) {
+        const int coff = k * hw_out;
+        if ((hw_out & 3) == 0) {  // adjacent column quads (no spread), valid as a whole
+          v = bload4(br, col[0].ok && kin ? static_cast<uint32_t>((col[0].base + coff) * 4)
+                                          : kOOB);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = bload(br, col[e].ok && kin
+                                 ? static_cast<uint32_t>((col[e].base + coff) * 4) : kOOB);
+        }
+      } else {
+        // output pixel * stride = input pixel + pad - tap - offset (stride holes: none)
+        const int co = g.fd_taps.div(k), t = k - co * g.taps;
+        const int th = g.fd_kw.div(t), tw = t - th * g.kw;
+        if (g.sh == 1 && g.sw == 1) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int y = col[e].y - th, x = col[e].x - tw;
-            const bool ok = col[e].ok && kin && y >= 0 && y < g.zh && x >= 0 && x < g.zw;
+            const bool ok = col[e].ok && kin && y >= 0 && y < g.ho && x >= 0 && x < g.wo;
             v[e] = bload(br, ok ? static_cast<uint32_t>(
-                                      (col[e].base + (co * g.zh + y) * g.zw + x) * 4) : kOOB);
-          }
-        } else if (kPlain || g.scatter) {
-          const int coff = k * hw_out;
-          if (((hw_out & 3) == 0) && col[3].ok && kin) {
-            v = bload4(br, static_cast<uint32_t>((col[0].base + coff) * 4));
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              v[e] = bload(br, col[e].ok && kin
-                                   ? static_cast<uint32_t>((col[e].base + coff) * 4) : kOOB);
+                                      (col[e].base + co * hw_out + y * g.wo + x) * 4) : kOOB);
           }
         } else {
-          // output pixel * stride = input pixel + pad - tap - offset (stride holes: none)
-          const int co = g.fd_taps.div(k), t = k - co * g.taps;
-          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
-          if (g.sh == 1 && g.sw == 1) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int y = col[e].y - th, x = col[e].x - tw;
-              const bool ok = col[e].ok && kin && y >= 0 && y < g.ho && x >= 0 && x < g.wo;
-              v[e] = bload(br, ok ? static_cast<uint32_t>(
-                                        (col[e].base + co * hw_out + y * g.wo + x) * 4) : kOOB);
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int ys = col[e].y - th, xs = col[e].x - tw;
-              const int y = ys / g.sh, x = xs / g.sw;
-              const bool ok = col[e].ok && kin && ys >= 0 && xs >= 0 && y * g.sh == ys &&
-                              x * g.sw == xs && y < g.ho && x < g.wo;
-              v[e] = bload(br, ok ? static_cast<uint32_t>(
-                                        (col[e].base + co * hw_out + y * g.wo + x) * 4) : kOOB);
-            }
-          }
-        }
-        rb[i] = v;
-      }
-    } else {
-      // relu(X) taps: B[k = output pixel (n, p)][j = (ci, t)]
-      const int k = k0 + 4 * (tid & 7);
-#pragma unroll
-      for (int i = 0; i < C::kBQuadsK; ++i) {
-        const int j = n0 + (tid >> 3) + (kThreads / 8) * i;
-        const int ci = g.fd_taps.div(j), t = j - ci * g.taps;
-        floatx4 v;
-        if (quads && j < N && k + 3 < k_end) {
-          const int n = g.fd_hwo.div(k), p = k - n * hw_out;
-          v = bload4(br, static_cast<uint32_t>(((n * g.ci + ci) * hw_in + p) * 4));
-        } else {
-          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            uint32_t off = kOOB;
-            if (j < N && k + e < k_end) {
-              const int n = g.fd_hwo.div(k + e), p = k + e - n * hw_out;
-              const int y = g.fd_wo.div(p), x = p - y * g.wo;
-              const int yi = y * g.sh - g.ph + th + g.oh, xi = x * g.sw - g.pw + tw + g.ow;
-              if (yi >= 0 && yi < g.h && xi >= 0 && xi < g.w)
-                off = static_cast<uint32_t>((((n * g.ci + ci) * g.h + yi) * g.w + xi) * 4);
-            }
-            v[e] = bload(br, off);
+            const int ys = col[e].y - th, xs = col[e].x - tw;
+            const int y = ys / g.sh, x = xs / g.sw;
+            const bool ok = col[e].ok && kin && ys >= 0 && xs >= 0 && y * g.sh == ys &&
+                            x * g.sw == xs && y < g.ho && x < g.wo;
+            v[e] = bload(br, ok ? static_cast<uint32_t>(
+                                      (col[e].base + co * hw_out + y * g.wo + x) * 4) : kOOB);
           }
         }
-        rb[i] = v;  // (ReLU at store time)
+      }
+    } else {
+      // relu(X) taps: B[k = output pixel (n, p)][j = (ci, t)]  (ReLU at store time)
+      const int k = k0 + 4 * (tid & 7);
+      const int j = n0 + (tid >> 3) + (kThreads / 8) * i;
+      const int ci = g.fd_taps.div(j), t = j - ci * g.taps;
+      if (quads) {  // 1x1 stride 1 over planes of 4k pixels: a k quad is 4 adjacent pixels
+        const int n = g.fd_hwo.div(k), p = k - n * hw_out;
+        v = bload4(br, j < N && k < k_end
+                           ? static_cast<uint32_t>(((n * g.ci + ci) * hw_in + p) * 4) : kOOB);
+      } else {
+        const int th = g.fd_kw.div(t), tw = t - th * g.kw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t off = kOOB;
+          if (j < N && k + e < k_end) {
+            const int n = g.fd_hwo.div(k + e), p = k + e - n * hw_out;
+            const int y = g.fd_wo.div(p), x = p - y * g.wo;
+            const int yi = y * g.sh - g.ph + th + g.oh, xi = x * g.sw - g.pw + tw + g.ow;
+            if (yi >= 0 && yi < g.h && xi >= 0 && xi < g.w)
+              off = static_cast<uint32_t>((((n * g.ci + ci) * g.h + yi) * g.w + xi) * 4);
+          }
+          v[e] = bload(br, off);
+        }
       }
     }
+    return v;
   };
 
-  auto load_stage = [&](int k0) {
-#pragma unroll
-    for (int u = 0; u < SUB; ++u) {
-      load_a(k0 + u * kBK, ra[u]);
-      load_b(k0 + u * kBK, rb[u]);
-    }
+  // load unit q of sub-stage u (A quads first, then B quads) for the stage at k0
+  constexpr int kUnits = C::kAQuads + kRB;
+  auto load_unit = [&](int k0, int u, int q) {
+    if (q < C::kAQuads)
+      ra[u][q] = load_a(k0 + u * kBK, q);
+    else
+      rb[u][q - C::kAQuads] = load_b(k0 + u * kBK, q - C::kAQuads);
   };
   // The forward / weight-gradient ReLU of X is applied here, after the stage's MFMAs:
   // applied in load_b it made every prefetch wait for its own loads (vmcnt(0) right
@@ -611,19 +612,53 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads) void conv_gemm_kernel(
   constexpr int kStageK = kBK * SUB;
   const int stages = (k_end - k_begin + kStageK - 1) / kStageK;
   if (stages > 0) {
-    load_stage(k_begin);
+#pragma unroll
+    for (int u = 0; u < SUB; ++u)
+#pragma unroll
+      for (int q = 0; q < kUnits; ++q) load_unit(k_begin, u, q);
     store_stage(0);
     __syncthreads();
-    for (int s = 0; s < stages; ++s) {
+    // (the last stage is peeled off: with a `more` test inside the loop the compiler's
+    // path-insensitive wait analysis assumed loads still in flight at the loop head and
+    // put a vmcnt(0) in front of the interleaved loads)
+    for (int s = 0; s + 1 < stages; ++s) {
       const int buf = s & 1;
-      const bool more = s + 1 < stages;
-      if (more) load_stage(k_begin + (s + 1) * kStageK);
+      const int k_next = k_begin + (s + 1) * kStageK;
+      // Sub-stage u's MFMA groups carry the next stage's sub-stage u loads: unit q after
+      // group q * G / kUnits, so the address arithmetic, exec masks and load issue of a
+      // unit run while the matrix core works through the dependent MFMA chain instead of
+      // in front of it (~200 instructions per stage serialised with 1024 MFMA cycles:
+      // 0.41-0.47 MFMA busy on the AmoebaNet 7^2 / 14^2 shapes, profiles/r4/pmc).
+      // (The 8-wave 128 x 128 tile keeps its loads in front: interleaved, its unit temporaries
+      // pass the 128 registers of two workgroups per CU and spill.)
+      constexpr bool kInterleave = CFG != 1;
+      if constexpr (!kInterleave) {
+#pragma unroll
+        for (int u = 0; u < SUB; ++u)
+#pragma unroll
+          for (int q = 0; q < kUnits; ++q) load_unit(k_next, u, q);
+      }
 #pragma unroll
       for (int u = 0; u < SUB; ++u)
-        mfma_stage<CFG, kBK_major>(acc, aimg(buf, u), bimg(buf, u), lane, wm, wn);
-      if (more) store_stage(buf ^ 1);
+        mfma_stage<CFG, kBK_major>(acc, aimg(buf, u), bimg(buf, u), lane, wm, wn,
+                                   [&](int grp) {
+                                     if constexpr (kInterleave) {
+#pragma unroll
+                                       for (int q = 0; q < kUnits; ++q)
+                                         if (q * (kBK / 4) / kUnits == grp) {
+                                           load_unit(k_next, u, q);
+                                           __builtin_amdgcn_sched_barrier(0);
+                                         }
+                                     }
+                                   });
+      store_stage(buf ^ 1);
       __syncthreads();
     }
+#pragma unroll
+    for (int u = 0; u < SUB; ++u)
+      mfma_stage<CFG, kBK_major>(acc, aimg((stages - 1) & 1, u), bimg((stages - 1) & 1, u),
+                                 lane, wm, wn, [](int) {});
+    __syncthreads();
   }
 
   // ---- epilogues ----
