@@ -624,10 +624,9 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
     for (int s = 0; s + 1 < stages; ++s) {
       const int buf = s & 1;
       const int k_next = k_begin + (s + 1) * kStageK;
-      // Sub-stage u's MFMA groups carry the next stage's sub-stage u loads: unit q after
-      // group q * G / kUnits, so the address arithmetic, exec masks and load issue of a
-      // unit run while the matrix core works through the dependent MFMA chain instead of
-      // in front of it (~200 instructions per stage serialised with 1024 MFMA cycles:
+      // The MFMA groups carry the next stage's loads, so the address arithmetic, exec masks
+      // and load issue of a unit run while the matrix core works through the dependent MFMA
+      // chain instead of in front of it (~200 instructions per stage serialised with 1024 MFMA cycles:
       // 0.41-0.47 MFMA busy on the AmoebaNet 7^2 / 14^2 shapes, profiles/r4/pmc).
       // (The 8-wave 128 x 128 tile keeps its loads in front: interleaved, its unit temporaries
       // pass the 128 registers of two workgroups per CU and spill.)
@@ -638,6 +637,9 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
 #pragma unroll
           for (int q = 0; q < kUnits; ++q) load_unit(k_next, u, q);
       }
+      // sub-stage u's MFMA groups carry the next stage's sub-stage u loads, spread over the
+      // first half of the groups: each unit then keeps half a sub-stage of MFMAs to cover
+      // its latency before store_stage waits for it
 #pragma unroll
       for (int u = 0; u < SUB; ++u)
         mfma_stage<CFG, kBK_major>(acc, aimg(buf, u), bimg(buf, u), lane, wm, wn,
@@ -645,7 +647,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
                                      if constexpr (kInterleave) {
 #pragma unroll
                                        for (int q = 0; q < kUnits; ++q)
-                                         if (q * (kBK / 4) / kUnits == grp) {
+                                         if (q * (kBK / 8) / kUnits == grp) {
                                            load_unit(k_next, u, q);
                                            __builtin_amdgcn_sched_barrier(0);
                                          }
