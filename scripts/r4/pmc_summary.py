@@ -9,7 +9,8 @@ import csv
 import os
 import sys
 
-print('| probe | kernel | dispatches | MFMA busy | wait / wave cycles | LDS bank conflicts per dispatch |')
+print('| probe | kernel | dispatches | MFMA busy | wait / wave cycles |'
+      ' LDS bank conflicts per dispatch |')
 print('|---|---|---:|---:|---:|---:|')
 for path in sys.argv[1:]:
     agg = collections.defaultdict(lambda: collections.defaultdict(float))

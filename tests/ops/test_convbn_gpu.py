@@ -67,7 +67,7 @@ def _geo(kh, kw, stride, pad, offset):
     return [kh, kw, stride, stride, ph, pw, offset, offset]
 
 
-@pytest.fixture(params=[-1, 0, 1, 2, 3, 4, 5], ids=['tuned'] + [f'cfg{i}' for i in range(6)])
+@pytest.fixture(params=[-1, 0, 1, 2, 3, 4, 5, 6], ids=['tuned'] + [f'cfg{i}' for i in range(7)])
 def tile_cfg(request):
     """Every tile configuration of the implicit-GEMM kernel, then the tuned plans."""
     ops().conv_gemm_force_cfg(request.param)
@@ -256,13 +256,16 @@ def test_gemm_conv2d_module_matches_conv2d():
 @pytest.mark.parametrize('stride', [1, 2])
 @pytest.mark.parametrize('hw', [(7, 7), (12, 9), (1, 1), (2, 3), (120, 121)])
 @pytest.mark.parametrize('with_add', [False, True])
-def test_avgpool3_matches_fp64(stride, hw, with_add):
+@pytest.mark.parametrize('nc', [(3, 5), (7, 37)])
+def test_avgpool3_matches_fp64(stride, hw, with_add, nc):
+    """Every pool kernel: <= 64-pixel planes (four per wave, several waves per workgroup,
+    a partial last workgroup), one plane per workgroup, thread per output."""
     from torchgpipe_amd.ops.pool import AvgPool3x3
     _ext.require()
     torch.manual_seed(0)
-    x = torch.randn(3, 5, *hw, device='cuda', requires_grad=True)
+    x = torch.randn(*nc, *hw, device='cuda', requires_grad=True)
     ho, wo = (hw[0] - 1) // stride + 1, (hw[1] - 1) // stride + 1
-    add = torch.randn(3, 5, ho, wo, device='cuda', requires_grad=True) if with_add else None
+    add = torch.randn(*nc, ho, wo, device='cuda', requires_grad=True) if with_add else None
     pool = AvgPool3x3(stride)
     y = pool(x, add)
     x64 = x.detach().double().requires_grad_()

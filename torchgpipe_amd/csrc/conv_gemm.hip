@@ -63,6 +63,7 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kBK = 32;
+constexpr int kConvGemmCfgs = 7;  // tile configurations (Cfg<0..6>)
 // mfma_stage: all of a stage's LDS fragment reads ahead of its MFMAs (see there)
 constexpr bool kMfmaReadsFirst = true;
 constexpr uint32_t kOOB = 0x7ffffff0u;  // buffer offset past every tensor (< 2 GiB)
@@ -133,13 +134,13 @@ struct Geo {
 // from one workgroup, so one wave's MFMAs cover the other's LDS reads and barrier;
 // CFG 2: 128 x 128 block, 4 waves (2 x 2) of 64 x 64 (2 x 2 tiles): each A / B fragment
 // read from LDS feeds two MFMAs, half the LDS traffic per MFMA of CFG 1.
-// CFG 3 / 4 / 5: CFG 0 / 1 / 2 with SUB = 4 / 2 / 2 BK-deep sub-stages per barrier and
+// CFG 3 / 4 / 5 / 6: CFG 0 / 1 / 2 / 0 with SUB = 4 / 2 / 2 / 2 BK-deep sub-stages per barrier and
 // per prefetch: a small grid (one workgroup per CU) then keeps SUB x more loads in flight
 // per wave -- each stage's MFMAs cover one global-load latency instead of a fraction.
 template <int CFG>
 struct Cfg {
   static constexpr int TILE = CFG % 3;
-  static constexpr int SUB = CFG < 3 ? 1 : (CFG == 3 ? 4 : 2);
+  static constexpr int SUB = CFG < 3 ? 1 : (CFG == 3 ? 4 : 2);  // (CFG 6: 64 x 64, 2 x 80 KiB)
   static constexpr int WVM = 2;
   static constexpr int WVN = TILE == 1 ? 4 : 2;
   static constexpr int TM = TILE == 0 ? 1 : 2;   // 32 x 32 MFMA tiles per wave (rows)
@@ -147,7 +148,8 @@ struct Cfg {
   static constexpr int kThreads = 64 * WVM * WVN;
   // waves per SIMD when the LDS footprint's workgroups per CU are resident (4 x 40 KiB /
   // 2 x 72 KiB / 1 x 147-160 KiB): the register budget __launch_bounds__ holds them to
-  static constexpr int kWavesPerSimd = CFG == 0 || CFG == 1 ? 4 : (CFG == 2 || CFG == 4 ? 2 : 1);
+  static constexpr int kWavesPerSimd =
+      CFG == 0 || CFG == 1 ? 4 : (CFG == 2 || CFG == 4 || CFG == 6 ? 2 : 1);
   static constexpr int BM = WVM * 32 * TM;
   static constexpr int BN = WVN * 32 * TN;
   static constexpr int kAImg = kBK * BM;          // K-major image (one sub-stage)
@@ -959,6 +961,72 @@ __global__ __launch_bounds__(256) void split_reduce_stats_kernel(
   }
 }
 
+// Planes of <= 64 pixels (AmoebaNet's 7^2): one wave per plane spent its life on one
+// chain of `splits` dependent loads (58 us per call for 40 k planes at micro-batch 40 in
+// the stage-6 trace, profiles/r4/rocprof/).  Here a wave takes 4 planes and loads two splits
+// of all of them before adding -- 8 loads in flight -- summing each plane in split order
+// (bitwise the sums of the kernel above), then the four planes' statistics.
+__global__ __launch_bounds__(256) void split_reduce_stats_small_kernel(
+    const float* __restrict__ ws, int splits, int64_t stride, float* __restrict__ z,
+    float* __restrict__ pm, float* __restrict__ pm2, int64_t planes, int c, int hw, int c_total,
+    int c_off) {
+  constexpr int P = 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t p0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * P;
+  if (p0 >= planes) return;
+  bool ok[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) ok[k] = lane < hw && p0 + k < planes;
+  float v[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) v[k] = 0.f;
+  const float* src = ws + p0 * hw + lane;
+  int s = 0;
+  for (; s + 1 < splits; s += 2) {
+    float a[P], b[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      a[k] = ok[k] ? src[s * stride + k * hw] : 0.f;
+      b[k] = ok[k] ? src[(s + 1) * stride + k * hw] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = (v[k] + a[k]) + b[k];
+  }
+  if (s < splits) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] += ok[k] ? src[s * stride + k * hw] : 0.f;
+  }
+  float sum[P], m2[P], mean[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) sum[k] = ok[k] ? v[k] : 0.f;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < P; ++k) sum[k] += __shfl_xor(sum[k], off);
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    mean[k] = sum[k] / static_cast<float>(hw);
+    const float d = v[k] - mean[k];
+    m2[k] = ok[k] ? d * d : 0.f;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < P; ++k) m2[k] += __shfl_xor(m2[k], off);
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    if (p0 + k >= planes) break;
+    const int64_t plane = p0 + k;
+    const int64_t img = plane / c;
+    const int ch = static_cast<int>(plane - img * c);
+    if (ok[k]) z[(img * c_total + c_off + ch) * hw + lane] = v[k];
+    if (lane == 0) {
+      pm[img * c_total + c_off + ch] = mean[k];
+      pm2[img * c_total + c_off + ch] = m2[k];
+    }
+  }
+}
+
 void launch_split_reduce_stats(const float* ws, int splits, int64_t stride, float* z, float* pm,
                                float* pm2, int64_t n, int c, int hw, int c_total, int c_off,
                                hipStream_t stream) {
@@ -969,8 +1037,11 @@ void launch_split_reduce_stats(const float* ws, int splits, int64_t stride, floa
     hipLaunchKernelGGL(kern, grid, block, 0, stream, ws, splits, stride, z, pm, pm2, planes, c, hw,
                        c_total, c_off);
   };
-  if (hw <= 64) go(split_reduce_stats_kernel<1>);
-  else if (hw <= 256) go(split_reduce_stats_kernel<4>);
+  if (hw <= 64) {
+    hipLaunchKernelGGL(split_reduce_stats_small_kernel,
+                       dim3(static_cast<unsigned>((planes + 15) / 16)), block, 0, stream, ws,
+                       splits, stride, z, pm, pm2, planes, c, hw, c_total, c_off);
+  } else if (hw <= 256) go(split_reduce_stats_kernel<4>);
   else if (hw <= 1024) go(split_reduce_stats_kernel<16>);
   else go(split_reduce_stats_kernel<0>);
 }
@@ -1151,7 +1222,7 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
   gemm_dims(mode, g, M, N, K);
   std::vector<ConvGemmPlan> out;
   const int max_split = std::max(1, K / (4 * kBK));
-  for (int cfg = 0; cfg < 6; ++cfg) {
+  for (int cfg = 0; cfg < kConvGemmCfgs; ++cfg) {
     const int64_t tiles = cfg % 3 ? static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128)
                                   : static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
     int last = 0;
@@ -1224,6 +1295,7 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
   using C3 = std::integral_constant<int, 3>;
   using C4 = std::integral_constant<int, 4>;
   using C5 = std::integral_constant<int, 5>;
+  using C6 = std::integral_constant<int, 6>;
   auto by_cfg = [&](auto mode_c, float* p1, float* p2, const float* mask) {
     switch (plan.cfg) {
       case 1: go(mode_c, C1{}, p1, p2, mask); break;
@@ -1231,6 +1303,7 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
       case 3: go(mode_c, C3{}, p1, p2, mask); break;
       case 4: go(mode_c, C4{}, p1, p2, mask); break;
       case 5: go(mode_c, C5{}, p1, p2, mask); break;
+      case 6: go(mode_c, C6{}, p1, p2, mask); break;
       default: go(mode_c, C0{}, p1, p2, mask); break;
     }
   };
@@ -1281,6 +1354,7 @@ void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
     case 3: go(std::integral_constant<int, 3>{}); break;
     case 4: go(std::integral_constant<int, 4>{}); break;
     case 5: go(std::integral_constant<int, 5>{}); break;
+    case 6: go(std::integral_constant<int, 6>{}); break;
     default: go(std::integral_constant<int, 0>{}); break;
   }
 }

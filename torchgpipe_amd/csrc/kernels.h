@@ -176,8 +176,8 @@ std::vector<ConvGemmPhase> conv_gemm_phases(const ConvGemmGeo& g);
 // splits > 1 needs a workspace of conv_gemm_workspace() floats.
 struct ConvGemmPlan {
   int cfg = 1;           // tiles: 0 = 64 x 64 (4 waves), 1 = 128 x 128 (8 waves),
-                         // 2 = 128 x 128 (4 waves of 2 x 2 MFMA tiles); 3 / 4 / 5 = 0 / 1 /
-                         // 2 with 4 / 2 / 2 BK steps per pipeline stage
+                         // 2 = 128 x 128 (4 waves of 2 x 2 MFMA tiles); 3 / 4 / 5 / 6 = 0 / 1 /
+                         // 2 / 0 with 4 / 2 / 2 / 2 BK steps per pipeline stage
   int splits = 1;        // reduction splits (grid.y), > 1: workspace slices + split_reduce
   int col_width = 128;   // forward: columns per statistics block
   int col_blocks = 0;    // forward: statistics blocks

@@ -143,6 +143,88 @@ __global__ __launch_bounds__(256) void avgpool3_bwd_plane_kernel(const float* __
   }
 }
 
+// Planes of <= 64 pixels (AmoebaNet's 7^2 cells): one workgroup per plane left each
+// workgroup a single wave with one load, one LDS round trip and one store -- a latency chain
+// of a few microseconds, 40 k of them per pool at 40 images x 1024 channels (31 us per
+// pool, profiles/r4/rocprof/).  Here each wave takes kSmallPlanes planes, every lane issuing
+// its pixel's loads of all of them before using any, and a workgroup holds 4 waves.
+constexpr int kSmallPlanes = 4;
+
+__global__ __launch_bounds__(256) void avgpool3_fwd_small_kernel(
+    const float* __restrict__ x, const float* __restrict__ add, float* __restrict__ y,
+    int64_t planes, int h, int w, int ho, int wo, int stride) {
+  __shared__ float pl[4][kSmallPlanes][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int in = h * w, out = ho * wo;
+  const int64_t p0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * kSmallPlanes;
+  float v[kSmallPlanes];
+#pragma unroll
+  for (int k = 0; k < kSmallPlanes; ++k)
+    v[k] = lane < in && p0 + k < planes ? x[(p0 + k) * in + lane] : 0.f;
+#pragma unroll
+  for (int k = 0; k < kSmallPlanes; ++k) pl[wave][k][lane] = v[k];
+  __syncthreads();
+  if (lane >= out) return;
+  const int oy = lane / wo, ox = lane - oy * wo;
+  const int cy = oy * stride, cx = ox * stride;
+  const int y0 = max(cy - 1, 0), y1 = min(cy + 1, h - 1);
+  const int x0 = max(cx - 1, 0), x1 = min(cx + 1, w - 1);
+  const float area = static_cast<float>((y1 - y0 + 1) * (x1 - x0 + 1));
+  float a[kSmallPlanes];
+#pragma unroll
+  for (int k = 0; k < kSmallPlanes; ++k)
+    a[k] = add && p0 + k < planes ? add[(p0 + k) * out + lane] : 0.f;
+#pragma unroll
+  for (int k = 0; k < kSmallPlanes; ++k) {
+    if (p0 + k >= planes) break;
+    float sum = 0.f;
+    for (int yy = y0; yy <= y1; ++yy)
+      for (int xx = x0; xx <= x1; ++xx) sum += pl[wave][k][yy * w + xx];
+    y[(p0 + k) * out + lane] = sum / area + a[k];  // (the plane kernel's arithmetic)
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool3_bwd_small_kernel(
+    const float* __restrict__ dy, float* __restrict__ dx, int64_t planes, int h, int w, int ho,
+    int wo, int stride, int channels, int64_t dy_img) {
+  __shared__ float pl[4][kSmallPlanes][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int in = h * w, out = ho * wo;
+  const int64_t p0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * kSmallPlanes;
+  float g[kSmallPlanes];
+  float area = 1.f;
+  if (lane < out) {
+    const int oy = lane / wo, ox = lane - oy * wo;
+    const int cy = oy * stride, cx = ox * stride;
+    area = static_cast<float>((min(cy + 1, h - 1) - max(cy - 1, 0) + 1) *
+                              (min(cx + 1, w - 1) - max(cx - 1, 0) + 1));
+  }
+#pragma unroll
+  for (int k = 0; k < kSmallPlanes; ++k) {
+    const int64_t plane = p0 + k;
+    g[k] = 0.f;
+    if (lane < out && plane < planes) {
+      const int64_t img = plane / channels;
+      g[k] = dy[img * dy_img + (plane - img * channels) * out + lane];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kSmallPlanes; ++k) pl[wave][k][lane] = g[k] / area;
+  __syncthreads();
+  if (lane >= in) return;
+  const int iy = lane / w, ix = lane - iy * w;
+  const int oy0 = max((iy - 1 + stride - 1) / stride, 0), oy1 = min((iy + 1) / stride, ho - 1);
+  const int ox0 = max((ix - 1 + stride - 1) / stride, 0), ox1 = min((ix + 1) / stride, wo - 1);
+#pragma unroll
+  for (int k = 0; k < kSmallPlanes; ++k) {
+    if (p0 + k >= planes) break;
+    float sum = 0.f;
+    for (int oy = oy0; oy <= oy1; ++oy)
+      for (int ox = ox0; ox <= ox1; ++ox) sum += pl[wave][k][oy * wo + ox];
+    dx[(p0 + k) * in + lane] = sum;
+  }
+}
+
 unsigned plane_threads(int64_t elems) {
   const int64_t t = (elems + 63) / 64 * 64;
   return static_cast<unsigned>(t < 256 ? t : 256);
@@ -158,6 +240,13 @@ unsigned blocks_for(int64_t work) {
 void launch_avgpool3_forward(const float* x, const float* add, float* y, int64_t planes, int h,
                              int w, int stride, hipStream_t stream) {
   const int ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  if (h * w <= 64 && planes < (int64_t{1} << 31)) {
+    const int64_t per_block = 4 * kSmallPlanes;
+    hipLaunchKernelGGL(avgpool3_fwd_small_kernel,
+                       dim3(static_cast<unsigned>((planes + per_block - 1) / per_block)), dim3(256),
+                       0, stream, x, add, y, planes, h, w, ho, wo, stride);
+    return;
+  }
   if (static_cast<int64_t>(h) * w <= kPlaneMax && planes < (int64_t{1} << 31)) {
     hipLaunchKernelGGL(avgpool3_fwd_plane_kernel, dim3(static_cast<unsigned>(planes)),
                        dim3(plane_threads(static_cast<int64_t>(h) * w)),
@@ -178,6 +267,14 @@ void launch_avgpool3_backward(const float* dy, float* dx, int64_t images, int64_
   const int ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
   const int64_t planes = images * channels;
   if (dy_img <= 0) dy_img = channels * ho * wo;
+  if (h * w <= 64 && planes < (int64_t{1} << 31)) {
+    const int64_t per_block = 4 * kSmallPlanes;
+    hipLaunchKernelGGL(avgpool3_bwd_small_kernel,
+                       dim3(static_cast<unsigned>((planes + per_block - 1) / per_block)), dim3(256),
+                       0, stream, dy, dx, planes, h, w, ho, wo, stride, static_cast<int>(channels),
+                       dy_img);
+    return;
+  }
   if (avgpool3_backward_strided_ok(h, w) && planes < (int64_t{1} << 31)) {
     hipLaunchKernelGGL(avgpool3_bwd_plane_kernel, dim3(static_cast<unsigned>(planes)),
                        dim3(plane_threads(static_cast<int64_t>(h) * w)),
