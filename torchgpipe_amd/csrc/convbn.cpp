@@ -62,10 +62,10 @@ void conv_gemm_force_cfg(int64_t cfg, int64_t splits) {
   forced_splits.store(static_cast<int>(splits));
 }
 
-ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* mask, float* out,
-                        float* pm, float* pm2, const ConvGemmGeo& g, bool accumulate,
-                        int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
-                        int64_t out_numel) {
+ConvGemmPlan tuned_plan_raw(int mode, const float* a, const float* b, const float* mask,
+                            float* out, float* pm, float* pm2, const ConvGemmGeo& g,
+                            bool accumulate, int64_t a_bytes, int64_t b_bytes,
+                            const at::Tensor& like, int64_t out_numel) {
   // Timing trials only when asked for (TGPIPE_CG_TUNE=1: benchmarks/tune_plans.py, the
   // offline tuner): a training step never synchronises the host to time candidates, and
   // every rank of a pipeline picks the same plan for the same shape.  A shape missing from
@@ -137,6 +137,28 @@ ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* m
   hipEventDestroy(t1);
   plan_cache[key] = best;
   return best;
+}
+
+// TGPIPE_CG_SPLIT_CAP=N (profiling knob): forward / backward-data plans split the reduction
+// at most N ways (same tile config), so a stage whose cells already run several GEMMs
+// side by side on their streams can trade the split-reduction passes for a less full
+// single-kernel grid.  The plans were timed one kernel at a time.
+ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* mask, float* out,
+                        float* pm, float* pm2, const ConvGemmGeo& g, bool accumulate,
+                        int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
+                        int64_t out_numel) {
+  static const int cap = env_int("TGPIPE_CG_SPLIT_CAP", 0);
+  ConvGemmPlan p = tuned_plan_raw(mode, a, b, mask, out, pm, pm2, g, accumulate, a_bytes,
+                                  b_bytes, like, out_numel);
+  if (cap <= 0 || mode == 2 || p.splits <= cap) return p;
+  ConvGemmPlan pick = p;
+  bool found = false;
+  for (const auto& cand : conv_gemm_candidates(mode, g))
+    if (cand.cfg == p.cfg && cand.splits <= cap && (!found || cand.splits > pick.splits)) {
+      pick = cand;
+      found = true;
+    }
+  return found ? pick : p;
 }
 
 // One line per plan: "mode n ci h w co kh kw sh sw ph pw oh ow co_total cfg splits".

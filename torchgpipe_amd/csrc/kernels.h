@@ -163,6 +163,8 @@ struct ConvGemmPhase {
   int th0, tw0;
 };
 bool conv_gemm_phased(const ConvGemmGeo& g);
+// Integer environment setting (conv_gemm.hip): `fallback` when unset or empty.
+int env_int(const char* name, int fallback);
 std::vector<ConvGemmPhase> conv_gemm_phases(const ConvGemmGeo& g);
 // mode 0: forward  Z[:, co_off:co_off+co] = conv(relu(X)); a = W[co][ci*kh*kw], b = X;
 //         part_mean / part_m2 (may be null): BatchNorm statistics partials of each output
