@@ -630,9 +630,10 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
       // and load issue of a unit run while the matrix core works through the dependent MFMA
       // chain instead of in front of it (~200 instructions per stage serialised with 1024 MFMA cycles:
       // 0.41-0.47 MFMA busy on the AmoebaNet 7^2 / 14^2 shapes, profiles/r4/pmc).
-      // (The 8-wave 128 x 128 tile keeps its loads in front: interleaved, its unit temporaries
-      // pass the 128 registers of two workgroups per CU and spill.)
-      constexpr bool kInterleave = CFG != 1;
+      // (The 8-wave 128 x 128 tile keeps its loads in front for the gathered forward and
+      // the backward-data: interleaved, their unit temporaries pass the 128 registers of two
+      // workgroups per CU and spill.)
+      constexpr bool kInterleave = CFG != 1 || MODE == kWgrad || (MODE == kFwd && kPlain);
       if constexpr (!kInterleave) {
 #pragma unroll
         for (int u = 0; u < SUB; ++u)
