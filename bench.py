@@ -148,7 +148,7 @@ def parse() -> argparse.Namespace:
     p.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
                    help='one-GPU runs: capture the whole step (forward, backward, SGD) into a '
                         'hipGraph after the warm-up and replay it (RNG-free models only: '
-                        'AmoebaNet; parallel/graph.py; auto: on for one-GPU AmoebaNet)')
+                        'AmoebaNet; parallel/graph.py; auto: off -- captured cells instead)')
     p.add_argument('--cell-streams', choices=['auto', 'on', 'off'], default='auto',
                    help="AmoebaNet: run each cell's independent nodes on several HIP streams "
                         '(TGPIPE_CELL_STREAMS, default 3; auto: on)')
@@ -166,7 +166,7 @@ def parse() -> argparse.Namespace:
                    help='replay each micro-batch of a stage as captured hipGraphs, transfers '
                         'issued between them (PipelineStage(graph_cells=True), '
                         'parallel/segments.py; instead of the one-GPU whole-step graph; '
-                        'auto: on for N > 1)')
+                        'auto: on for N > 1 and for AmoebaNet)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -328,7 +328,9 @@ class Bench:
         # enqueue 4-5 % of device time on the U-Net p8 stages instead of 28-46 %
         # (profiles/r4/stage_harness_unet_p8_ref_*.jsonl), so no rank's host sits on the
         # pipeline's critical path
-        graph_cells = choice(args.graph_cells, self.world > 1) and self.gpu
+        # (one GPU: AmoebaNet too -- three-stream cells in per-pass captures, 392.0 vs 389.4
+        # samples/s for the two-stream whole-step graph, profiles/r4/amoeba_n1_graph_modes.md)
+        graph_cells = choice(args.graph_cells, self.world > 1 or kind == 'amoebanet') and self.gpu
         stage = PipelineStage(self.build(kind), balance, device=self.device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
                               overlap_recompute=overlap, overlap_forward=overlap_fwd,
@@ -548,6 +550,7 @@ def main() -> None:
         amoeba['experiment'] = aexp['name']
         amoeba['cell_streams'] = ar['cell_streams']
         amoeba['hipgraph'] = ar['hipgraph']
+        amoeba['graph_cells'] = ar['graph_cells']
         if world == 2:
             d = dict(AMOEBA_N2M1)
             if args.tiny:
