@@ -124,14 +124,25 @@ void copy_segments(at::TensorList srcs, at::TensorList dsts) {
   }
 }
 
-at::Tensor wino_weight(const at::Tensor& w, bool flip) {
+// `out` (optional): an existing transform of the same shape to overwrite in place (the
+// per-step cache refresh, ops/conv.py) instead of a new tensor plus a copy.
+at::Tensor transform_out(const c10::optional<at::Tensor>& out, at::IntArrayRef shape,
+                         const at::Tensor& like) {
+  if (!out.has_value() || !out->defined()) return at::empty(shape, like.options());
+  check_f32_gpu(*out, "out");
+  TORCH_CHECK(out->sizes() == shape && out->device() == like.device(),
+              "out must be the transform's shape on the weight's device");
+  return *out;
+}
+
+at::Tensor wino_weight(const at::Tensor& w, bool flip, const c10::optional<at::Tensor>& out) {
   check_f32_gpu(w, "weight");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "weight must be [K][C][3][3]");
   const int64_t out_channels = flip ? w.size(1) : w.size(0);
   const int64_t red_channels = flip ? w.size(0) : w.size(1);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
-  auto u = at::empty({wino_pad_reduction(red_channels), wino_pad_output(out_channels), 16},
-                     w.options());
+  auto u = transform_out(
+      out, {wino_pad_reduction(red_channels), wino_pad_output(out_channels), 16}, w);
   launch_wino_weight(w.data_ptr<float>(), u.data_ptr<float>(), out_channels, red_channels, flip,
                      stream_of(w));
   return u;
@@ -173,14 +184,14 @@ at::Tensor wino_conv(const at::Tensor& x_in, const at::Tensor& u,
   return y;
 }
 
-at::Tensor wino4_weight(const at::Tensor& w, bool flip) {
+at::Tensor wino4_weight(const at::Tensor& w, bool flip, const c10::optional<at::Tensor>& out) {
   check_f32_gpu(w, "weight");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "weight must be [K][C][3][3]");
   const int64_t out_channels = flip ? w.size(1) : w.size(0);
   const int64_t red_channels = flip ? w.size(0) : w.size(1);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
-  auto u = at::empty({wino4_pad_reduction(red_channels), wino4_pad_output(out_channels), 36},
-                     w.options());
+  auto u = transform_out(
+      out, {wino4_pad_reduction(red_channels), wino4_pad_output(out_channels), 36}, w);
   launch_wino4_weight(w.data_ptr<float>(), u.data_ptr<float>(), out_channels, red_channels, flip,
                       stream_of(w));
   return u;
@@ -307,7 +318,8 @@ at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t 
 
 // Batched-GEMM Winograd F(4x4): weights in the GEMM operand layout (cached per step by
 // ops/conv.py), and the convolution (input transform, 36 GEMMs, output transform).
-at::Tensor bg_weight(const at::Tensor& w, bool flip, int64_t kind) {
+at::Tensor bg_weight(const at::Tensor& w, bool flip, int64_t kind,
+                     const c10::optional<at::Tensor>& out) {
   check_f32_gpu(w, "weight");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "weight must be [K][C][3][3]");
   auto wc = w.contiguous();
@@ -315,8 +327,8 @@ at::Tensor bg_weight(const at::Tensor& w, bool flip, int64_t kind) {
   const int64_t red_channels = flip ? w.size(0) : w.size(1);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
   TORCH_CHECK(kind == 4 || kind == 2, "kind must be 4 (F(4x4)) or 2 (F(2x2))");
-  auto a = at::empty({bg_weight_numel(out_channels, red_channels, static_cast<int>(kind))},
-                     w.options());
+  auto a =
+      transform_out(out, {bg_weight_numel(out_channels, red_channels, static_cast<int>(kind))}, w);
   launch_bg_weight(wc.data_ptr<float>(), a.data_ptr<float>(), out_channels, red_channels, flip,
                    static_cast<int>(kind), stream_of(w));
   return a;
@@ -370,15 +382,15 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("philox_uniform(int n, int seed, int offset, Device device, Tensor? rng=None) -> Tensor");
   m.def("spin(int ns, Device device) -> ()");
   m.def("copy_segments(Tensor[] srcs, Tensor(a!)[] dsts) -> ()");
-  m.def("wino_weight(Tensor w, bool flip) -> Tensor");
+  m.def("wino_weight(Tensor w, bool flip, Tensor? out=None) -> Tensor");
   m.def("wino_wgrad(Tensor x, Tensor dy, int splits=0, int variant=-1, Tensor? into=None) -> Tensor");
   m.def("wino_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
-  m.def("wino4_weight(Tensor w, bool flip) -> Tensor");
+  m.def("wino4_weight(Tensor w, bool flip, Tensor? out=None) -> Tensor");
   m.def("wino4_wgrad(Tensor x, Tensor dy, int splits=0, int variant=0, Tensor? into=None) -> Tensor");
   m.def("wino4_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
-  m.def("bg_weight(Tensor w, bool flip, int kind=4) -> Tensor");
+  m.def("bg_weight(Tensor w, bool flip, int kind=4, Tensor? out=None) -> Tensor");
   m.def("bg_conv(Tensor x, Tensor a, Tensor? bias, int out_channels, int bn=0, int splits=0, "
         "int kind=4, int waves=0, int sub=0) -> Tensor");
 }

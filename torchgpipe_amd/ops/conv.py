@@ -110,19 +110,23 @@ def size_cache_budget(device: torch.device, peak_bytes: int,
     return budget
 
 
-def _derive(weight: Tensor, slot: Tuple) -> Tensor:
+def _derive(weight: Tensor, slot: Tuple, out: Optional[Tensor] = None) -> Tensor:
     """The derived weight of one cache slot: ``(flip, f4, bg)`` Winograd transforms, or
-    ``(True, True, 'T')`` the ``[ci][co][kh][kw]`` transpose."""
+    ``(True, True, 'T')`` the ``[ci][co][kh][kw]`` transpose -- written into ``out`` when
+    given (the per-step refresh: one pass over the transform, not a new one and a copy;
+    U-Net(5,64)'s transforms are ~7 GB per step)."""
     with torch.no_grad():
         w = weight.detach()
         if slot[2] == 'T':
+            if out is not None:
+                return out.copy_(w.transpose(0, 1))
             return w.transpose(0, 1).contiguous()
         ops = _ext.require(weight)
         flip, f4, bg = slot
         w = w.contiguous()
         if bg:
-            return ops.bg_weight(w, flip, bg)
-        return ops.wino4_weight(w, flip) if f4 else ops.wino_weight(w, flip)
+            return ops.bg_weight(w, flip, bg, out)
+        return ops.wino4_weight(w, flip, out) if f4 else ops.wino_weight(w, flip, out)
 
 
 def _ready_event(t: Tensor) -> Optional[Any]:
@@ -197,7 +201,7 @@ class _TransformCache:
             if old[0] != key[0] or old[2] != key[2]:
                 continue  # another weight storage (module surgery): left to the lazy path
             if old != key:
-                u.copy_(_derive(weight, slot))
+                _derive(weight, slot, out=u)
             self._entries[slot] = (key, u, None)
 
     def clear(self) -> None:
