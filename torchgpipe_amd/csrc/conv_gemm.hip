@@ -129,6 +129,17 @@ struct Geo {
   int phase, zh, zw, dy0, dx0;
 };
 
+// All stride phases of one backward-data in one launch (grid.z = phase): what differs
+// between them (conv_gemm_phases), and each phase's slice of the concatenated weights.
+constexpr int kMaxPhases = 4;
+struct PhaseSet {
+  int count;  // 0: an ordinary launch
+  int kh[kMaxPhases], kw[kMaxPhases], ho[kMaxPhases], wo[kMaxPhases];
+  int dy0[kMaxPhases], dx0[kMaxPhases], oh[kMaxPhases], ow[kMaxPhases];
+  int64_t a_off[kMaxPhases], a_bytes[kMaxPhases];
+  FastDiv fd_taps[kMaxPhases], fd_kw[kMaxPhases], fd_hwo[kMaxPhases], fd_wo[kMaxPhases];
+};
+
 // Tile configurations.  CFG 0: 64 x 64 block, 4 waves (2 x 2) of one 32 x 32 MFMA tile;
 // CFG 1: 128 x 128 block, 8 waves (2 x 4) of 64 x 32 (two tiles) -- two waves per SIMD
 // from one workgroup, so one wave's MFMAs cover the other's LDS reads and barrier;
@@ -352,8 +363,30 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
     const float* __restrict__ a_src, const float* __restrict__ b_src,
     const float* __restrict__ x_mask, float* __restrict__ out, float* __restrict__ part_mean,
     float* __restrict__ part_m2, Geo g, int M, int N, int K, int k_chunk, int64_t split_stride,
-    int accumulate, int64_t a_bytes, int64_t b_bytes) {
+    int accumulate, int64_t a_bytes, int64_t b_bytes, PhaseSet ps) {
   using C = Cfg<CFG>;
+  if constexpr (MODE == kBwdData) {
+    if (ps.count > 0) {  // this workgroup's stride phase
+      const int z = blockIdx.z;
+      g.kh = ps.kh[z];
+      g.kw = ps.kw[z];
+      g.taps = g.kh * g.kw;
+      g.ho = ps.ho[z];
+      g.wo = ps.wo[z];
+      g.dy0 = ps.dy0[z];
+      g.dx0 = ps.dx0[z];
+      g.oh = ps.oh[z];
+      g.ow = ps.ow[z];
+      g.fd_taps = ps.fd_taps[z];
+      g.fd_kw = ps.fd_kw[z];
+      g.fd_hwo = ps.fd_hwo[z];
+      g.fd_wo = ps.fd_wo[z];
+      a_src += ps.a_off[z];
+      a_bytes = ps.a_bytes[z];
+      K = g.co * g.taps;
+      N = g.n * g.ho * g.wo;
+    }
+  }
   constexpr int WM = C::TM, WN = C::TN, kThreads = C::kThreads;
   constexpr bool kBK_major = MODE == kWgrad;
   constexpr int kBImg = kBK_major ? C::kBImgK : C::kBImgN;
@@ -375,6 +408,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
   if ((nblk & 7) == 0) bid = (bid & 7) * (nblk >> 3) + (bid >> 3);
   const int mblk = bid % mb_count, nb_i = bid / mb_count;
   const int m0 = mblk * C::BM, n0 = nb_i * C::BN;
+  if (n0 >= N) return;  // (a stride phase smaller than the grid's largest: whole workgroup)
   const int k_begin = blockIdx.y * k_chunk;
   const int k_end = min(K, k_begin + k_chunk);
 
@@ -795,7 +829,8 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
 template <int MODE, int CFG>
 void launch_cfg(const float* a, const float* b, const float* xm, float* out, float* pmean,
                 float* pm2, const Geo& g, int M, int N, int K, int splits, int64_t split_stride,
-                bool accumulate, int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
+                bool accumulate, int64_t a_bytes, int64_t b_bytes, hipStream_t stream,
+                const PhaseSet& ps = PhaseSet{}) {
   using C = Cfg<CFG>;
   const int mb = (M + C::BM - 1) / C::BM, nb = (N + C::BN - 1) / C::BN;
   int k_chunk = (K + splits - 1) / splits;
@@ -803,15 +838,15 @@ void launch_cfg(const float* a, const float* b, const float* xm, float* out, flo
   const int zs = (K + k_chunk - 1) / k_chunk;
   const bool plain = g.taps == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 &&
                      g.oh == 0 && g.ow == 0;
-  const dim3 grid(mb * nb, zs), block(C::kThreads);
+  const dim3 grid(mb * nb, zs, ps.count > 0 ? ps.count : 1), block(C::kThreads);
   if (plain)
     hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, true>), grid, block, 0, stream, a, b, xm,
                        out, pmean, pm2, g, M, N, K, k_chunk, split_stride, accumulate ? 1 : 0,
-                       a_bytes, b_bytes);
+                       a_bytes, b_bytes, ps);
   else
     hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, false>), grid, block, 0, stream, a, b, xm,
                        out, pmean, pm2, g, M, N, K, k_chunk, split_stride, accumulate ? 1 : 0,
-                       a_bytes, b_bytes);
+                       a_bytes, b_bytes, ps);
 }
 
 // Sum of the split partials: ws[s][plane][c][hw] -> out[plane][c_off + c][hw] (c_total
@@ -1348,6 +1383,51 @@ void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
     launch_cfg<kWgrad, decltype(cfg_c)::value>(a, b, nullptr, slab, nullptr, nullptr, g, M, N, K,
                                                plan.splits, stride, accumulate, a_bytes, b_bytes,
                                                stream);
+  };
+  switch (plan.cfg) {
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;
+    case 6: go(std::integral_constant<int, 6>{}); break;
+    default: go(std::integral_constant<int, 0>{}); break;
+  }
+}
+
+void launch_conv_gemm_phases(const float* a, const int64_t* a_off, const float* b,
+                             const float* x_mask, float* out, const ConvGemmPhase* phases,
+                             int count, const ConvGemmPlan& plan, bool accumulate,
+                             int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {
+  if (count <= 0) return;
+  PhaseSet ps{};
+  ps.count = count;
+  int N = 0, K = 0;
+  for (int p = 0; p < count; ++p) {
+    const ConvGemmGeo& q = phases[p].geo;
+    ps.kh[p] = q.kh;
+    ps.kw[p] = q.kw;
+    ps.ho[p] = q.ho;
+    ps.wo[p] = q.wo;
+    ps.dy0[p] = q.dy0;
+    ps.dx0[p] = q.dx0;
+    ps.oh[p] = q.oh;
+    ps.ow[p] = q.ow;
+    ps.a_off[p] = a_off[p];
+    ps.a_bytes[p] = (p + 1 < count ? a_off[p + 1] : a_bytes / 4) * 4 - a_off[p] * 4;
+    ps.fd_taps[p] = make_fastdiv(q.kh * q.kw);
+    ps.fd_kw[p] = make_fastdiv(q.kw);
+    ps.fd_hwo[p] = make_fastdiv(q.ho * q.wo);
+    ps.fd_wo[p] = make_fastdiv(q.wo);
+    N = std::max(N, q.n * q.ho * q.wo);
+    K = std::max(K, q.co * q.kh * q.kw);
+  }
+  Geo g = make_geo(phases[0].geo);
+  g.scatter = 1;
+  const int M = g.ci;
+  auto go = [&](auto cfg_c) {
+    launch_cfg<kBwdData, decltype(cfg_c)::value>(a, b, x_mask, out, nullptr, nullptr, g, M, N, K,
+                                                 1, 0, accumulate, a_bytes, b_bytes, stream, ps);
   };
   switch (plan.cfg) {
     case 1: go(std::integral_constant<int, 1>{}); break;

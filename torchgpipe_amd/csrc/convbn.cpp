@@ -250,7 +250,37 @@ void backward_data_into(const at::Tensor& wt, const at::Tensor& dz, const at::Te
                         at::Tensor& dx, ConvGemmGeo g, bool accumulate) {
   g.a_t = true;
   if (conv_gemm_phased(g)) {
-    for (const auto& ph : conv_gemm_phases(g)) {
+    const std::vector<ConvGemmPhase> phases = conv_gemm_phases(g);
+    static const bool batched = env_int("TGPIPE_CG_PHASE_BATCH", 1) != 0;
+    if (batched && phases.size() > 1 && phases.size() <= kConvGemmMaxPhases) {
+      // one launch for all phases (each is a small grid alone: 124 workgroups per phase on
+      // AmoebaNet's 14^2 reduction-cell shape), their weight slices back to back
+      std::vector<at::Tensor> slices;
+      std::vector<int64_t> offs;
+      int64_t off = 0;
+      size_t big = 0;
+      for (size_t p = 0; p < phases.size(); ++p) {
+        slices.push_back(wt.slice(2, phases[p].th0, c10::nullopt, g.sh)
+                             .slice(3, phases[p].tw0, c10::nullopt, g.sw)
+                             .reshape({-1}));
+        offs.push_back(off);
+        off += slices.back().numel();
+        if (phases[p].geo.kh * phases[p].geo.kw > phases[big].geo.kh * phases[big].geo.kw) big = p;
+      }
+      const at::Tensor wp = at::cat(slices);
+      // the tile config of the phase with the longest reduction (no split: phases scatter)
+      const ConvGemmPlan plan =
+          tuned_plan(1, wp.data_ptr<float>() + offs[big], dz.data_ptr<float>(),
+                     x.data_ptr<float>(), dx.data_ptr<float>(), nullptr, nullptr,
+                     phases[big].geo, accumulate, slices[big].numel() * 4, dz.numel() * 4, x,
+                     x.numel());
+      launch_conv_gemm_phases(wp.data_ptr<float>(), offs.data(), dz.data_ptr<float>(),
+                              x.data_ptr<float>(), dx.data_ptr<float>(), phases.data(),
+                              static_cast<int>(phases.size()), plan, accumulate,
+                              wp.numel() * 4, dz.numel() * 4, cur_stream(x));
+      return;
+    }
+    for (const auto& ph : phases) {
       const at::Tensor wp = wt.slice(2, ph.th0, c10::nullopt, g.sh)
                                 .slice(3, ph.tw0, c10::nullopt, g.sw)
                                 .contiguous();

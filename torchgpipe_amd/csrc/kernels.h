@@ -163,6 +163,15 @@ struct ConvGemmPhase {
   int th0, tw0;
 };
 bool conv_gemm_phased(const ConvGemmGeo& g);
+// Every phase of one backward-data in one launch (up to kConvGemmMaxPhases; grid.z = phase):
+// `a` holds the phases' weight slices back to back, phase p's starting a_off[p] floats in;
+// one reduction split.
+constexpr int kConvGemmMaxPhases = 4;
+struct ConvGemmPlan;
+void launch_conv_gemm_phases(const float* a, const int64_t* a_off, const float* b,
+                             const float* x_mask, float* out, const ConvGemmPhase* phases,
+                             int count, const ConvGemmPlan& plan, bool accumulate,
+                             int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
 // Integer environment setting (conv_gemm.hip): `fallback` when unset or empty.
 int env_int(const char* name, int fallback);
 std::vector<ConvGemmPhase> conv_gemm_phases(const ConvGemmGeo& g);
