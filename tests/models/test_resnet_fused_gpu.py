@@ -32,6 +32,11 @@ CASES = [
     (4, 32, 28, 32, 3, 2, 1),     # 3x3 stride 2: MIOpen + native BN(+ReLU)
     (2, 3, 64, 64, 7, 2, 3),      # the stem 7x7 stride 2: MIOpen + native BN(+ReLU)
     (4, 512, 7, 512, 1, 1, 0),    # 7x7 planes: split reduction, fused split statistics
+    # the strided geometries shipped on the fused native op (ops/fusion.py STRIDED_FUSED):
+    # implicit-GEMM forward + stride-phase backward-data
+    (2, 128, 56, 128, 3, 2, 1),
+    (2, 256, 56, 512, 1, 2, 0),
+    (2, 512, 14, 512, 3, 2, 1),
 ]
 
 

@@ -17,10 +17,9 @@ one native op needs the layers to cooperate:
   - 3x3 stride-1 convolutions: the Winograd F(4x4) / batched-GEMM kernels
     (``ops.conv``), then the native BatchNorm(+ReLU) pass (:func:`bn_act`);
   - strided convolutions (the 7x7 stem, the stride-2 3x3 and 1x1 of each stage's first
-    block): MIOpen, then :func:`bn_act` -- the implicit-GEMM kernel's strided backward-data
-    walks every input pixel (stride holes included) and measured 6 ms per call at
-    ResNet-101's shapes (B 110), several times MIOpen's
-    (``benchmarks/diag/resnet_kernel_table.py``, ``profiles/r3/resnet_kernel_tables.md``);
+    block): the fused native op (implicit-GEMM forward, stride-phase backward-data) for the
+    three geometries where it measured faster (``STRIDED_FUSED``), MIOpen then
+    :func:`bn_act` for the others;
 
   and marks its output as normalised (and rectified) by that BatchNorm;
 * :class:`BatchNormAct2d` passes a marked input through; otherwise it runs the native
@@ -171,17 +170,32 @@ def _pointwise(conv: nn.Conv2d) -> bool:
 # strided convolutions: geometry -> whether the fused implicit-GEMM op (its backward-data
 # on MIOpen where that timed faster) beat MIOpen + the native BatchNorm, forward + backward
 _STRIDED: Dict[tuple, bool] = {}
-# (opt-in, TGPIPE_STRIDED_CHOICE=1: not yet measured on the GPU; default MIOpen + BN)
+# TGPIPE_STRIDED_CHOICE=1: time both ways on the first eager call of a geometry (the
+# offline measurement's method); default: the shipped measured set below
 STRIDED_CHOICE = os.environ.get('TGPIPE_STRIDED_CHOICE', '0') != '0'
+# Strided Conv-BN(-ReLU) geometries (in channels, out channels, kernel, stride, padding,
+# input height) where the fused native op -- implicit-GEMM forward with the BatchNorm
+# statistics in its epilogue, stride-phase backward-data -- measured faster than MIOpen +
+# the native BatchNorm at ResNet-101's pipeline-1 micro-batch of 110
+# (benchmarks/diag/resnet_strided_probe.py, profiles/r4/resnet/resnet_strided_probe_r4ac.jsonl:
+# 1386 / 1612 / 1178 vs 1440 / 1714 / 1355 us forward + backward); the other strided
+# convolutions (the 7x7 stem, the 28^2 3x3, the 28^2 / 14^2 downsamples) stay on MIOpen.
+STRIDED_FUSED = frozenset({
+    (128, 128, (3, 3), (2, 2), (1, 1), 56),
+    (256, 512, (1, 1), (2, 2), (0, 0), 56),
+    (512, 512, (3, 3), (2, 2), (1, 1), 14),
+})
 
 
 def _strided_fused(conv: nn.Conv2d, bn: nn.BatchNorm2d, x: Tensor, relu: bool) -> bool:
-    """Time both ways of one strided Conv-BN(-ReLU) on the first eager call of its geometry
-    (on copies of the layers: the real ones' parameters, gradients and running statistics
-    are untouched); inside a stream capture an undecided geometry stays on MIOpen.
-    ResNet-101 shapes split both ways (``profiles/r3/resnet_strided_probe.jsonl``)."""
+    """Whether one strided Conv-BN(-ReLU) runs as the fused native op: the shipped measured
+    set (``STRIDED_FUSED``), or with ``TGPIPE_STRIDED_CHOICE=1`` both ways timed on the first
+    eager call of its geometry (on copies of the layers: the real ones' parameters,
+    gradients and running statistics are untouched; inside a stream capture an undecided
+    geometry stays on MIOpen)."""
     if not STRIDED_CHOICE:
-        return False
+        return (conv.in_channels, conv.out_channels, tuple(conv.kernel_size), tuple(conv.stride),
+                tuple(conv.padding), x.shape[2]) in STRIDED_FUSED  # type: ignore[arg-type]
     key = (tuple(x.shape), conv.out_channels, tuple(conv.kernel_size), tuple(conv.stride),
            tuple(conv.padding), relu, x.device)  # type: ignore[arg-type]
     hit = _STRIDED.get(key)
