@@ -1,0 +1,11 @@
+# Final-tree validation: the whole GPU suite, smoke() and the default one-GPU bench.
+set -o pipefail
+out=gpurun_out/r4aj
+mkdir -p $out
+timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $out/pytest.log 2>&1 || { tail -40 $out/pytest.log; exit 1; }
+tail -3 $out/pytest.log
+grep -c "AccumulateGrad" $out/pytest.log || true
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
+tail -1 $out/smoke.log
+timeout -k 10 900 python -u bench.py > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
+tail -1 $out/bench.log
