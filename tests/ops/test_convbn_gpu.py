@@ -40,6 +40,8 @@ CASES = [
     (4, 256, 7, 7, 256, 1, 7, 1, 3, 0),      # small grid: split reduction (atomics)
     (4, 1024, 7, 7, 256, 1, 1, 1, 0, 0),     # split reduction, 1x1
     (4, 96, 14, 14, 64, 1, 1, 2, 0, 1),      # strided scatter backward, even plane
+    (4, 96, 14, 14, 64, 1, 1, 2, 0, 0),      # strided 1x1 writing its holes' zeros (fill)
+    (2, 24, 15, 14, 16, 1, 1, 2, 0, 0),      # fill, odd height: the last block one row
     (2, 3, 32, 32, 16, 3, 3, 1, 1, 0),       # U-Net's 3-channel input convolution (2-D taps)
     (4, 32, 28, 28, 32, 3, 3, 2, 1, 0),      # reduction-cell 3x3 stride 2 (stride holes)
     (3, 16, 15, 15, 24, 3, 3, 2, 1, 0),      # 3x3 stride 2, odd plane
@@ -114,6 +116,28 @@ def test_strided_backward_data_phases_anisotropic(kernel, stride, pad):
     want.backward(dz.double())
     dx = ops().conv_gemm_backward_data(dz, x, wt, geo, True)
     assert rel_err(dx, x64.grad) < 2e-6
+
+
+@pytest.mark.parametrize('hw', [(14, 14), (15, 14)])
+def test_strided_1x1_backward_data_fill_overwrites_stale_memory(hw):
+    """The stride-2 1x1 backward-data allocates dX without a memset and writes the zeros
+    of the stride holes itself (ConvGemmGeo::fill): recycled allocator blocks full of NaN
+    must not leak through."""
+    torch.manual_seed(0)
+    h, w = hw
+    x = torch.randn(6, 64, h, w, device='cuda')
+    wt = torch.randn(48, 64, 1, 1, device='cuda') / 8.0
+    geo = [1, 1, 2, 2, 0, 0, 0, 0]
+    x64 = x.double().requires_grad_(True)
+    want = F.conv2d(F.relu(x64), wt.double(), stride=2)
+    dz = torch.randn(want.shape, device='cuda')
+    want.backward(dz.double())
+    for _ in range(3):
+        stale = torch.full_like(x, float('nan'))
+        del stale
+        dx = ops().conv_gemm_backward_data(dz, x, wt, geo, True)
+        assert torch.isfinite(dx).all()
+        assert rel_err(dx, x64.grad) < 2e-6
 
 
 def _block(kind, ci, co):

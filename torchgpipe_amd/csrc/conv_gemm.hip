@@ -127,6 +127,7 @@ struct Geo {
   // bwd-data of one stride phase (scatter set too): ho x wo = the phase grid, zh x zw =
   // the dZ plane, tap (th, tw) of column (y, x) reads dZ[y + dy0 - th][x + dx0 - tw]
   int phase, zh, zw, dy0, dx0;
+  int fill;  // strided 1x1 bwd-data: zeros into the 2x2 blocks' other pixels (ConvGemmGeo)
 };
 
 // All stride phases of one backward-data in one launch (grid.z = phase): what differs
@@ -366,7 +367,10 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
     int accumulate, int64_t a_bytes, int64_t b_bytes, PhaseSet ps) {
   using C = Cfg<CFG>;
   if constexpr (MODE == kBwdData) {
-    if (ps.count > 0) {  // this workgroup's stride phase
+    // this workgroup's stride phase (grid.z: one phase's grid after the other -- phases
+    // as the fastest block index, the tiles of one pixel block together on one XCD, ran
+    // the 3x3 stride-2 shapes 15-55 % slower, profiles/r4/phase_order/)
+    if (ps.count > 0) {
       const int z = blockIdx.z;
       g.kh = ps.kh[z];
       g.kw = ps.kw[z];
@@ -765,6 +769,11 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
         const int64_t off = ((static_cast<int64_t>(n) * g.ci + m) * g.h + yi) * g.w + xi;
         float val = v[e];
         if (g.relu && !(bload(mr, static_cast<uint32_t>(off * 4)) > 0.f)) val = 0.f;
+        if (g.fill) {  // (host-checked: stride 2, even width, no padding, offset or accumulate)
+          *reinterpret_cast<floatx2*>(out + off) = floatx2{val, 0.f};
+          if (yi + 1 < g.h) *reinterpret_cast<floatx2*>(out + off + g.w) = floatx2{0.f, 0.f};
+          continue;
+        }
         out[off] = accumulate ? out[off] + val : val;
       }
       continue;
@@ -1135,7 +1144,7 @@ Geo make_geo(const ConvGemmGeo& cg) {
   Geo g{cg.n, cg.ci, cg.h, cg.w, cg.co, cg.ho, cg.wo, cg.co_total, cg.co_off, cg.kh, cg.kw,
         cg.kh * cg.kw, cg.sh, cg.sw, cg.ph, cg.pw, cg.oh, cg.ow, cg.relu ? 1 : 0, 0,
         cg.a_t ? 1 : 0, spread, {}, {}, {}, {}, {},
-        cg.phase ? 1 : 0, cg.zh, cg.zw, cg.dy0, cg.dx0};
+        cg.phase ? 1 : 0, cg.zh, cg.zw, cg.dy0, cg.dx0, cg.fill ? 1 : 0};
   g.fd_taps = make_fastdiv(g.taps);
   g.fd_kw = make_fastdiv(g.kw);
   g.fd_hwo = make_fastdiv(g.ho * g.wo);

@@ -242,6 +242,16 @@ bool dx_needs_zero(const ConvGemmGeo& g) {
   return conv_gemm_plan(1, g).scatter;
 }
 
+// A strided 1x1 backward-data that writes its stride holes' zeros itself (ConvGemmGeo::fill:
+// stride 2, no padding / offset, even width), so its dX is allocated without a memset and
+// written in whole 2x2 blocks.  TGPIPE_CG_FILL=0: the memset + scattered stores instead.
+bool dx_fillable(const ConvGemmGeo& g) {
+  static const bool on = env_int("TGPIPE_CG_FILL", 1) != 0;
+  return on && !g.phase && g.kh == 1 && g.kw == 1 && g.sh == 2 && g.sw == 2 && g.ph == 0 &&
+         g.pw == 0 && g.oh == 0 && g.ow == 0 && g.w % 2 == 0 && g.ho == (g.h + 1) / 2 &&
+         g.wo == g.w / 2;
+}
+
 // Backward-data of one convolution into `dx` (accumulating onto it when asked) with the
 // transposed weight `wt` ([ci][co][kh][kw]) as the A operand.  A strided k x k convolution
 // runs as one GEMM per stride phase (conv_gemm_phases: the sub-pixel decomposition, no
@@ -732,6 +742,9 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
   auto ours_into = [&](bool use_into) -> at::Tensor {
     bool zero = false;
     for (const auto& g : p.geo) zero = zero || dx_needs_zero(g);
+    // (the first part writing every pixel, holes included: no memset for the others)
+    const bool fill = !use_into && dx_fillable(p.geo[0]);
+    zero = zero && !fill;
     at::Tensor d = use_into ? *dx_into
                             : (zero ? at::zeros_like(x) : at::empty_like(x));  // stride holes
     zero = zero || use_into;  // (from here: accumulate onto d)
@@ -753,8 +766,11 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
         wts.push_back(weights_t[i]);
       }
     }
-    for (size_t i = 0; i < p.geo.size(); ++i)
-      backward_data_into(wts[i], dz, x, d, p.geo[i], i > 0 || zero);
+    for (size_t i = 0; i < p.geo.size(); ++i) {
+      ConvGemmGeo gi = p.geo[i];
+      gi.fill = i == 0 && fill;
+      backward_data_into(wts[i], dz, x, d, gi, i > 0 || zero);
+    }
     return d;
   };
   if (need_dx) {
@@ -942,7 +958,8 @@ std::vector<at::Tensor> convbn_group_backward(
     g.co = static_cast<int>(c);
     g.co_total = static_cast<int>(c);
     g.co_off = 0;
-    const bool zero = dx_needs_zero(g);
+    g.fill = dx_fillable(g);
+    const bool zero = dx_needs_zero(g) && !g.fill;
     dx = zero ? at::zeros_like(x) : at::empty_like(x);
     backward_data_into(w_cat_t, dz, x, dx, g, zero);
   }
@@ -1084,7 +1101,9 @@ at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_
   Parts p = make_parts(x, {weight}, geo, relu);
   TORCH_CHECK(dz.size(1) == p.co_total && dz.size(2) == p.ho && dz.size(3) == p.wo,
               "dz does not match the convolution's output");
-  const bool zero = dx_needs_zero(p.geo[0]);
+  ConvGemmGeo g0 = p.geo[0];
+  g0.fill = dx_fillable(g0);
+  const bool zero = dx_needs_zero(g0) && !g0.fill;
   auto dx = zero ? at::zeros_like(x) : at::empty_like(x);
   at::Tensor wt;  // A = W^T (see convbn_backward)
   if (weight_t.has_value() && weight_t->defined()) {
@@ -1096,7 +1115,7 @@ at::Tensor conv_gemm_backward_data(const at::Tensor& dz_in, const at::Tensor& x_
   } else {
     wt = weight.transpose(0, 1).contiguous();
   }
-  backward_data_into(wt, dz, x, dx, p.geo[0], zero);
+  backward_data_into(wt, dz, x, dx, g0, zero);
   return dx;
 }
 

@@ -153,6 +153,9 @@ struct ConvGemmGeo {
   // taps, zh x zw the dZ plane, tap (i, j) reading dZ[y + dy0 - i][x + dx0 - j]
   bool phase = false;
   int zh = 0, zw = 0, dy0 = 0, dx0 = 0;
+  // strided 1x1 backward-data (stride 2, no padding / offset, even width): also write the
+  // zeros of the other three pixels of each 2x2 block, so dX needs no memset first
+  bool fill = false;
 };
 // Sub-pixel decomposition of a strided convolution's backward-data: input pixels of one
 // residue (a, b) modulo the stride receive exactly the taps th = th0 + sh*i, tw = tw0 + sw*j,
