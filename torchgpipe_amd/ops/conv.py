@@ -289,7 +289,7 @@ def _use_f4(x: Tensor, out_channels: int = 0) -> bool:
 # profiles/r3/bg_bench.json), F(2x2) on 6x6 planes (a 4x4 tile grid wastes 5/9 there).
 # TGPIPE_WINOGRAD_BG=0 keeps the older kernels.
 BG_ENABLED = os.environ.get('TGPIPE_WINOGRAD_BG', '1') != '0'
-BG_MIN_CHANNELS = 256
+BG_MIN_CHANNELS = int(os.environ.get('TGPIPE_WINOGRAD_BG_MIN_CHANNELS', '256'))
 
 
 def _bg_kind(x: Tensor, out_channels: int) -> int:
