@@ -1,6 +1,6 @@
 # Final-tree validation: the whole GPU suite, smoke() and the default one-GPU bench.
 set -o pipefail
-out=gpurun_out/r4aj
+out=gpurun_out/${OUT:-r4aj}
 mkdir -p $out
 timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $out/pytest.log 2>&1 || { tail -40 $out/pytest.log; exit 1; }
 tail -3 $out/pytest.log
