@@ -57,20 +57,21 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 # Reference (Tesla P40) throughputs of the same experiments, BASELINE.md §1/§2.
 # Batch / chunks / reference balance are the reference's experiment tables.
-# ``tuned`` balances for MI355X with the round-3 kernels (batched-GEMM Winograd for >= 256
-# channels): the reference-balance stage times of benchmarks/stage_harness.py
-# (profiles/r3/stage_harness_unet_p{2,4,8}_ref.json) spread over their layers by the
-# per-layer profile (profiles/unet_layer_profile_f4w.json) and min-max partitioned by
-# scripts/balance_from_harness.py: predicted max stage p2 532 / p4 235 / p8 171 ms against
-# 543 / 282 / 241 for the reference balances (profiles/r3/speedup_prediction.md).
+# ``tuned`` balances for MI355X: the stage times of benchmarks/stage_harness.py (reference and
+# earlier tuned balances) spread over their layers by the per-layer profile
+# (profiles/unet_layer_profile_f4w.json) and min-max partitioned by
+# scripts/balance_from_harness.py.  p2 from round 3; p4 / p8 re-derived on the round-4 tree
+# (profiles/r4/final/stage_harness_unet_p{4,8}_tuned{,2}.json): measured max stage p2 522 /
+# p4 235 / p8 176 ms against 537 / 283 / 240 for the reference balances
+# (profiles/r4/speedup_prediction.md).
 UNET_EXPERIMENTS = {
     1: dict(name='pipeline-1', batch=80, chunks=2, balance=[241], tuned=[241], ref=24.456),
     2: dict(name='pipeline-2', batch=512, chunks=32, balance=[104, 137], tuned=[100, 141],
             ref=35.502),
     4: dict(name='pipeline-4', batch=512, chunks=16, balance=[30, 66, 84, 61],
-            tuned=[44, 53, 70, 74], ref=67.042),
+            tuned=[38, 55, 74, 74], ref=67.042),
     8: dict(name='pipeline-8', batch=640, chunks=40, balance=[16, 27, 31, 44, 22, 57, 27, 17],
-            tuned=[18, 21, 29, 29, 26, 41, 44, 33], ref=88.497),
+            tuned=[18, 26, 27, 30, 22, 44, 40, 34], ref=88.497),
 }
 # the reference's speed-up denominator: U-Net without GPipe, one GPU
 UNET_BASELINE = dict(name='baseline', batch=40, ref=28.500)
