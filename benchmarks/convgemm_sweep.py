@@ -19,7 +19,8 @@ SHAPES = [  # N, Ci, H, Co, kh, kw
     (20, 64, 28, 64, 1, 7), (20, 64, 28, 256, 1, 1),
 ]
 CFG = {0: '64x64/4w', 1: '128x128/8w', 2: '128x128/4w', 3: '64x64/4w/sub4',
-       4: '128x128/8w/sub2', 5: '128x128/4w/sub2', 6: '64x64/4w/sub2'}
+       4: '128x128/8w/sub2', 5: '128x128/4w/sub2', 6: '64x64/4w/sub2',
+       7: 'emu 64x64/4w', 8: 'emu 128x128/4w', 9: 'emu 128x128/8w'}
 
 
 def main() -> None:

@@ -69,9 +69,10 @@ def _geo(kh, kw, stride, pad, offset):
     return [kh, kw, stride, stride, ph, pw, offset, offset]
 
 
-@pytest.fixture(params=[-1, 0, 1, 2, 3, 4, 5, 6], ids=['tuned'] + [f'cfg{i}' for i in range(7)])
+@pytest.fixture(params=[-1] + list(range(10)), ids=['tuned'] + [f'cfg{i}' for i in range(10)])
 def tile_cfg(request):
-    """Every tile configuration of the implicit-GEMM kernel, then the tuned plans."""
+    """Every tile configuration of the implicit-GEMM kernel (7-9: split-bf16 products, held
+    to the same fp64 error bounds as the f32 ones), then the tuned plans."""
     ops().conv_gemm_force_cfg(request.param)
     yield request.param
     ops().conv_gemm_force_cfg(-1)

@@ -225,40 +225,67 @@ BG_SHAPES = [  # (N, C, K, H, W)
 ]
 
 
+def _bg_run(x, wt, bias, flip, kind, emu, bn=0, splits=0, waves=0, sub=0):
+    ops = _ext.require(x)
+    out_channels = wt.shape[1] if flip else wt.shape[0]
+    return ops.bg_conv(x, ops.bg_weight(wt, flip, kind, emu=emu), bias, out_channels, bn,
+                       splits, kind, waves, sub, emu=emu)
+
+
+@pytest.mark.parametrize('emu', [0, 1], ids=['f32', 'split-bf16'])
 @pytest.mark.parametrize('shape', BG_SHAPES)
 @pytest.mark.parametrize('flip', [False, True])
 @pytest.mark.parametrize('kind', [4, 2])
-def test_batched_gemm_winograd_matches_conv2d(shape, flip, kind):
+def test_batched_gemm_winograd_matches_conv2d(shape, flip, kind, emu):
     """Forward (flip=False) and backward-data (flip=True: the rotated, transposed weights)
-    of the batched-GEMM path, F(4x4) and F(2x2), against fp64 PyTorch."""
+    of the batched-GEMM path, F(4x4) and F(2x2), f32 and split-bf16 GEMMs, against fp64."""
     n, c, k, h, w = shape
-    ops = _ext.require(torch.empty(0, device=cuda))
     torch.manual_seed(0)
     wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
     if flip:  # dx = conv_transpose(dy, w): input has k channels, output c
         x = torch.randn(n, k, h, w, device=cuda)
         want = F.conv_transpose2d(x.double(), wt.double(), padding=1)
-        got = ops.bg_conv(x, ops.bg_weight(wt, True, kind), None, c, 0, 0, kind)
+        got = _bg_run(x, wt, None, True, kind, emu)
     else:
         x = torch.randn(n, c, h, w, device=cuda)
         b = torch.randn(k, device=cuda)
         want = _ref(x, wt, b)
-        got = ops.bg_conv(x, ops.bg_weight(wt, False, kind), b, k, 0, 0, kind)
+        got = _bg_run(x, wt, b, False, kind, emu)
     torch.testing.assert_close(got.double(), want, rtol=1e-4,
                                atol=2e-5 * (want.abs().max().item() + 1))
 
 
+@pytest.mark.parametrize('shape', BG_SHAPES[:4])
+@pytest.mark.parametrize('kind', [4, 2])
+def test_split_bf16_gemm_is_as_accurate_as_f32(shape, kind):
+    """The split-bf16 products (six bf16 MFMAs per f32 product) carry no more error against
+    fp64 than the f32 MFMA GEMM of the same transformed operands: the Winograd transform
+    dominates both, the split adds < 2^-22 per product."""
+    n, c, k, h, w = shape
+    torch.manual_seed(2)
+    wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
+    x = torch.randn(n, c, h, w, device=cuda)
+    want = _ref(x, wt)
+    err = {}
+    for emu in (0, 1):
+        got = _bg_run(x, wt, None, False, kind, emu).double()
+        err[emu] = ((got - want).norm() / want.norm()).item()
+    assert err[1] <= 1.25 * err[0] + 1e-7, err
+
+
+@pytest.mark.parametrize('emu', [0, 1], ids=['f32', 'split-bf16'])
 @pytest.mark.parametrize('waves,bn,sub', [(4, 48, 1), (4, 64, 1), (4, 96, 1), (4, 128, 1),
                                           (4, 48, 2), (4, 64, 2), (4, 96, 2), (4, 128, 2),
                                           (8, 64, 1), (8, 96, 1), (8, 128, 1), (8, 144, 1)])
 @pytest.mark.parametrize('splits', [1, 3])
-def test_batched_gemm_tile_shapes_and_splits(waves, bn, sub, splits):
+def test_batched_gemm_tile_shapes_and_splits(waves, bn, sub, splits, emu):
+    """Every tile shape (split-bf16: 4 waves x 64 / 96 / 128, one step per stage; other
+    requests fall back to its automatic width) with and without split-K."""
     n, c, k, h, w = 4, 96, 300, 20, 20
-    ops = _ext.require(torch.empty(0, device=cuda))
     torch.manual_seed(1)
     x = torch.randn(n, c, h, w, device=cuda)
     wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
-    got = ops.bg_conv(x, ops.bg_weight(wt, False), None, k, bn, splits, 4, waves, sub)
+    got = _bg_run(x, wt, None, False, 4, emu, bn, splits, waves, sub)
     want = _ref(x, wt)
     torch.testing.assert_close(got.double(), want, rtol=1e-4,
                                atol=2e-5 * (want.abs().max().item() + 1))

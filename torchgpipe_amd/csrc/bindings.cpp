@@ -319,7 +319,7 @@ at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t 
 // Batched-GEMM Winograd F(4x4): weights in the GEMM operand layout (cached per step by
 // ops/conv.py), and the convolution (input transform, 36 GEMMs, output transform).
 at::Tensor bg_weight(const at::Tensor& w, bool flip, int64_t kind,
-                     const c10::optional<at::Tensor>& out) {
+                     const c10::optional<at::Tensor>& out, int64_t emu) {
   check_f32_gpu(w, "weight");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "weight must be [K][C][3][3]");
   auto wc = w.contiguous();
@@ -328,22 +328,24 @@ at::Tensor bg_weight(const at::Tensor& w, bool flip, int64_t kind,
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
   TORCH_CHECK(kind == 4 || kind == 2, "kind must be 4 (F(4x4)) or 2 (F(2x2))");
   auto a =
-      transform_out(out, {bg_weight_numel(out_channels, red_channels, static_cast<int>(kind))}, w);
+      transform_out(out, {bg_weight_numel(out_channels, red_channels, static_cast<int>(kind),
+                                          static_cast<int>(emu))}, w);
   launch_bg_weight(wc.data_ptr<float>(), a.data_ptr<float>(), out_channels, red_channels, flip,
-                   static_cast<int>(kind), stream_of(w));
+                   static_cast<int>(kind), stream_of(w), static_cast<int>(emu));
   return a;
 }
 
 at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
                    const c10::optional<at::Tensor>& bias, int64_t out_channels, int64_t bn,
-                   int64_t splits, int64_t kind, int64_t waves, int64_t sub) {
+                   int64_t splits, int64_t kind, int64_t waves, int64_t sub, int64_t emu) {
   auto x = x_in.contiguous();
   check_f32_gpu(x, "x");
   check_f32_gpu(a, "a");
   TORCH_CHECK(x.dim() == 4, "x must be NCHW");
   const int64_t n = x.size(0), r = x.size(1), h = x.size(2), w = x.size(3);
   TORCH_CHECK(kind == 4 || kind == 2, "kind must be 4 (F(4x4)) or 2 (F(2x2))");
-  TORCH_CHECK(a.dim() == 1 && a.numel() == bg_weight_numel(out_channels, r, static_cast<int>(kind)),
+  TORCH_CHECK(a.dim() == 1 && a.numel() == bg_weight_numel(out_channels, r, static_cast<int>(kind),
+                                                           static_cast<int>(emu)),
               "batched-GEMM transformed weight does not match the input/output channels");
   TORCH_CHECK(a.device() == x.device(), "a must live on the input's device");
   TORCH_CHECK(wino4_supported(n, r, h, w, out_channels),
@@ -359,7 +361,8 @@ at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
   if (n == 0 || h == 0 || w == 0 || out_channels == 0) return y;
   const BgPlan plan = bg_plan(n, r, h, w, out_channels, static_cast<int>(bn),
                               static_cast<int>(splits), static_cast<int>(kind),
-                              static_cast<int>(waves), static_cast<int>(sub));
+                              static_cast<int>(waves), static_cast<int>(sub),
+                              static_cast<int>(emu));
   // 32-bit tile / element indices of the GEMM and transform kernels
   TORCH_CHECK(plan.ksteps * 16 * plan.np < (int64_t{1} << 31) &&
                   plan.mp * plan.np < (int64_t{1} << 31),
@@ -390,9 +393,9 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("wino4_wgrad(Tensor x, Tensor dy, int splits=0, int variant=0, Tensor? into=None) -> Tensor");
   m.def("wino4_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
-  m.def("bg_weight(Tensor w, bool flip, int kind=4, Tensor? out=None) -> Tensor");
+  m.def("bg_weight(Tensor w, bool flip, int kind=4, Tensor? out=None, int emu=-1) -> Tensor");
   m.def("bg_conv(Tensor x, Tensor a, Tensor? bias, int out_channels, int bn=0, int splits=0, "
-        "int kind=4, int waves=0, int sub=0) -> Tensor");
+        "int kind=4, int waves=0, int sub=0, int emu=-1) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {

@@ -61,9 +61,12 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kBK = 32;
-constexpr int kConvGemmCfgs = 7;  // tile configurations (Cfg<0..6>)
+constexpr int kConvGemmCfgs = 10;  // tile configurations (Cfg<0..9>; 7..9 split-bf16)
+constexpr int kFirstEmuCfg = 7;
 // mfma_stage: all of a stage's LDS fragment reads ahead of its MFMAs (see there)
 constexpr bool kMfmaReadsFirst = true;
 constexpr uint32_t kOOB = 0x7ffffff0u;  // buffer offset past every tensor (< 2 GiB)
@@ -149,10 +152,15 @@ struct PhaseSet {
 // CFG 3 / 4 / 5 / 6: CFG 0 / 1 / 2 / 0 with SUB = 4 / 2 / 2 / 2 BK-deep sub-stages per barrier and
 // per prefetch: a small grid (one workgroup per CU) then keeps SUB x more loads in flight
 // per wave -- each stage's MFMAs cover one global-load latency instead of a fraction.
+//
+// CFG 7 / 8 / 9: the tiles of CFG 0 / 2 / 1 on the bf16 matrix pipes (EMU, see
+// "split-bf16 products" below): 64 x 64 (3 x 48 KiB per CU), 128 x 128 / 4 waves and
+// 128 x 128 / 8 waves (96 KiB).
 template <int CFG>
 struct Cfg {
-  static constexpr int TILE = CFG % 3;
-  static constexpr int SUB = CFG < 3 ? 1 : (CFG == 3 ? 4 : 2);  // (CFG 6: 64 x 64, 2 x 80 KiB)
+  static constexpr bool EMU = CFG >= kFirstEmuCfg;
+  static constexpr int TILE = !EMU ? CFG % 3 : (CFG == 7 ? 0 : (CFG == 8 ? 2 : 1));
+  static constexpr int SUB = EMU || CFG < 3 ? 1 : (CFG == 3 ? 4 : 2);  // (CFG 6: 2 x 80 KiB)
   static constexpr int WVM = 2;
   static constexpr int WVN = TILE == 1 ? 4 : 2;
   static constexpr int TM = TILE == 0 ? 1 : 2;   // 32 x 32 MFMA tiles per wave (rows)
@@ -161,18 +169,22 @@ struct Cfg {
   // waves per SIMD when the LDS footprint's workgroups per CU are resident (4 x 40 KiB /
   // 2 x 72 KiB / 1 x 147-160 KiB): the register budget __launch_bounds__ holds them to
   static constexpr int kWavesPerSimd =
-      CFG == 0 || CFG == 1 ? 4 : (CFG == 2 || CFG == 4 || CFG == 6 ? 2 : 1);
+      CFG == 0 || CFG == 1 ? 4
+      : CFG == 7           ? 3
+      : (CFG == 2 || CFG == 4 || CFG == 6 || CFG == 9 ? 2 : 1);
   static constexpr int BM = WVM * 32 * TM;
   static constexpr int BN = WVN * 32 * TN;
-  static constexpr int kAImg = kBK * BM;          // K-major image (one sub-stage)
-  static constexpr int kBImgK = kBK * BN;         // K-major image
+  // K-major images (one sub-stage): f32 [BK][rows], or EMU three bf16 planes of
+  // [BK/8][rows][8] (emu_off)
+  static constexpr int kAImg = EMU ? 3 * kBK * BM / 2 : kBK * BM;
+  static constexpr int kBImgK = EMU ? 3 * kBK * BN / 2 : kBK * BN;
   static constexpr int kBStrideN = BN + 32;       // N-major row stride
-  static constexpr int kBImgN = kBK * kBStrideN;  // N-major image
+  static constexpr int kBImgN = kBK * kBStrideN;  // N-major image (f32 only)
   // epilogue C tile row stride: rows 4 apart (the two halves of an MFMA result
   // register) land 32 banks apart
   static constexpr int kCStride = BN + 8;
   static constexpr int kOpFloats(bool k_major) {
-    return 2 * SUB * (kAImg + (k_major ? kBImgK : kBImgN));
+    return 2 * SUB * (kAImg + (k_major || EMU ? kBImgK : kBImgN));
   }
   // operand images (double-buffered), reused by the epilogue's C tile (forward /
   // bwd-data); 128 x 128: 72 KiB -> two workgroups per CU
@@ -233,7 +245,93 @@ __device__ __forceinline__ void store_nmajor(float* img, const floatx4 (&v)[Q], 
   }
 }
 
+// ---- split-bf16 products (EMU configurations) -------------------------------------------------
+// An f32 x is exactly hi + mid + lo with three bf16 (8-bit significands, round to nearest
+// each: x - hi has at most 16 significant bits, x - hi - mid at most 8).  A product a * b
+// is then the nine partial products of the parts, each exact in f32; the six kept here
+// (hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi) leave out terms below 2^-24 |a b| -- less
+// than the rounding of one f32 product -- and run on v_mfma_f32_32x32x16_bf16, 16x the f32
+// MFMA's rate per product: six of them cost 3/8 of the f32 MFMA time of the same tile.
+// Accumulation stays f32 in the MFMA accumulators; the fp64 tests hold these
+// configurations to the same error bounds as the f32 ones (tests/ops/test_convbn_gpu.py).
+__device__ __forceinline__ void split3(const floatx4& v, bf16x4& hi, bf16x4& mid, bf16x4& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h = static_cast<__bf16>(v[e]);
+    const float r = v[e] - static_cast<float>(h);
+    const __bf16 m = static_cast<__bf16>(r);
+    hi[e] = h;
+    mid[e] = m;
+    lo[e] = static_cast<__bf16>(r - static_cast<float>(m));
+  }
+}
+
+// EMU image of one K-major operand plane: [slot j = k / 8][row ^ 2j][8 k], 16 bytes per
+// (slot, row), three planes (hi, mid, lo) of BK x ROWS bf16 each.  Lane half h of a
+// 32x32x16 MFMA at k step s reads slot j = 2s + h of 32 consecutive rows with one
+// ds_read_b128 (512 contiguous bytes: conflict-free); a k quad q (k = 4q .. 4q+3) of a row
+// is the 8-byte half (q & 1) of slot q >> 1, and the row ^ 2j swizzle puts the 16 lanes of
+// a ds_write_b64 (8 quads x 2 rows) on 16 distinct 8-byte bank pairs.
+template <int ROWS>
+__device__ __forceinline__ int emu_off(int j, int row) {  // in bf16 elements
+  return (j * ROWS + (row ^ (2 * j))) * 8;
+}
+
+template <int ROWS>
+__device__ __forceinline__ void store_emu_quad(float* img, const floatx4& v, int row, int q) {
+  bf16x4 hi, mid, lo;
+  split3(v, hi, mid, lo);
+  __bf16* p = reinterpret_cast<__bf16*>(img) + emu_off<ROWS>(q >> 1, row) + 4 * (q & 1);
+  constexpr int kPlane = kBK * ROWS;
+  *reinterpret_cast<bf16x4*>(p) = hi;
+  *reinterpret_cast<bf16x4*>(p + kPlane) = mid;
+  *reinterpret_cast<bf16x4*>(p + 2 * kPlane) = lo;
+}
+
 // ---- the GEMM core ------------------------------------------------------------------------
+
+// EMU stage: two k steps of 16; per 32 x 32 tile and step six MFMAs (small parts first).
+// All fragments of the stage are read ahead of its MFMAs; `between(0..3)` carries the next
+// stage's loads (after the first four MFMA groups: the stage is 3/8 as long as an f32 one).
+template <int CFG, typename Between>
+__device__ __forceinline__ void mfma_stage_emu(floatx16 (&acc)[Cfg<CFG>::TM][Cfg<CFG>::TN],
+                                               const float* aimg, const float* bimg, int lane,
+                                               int wm, int wn, Between&& between) {
+  using C = Cfg<CFG>;
+  constexpr int WM = C::TM, WN = C::TN, S = kBK / 16;
+  const int h = lane >> 5, l32 = lane & 31;
+  const __bf16* ab = reinterpret_cast<const __bf16*>(aimg);
+  const __bf16* bb = reinterpret_cast<const __bf16*>(bimg);
+  bf16x8 a[S][3][WM], b[S][3][WN];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+        a[s][p][i] = *reinterpret_cast<const bf16x8*>(
+            ab + p * kBK * C::BM + emu_off<C::BM>(2 * s + h, wm * 32 * WM + i * 32 + l32));
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        b[s][p][j] = *reinterpret_cast<const bf16x8*>(
+            bb + p * kBK * C::BN + emu_off<C::BN>(2 * s + h, wn * 32 * WN + j * 32 + l32));
+    }
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr int kPairs[6][2] = {{2, 0}, {0, 2}, {1, 1}, {1, 0}, {0, 1}, {0, 0}};
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              a[s][kPairs[t][0]][i], b[s][kPairs[t][1]][j], acc[i][j], 0, 0, 0);
+      if (s == 0 && t < 4) between(t);  // the loads within the stage's first third
+    }
+  }
+}
 
 // `between(g)` runs after MFMA group g (the two k-steps of k quad g): the main loop issues the
 // next stage's loads from it, pinned there by scheduling barriers.
@@ -393,7 +491,8 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
   }
   constexpr int WM = C::TM, WN = C::TN, kThreads = C::kThreads;
   constexpr bool kBK_major = MODE == kWgrad;
-  constexpr int kBImg = kBK_major ? C::kBImgK : C::kBImgN;
+  constexpr bool kEmu = C::EMU;
+  constexpr int kBImg = kBK_major || kEmu ? C::kBImgK : C::kBImgN;
   constexpr int SUB = C::SUB;
   __shared__ __attribute__((aligned(16))) float lds[C::kLdsFloats(MODE)];
   // buffer b, sub-stage u
@@ -433,7 +532,11 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
                          (MODE == kBwdData && (kPlain || (g.scatter && !g.phase)))) &&
                         (hw_out & 3) == 0);
   Col col[4];
-  if constexpr (!kBK_major) {
+  if constexpr (!kBK_major && kEmu) {
+    // EMU: one column per thread, gathered as k quads of that column (the EMU image is
+    // K-major for both operands)
+    col[0] = make_col<MODE, kPlain>(g, n0 + tid % C::BN, N);
+  } else if constexpr (!kBK_major) {
     const int jq = n0 + (tid % QPR) * (spread ? 1 : 4);
     const int cstep = spread ? QPR : 1;
 #pragma unroll
@@ -609,11 +712,64 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
     return v;
   };
 
+  // EMU forward / backward-data B: k quad kq_of(i) of this thread's column col[0], one
+  // element load per k (the lanes of a load read consecutive columns)
+  auto kq_of = [&](int i) { return tid / C::BN + (kThreads / C::BN) * i; };
+  auto load_b_emu = [&](int k0, int i) -> floatx4 {
+    floatx4 v;
+    const Col& c = col[0];
+    const int kb = k0 + 4 * kq_of(i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = kb + e;
+      const bool kin = c.ok && k < k_end;
+      uint32_t off = kOOB;
+      if constexpr (MODE == kFwd) {
+        if constexpr (kPlain) {
+          if (kin) off = static_cast<uint32_t>((c.base + k * hw_in) * 4);
+        } else {
+          const int ci = g.fd_taps.div(k), t = k - ci * g.taps;
+          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
+          const int yi = c.y + th, xi = c.x + tw;
+          if (kin && yi >= 0 && yi < g.h && xi >= 0 && xi < g.w)
+            off = static_cast<uint32_t>((c.base + (ci * g.h + yi) * g.w + xi) * 4);
+        }
+      } else {
+        if (g.phase) {
+          const int co = g.fd_taps.div(k), t = k - co * g.taps;
+          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
+          const int y = c.y - th, x = c.x - tw;
+          if (kin && y >= 0 && y < g.zh && x >= 0 && x < g.zw)
+            off = static_cast<uint32_t>((c.base + (co * g.zh + y) * g.zw + x) * 4);
+        } else if (kPlain || g.scatter) {
+          if (kin) off = static_cast<uint32_t>((c.base + k * hw_out) * 4);
+        } else {
+          const int co = g.fd_taps.div(k), t = k - co * g.taps;
+          const int th = g.fd_kw.div(t), tw = t - th * g.kw;
+          const int ys = c.y - th, xs = c.x - tw;
+          if (g.sh == 1 && g.sw == 1) {
+            if (kin && ys >= 0 && ys < g.ho && xs >= 0 && xs < g.wo)
+              off = static_cast<uint32_t>((c.base + co * hw_out + ys * g.wo + xs) * 4);
+          } else {
+            const int y = ys / g.sh, x = xs / g.sw;
+            if (kin && ys >= 0 && xs >= 0 && y * g.sh == ys && x * g.sw == xs && y < g.ho &&
+                x < g.wo)
+              off = static_cast<uint32_t>((c.base + co * hw_out + y * g.wo + x) * 4);
+          }
+        }
+      }
+      v[e] = bload(br, off);
+    }
+    return v;
+  };
+
   // load unit q of sub-stage u (A quads first, then B quads) for the stage at k0
   constexpr int kUnits = C::kAQuads + kRB;
   auto load_unit = [&](int k0, int u, int q) {
     if (q < C::kAQuads)
       ra[u][q] = load_a(k0 + u * kBK, q);
+    else if constexpr (kEmu && !kBK_major)
+      rb[u][q - C::kAQuads] = load_b_emu(k0 + u * kBK, q - C::kAQuads);
     else
       rb[u][q - C::kAQuads] = load_b(k0 + u * kBK, q - C::kAQuads);
   };
@@ -630,6 +786,24 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
 #pragma unroll
             for (int e = 0; e < 4; ++e) rb[u][i][e] = relu(rb[u][i][e]);
       }
+    }
+    if constexpr (kEmu) {
+#pragma unroll
+      for (int u = 0; u < SUB; ++u) {
+#pragma unroll
+        for (int i = 0; i < C::kAQuads; ++i)
+          store_emu_quad<C::BM>(aimg(buf, u), ra[u][i], (tid >> 3) + (kThreads / 8) * i,
+                                tid & 7);
+#pragma unroll
+        for (int i = 0; i < kRB; ++i) {
+          if constexpr (kBK_major)
+            store_emu_quad<C::BN>(bimg(buf, u), rb[u][i], (tid >> 3) + (kThreads / 8) * i,
+                                  tid & 7);
+          else
+            store_emu_quad<C::BN>(bimg(buf, u), rb[u][i], tid % C::BN, kq_of(i));
+        }
+      }
+      return;
     }
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
@@ -649,6 +823,12 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  auto run_stage = [&](const float* ai, const float* bi, auto&& between) {
+    if constexpr (kEmu)
+      mfma_stage_emu<CFG>(acc, ai, bi, lane, wm, wn, between);
+    else
+      mfma_stage<CFG, kBK_major>(acc, ai, bi, lane, wm, wn, between);
+  };
   constexpr int kStageK = kBK * SUB;
   const int stages = (k_end - k_begin + kStageK - 1) / kStageK;
   if (stages > 0) {
@@ -683,8 +863,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
       // its latency before store_stage waits for it
 #pragma unroll
       for (int u = 0; u < SUB; ++u)
-        mfma_stage<CFG, kBK_major>(acc, aimg(buf, u), bimg(buf, u), lane, wm, wn,
-                                   [&](int grp) {
+        run_stage(aimg(buf, u), bimg(buf, u), [&](int grp) {
                                      if constexpr (kInterleave) {
 #pragma unroll
                                        for (int q = 0; q < kUnits; ++q)
@@ -699,8 +878,7 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
     }
 #pragma unroll
     for (int u = 0; u < SUB; ++u)
-      mfma_stage<CFG, kBK_major>(acc, aimg((stages - 1) & 1, u), bimg((stages - 1) & 1, u),
-                                 lane, wm, wn, [](int) {});
+      run_stage(aimg((stages - 1) & 1, u), bimg((stages - 1) & 1, u), [](int) {});
     __syncthreads();
   }
 
@@ -1163,6 +1341,32 @@ void gemm_dims(int mode, const Geo& g, int& M, int& N, int& K) {
   }
 }
 
+// Block width (rows = columns) of a tile configuration, and the runtime -> template dispatch.
+int cfg_width(int cfg) { return cfg == 0 || cfg == 3 || cfg == 6 || cfg == 7 ? 64 : 128; }
+
+template <typename F>
+void with_cfg(int cfg, F&& f) {
+  switch (cfg) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    case 6: f(std::integral_constant<int, 6>{}); break;
+    case 7: f(std::integral_constant<int, 7>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 9: f(std::integral_constant<int, 9>{}); break;
+    default: f(std::integral_constant<int, 0>{}); break;
+  }
+}
+
+// TGPIPE_CG_EMU=0: the split-bf16 configurations are never candidates (exact f32 MFMA only;
+// a plan naming one falls back to the heuristic).
+bool emu_enabled() {
+  static const bool on = env_int("TGPIPE_CG_EMU", 1) != 0;
+  return on;
+}
+
 bool scatter_bwd(const ConvGemmGeo& cg) {
   return cg.phase || (cg.kh == 1 && cg.kw == 1 && (cg.sh > 1 || cg.sw > 1));
 }
@@ -1254,7 +1458,7 @@ ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
   int k_chunk = (K + plan.splits - 1) / plan.splits;
   k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
   plan.splits = std::max(1, (K + k_chunk - 1) / k_chunk);
-  plan.col_width = plan.cfg % 3 ? 128 : 64;
+  plan.col_width = cfg_width(plan.cfg);
   plan.col_blocks = static_cast<int>((N + plan.col_width - 1) / plan.col_width);
   plan.scatter = g.scatter;
   return plan;
@@ -1267,9 +1471,10 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
   gemm_dims(mode, g, M, N, K);
   std::vector<ConvGemmPlan> out;
   const int max_split = std::max(1, K / (4 * kBK));
-  for (int cfg = 0; cfg < kConvGemmCfgs; ++cfg) {
-    const int64_t tiles = cfg % 3 ? static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128)
-                                  : static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64);
+  const int cfgs = emu_enabled() ? kConvGemmCfgs : kFirstEmuCfg;
+  for (int cfg = 0; cfg < cfgs; ++cfg) {
+    const int wd = cfg_width(cfg);
+    const int64_t tiles = static_cast<int64_t>((M + wd - 1) / wd) * ((N + wd - 1) / wd);
     int last = 0;
     for (int s : {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256, 512, 1024}) {
       if (s > 1 && (s > max_split || g.scatter || tiles * s > 8192)) break;
@@ -1281,7 +1486,7 @@ std::vector<ConvGemmPlan> conv_gemm_candidates(int mode, const ConvGemmGeo& cg) 
       ConvGemmPlan p;
       p.cfg = cfg;
       p.splits = real;
-      p.col_width = cfg % 3 ? 128 : 64;
+      p.col_width = wd;
       p.col_blocks = static_cast<int>((N + p.col_width - 1) / p.col_width);
       p.scatter = g.scatter;
       out.push_back(p);
@@ -1334,23 +1539,8 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
   using F = std::integral_constant<int, kFwd>;
   using D = std::integral_constant<int, kBwdData>;
   using W = std::integral_constant<int, kWgrad>;
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  using C2 = std::integral_constant<int, 2>;
-  using C3 = std::integral_constant<int, 3>;
-  using C4 = std::integral_constant<int, 4>;
-  using C5 = std::integral_constant<int, 5>;
-  using C6 = std::integral_constant<int, 6>;
   auto by_cfg = [&](auto mode_c, float* p1, float* p2, const float* mask) {
-    switch (plan.cfg) {
-      case 1: go(mode_c, C1{}, p1, p2, mask); break;
-      case 2: go(mode_c, C2{}, p1, p2, mask); break;
-      case 3: go(mode_c, C3{}, p1, p2, mask); break;
-      case 4: go(mode_c, C4{}, p1, p2, mask); break;
-      case 5: go(mode_c, C5{}, p1, p2, mask); break;
-      case 6: go(mode_c, C6{}, p1, p2, mask); break;
-      default: go(mode_c, C0{}, p1, p2, mask); break;
-    }
+    with_cfg(plan.cfg, [&](auto cfg_c) { go(mode_c, cfg_c, p1, p2, mask); });
   };
   if (mode == kFwd)
     by_cfg(F{}, pm, pm2, x_mask);
@@ -1393,15 +1583,7 @@ void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
                                                plan.splits, stride, accumulate, a_bytes, b_bytes,
                                                stream);
   };
-  switch (plan.cfg) {
-    case 1: go(std::integral_constant<int, 1>{}); break;
-    case 2: go(std::integral_constant<int, 2>{}); break;
-    case 3: go(std::integral_constant<int, 3>{}); break;
-    case 4: go(std::integral_constant<int, 4>{}); break;
-    case 5: go(std::integral_constant<int, 5>{}); break;
-    case 6: go(std::integral_constant<int, 6>{}); break;
-    default: go(std::integral_constant<int, 0>{}); break;
-  }
+  with_cfg(plan.cfg, go);
 }
 
 void launch_conv_gemm_phases(const float* a, const int64_t* a_off, const float* b,
@@ -1438,15 +1620,7 @@ void launch_conv_gemm_phases(const float* a, const int64_t* a_off, const float* 
     launch_cfg<kBwdData, decltype(cfg_c)::value>(a, b, x_mask, out, nullptr, nullptr, g, M, N, K,
                                                  1, 0, accumulate, a_bytes, b_bytes, stream, ps);
   };
-  switch (plan.cfg) {
-    case 1: go(std::integral_constant<int, 1>{}); break;
-    case 2: go(std::integral_constant<int, 2>{}); break;
-    case 3: go(std::integral_constant<int, 3>{}); break;
-    case 4: go(std::integral_constant<int, 4>{}); break;
-    case 5: go(std::integral_constant<int, 5>{}); break;
-    case 6: go(std::integral_constant<int, 6>{}); break;
-    default: go(std::integral_constant<int, 0>{}); break;
-  }
+  with_cfg(plan.cfg, go);
 }
 
 void launch_slab_flush(const SlabFlushEntry* entries, int count, hipStream_t stream) {

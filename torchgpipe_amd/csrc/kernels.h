@@ -97,16 +97,21 @@ struct BgPlan {
   int bn = 64;            // GEMM tile width (tiles): 48-128 (4 waves), 64-144 (8 waves)
   int sub = 1;            // 16-deep reduction steps per pipeline stage (1 or 2)
   int splits = 1;         // split-K slabs
+  bool emu = false;       // split-bf16 operands on the bf16 matrix pipes (bn 64 / 96 / 128)
   int64_t mp = 0, np = 0, ksteps = 0;
   int64_t workspace = 0;  // floats: V + split slabs of M
 };
-int bg_pick_bn(int64_t tiles, int kind);
+// Whether `emu` (-1: the process default, TGPIPE_BG_EMU, on unless =0) asks for the
+// split-bf16 batched GEMM.
+bool bg_emu(int emu);
+int bg_pick_bn(int64_t tiles, int kind, bool emu = false);
 BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
-               int bn, int splits, int kind, int waves, int sub);
-// weights in the GEMM's operand layout U[36 or 16][2 ceil(R/32)][round(O, 256)][16]
-int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind);
+               int bn, int splits, int kind, int waves, int sub, int emu = -1);
+// weights in the GEMM's operand layout U[36 or 16][2 ceil(R/32)][round(O, 256)][16] (f32),
+// or the split-bf16 image of the same values (1.5x the bytes)
+int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind, int emu = -1);
 void launch_bg_weight(const float* w, float* a, int64_t out_channels, int64_t red_channels,
-                      bool flip, int kind, hipStream_t stream);
+                      bool flip, int kind, hipStream_t stream, int emu = -1);
 void launch_bg_conv(const float* x, const float* a, const float* bias, float* y, float* ws,
                     int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
                     const BgPlan& plan, hipStream_t stream);

@@ -38,6 +38,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 #include <type_traits>
 
 #include "kernels.h"
@@ -1517,6 +1519,269 @@ __global__ __launch_bounds__(64 * kWaves, 512 / (64 * kWaves)) void bg_gemm_kern
   }
 }
 
+// ---- split-bf16 batched GEMM (EMU) -------------------------------------------------------
+// The same 36 / 16 GEMMs on the bf16 matrix pipes, fp32-accurate: every transformed operand
+// value v is stored as three bf16 hi + mid + lo == v (exact: round-to-nearest splits, 8
+// significant bits each), and a product of two values as the six partial products that
+// matter (hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi -- the three left out are below
+// 2^-24 of it, under one f32 rounding), each exact, accumulated in f32 by
+// v_mfma_f32_32x32x16_bf16 at 16x the f32 MFMA's rate: 3/8 of the f32 matrix time.
+// (conv_gemm.hip's EMU tile configurations use the same split.)  The transforms write the
+// split once per value, so the GEMM moves 1.5x the bytes but does no conversion work.
+//
+// Operand image (bf16): X[pos][step][plane p][half h][rows][8]: the 16-byte chunk
+// (p, h, row) holds plane p of reduction values 8h .. 8h+7 of that row, i.e. exactly the
+// fragment lane (row, h) of a 32x32x16 MFMA reads -- 32 consecutive rows are 512 contiguous
+// bytes for one ds_read_b128 (conflict-free), and a step's tile is 6 contiguous runs of
+// rows in global memory, copied by LDS-DMA.
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void bg_split3(const floatx4& v, bf16x4& hi, bf16x4& mid, bf16x4& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h = static_cast<__bf16>(v[e]);
+    const float r = v[e] - static_cast<float>(h);
+    const __bf16 m = static_cast<__bf16>(r);
+    hi[e] = h;
+    mid[e] = m;
+    lo[e] = static_cast<__bf16>(r - static_cast<float>(m));
+  }
+}
+
+// Four consecutive reduction values k = 4g .. 4g+3 of one row at every position: one 8-byte
+// store per (position, plane).  `rows` = Mp or Np.
+template <int NPOS>
+__device__ __forceinline__ void bg_emu_store(float* out, const float (&v)[4][NPOS], int st, int row,
+                                             int g, int rows, int ksteps) {
+  __bf16* base = reinterpret_cast<__bf16*>(out);
+  const int64_t pstride = static_cast<int64_t>(rows) * 8;  // one (plane, half) run
+  const int64_t off = (static_cast<int64_t>(st) * 6 + (g >> 1)) * pstride +
+                      static_cast<int64_t>(row) * 8 + 4 * (g & 1);
+  const int64_t pos_stride = static_cast<int64_t>(ksteps) * 6 * pstride;
+#pragma unroll
+  for (int b = 0; b < NPOS; ++b) {
+    bf16x4 hi, mid, lo;
+    bg_split3(floatx4{v[0][b], v[1][b], v[2][b], v[3][b]}, hi, mid, lo);
+    __bf16* dst = base + b * pos_stride + off;
+    *reinterpret_cast<bf16x4*>(dst) = hi;
+    *reinterpret_cast<bf16x4*>(dst + 2 * pstride) = mid;
+    *reinterpret_cast<bf16x4*>(dst + 4 * pstride) = lo;
+  }
+}
+
+// U (EMU image) of (output channel m, reduction channels st*16 + 4g .. +3).
+__global__ __launch_bounds__(256) void bg_weight_f4_emu_kernel(const float* __restrict__ w,
+                                                              float* __restrict__ a, int O, int R,
+                                                              int Mp, int ksteps, bool flip) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 4 * Mp) return;
+  const int g = static_cast<int>(idx & 3);
+  const int64_t rest = idx >> 2;
+  const int m = static_cast<int>(rest % Mp);
+  const int st = static_cast<int>(rest / Mp);
+  float v[4][kP];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) f4_weight_tile(w, O, R, m, st * 16 + 4 * g + e, flip, v[e]);
+  bg_emu_store<kP>(a, v, st, m, g, Mp, ksteps);
+}
+
+// V (EMU image) of (tile t, channels st*16 + 4g .. +3); zeros in the padding.
+template <bool kVec>
+__global__ __launch_bounds__(256) void bg_input_f4_emu_kernel(const float* __restrict__ x,
+                                                             float* __restrict__ v, int R, int H,
+                                                             int W, int TW, int tpi, int P, int Np,
+                                                             int ksteps, uint32_t x_bytes) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 4 * Np) return;
+  const int g = static_cast<int>(idx & 3);
+  const int64_t rest = idx >> 2;
+  const int t = static_cast<int>(rest % Np);
+  const int st = static_cast<int>(rest / Np);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                        static_cast<int>(x_bytes), 0x00020000);
+  float out[4][kP];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = st * 16 + 4 * g + e;
+    F4Patch p;
+    if (t < P && c < R) {
+      f4_fwd_offsets(p, t, c, P, tpi, TW, R, H, W);
+      f4_load_patch<kVec>(p, xr, 0);
+      f4_transform(p);
+    } else {
+#pragma unroll
+      for (int b = 0; b < kP; ++b) p.d[b] = 0.f;
+    }
+#pragma unroll
+    for (int b = 0; b < kP; ++b) out[e][b] = p.d[b];
+  }
+  bg_emu_store<kP>(v, out, st, t, g, Np, ksteps);
+}
+
+// C[z][b][Mp][Np] = sum over the split's steps of A[b]^T B[b] on split-bf16 operands.
+// Four waves, a 128 x BN tile (BN = 64 / 96 / 128): wave w owns rows 32w .. 32w+31 and all
+// BN columns as BN/32 tiles of v_mfma_f32_32x32x16_bf16, six MFMAs per tile and 16-deep
+// step.  A step's (128 + BN) x 96 bytes arrive by LDS-DMA (1 KiB pieces) into a three-slot
+// ring two steps ahead; the fragments of step k+1 are read while step k's MFMAs run.
+template <int BN>
+__global__ __launch_bounds__(256, 2) void bg_gemm_emu_kernel(
+    const float* __restrict__ a, const float* __restrict__ bmat, float* __restrict__ c, int Mp,
+    int Np, int ksteps, int mtiles, int ntiles, int batch, int splits) {
+  constexpr int kWaves = 4, BM = 128;
+  constexpr int kABytes = 96 * BM, kBBytes = 96 * BN, kStage = kABytes + kBBytes;
+  constexpr int kAPieces = kABytes / 1024, kPieces = kStage / 1024;
+  constexpr int kPer = (kPieces + kWaves - 1) / kWaves;
+  constexpr int kNT = BN / 32;
+  static_assert(BN % 32 == 0 && (96 * BN) % 1024 == 0 && kPer <= 8, "tile shape");
+  __shared__ __attribute__((aligned(16))) char lds[3 * kStage];
+
+  const int nwg = ntiles * mtiles * batch * splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int qq = nwg >> 3, rr = nwg & 7;
+  // consecutive work ids (same A tile, consecutive N tiles) on one XCD: one L2 serves them
+  int wid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int nt = wid % ntiles;
+  wid /= ntiles;
+  const int mt = wid % mtiles;
+  wid /= mtiles;
+  const int bb = wid % batch;
+  const int z = wid / batch;
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int64_t astep = static_cast<int64_t>(Mp) * 96, bstep = static_cast<int64_t>(Np) * 96;
+  const char* abase = reinterpret_cast<const char*>(a) + static_cast<int64_t>(bb) * ksteps * astep;
+  const char* bbase =
+      reinterpret_cast<const char*>(bmat) + static_cast<int64_t>(bb) * ksteps * bstep;
+  const int s0 = static_cast<int>(static_cast<int64_t>(z) * ksteps / splits);
+  const int s1 = static_cast<int>(static_cast<int64_t>(z + 1) * ksteps / splits);
+
+  // this lane's source offset (bytes, within one step) of each of its pieces
+  int64_t src_off[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int piece = i * kWaves + wave;
+    src_off[i] = 0;
+    if (piece < kAPieces) {
+      const int f = piece * 64 + lane;  // (plane-half, row) of the A image
+      const int ph = f / BM, row = f - ph * BM;
+      src_off[i] = (static_cast<int64_t>(ph) * Mp + mt * BM + row) * 16;
+    } else if (piece < kPieces) {
+      const int f = (piece - kAPieces) * 64 + lane;
+      const int ph = f / BN, row = f - ph * BN;
+      src_off[i] = (static_cast<int64_t>(ph) * Np + static_cast<int64_t>(nt) * BN + row) * 16;
+    }
+  }
+  auto issue = [&](int st, int buf) {
+    char* dst = lds + buf * kStage;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int piece = i * kWaves + wave;
+      if (piece < kPieces) {
+        const char* src = (piece < kAPieces ? abase + st * astep : bbase + st * bstep) +
+                          src_off[i];
+        __builtin_amdgcn_global_load_lds((glob_void_t*)src, (lds_void_t*)(dst + piece * 1024),
+                                         16, 0, 0);
+      }
+    }
+  };
+  const int mine = (kPieces - wave + kWaves - 1) / kWaves;
+  auto wait_stages_in_flight = [&](int k) {
+    switch (k * mine) {
+      case 0: bg_wait_vm<0>(); break;
+      case 1: bg_wait_vm<1>(); break;
+      case 2: bg_wait_vm<2>(); break;
+      case 3: bg_wait_vm<3>(); break;
+      case 4: bg_wait_vm<4>(); break;
+      case 5: bg_wait_vm<5>(); break;
+      case 6: bg_wait_vm<6>(); break;
+      case 7: bg_wait_vm<7>(); break;
+      case 8: bg_wait_vm<8>(); break;
+      case 9: bg_wait_vm<9>(); break;
+      case 10: bg_wait_vm<10>(); break;
+      case 11: bg_wait_vm<11>(); break;
+      case 12: bg_wait_vm<12>(); break;
+      case 13: bg_wait_vm<13>(); break;
+      case 14: bg_wait_vm<14>(); break;
+      case 15: bg_wait_vm<15>(); break;
+      default: bg_wait_vm<16>(); break;
+    }
+  };
+
+  floatx16 acc[kNT];
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  const int h = lane >> 5, l32 = lane & 31;
+  // byte offsets of this lane's fragments in a slot: plane p at + p * 2 * rows * 16
+  const int aoff = (h * BM + wave * 32 + l32) * 16;
+  const int boff = kABytes + (h * BN + l32) * 16;
+  bf16x8 af[3], bf[3][kNT];
+  auto fetch = [&](int buf) {
+    const char* base = lds + buf * kStage;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      af[p] = *reinterpret_cast<const bf16x8*>(base + aoff + p * 2 * BM * 16);
+#pragma unroll
+      for (int j = 0; j < kNT; ++j)
+        bf[p][j] = *reinterpret_cast<const bf16x8*>(base + boff + p * 2 * BN * 16 + j * 512);
+    }
+  };
+
+  const int nst = s1 - s0;
+  if (nst > 0) {
+    issue(s0, 0);
+    if (nst > 1) issue(s0 + 1, 1);
+    if (nst > 2) issue(s0 + 2, 2);
+    wait_stages_in_flight(nst > 2 ? 2 : nst - 1);
+    __builtin_amdgcn_s_barrier();
+    fetch(0);
+  }
+  constexpr int kPairs[6][2] = {{2, 0}, {0, 2}, {1, 1}, {1, 0}, {0, 1}, {0, 0}};
+  int buf = 0;
+  for (int k = 0; k < nst; ++k) {
+    bf16x8 ac[3], bc[3][kNT];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      ac[p] = af[p];
+#pragma unroll
+      for (int j = 0; j < kNT; ++j) bc[p][j] = bf[p][j];
+    }
+    const int nb = buf == 2 ? 0 : buf + 1;
+    if (k + 1 < nst) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's reads are done
+      wait_stages_in_flight(k + 2 < nst ? 1 : 0);          // step k+1 landed
+      __builtin_amdgcn_s_barrier();
+      if (k + 3 < nst) issue(s0 + k + 3, buf);
+      fetch(nb);
+    }
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+      for (int j = 0; j < kNT; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ac[kPairs[t][0]], bc[kPairs[t][1]][j],
+                                                         acc[j], 0, 0, 0);
+    buf = nb;
+  }
+
+  float* cz = c + (static_cast<int64_t>(z) * batch + bb) * Mp * Np;
+  const int m0 = mt * BM + wave * 32 + 4 * h;
+#pragma unroll
+  for (int j = 0; j < kNT; ++j) {
+    const int64_t n = static_cast<int64_t>(nt) * BN + j * 32 + l32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      cz[static_cast<int64_t>(m0 + (r & 3) + 8 * (r >> 2)) * Np + n] = acc[j][r];
+  }
+}
+
 // Y = A^T (sum_z M[z]) A (+ bias): one thread per (output channel, tile), consecutive
 // threads on consecutive tiles (coalesced reads of each position's M row).
 __global__ __launch_bounds__(256) void bg_output_f4_kernel(
@@ -1575,16 +1840,9 @@ __global__ __launch_bounds__(256) void bg_output_f4_kernel(
 // U-Net level's 2048 x 2048 layers read 268 MB of U per call instead of 604 MB.
 constexpr int kP2 = 16;
 
-__global__ __launch_bounds__(256) void bg_weight_f2_kernel(const float* __restrict__ w,
-                                                          float* __restrict__ a, int O, int R,
-                                                          int Mp, int ksteps, bool flip) {
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (idx >= static_cast<int64_t>(ksteps) * 16 * Mp) return;
-  const int k = static_cast<int>(idx & 15);
-  const int64_t rest = idx >> 4;
-  const int m = static_cast<int>(rest % Mp);
-  const int st = static_cast<int>(rest / Mp);
-  const int r = st * 16 + k;
+// G g G^T of (output channel m, reduction channel r): the 16 F(2x2) positions (0 outside)
+__device__ __forceinline__ void f2_weight_tile(const float* __restrict__ w, int O, int R, int m,
+                                               int r, bool flip, float (&v)[kP2]) {
   float g[3][3] = {};
   if (r < R && m < O) {
     const float* src = flip ? w + (static_cast<int64_t>(r) * O + m) * 9
@@ -1603,7 +1861,6 @@ __global__ __launch_bounds__(256) void bg_weight_f2_kernel(const float* __restri
     t[2][jc] = 0.5f * (g[0][jc] - g[1][jc] + g[2][jc]);
     t[3][jc] = g[2][jc];
   }
-  float v[kP2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     v[i * 4 + 0] = t[i][0];
@@ -1611,23 +1868,29 @@ __global__ __launch_bounds__(256) void bg_weight_f2_kernel(const float* __restri
     v[i * 4 + 2] = 0.5f * (t[i][0] - t[i][1] + t[i][2]);
     v[i * 4 + 3] = t[i][2];
   }
+}
+
+__global__ __launch_bounds__(256) void bg_weight_f2_kernel(const float* __restrict__ w,
+                                                          float* __restrict__ a, int O, int R,
+                                                          int Mp, int ksteps, bool flip) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 16 * Mp) return;
+  const int k = static_cast<int>(idx & 15);
+  const int64_t rest = idx >> 4;
+  const int m = static_cast<int>(rest % Mp);
+  const int st = static_cast<int>(rest / Mp);
+  float v[kP2];
+  f2_weight_tile(w, O, R, m, st * 16 + k, flip, v);
   const int64_t plane = static_cast<int64_t>(ksteps) * Mp * 16;
   float* dst = a + (static_cast<int64_t>(st) * Mp + m) * 16 + bg_slot(k, m);
 #pragma unroll
   for (int b = 0; b < kP2; ++b) dst[b * plane] = v[b];
 }
 
-__global__ __launch_bounds__(256) void bg_input_f2_kernel(const float* __restrict__ x,
-                                                         float* __restrict__ v, int R, int H,
-                                                         int W, int TW, int tpi, int P, int Np,
-                                                         int ksteps) {
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (idx >= static_cast<int64_t>(ksteps) * 16 * Np) return;
-  const int k = static_cast<int>(idx & 15);
-  const int64_t rest = idx >> 4;
-  const int t = static_cast<int>(rest % Np);
-  const int st = static_cast<int>(rest / Np);
-  const int c = st * 16 + k;
+// B^T d B of (tile t, channel c): the 16 F(2x2) positions (0 in the padding)
+__device__ __forceinline__ void f2_input_tile(const float* __restrict__ x, int R, int H, int W,
+                                              int TW, int tpi, int P, int t, int c,
+                                              float (&vv)[kP2]) {
   float d[4][4] = {};
   if (t < P && c < R) {
     const int n = t / tpi;
@@ -1654,7 +1917,6 @@ __global__ __launch_bounds__(256) void bg_input_f2_kernel(const float* __restric
     e[2][jc] = d[2][jc] - d[1][jc];
     e[3][jc] = d[1][jc] - d[3][jc];
   }
-  float vv[kP2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     vv[i * 4 + 0] = e[i][0] - e[i][2];
@@ -1662,10 +1924,56 @@ __global__ __launch_bounds__(256) void bg_input_f2_kernel(const float* __restric
     vv[i * 4 + 2] = e[i][2] - e[i][1];
     vv[i * 4 + 3] = e[i][1] - e[i][3];
   }
+}
+
+__global__ __launch_bounds__(256) void bg_input_f2_kernel(const float* __restrict__ x,
+                                                         float* __restrict__ v, int R, int H,
+                                                         int W, int TW, int tpi, int P, int Np,
+                                                         int ksteps) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 16 * Np) return;
+  const int k = static_cast<int>(idx & 15);
+  const int64_t rest = idx >> 4;
+  const int t = static_cast<int>(rest % Np);
+  const int st = static_cast<int>(rest / Np);
+  float vv[kP2];
+  f2_input_tile(x, R, H, W, TW, tpi, P, t, st * 16 + k, vv);
   const int64_t plane = static_cast<int64_t>(ksteps) * Np * 16;
   float* dst = v + (static_cast<int64_t>(st) * Np + t) * 16 + bg_slot(k, t);
 #pragma unroll
   for (int b = 0; b < kP2; ++b) dst[b * plane] = vv[b];
+}
+
+// F(2x2) EMU images: as bg_weight_f4_emu_kernel / bg_input_f4_emu_kernel, 16 positions.
+__global__ __launch_bounds__(256) void bg_weight_f2_emu_kernel(const float* __restrict__ w,
+                                                              float* __restrict__ a, int O, int R,
+                                                              int Mp, int ksteps, bool flip) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 4 * Mp) return;
+  const int g = static_cast<int>(idx & 3);
+  const int64_t rest = idx >> 2;
+  const int m = static_cast<int>(rest % Mp);
+  const int st = static_cast<int>(rest / Mp);
+  float v[4][kP2];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) f2_weight_tile(w, O, R, m, st * 16 + 4 * g + e, flip, v[e]);
+  bg_emu_store<kP2>(a, v, st, m, g, Mp, ksteps);
+}
+
+__global__ __launch_bounds__(256) void bg_input_f2_emu_kernel(const float* __restrict__ x,
+                                                             float* __restrict__ v, int R, int H,
+                                                             int W, int TW, int tpi, int P, int Np,
+                                                             int ksteps) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 4 * Np) return;
+  const int g = static_cast<int>(idx & 3);
+  const int64_t rest = idx >> 2;
+  const int t = static_cast<int>(rest % Np);
+  const int st = static_cast<int>(rest / Np);
+  float vv[4][kP2];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) f2_input_tile(x, R, H, W, TW, tpi, P, t, st * 16 + 4 * g + e, vv[e]);
+  bg_emu_store<kP2>(v, vv, st, t, g, Np, ksteps);
 }
 
 __global__ __launch_bounds__(256) void bg_output_f2_kernel(
@@ -1916,13 +2224,23 @@ constexpr int kBgTiles[][2] = {{4, 48}, {4, 64}, {4, 96}, {4, 128},
 int64_t bg_ksteps(int64_t red_channels) { return (red_channels + 31) / 32 * 2; }
 }  // namespace
 
-int bg_pick_bn(int64_t tiles, int kind) {
+bool bg_emu(int emu) {
+  static const bool dflt = [] {
+    const char* v = std::getenv("TGPIPE_BG_EMU");
+    return v == nullptr || *v == 0 || std::string(v) != "0";
+  }();
+  return emu < 0 ? dflt : emu != 0;
+}
+
+int bg_pick_bn(int64_t tiles, int kind, bool emu) {
   // The 128-row tile width that pads the tile count least; ties go to the width measured
   // fastest (benchmarks/bg_bench.py, profiles/r3/bg_bench.json): 48 for F(4x4) (128 on
-  // the widest grids), 128 then 96 for F(2x2).
+  // the widest grids), 128 then 96 for F(2x2).  The split-bf16 GEMM's tiles are 32-column
+  // multiples.
   static constexpr int kF4[] = {48, 64, 128, 96};
   static constexpr int kF2[] = {128, 96, 48, 64};
-  const int* order = kind == 2 ? kF2 : kF4;
+  static constexpr int kEmu[] = {128, 64, 96, 128};
+  const int* order = emu ? kEmu : (kind == 2 ? kF2 : kF4);
   int best = order[0];
   int64_t best_pad = bg_round(tiles, best);
   for (int i = 1; i < 4; ++i) {
@@ -1937,9 +2255,10 @@ int bg_pick_bn(int64_t tiles, int kind) {
 }
 
 BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
-               int bn, int splits, int kind, int waves, int sub) {
+               int bn, int splits, int kind, int waves, int sub, int emu) {
   BgPlan plan;
   plan.kind = kind == 2 ? 2 : 4;
+  plan.emu = bg_emu(emu);
   const int tile = plan.kind;
   const int64_t npos = plan.kind == 2 ? kP2 : kP;
   const int64_t P = n * ((h + tile - 1) / tile) * ((w + tile - 1) / tile);
@@ -1947,6 +2266,15 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
   plan.mp = bg_round(out_channels, kBgRowPad);
   bool valid = false;
   for (const auto& t : kBgTiles) valid |= t[0] == waves && t[1] == bn;
+  if (plan.emu) {  // 4 waves x bn 64 / 96 / 128, one step per stage
+    valid = waves == 4 && (bn == 64 || bn == 96 || bn == 128);
+    sub = 1;
+    if (!valid) {
+      waves = 4;
+      bn = bg_pick_bn(P, plan.kind, true);
+      valid = true;
+    }
+  }
   if (!valid) {
     // Auto: 128-row tiles (4 waves), which beat the 256-row ones on every measured U-Net
     // shape once the fragment reads were software-pipelined (profiles/r3/bg_bench.json)
@@ -1973,19 +2301,29 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
   // every split owns >= 1 pipeline stage
   plan.splits = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(plan.splits,
                                                                         plan.ksteps / plan.sub)));
-  plan.workspace = npos * plan.ksteps * 16 * plan.np + plan.splits * npos * plan.mp * plan.np;
+  // (split-bf16 V: 24 floats' worth of bytes per row and step instead of 16)
+  plan.workspace = npos * plan.ksteps * (plan.emu ? 24 : 16) * plan.np +
+                   plan.splits * npos * plan.mp * plan.np;
   return plan;
 }
 
-int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind) {
-  return (kind == 2 ? kP2 : kP) * bg_ksteps(red_channels) * 16 *
+int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind, int emu) {
+  return (kind == 2 ? kP2 : kP) * bg_ksteps(red_channels) * (bg_emu(emu) ? 24 : 16) *
          bg_round(out_channels, kBgRowPad);
 }
 
 void launch_bg_weight(const float* w, float* a, int64_t out_channels, int64_t red_channels,
-                      bool flip, int kind, hipStream_t stream) {
+                      bool flip, int kind, hipStream_t stream, int emu) {
   const int64_t mp = bg_round(out_channels, kBgRowPad);
   const int64_t ksteps = bg_ksteps(red_channels);
+  if (bg_emu(emu)) {
+    const int64_t total = ksteps * 4 * mp;
+    hipLaunchKernelGGL(kind == 2 ? bg_weight_f2_emu_kernel : bg_weight_f4_emu_kernel,
+                       dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, stream, w,
+                       a, static_cast<int>(out_channels), static_cast<int>(red_channels),
+                       static_cast<int>(mp), static_cast<int>(ksteps), flip);
+    return;
+  }
   const int64_t total = ksteps * 16 * mp;
   hipLaunchKernelGGL(kind == 2 ? bg_weight_f2_kernel : bg_weight_f4_kernel,
                      dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, stream, w, a,
@@ -2001,9 +2339,24 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
   const int64_t th = (h + tile - 1) / tile, tw = (w + tile - 1) / tile;
   const int64_t P = n * th * tw;
   float* v = ws;
-  float* cbuf = ws + npos * plan.ksteps * 16 * plan.np;
+  float* cbuf = ws + npos * plan.ksteps * (plan.emu ? 24 : 16) * plan.np;
   const int64_t vt = plan.ksteps * 16 * plan.np;
-  if (plan.kind == 2) {
+  if (plan.emu) {
+    const int64_t vt4 = plan.ksteps * 4 * plan.np;
+    const dim3 grid(static_cast<unsigned>((vt4 + 255) / 256));
+    if (plan.kind == 2)
+      hipLaunchKernelGGL(bg_input_f2_emu_kernel, grid, dim3(256), 0, stream, x, v,
+                         static_cast<int>(red_channels), static_cast<int>(h), static_cast<int>(w),
+                         static_cast<int>(tw), static_cast<int>(th * tw), static_cast<int>(P),
+                         static_cast<int>(plan.np), static_cast<int>(plan.ksteps));
+    else
+      hipLaunchKernelGGL((w & 3) == 0 ? bg_input_f4_emu_kernel<true> : bg_input_f4_emu_kernel<false>,
+                         grid, dim3(256), 0, stream, x, v, static_cast<int>(red_channels),
+                         static_cast<int>(h), static_cast<int>(w), static_cast<int>(tw),
+                         static_cast<int>(th * tw), static_cast<int>(P), static_cast<int>(plan.np),
+                         static_cast<int>(plan.ksteps),
+                         static_cast<uint32_t>(n * red_channels * h * w * 4));
+  } else if (plan.kind == 2) {
     hipLaunchKernelGGL(bg_input_f2_kernel, dim3(static_cast<unsigned>((vt + 255) / 256)),
                        dim3(256), 0, stream, x, v, static_cast<int>(red_channels),
                        static_cast<int>(h), static_cast<int>(w), static_cast<int>(tw),
@@ -2023,7 +2376,10 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
   const int64_t nwg = static_cast<int64_t>(mtiles) * ntiles * npos * plan.splits;
   using Gemm = void (*)(const float*, const float*, float*, int, int, int, int, int, int, int);
   Gemm gemm = bg_gemm_kernel<4, 64, 2>;
-  switch (plan.waves * 10000 + plan.bn * 10 + plan.sub) {
+  if (plan.emu) {
+    gemm = plan.bn == 64 ? bg_gemm_emu_kernel<64>
+           : plan.bn == 96 ? bg_gemm_emu_kernel<96> : bg_gemm_emu_kernel<128>;
+  } else switch (plan.waves * 10000 + plan.bn * 10 + plan.sub) {
     case 40481: gemm = bg_gemm_kernel<4, 48, 1>; break;
     case 40641: gemm = bg_gemm_kernel<4, 64, 1>; break;
     case 40961: gemm = bg_gemm_kernel<4, 96, 1>; break;

@@ -30,6 +30,7 @@ output tensors + skips stashed for other ranks, so checkpointing
 from collections import OrderedDict
 import contextlib
 import datetime
+import threading
 import time
 from typing import Any, Callable, Dict, Hashable, List, Optional, Sequence, Tuple, Union
 
@@ -106,12 +107,30 @@ def _shared_accumulators() -> Any:
     micro-batches on different streams by design, so the engine orders each accumulation
     after the producing lane (the ordering the lanes need) and warns about the mismatch;
     here it is intentional, and the warning is off for the duration of the backward.
+
+    The flag is process-global: nested or concurrent stages count their holders, and the
+    last one out restores what the flag was before the first one came in (a user's own
+    ``set_warn_on_accumulate_grad_stream_mismatch(False)`` stays in force).
     """
-    torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
+    global _accumulator_holders, _accumulator_saved
+    with _accumulator_lock:
+        if _accumulator_holders == 0:
+            _accumulator_saved = bool(torch._C._warn_on_accumulate_grad_stream_mismatch())
+            torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
+        _accumulator_holders += 1
     try:
         yield
     finally:
-        torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(True)
+        with _accumulator_lock:
+            _accumulator_holders -= 1
+            if _accumulator_holders == 0:
+                torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(
+                    _accumulator_saved)
+
+
+_accumulator_lock = threading.Lock()
+_accumulator_holders = 0
+_accumulator_saved = True
 
 
 class _RemoteSkipTracker(SkipTracker):
