@@ -19,9 +19,10 @@ The top-level ``value`` is the U-Net headline.  After it, every run also times
   is measured on the same box as the headline;
 * ``amoebanet``: AmoebaNet-D(18,256), n{N}m32 at the reference balance (n1m32, B=640
   at N=1), and at N=2 the reference's own denominator n2m1 (B=96, ``always``);
-* ``resnet`` (N <= 2): ResNet-101 pipeline-1 (B=220, m=2) at N=1, BASELINE.json's config
-  #2 (pipeline-2, chunks=32, ``always``) at N=2, and the reference's ResNet denominator
-  (no GPipe, B=118) on rank 0's GPU;
+* ``resnet``: ResNet-101 pipeline-1 (B=220, m=2) at N=1, BASELINE.json's config #2
+  (pipeline-2, chunks=32, ``always``) at N=2, the reference's pipeline-4 / -8 (B=5632,
+  m=256 / B=5400, m=150) at N=4 / 8, and the reference's ResNet denominator (no GPipe,
+  B=118) on rank 0's GPU;
 * for N > 1, one extra *diagnostic* step (not timed) in which every rank measures
   how long its streams waited for activations / gradients (``per_rank``).
 
@@ -95,11 +96,18 @@ AMOEBA_N2M1 = dict(name='n2m1', batch=96, chunks=1, balance=[7, 17], ref=26.733)
 # a P40 sizing: 15-image micro-batches leave an MI355X's GEMMs underfed (the stages run at
 # half of pipeline-1's per-image speed, profiles/r4/speedup_prediction.md), so the 32
 # micro-batches here hold pipeline-1's 110 images each (B = 3520).
+# pipeline-2 is therefore not the reference's p2 configuration and carries no P40 number
+# (``ref=None``; BASELINE.md's 135.539 is for B=25000, m=1667).  Pipeline-4 / -8 are the
+# reference's own (B=5632, m=256 / B=5400, m=150: 22 / 36 images per micro-batch).
 RESNET_EXPERIMENTS = {
     1: dict(name='pipeline-1', batch=220, chunks=2, balance=[370], checkpoint='except_last',
             ref=81.796),
-    2: dict(name='pipeline-2 (chunks=32, always)', batch=3520, chunks=32, balance=[135, 235],
-            checkpoint='always', ref=135.539),
+    2: dict(name='pipeline-2 (BASELINE config #2: chunks=32, always, 110-image micro-batches)',
+            batch=3520, chunks=32, balance=[135, 235], checkpoint='always', ref=None),
+    4: dict(name='pipeline-4', batch=5632, chunks=256, balance=[44, 92, 124, 110],
+            checkpoint='except_last', ref=265.958),
+    8: dict(name='pipeline-8', batch=5400, chunks=150,
+            balance=[26, 22, 33, 44, 44, 66, 66, 69], checkpoint='except_last', ref=411.662),
 }
 # the reference's ResNet speed-up denominator: ResNet-101 without GPipe, one GPU
 RESNET_BASELINE = dict(name='baseline', batch=118, ref=95.862)
@@ -133,7 +141,7 @@ def parse() -> argparse.Namespace:
     p.add_argument('--probe', choices=['auto', 'on', 'off'], default='auto',
                    help='one extra untimed step in which every rank measures its receive '
                         'waits (auto: N > 1)')
-    p.add_argument('--timeout', type=float, default=300.0,
+    p.add_argument('--timeout', type=float, default=120.0,
                    help='seconds any pipeline wait may take before the run fails (RCCL '
                         'watchdog and gloo waits): a dead or stuck rank ends the job')
     p.add_argument('--cudnn-benchmark', action='store_true',
@@ -167,7 +175,7 @@ def parse() -> argparse.Namespace:
                    help='replay each micro-batch of a stage as captured hipGraphs, transfers '
                         'issued between them (PipelineStage(graph_cells=True), '
                         'parallel/segments.py; instead of the one-GPU whole-step graph; '
-                        'auto: on for N > 1 and for AmoebaNet)')
+                        'auto: on for one-GPU AmoebaNet)')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -324,14 +332,16 @@ class Bench:
         # (auto: off -- with the two-stream cells it measured 280.3 vs 328.6 samples/s on one
         # box, profiles/r2/bench_amoeba_s13.md)
         wgrad_stream = choice(args.wgrad_stream, False)
-        # captured cells (parallel/segments.py): multi-rank stages replay each micro-batch's
-        # forward / recomputation / backward as hipGraphs, transfers in between -- host
-        # enqueue 4-5 % of device time on the U-Net p8 stages instead of 28-46 %
-        # (profiles/r4/stage_harness_unet_p8_ref_*.jsonl), so no rank's host sits on the
-        # pipeline's critical path
-        # (one GPU: AmoebaNet too -- three-stream cells in per-pass captures, 392.0 vs 389.4
-        # samples/s for the two-stream whole-step graph, profiles/r4/amoeba_n1_graph_modes.md)
-        graph_cells = choice(args.graph_cells, self.world > 1 or kind == 'amoebanet') and self.gpu
+        # captured cells (parallel/segments.py): one GPU, AmoebaNet -- three-stream cells in
+        # per-pass captures, 392.0 vs 389.4 samples/s for the two-stream whole-step graph
+        # (profiles/r4/amoeba_n1_graph_modes.md).  Multi-rank runs stay eager by default: in
+        # one-GPU stage emulation the captured stages ran within 0-2.5 % of the eager ones
+        # (U-Net p8 stages 134.3 / 267.3 / 191.6 vs 133.8 / 268.6 / 194.2 ms, AmoebaNet
+        # n8m32 stage 6 494.1 vs 506.6 ms: profiles/r4/stage_harness_*_ref_{eager,
+        # graph_cells}.jsonl), which does not pay for running RCCL receives into captured
+        # graphs' buffers before any multi-GPU node has (--graph-cells on to opt in).
+        graph_cells = choice(args.graph_cells, self.world == 1 and kind == 'amoebanet') \
+            and self.gpu
         stage = PipelineStage(self.build(kind), balance, device=self.device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
                               overlap_recompute=overlap, overlap_forward=overlap_fwd,
@@ -342,7 +352,10 @@ class Bench:
             from torchgpipe_amd.models.amoebanet import DEFAULT_CELL_STREAMS, set_cell_streams
             set_cell_streams(stage.partition, True)
             cell_streams = DEFAULT_CELL_STREAMS  # streams per cell (TGPIPE_CELL_STREAMS)
-        optimizer = torch.optim.SGD(stage.parameters(), lr=0.1)
+        # (a partition may hold no parameters at all -- pooling-only stages of a small model
+        # split eight ways -- and SGD refuses an empty list: nothing to update there)
+        params = list(stage.parameters())
+        optimizer = torch.optim.SGD(params, lr=0.1) if params else None
         x, target, loss_fn, shape = self.data(kind, batch, stage.is_first, stage.is_last)
         signature = signature_of(torch.empty(batch, *shape, device='meta'))
 
@@ -362,8 +375,9 @@ class Bench:
                 graph.step(x, target)  # type: ignore[arg-type]
                 return
             stage.train_step(x, target, loss_fn, signature=signature)
-            optimizer.step()
-            optimizer.zero_grad(set_to_none=True)
+            if optimizer is not None:
+                optimizer.step()
+                optimizer.zero_grad(set_to_none=True)
 
         if self.gpu:
             torch.cuda.reset_peak_memory_stats(self.device)
@@ -511,7 +525,19 @@ def main() -> None:
     batch, chunks, balance = exp['batch'], exp['chunks'], list(exp['balance'])
     probe = choice(args.probe, world > 1)
 
+    # wall seconds of every timed section (warm-up, capture and diagnostics included), so a
+    # multi-GPU run's budget can be checked section by section
+    section_s: Dict[str, float] = {}
+    t_sec = time.time()
+
+    def lap(name: str) -> None:
+        nonlocal t_sec
+        section_s[name] = round(time.time() - t_sec, 1)
+        b.log(f'section {name}: {section_s[name]} s')
+        t_sec = time.time()
+
     main_run = b.pipeline(kind, exp, balance, checkpoint, args.steps, 'headline', probe=probe)
+    lap('headline')
     elapsed = main_run['elapsed']
     tuned = None
     also = args.also_tuned == 'yes' or (args.also_tuned == 'auto' and world > 1
@@ -521,6 +547,7 @@ def main() -> None:
         tuned = {'balance': tuned_balance,
                  'value': round(batch * args.steps / t['elapsed'], 3),
                  'ms_per_step': round(1000 * t['elapsed'] / args.steps, 3)}
+        lap('tuned')
 
     sections = ({'baseline', 'amoebanet'} | ({'resnet'} if world in RESNET_EXPERIMENTS else set())
                 if kind == 'unet' else set()) \
@@ -535,6 +562,7 @@ def main() -> None:
         if bl is not None:
             baseline = summary(bl, None if args.tiny else UNET_BASELINE['ref'])
             baseline['experiment'] = 'baseline (no GPipe, rank 0 GPU)'
+        lap('baseline')
 
     amoeba = None
     if 'amoebanet' in sections and kind == 'unet':
@@ -559,6 +587,7 @@ def main() -> None:
             dr = b.pipeline('amoebanet', d, d['balance'], 'always', sec_steps, 'amoebanet-n2m1')
             amoeba['n2m1'] = summary(dr, None if args.tiny else d['ref'])
             amoeba['speedup_vs_n2m1'] = round(amoeba['value'] / amoeba['n2m1']['value'], 3)
+        lap('amoebanet')
 
     resnet = None
     if 'resnet' in sections and kind == 'unet' and world in RESNET_EXPERIMENTS:
@@ -577,6 +606,7 @@ def main() -> None:
             resnet['baseline'] = summary(rb, None if args.tiny else RESNET_BASELINE['ref'])
             resnet['speedup_vs_baseline'] = round(resnet['value'] / resnet['baseline']['value'],
                                                   3)
+        lap('resnet')
 
     if b.rank == 0:
         ref = None if args.tiny else exp.get('ref')
@@ -634,6 +664,7 @@ def main() -> None:
             record['resnet101'] = resnet
         if 'per_rank' in main_run:
             record['per_rank'] = main_run['per_rank']
+        record['section_s'] = section_s
         print(json.dumps(record), file=result_out, flush=True)
     if world > 1:
         dist.barrier()

@@ -17,13 +17,23 @@ MODELS = ('unet', 'amoebanet')
 
 
 def build(kind: str) -> nn.Sequential:
+    """``unet`` / ``amoebanet``: small models for 2-4 ranks.  ``unet-p8`` / ``amoebanet-p8``:
+    the benchmark architectures themselves -- U-Net(5,5) with all 241 layers (and all four
+    long skips), AmoebaNet-D(18) with all 24 layers -- at tiny widths, for the reference's
+    8-partition balances."""
     torch.manual_seed(7)
     if kind == 'unet':
         from torchgpipe_amd.models import unet
         model = unet(depth=3, num_convs=1, base_channels=8, input_channels=3, output_channels=1)
+    elif kind == 'unet-p8':
+        from torchgpipe_amd.models import unet
+        model = unet(depth=5, num_convs=5, base_channels=2, input_channels=3, output_channels=1)
     elif kind == 'amoebanet':
         from torchgpipe_amd.models import amoebanetd
         model = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
+    elif kind == 'amoebanet-p8':
+        from torchgpipe_amd.models import amoebanetd
+        model = amoebanetd(num_classes=10, num_layers=18, num_filters=16)
     else:
         raise ValueError(kind)
     for m in model.modules():
@@ -34,9 +44,10 @@ def build(kind: str) -> nn.Sequential:
 
 def data(kind: str, device: torch.device):
     gen = torch.Generator().manual_seed(11)
-    if kind == 'unet':
-        x = torch.rand(6, 3, 16, 16, generator=gen)
-        t = torch.rand(6, 1, 16, 16, generator=gen)
+    if kind.startswith('unet'):
+        side = 64 if kind == 'unet-p8' else 16  # five 2x poolings: a 2x2 bottom plane
+        x = torch.rand(6, 3, side, side, generator=gen)
+        t = torch.rand(6, 1, side, side, generator=gen)
     else:
         x = torch.rand(6, 3, 224, 224, generator=gen)
         t = torch.randint(10, (6,), generator=gen)
@@ -44,7 +55,7 @@ def data(kind: str, device: torch.device):
 
 
 def loss_fn(kind: str):
-    return F.binary_cross_entropy_with_logits if kind == 'unet' else F.cross_entropy
+    return F.binary_cross_entropy_with_logits if kind.startswith('unet') else F.cross_entropy
 
 
 def balance(kind: str, world: int) -> list:
@@ -55,14 +66,24 @@ def balance(kind: str, world: int) -> list:
         ('unet', 4): [8, 10, 6, n - 24],     # rank 0 stashes for two different ranks
         ('amoebanet', 2): [3, n - 3],        # (x, skip) tuple boundary
         ('amoebanet', 4): [2, 2, 2, n - 6],
+        # the reference's 8-partition benchmark balances (benchmarks/unet-speed/main.py:23-68,
+        # benchmarks/amoebanetd-speed/main.py:35-96)
+        ('unet-p8', 8): [16, 27, 31, 44, 22, 57, 27, 17],
+        ('amoebanet-p8', 8): [2, 2, 2, 3, 3, 4, 4, 4],
     }
     return table[(kind, world)]
 
 
-def reference(kind: str, device: torch.device, chunks: int):
-    """Gradients and loss of the whole model on one device, same micro-batching."""
-    model = build(kind).to(device)
-    x, t = data(kind, device)
+def _cast(x: torch.Tensor, dtype) -> torch.Tensor:
+    return x.to(dtype) if dtype is not None and x.is_floating_point() else x
+
+
+def reference(kind: str, device: torch.device, chunks: int, dtype=None):
+    """Gradients and loss of the whole model on one device, same micro-batching
+    (``dtype``: e.g. float64 for the deep tiny-width models, whose fp32 gradients differ
+    from fp64 by percents under any summation order)."""
+    model = build(kind).to(device=device, dtype=dtype)
+    x, t = (_cast(v, dtype) for v in data(kind, device))
     fn = loss_fn(kind)
     total = float(x.size(0))
     loss_sum = 0.0
@@ -91,18 +112,22 @@ def stage_worker(rank: int, world: int, kind: str, chunks: int, checkpoint: str,
     options = dict(options or {})
     cell_streams = options.pop('cell_streams', False)
     steps = options.pop('steps', 2)
+    dtype = options.pop('dtype', None)
     if device_type == 'cuda':
         device = torch.device('cuda', rank)
     elif device_type == 'cuda-shared':
         device = torch.device('cuda', 0)
     else:
         device = torch.device('cpu')
-    stage = PipelineStage(build(kind), balance(kind, world), device=device, chunks=chunks,
+    model = build(kind)
+    if dtype is not None:
+        model = model.to(dtype)
+    stage = PipelineStage(model, balance(kind, world), device=device, chunks=chunks,
                           checkpoint=checkpoint, timeout=60, **options)
     if cell_streams:
         from torchgpipe_amd.models.amoebanet import set_cell_streams
         set_cell_streams(stage.partition, True)
-    x, t = data(kind, device)
+    x, t = (_cast(v, dtype) for v in data(kind, device))
     loss = None
     phases = []
     for _ in range(steps):

@@ -40,8 +40,12 @@ def _run(nproc: int, *extra: str) -> dict:
 
 
 @pytest.mark.parametrize('nproc,model', [(1, 'unet'), (2, 'unet'), (2, 'amoebanet'),
-                                         (1, 'resnet')])
+                                         (1, 'resnet'), (4, 'unet'), (8, 'unet'),
+                                         (8, 'amoebanet')])
 def test_bench_json_contract(nproc, model):
+    """The driver's N = 1 / 2 / 4 / 8 invocations (``torch.distributed.run``, one rank per
+    GPU; here gloo CPU ranks and the tiny model variants): every section runs at every N,
+    the 8-rank run included, and reports its wall time."""
     rec = _run(nproc, '--model', model)
     assert KEYS <= set(rec)
     assert rec['n_gpus'] == nproc and rec['steps'] == 1 and rec['warmup'] == 1
@@ -63,10 +67,12 @@ def test_bench_json_contract(nproc, model):
         assert amoeba['value'] > 0 and amoeba['steps'] == 1
         if nproc == 2:
             assert amoeba['n2m1']['chunks'] == 1 and amoeba['speedup_vs_n2m1'] > 0
-        # ResNet-101 section (tiny stand-in): pipeline-1 at N=1, config #2's shape at N=2
+        # ResNet-101 section (tiny stand-in): pipeline-1 at N=1, config #2's shape at N=2,
+        # the reference's pipeline-4 / -8 at N=4 / 8
         res = rec['resnet101']
-        assert res['value'] > 0 and res['checkpoint'] == ('except_last' if nproc == 1
-                                                           else 'always')
+        assert res['value'] > 0 and res['checkpoint'] == ('always' if nproc == 2
+                                                           else 'except_last')
+        assert set(rec['section_s']) == {'headline', 'baseline', 'amoebanet', 'resnet'}
         # with its own no-GPipe denominator (the reference's ResNet baseline, B=118)
         assert res['baseline']['value'] > 0
         assert res['speedup_vs_baseline'] == pytest.approx(

@@ -175,3 +175,81 @@ def test_graph_cells_deferred_batch_norm_commits():
             torch.testing.assert_close(bb, ba, rtol=1e-5, atol=1e-6, msg=name)
         else:
             assert torch.equal(bb, ba), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('graph_warmup', [1, 2])
+def test_graph_cells_accumulate_over_train_steps_like_eager(graph_warmup):
+    """Two ``train_step`` calls before ``optimizer.step()`` (gradient accumulation) give
+    eager's summed gradients in every phase -- including the capture step with a single
+    warm-up step, whose captures meet the weight-transform caches empty -- and a parameter
+    no backward reaches keeps ``.grad`` None."""
+    dev = torch.device('cuda', 0)
+    base, shape, classes = _models('unet')
+    unused = nn.Parameter(torch.ones(3, device=dev))
+    a, b = copy.deepcopy(base), copy.deepcopy(base)
+    b.register_parameter('unused_weight', nn.Parameter(unused.detach().clone()))
+    sa = PipelineStage(a, [len(a)], device=dev, chunks=4)
+    sb = PipelineStage(b, [len(b)], device=dev, chunks=4, graph_cells=True,
+                       graph_warmup=graph_warmup)
+    gen = torch.Generator(device=dev).manual_seed(7)
+    phases = []
+    for step in range(5):
+        for _ in range(2):
+            x, y, loss_fn = _batch('unet', shape, classes, gen, dev)
+            sa.train_step(x, y, loss_fn)
+            sb.train_step(x, y, loss_fn)
+            phases.append(sb.graph_phase)
+        torch.cuda.synchronize()
+        for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+            scale = pa.grad.abs().max().item() + 1e-12
+            torch.testing.assert_close(pb.grad, pa.grad, rtol=1e-4, atol=1e-5 * scale,
+                                       msg=lambda m: f'step {step} {name}: {m}')
+        if 'replay' in phases:
+            assert b.unused_weight.grad is None
+        with torch.no_grad():
+            for pa, pb in zip(a.parameters(), b.parameters()):
+                pa.sub_(0.05 * pa.grad)
+                pb.copy_(pa)
+        for p in a.parameters():
+            p.grad = None
+        for p in b.parameters():
+            p.grad = None
+    assert 'capture' in phases and phases[-1] == 'replay'
+
+
+@pytest.mark.gpu
+def test_graph_cells_zero_grad_in_place_between_steps():
+    """``zero_grad(set_to_none=False)`` between steps: the static buffers are zeroed in
+    place by the user and the replays accumulate from zero."""
+    dev = torch.device('cuda', 0)
+    base, shape, classes = _models('unet')
+    a, b = copy.deepcopy(base), copy.deepcopy(base)
+    sa = PipelineStage(a, [len(a)], device=dev, chunks=2)
+    sb = PipelineStage(b, [len(b)], device=dev, chunks=2, graph_cells=True)
+    oa = torch.optim.SGD(a.parameters(), lr=0.05)
+    ob = torch.optim.SGD(b.parameters(), lr=0.05)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    for step in range(5):
+        x, y, loss_fn = _batch('unet', shape, classes, gen, dev)
+        sa.train_step(x, y, loss_fn)
+        sb.train_step(x, y, loss_fn)
+        torch.cuda.synchronize()
+        for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+            scale = pa.grad.abs().max().item() + 1e-12
+            torch.testing.assert_close(pb.grad, pa.grad, rtol=1e-4, atol=1e-5 * scale,
+                                       msg=lambda m: f'step {step} {name}: {m}')
+        oa.step()
+        with torch.no_grad():
+            for pa, pb in zip(a.parameters(), b.parameters()):
+                pb.copy_(pa)
+        oa.zero_grad(set_to_none=False)
+        ob.zero_grad(set_to_none=False)
+    assert sb.graph_phase == 'replay'
+
+
+def test_graph_cells_reject_cumulative_deferred_batch_norm():
+    from torchgpipe_amd.batchnorm import DeferredBatchNorm
+    model = nn.Sequential(nn.Conv2d(3, 4, 1), DeferredBatchNorm(4, momentum=None, chunks=2))
+    with pytest.raises(ValueError, match='momentum=None'):
+        PipelineStage(model, [2], chunks=2, graph_cells=True)

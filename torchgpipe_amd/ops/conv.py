@@ -169,6 +169,13 @@ class _TransformCache:
         if hit is not None and hit[0] == key:
             _await(hit[1], hit[2])
             return hit[1]
+        if weight.is_cuda and torch.cuda.is_current_stream_capturing():
+            # Inside a hipGraph capture the cache is read, never written: an entry created
+            # here would live in that graph's private pool with no ready event, and another
+            # graph replayed on another lane could hit it before this graph has run (a
+            # stage with one warm-up step captures before any cached step).  The graph
+            # derives its own copy on every replay instead.
+            return _derive(weight, slot)
         if hit is not None:  # stale: release before transforming again
             _CACHE_BYTES[dev] -= hit[1].numel() * hit[1].element_size()
             del self._entries[slot]

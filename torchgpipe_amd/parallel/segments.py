@@ -32,8 +32,13 @@ How static addresses are kept without copies:
   read in place; the first stage copies its micro-batch into a persistent input buffer;
 * derived weights (Winograd transforms, transposes, grouped-GEMM concatenations) are
   refreshed *in place* at the start of every step (``ops.conv.refresh_step_caches``);
-* parameter gradients are allocated before the capture and re-attached and zeroed at the
-  start of every step (the replays accumulate into them);
+* parameter gradients are allocated before the capture; the replays accumulate into them.
+  At the start of a step a buffer is zeroed only when the user released the gradient
+  (``zero_grad(set_to_none=True)``: ``.grad`` is None) -- a ``.grad`` still attached keeps
+  its value and the step adds to it, as eager autograd does (gradient accumulation over
+  several ``train_step`` calls); a ``.grad`` the user replaced is copied into the buffer
+  first.  Parameters that no captured backward reaches keep ``.grad`` None, as in eager
+  mode (an optimizer then skips them);
 * dropout reads a device-resident Philox state per cell (``utils.rng.PhiloxSlot``) that
   the host fills with freshly reserved ``(seed, offset)`` values before the step's replays,
   so masks change every step and ``F_i`` / ``R_i`` agree bit for bit.
@@ -139,6 +144,7 @@ class Segments:
         self.cells = [SegmentCell(i, i < stop, rng.PhiloxSlot(self.slots[i]))
                       for i in range(cells)]
         self.grads: List[Tuple[Tensor, Tensor]] = []
+        self.used: set = set()  # ids of the parameters the captured backwards reach
         self.pending: List[Any] = []
         self._zeros: List[Tensor] = []
         # host seconds spent inside graph launches (hipGraphLaunch enqueues every node;
@@ -155,27 +161,52 @@ class Segments:
         return 'capture' if self.steps > self.warmup else 'eager'
 
     def begin_step(self) -> str:
-        """Start a step: returns its phase.  Capture / replay steps get static, zeroed
-        gradients and, for replays, fresh Philox values in every cell's slot."""
+        """Start a step: returns its phase.  Capture / replay steps attach the static
+        gradient buffers -- zeroed where the user released ``.grad``, holding the user's
+        gradient otherwise, so the step accumulates like eager autograd -- and replays get
+        fresh Philox values in every cell's slot."""
         self.steps += 1
         phase = self.phase
         if phase == 'capture':
             self.grads = []
+            self.used = set()
             for p in self.partition.parameters():
                 if not p.requires_grad:
                     continue
-                if p.grad is None or not p.grad.is_contiguous() or p.grad.dtype != p.dtype:
-                    p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                self.grads.append((p, p.grad))
-        if phase in ('capture', 'replay'):
+                g = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                if p.grad is not None:
+                    g.copy_(p.grad)
+                p.grad = g
+                self.grads.append((p, g))
+        elif phase == 'replay':
+            zero = []
             for p, g in self.grads:
-                if p.grad is not g:
+                if p.grad is None:
                     p.grad = g
-            if self.grads:
-                torch._foreach_zero_([g for _, g in self.grads])
+                    zero.append(g)
+                elif p.grad is not g:
+                    g.copy_(p.grad)
+                    p.grad = g
+            if zero:
+                torch._foreach_zero_(zero)
         if phase == 'replay':
             self._fill_slots(self.cells)
         return phase
+
+    def _note_reached(self, outputs: Sequence[Tensor]) -> None:
+        """Record the parameters the autograd graph of ``outputs`` reaches (their
+        AccumulateGrad nodes), before a backward capture consumes that graph."""
+        seen = set()
+        todo = [t.grad_fn for t in outputs if t.grad_fn is not None]
+        while todo:
+            fn = todo.pop()
+            if fn is None or fn in seen:
+                continue
+            seen.add(fn)
+            var = getattr(fn, 'variable', None)
+            if var is not None:
+                self.used.add(id(var))
+            todo.extend(nxt for nxt, _ in fn.next_functions if nxt is not None)
 
     def _fill_slots(self, cells: Sequence[SegmentCell]) -> None:
         """Reserve the cells' Philox counters from the device generator and write the
@@ -302,6 +333,7 @@ class Segments:
                 else:
                     cell.gouts.append(g.detach() if keep else g.detach().clone())
             pairs = [(y, g) for y, g in zip(cell.rec_out, cell.gouts) if g is not None]
+            self._note_reached([p[0] for p in pairs])
             graph = torch.cuda.CUDAGraph()
             with _capturing(graph, self.streams[k], self.pools[k]):
                 if pairs:
@@ -338,6 +370,16 @@ class Segments:
         if not self.captured and self.phase == 'capture':
             self.pending = gradacc.pending_snapshot(self.device)
             self.captured = all(c.bwd is not None for c in self.cells)
+            if self.captured:
+                # parameters no captured backward reaches get no gradient, as in eager mode
+                # (their buffers held the user's gradient or zeros: give the former back)
+                keep = []
+                for p, g in self.grads:
+                    if id(p) in self.used:
+                        keep.append((p, g))
+                    elif p.grad is g:
+                        p.grad = None if not bool(g.any()) else g
+                self.grads = keep
         elif self.captured:
             gradacc.register_pending(self.device, self.pending)
         for c in self.cells:

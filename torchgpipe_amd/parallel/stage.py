@@ -339,6 +339,14 @@ class PipelineStage:
         if graph_warmup < 1:
             raise ValueError('graph_cells needs at least one eager warm-up step')
         self.graph_cells = graph_cells and device.type == 'cuda'
+        if graph_cells:
+            from torchgpipe_amd.batchnorm import DeferredBatchNorm as _DBN
+            if any(isinstance(m, _DBN) and m.momentum is None
+                   for m in self.partition.modules()):
+                # the cumulative average's factor 1/n is read on the host at commit time:
+                # a captured commit would freeze it
+                raise ValueError('graph_cells does not support DeferredBatchNorm with '
+                                 'momentum=None (cumulative moving average)')
         self.graph_warmup = graph_warmup
         self._segments: Optional[Any] = None
         self._seg_key: Optional[Tuple[Any, ...]] = None
