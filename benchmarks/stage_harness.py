@@ -51,6 +51,22 @@ def build(kind: str, dev: torch.device) -> torch.nn.Sequential:
         return resnet101(num_classes=1000)
 
 
+def sent_bytes(transport: LoopbackP2P) -> Dict[str, int]:
+    """``{'act->j' / 'skip->j': bytes}`` of micro-batch 0's sends."""
+    out: Dict[str, int] = {}
+    for (kind, i, dst), metas in transport._sent.items():
+        if i != 0 or kind not in ('act', 'skip'):
+            continue
+        nbytes = 0
+        for m in metas:
+            numel = 1
+            for d in m.shape:
+                numel *= d
+            nbytes += numel * torch.empty(0, dtype=m.dtype).element_size()
+        out[f'{kind}->{dst}'] = out.get(f'{kind}->{dst}', 0) + nbytes
+    return out
+
+
 def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, object]:
     torch.manual_seed(0)
     model = build(args.model, dev).train()
@@ -75,9 +91,11 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
     lanes = {'auto': args.model == 'unet', 'on': True, 'off': False}[args.lanes]
     # placeholder transport until the stage knows its skip routes
     transport = LoopbackP2P(dev, acts, atomic, {})
+    # (as bench.py: ResNet-101 recomputes on a lane too, forward lanes are U-Net's only)
+    recompute_lane = lanes or (args.lanes == 'auto' and args.model == 'resnet101')
     stage = PipelineStage(model, args.balance, rank=k, device=dev, chunks=args.chunks,
                           checkpoint=args.checkpoint, transport=transport,
-                          overlap_recompute=lanes, overlap_forward=lanes,
+                          overlap_recompute=recompute_lane, overlap_forward=lanes,
                           graph_cells=args.graph_cells)
     skips: Dict[int, List[torch.Tensor]] = {}
     for src, key in stage.in_skips:
@@ -142,7 +160,11 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
            'idle_fwd_graph_launch_ms': None if idle_launch_ms is None
            else round(idle_launch_ms, 3),
            'warmup_s': round(warm_s, 1),
-           'peak_mem_gib': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)}
+           'peak_mem_gib': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
+           # bytes this stage sends per micro-batch, per (kind, destination stage): the
+           # boundary activation and the cross-stage skips (their gradients come back the
+           # same size) -- the transfer model of scripts/r5/predict.py
+           'sent_bytes': sent_bytes(transport)}
     del stage, optimizer, model, x, target, acts, skips, transport
     torch.cuda.empty_cache()
     torch.cuda.reset_peak_memory_stats(dev)

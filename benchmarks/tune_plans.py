@@ -24,7 +24,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 UNET_MICRO = (40, 16, 32)       # pipeline-1 80/2, -2 512/32 and -8 640/40, -4 512/16
 AMOEBA_MICRO = (20, 40, 36, 96)  # n1m32 640/32, n2/n8 1280/32, n4 1152/32, n2m1 96/1
-RESNET_MICRO = (110, 15)        # pipeline-1 220/2, pipeline-2 480/32 (bench.py)
+# pipeline-1 220/2, pipeline-2 3520/32, the reference's pipeline-4 5632/256 and -8 5400/150,
+# its pipeline-2 25000/1667
+RESNET_MICRO = (110, 22, 36, 15)
 
 
 def run(model: torch.nn.Module, micro: int, shape, target_fn) -> None:
