@@ -76,17 +76,18 @@ UNET_EXPERIMENTS = {
 }
 # the reference's speed-up denominator: U-Net without GPipe, one GPU
 UNET_BASELINE = dict(name='baseline', batch=40, ref=28.500)
-# AmoebaNet tuned balances: every layer timed as its own stage at micro-batch 40 (32
-# micro-batches, three-stream cells: profiles/r3/stage_harness_amoeba_layers_mb40.json),
-# min-max partitions by scripts/balance_from_layers.py: predicted n2 854 vs 735, n4 1353 vs
-# 1217, n8 2536 vs 2118 samples/s for the reference balances (profiles/r3/speedup_prediction.md).
+# AmoebaNet tuned balances: n4 from round 3 (every layer timed as its own stage at
+# micro-batch 40, min-max partitioned: profiles/r3/speedup_prediction.md); n2 / n8 searched
+# in round 5 with the step simulator at 100 GB/s links (scripts/r5/tune_transfer.py) and
+# measured stage by stage (profiles/r5/harness/*_search.json): n2 [10, 14] predicts 1.784x
+# over n2m1 where round 3's [11, 13] predicts 1.679x, n8 4.991x vs 4.956x.
 AMOEBA_EXPERIMENTS = {
     1: dict(name='n1m32', batch=640, chunks=32, balance=[24], tuned=[24], ref=None),
-    2: dict(name='n2m32', batch=1280, chunks=32, balance=[9, 15], tuned=[11, 13], ref=47.386),
+    2: dict(name='n2m32', batch=1280, chunks=32, balance=[9, 15], tuned=[10, 14], ref=47.386),
     4: dict(name='n4m32', batch=1152, chunks=32, balance=[3, 6, 7, 8], tuned=[5, 6, 6, 7],
             ref=72.412),
     8: dict(name='n8m32', batch=1280, chunks=32, balance=[2, 2, 2, 3, 3, 4, 4, 4],
-            tuned=[2, 3, 3, 3, 3, 3, 3, 4], ref=132.413),
+            tuned=[2, 2, 3, 3, 3, 3, 3, 5], ref=132.413),
 }
 # the reference's AmoebaNet speed-up denominator (benchmarks/amoebanetd-speed/main.py:39-45)
 AMOEBA_N2M1 = dict(name='n2m1', batch=96, chunks=1, balance=[7, 17], ref=26.733)
@@ -580,6 +581,14 @@ def main() -> None:
         amoeba['cell_streams'] = ar['cell_streams']
         amoeba['hipgraph'] = ar['hipgraph']
         amoeba['graph_cells'] = ar['graph_cells']
+        a_tuned = list(aexp.get('tuned', aexp['balance']))
+        if world > 1 and not args.tiny and a_tuned != list(aexp['balance']):
+            # the MI355X-searched balance too (AMOEBA_EXPERIMENTS 'tuned')
+            at = b.pipeline('amoebanet', aexp, a_tuned, 'except_last', sec_steps,
+                            'amoebanet-tuned')
+            amoeba['tuned'] = {'balance': a_tuned,
+                               'value': round(aexp['batch'] * sec_steps / at['elapsed'], 3),
+                               'ms_per_step': round(1000 * at['elapsed'] / sec_steps, 3)}
         if world == 2:
             d = dict(AMOEBA_N2M1)
             if args.tiny:
