@@ -177,6 +177,14 @@ def parse() -> argparse.Namespace:
                         'issued between them (PipelineStage(graph_cells=True), '
                         'parallel/segments.py; instead of the one-GPU whole-step graph; '
                         'auto: on for one-GPU AmoebaNet)')
+    p.add_argument('--stripes', choices=['auto', 'on', 'off'], default='auto',
+                   help='multi-path transfers: messages of at least --stripe-mb also travel '
+                        'through up to 3 idle ranks over otherwise unused links '
+                        '(PipelineStage(stripes=...), parallel/stripes.py; planned from the '
+                        'first step, so the warm-up runs until the plan exists; auto: on at '
+                        'N >= 3)')
+    p.add_argument('--stripe-mb', type=float, default=16.0,
+                   help='smallest striped message, MB')
     p.add_argument('--profile-steps', type=int, default=0,
                    help='after timing, run N more steps under torch.profiler (rank 0)')
     return p.parse_args()
@@ -343,10 +351,14 @@ class Bench:
         # graphs' buffers before any multi-GPU node has (--graph-cells on to opt in).
         graph_cells = choice(args.graph_cells, self.world == 1 and kind == 'amoebanet') \
             and self.gpu
+        # multi-path transfers (parallel/stripes.py): U-Net p8's 226 MB skip and AmoebaNet
+        # n8's 321 MB boundary outrun one xGMI link (profiles/r5/speedup_prediction.md)
+        stripes = choice(args.stripes, self.world >= 3)
         stage = PipelineStage(self.build(kind), balance, device=self.device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
                               overlap_recompute=overlap, overlap_forward=overlap_fwd,
-                              wgrad_stream=wgrad_stream, graph_cells=graph_cells)
+                              wgrad_stream=wgrad_stream, graph_cells=graph_cells,
+                              stripes=max(1, int(args.stripe_mb * 1e6)) if stripes else None)
         if args.channels_last and not unet:
             stage.partition.to(memory_format=torch.channels_last)
         if cell_streams:
@@ -387,6 +399,8 @@ class Bench:
             settle = lambda: graph.captured  # noqa: E731
         elif graph_cells:
             settle = lambda: stage._segments is not None and stage._segments.captured  # noqa: E731
+        elif stripes:  # the step that plans the stripes (and opens relay links) is untimed
+            settle = lambda: stage.stripes_ready  # noqa: E731
         res: Dict[str, Any] = self.timed(step, steps, args.warmup, tag, settle=settle)
         res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
                    steps=steps, overlap_recompute=overlap,
@@ -394,7 +408,8 @@ class Bench:
                    cell_streams=min(int(cell_streams), _capture_streams())
                    if graph is not None and cell_streams else int(cell_streams),
                    overlap_forward=overlap_fwd, wgrad_stream=wgrad_stream,
-                   hipgraph=graph is not None, graph_cells=graph_cells)
+                   hipgraph=graph is not None, graph_cells=graph_cells,
+                   striped_routes=stage.striped_routes)
         if probe and graph is None:
             # one untimed diagnostic step: per-rank receive waits and busy time
             mine = stage.probe_step(step)
@@ -581,6 +596,7 @@ def main() -> None:
         amoeba['cell_streams'] = ar['cell_streams']
         amoeba['hipgraph'] = ar['hipgraph']
         amoeba['graph_cells'] = ar['graph_cells']
+        amoeba['striped_routes'] = ar['striped_routes']
         a_tuned = list(aexp.get('tuned', aexp['balance']))
         if world > 1 and not args.tiny and a_tuned != list(aexp['balance']):
             # the MI355X-searched balance too (AMOEBA_EXPERIMENTS 'tuned')
@@ -609,6 +625,7 @@ def main() -> None:
         resnet['experiment'] = rexp['name']
         resnet['hipgraph'] = rr['hipgraph']
         resnet['graph_cells'] = rr['graph_cells']
+        resnet['striped_routes'] = rr['striped_routes']
         rb = b.plain('resnet', 4 if args.tiny else RESNET_BASELINE['batch'], sec_steps,
                      'resnet-baseline')
         if rb is not None:
@@ -659,6 +676,7 @@ def main() -> None:
                 'wgrad_stream': main_run['wgrad_stream'],
                 'overlap_forward': main_run['overlap_forward'],
                 'graph_cells': main_run['graph_cells'],
+                'striped_routes': main_run['striped_routes'],
             },
             'tuned': tuned,
         }

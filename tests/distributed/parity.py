@@ -138,7 +138,10 @@ def stage_worker(rank: int, world: int, kind: str, chunks: int, checkpoint: str,
         phases.append(stage.graph_phase)
     if device.type == 'cuda':
         torch.cuda.synchronize(device)
-    return {'grads': [p.grad.detach().cpu().clone() for p in stage.parameters()],
+    plans = [v for v in stage._stripe_plans.values() if not isinstance(v, (list, str))]
+    return {'stripes': dict(plans[0].stripes) if plans else {},
+            'relay_jobs': [tuple(j[:2]) for j in plans[0].jobs] if plans else [],
+            'grads': [p.grad.detach().cpu().clone() for p in stage.parameters()],
             'loss': None if loss is None else loss.item(),
             'skip_peers': sorted({d for d, _ in stage.out_skips} | {s for s, _ in stage.in_skips}),
             'phases': phases}

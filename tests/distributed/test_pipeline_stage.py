@@ -249,6 +249,30 @@ def test_reference_eight_partition_balances_match_one_process(tmp_path, kind):
         assert sum(1 for r in results if r['skip_peers']) >= 4, [r['skip_peers'] for r in results]
 
 
+@pytest.mark.parametrize('kind', ['unet-p8', 'amoebanet-p8'])
+def test_striped_transfers_match_one_process(tmp_path, kind):
+    """Multi-path transfers (``parallel/stripes.py``) on the 8-rank topologies: with a
+    1-byte threshold every route of one message kind is striped over idle ranks.  Step 1
+    records, step 2 plans and runs striped, step 3 runs striped again (relay rings reused);
+    the gradients equal one process in float64, and the plan really relays."""
+    chunks = 3
+    results = run(parity.stage_worker, 8, tmp_path, kind, chunks, 'except_last', 'cpu',
+                  {'dtype': torch.float64, 'stripes': 1, 'steps': 3})
+    grads, loss = parity.reference(kind, torch.device('cpu'), chunks, dtype=torch.float64)
+    parity.assert_parity(results, grads, loss, rel=1e-9)
+    plans = [r['stripes'] for r in results]
+    assert all(p == plans[0] for p in plans), plans  # every rank planned alike
+    print(kind, 'striped routes:', plans[0])
+    assert plans[0], 'nothing striped'
+    jobs = [j for r in results for j in r['relay_jobs']]
+    assert jobs and all(j in plans[0] for j in jobs), (jobs, plans[0])
+    # a relay never relays a route it is an end of, nor over a link the pipeline uses
+    for rank, r in enumerate(results):
+        for src, dst in r['relay_jobs']:
+            assert rank not in (src, dst)
+            assert rank in plans[0][(src, dst)]
+
+
 # -- failure detection: a dead or mis-ordered peer raises within the timeout --------------
 
 def _dead_peer_worker(rank, world):

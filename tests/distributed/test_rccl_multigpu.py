@@ -70,3 +70,19 @@ def test_rccl_eager_communicator_with_link_groups(tmp_path, kind):
                   backend='nccl', timeout=120)
     grads, loss = parity.reference(kind, torch.device('cuda', 0), 3)
     parity.assert_parity(results, grads, loss, rel=1e-4)
+
+
+@pytest.mark.parametrize('kind,world', [('amoebanet', 4), ('unet-p8', 8)])
+def test_rccl_striped_transfers_match_single_gpu(tmp_path, kind, world):
+    """Multi-path transfers over RCCL (``parallel/stripes.py``): relay chains stream-ordered
+    on each relay's route streams, relay links opened in one sorted order; every route
+    of one message kind striped (1-byte threshold), record + plan + two striped steps."""
+    if torch.cuda.device_count() < world:
+        pytest.skip(f'needs {world} GPUs')
+    chunks = 3
+    results = run(parity.stage_worker, world, tmp_path, kind, chunks, 'except_last', 'cuda',
+                  dict(stripes=1, steps=4), backend='nccl-lazy', timeout=120)
+    grads, loss = parity.reference(kind, torch.device('cuda', 0), chunks)
+    # (fp32 on the 241-layer U-Net: summation order differs between one and eight GPUs)
+    parity.assert_parity(results, grads, loss, rel=1e-4 if world == 4 else 1e-3)
+    assert results[0]['stripes'] and any(r['relay_jobs'] for r in results)

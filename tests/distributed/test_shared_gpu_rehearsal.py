@@ -49,3 +49,25 @@ def test_overlapped_stage_matches_one_gpu(tmp_path, kind, checkpoint, options):
     if options.get('graph_cells'):
         want = ['eager', 'eager', 'capture', 'replay', 'replay']
         assert all(r['phases'] == want for r in results), [r['phases'] for r in results]
+
+
+@pytest.mark.parametrize('kind,options', [
+    ('amoebanet', dict(cell_streams=True, stripes=1, steps=3)),
+    # (a 4-rank U-Net's skips leave no idle detour: nothing would be striped)
+    ('amoebanet', dict(cell_streams=True, overlap_recompute=True, stripes=1, steps=3)),
+])
+def test_striped_stage_matches_one_gpu(tmp_path, kind, options):
+    """Multi-path transfers (``parallel/stripes.py``) with device tensors: four ranks on
+    ``cuda:0``, the 0 -> 1 boundary striped (1-byte threshold) through rank 3 (the one
+    idle detour of a 4-stage chain), whose relay threads forward host-staged pieces; record, plan, two striped
+    steps.  (RCCL relays run the same chains stream-ordered; one GPU cannot host two RCCL
+    ranks.)"""
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    chunks = 3
+    results = run(parity.stage_worker, 4, tmp_path, kind, chunks, 'except_last', 'cuda-shared',
+                  options, backend='gloo', timeout=120)
+    grads, loss = parity.reference(kind, torch.device('cuda', 0), chunks)
+    parity.assert_parity(results, grads, loss, rel=1e-4)
+    assert results[0]['stripes'], 'nothing striped'
+    assert any(r['relay_jobs'] for r in results)

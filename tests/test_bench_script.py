@@ -88,6 +88,19 @@ def test_bench_json_contract(nproc, model):
         assert ranks[1]['fwd_wait_ms'] > 0 and ranks[0]['bwd_wait_ms'] > 0
 
 
+def test_bench_striped_eight_ranks():
+    """``--stripes`` at 8 ranks with a threshold every tiny message clears: the headline
+    U-Net's routes are planned after the first warm-up step (an extra untimed step), relayed
+    in the timed step, and reported."""
+    rec = _run(8, '--model', 'unet', '--stripe-mb', '0.000001', '--sections', 'none')
+    routes = rec['config']['striped_routes']
+    assert routes, rec['config']
+    for route, relays in routes.items():
+        src, dst = map(int, route.split('->'))
+        assert relays and not {src, dst} & set(relays)
+    assert rec['value'] > 0
+
+
 def test_bench_headline_uses_reference_balance_and_reports_tuned():
     """N > 1: the headline runs the reference balance; --also-tuned adds the MI355X one."""
     rec = _run(2, '--model', 'unet', '--also-tuned', 'yes')

@@ -1,0 +1,106 @@
+"""The multi-path transfer planner (``parallel/stripes.py``): pieces and relay choice."""
+import pytest
+
+from torchgpipe_amd.parallel.stripes import Send, message_kind, pieces, plan
+
+
+@pytest.mark.parametrize('nbytes', [0, 1, 255, 256, 1000, 4096, 10 ** 6, 226_492_416])
+@pytest.mark.parametrize('relays', [0, 1, 2, 3])
+def test_pieces_tile_the_message(nbytes, relays):
+    got = pieces(nbytes, relays)
+    pos = 0
+    for off, n, path in got:
+        assert off == pos and n > 0 and 0 <= path <= relays
+        assert off % 256 == 0
+        pos += n
+    assert pos == nbytes
+    # each detour's share is cut into at most 4 forwarded pieces
+    for k in range(1, relays + 1):
+        assert sum(1 for _, _, p in got if p == k) <= 4
+
+
+def test_pieces_balance_the_paths():
+    """The direct link carries (sub+1)/sub of each detour's share: a detour stores and
+    forwards, so its time is (sub+1)/sub of its share's one-link time."""
+    nbytes = 400 * 2 ** 20
+    got = pieces(nbytes, 3, sub=4)
+    share = {k: sum(n for _, n, p in got if p == k) for k in range(4)}
+    unit = nbytes / (1.25 + 3)
+    assert share[0] == pytest.approx(1.25 * unit, rel=1e-4)
+    for k in (1, 2, 3):
+        assert share[k] == pytest.approx(unit, rel=1e-4)
+
+
+def test_message_kind():
+    assert message_kind(('sig', True, True, 'skip', 0, 1, 6)) == 'skip'
+    assert message_kind(('x', 1)) is None
+
+
+def _chain(n, sizes, skips=()):
+    """Sends of an n-stage chain: activation j -> j+1 of sizes[j], skips (src, dst, bytes),
+    and the gradients back; two micro-batches."""
+    sends = {j: [] for j in range(n)}
+    for _ in range(2):
+        for j in range(n - 1):
+            sends[j].append(Send(j + 1, 'act', sizes[j]))
+        for src, dst, b in skips:
+            sends[src].append(Send(dst, 'skip', b))
+    for _ in range(2):
+        for j in range(n - 1):
+            sends[j + 1].append(Send(j, 'gact', sizes[j]))
+        for src, dst, b in skips:
+            sends[dst].append(Send(src, 'gskip', b))
+    return sends
+
+
+def test_plan_relays_only_over_idle_links():
+    sends = _chain(8, [300, 200, 10, 10, 10, 10, 10], skips=[(1, 6, 250)])
+    stripes, jobs = plan(sends, list(range(8)), min_bytes=100)
+    busy = {frozenset((j, j + 1)) for j in range(7)} | {frozenset((1, 6))}
+    assert set(stripes) >= {(0, 1), (1, 0), (1, 2), (2, 1), (1, 6), (6, 1)}
+    seen = set()
+    for (src, dst), relays in stripes.items():
+        assert relays == stripes[(dst, src)]  # gradients come back the same way
+        for r in relays:
+            assert r not in (src, dst)
+            for pair in (frozenset((src, r)), frozenset((r, dst))):
+                assert pair not in busy
+                if src < dst:
+                    assert pair not in seen  # a detour link carries one route
+                    seen.add(pair)
+    # small routes stay direct
+    assert (3, 4) not in stripes
+    # every relay of every route has a job with its pieces of both directions
+    for (src, dst), relays in stripes.items():
+        if src > dst:
+            continue
+        for k, r in enumerate(relays, start=1):
+            job = [j for j in jobs[r] if (j.src, j.dst) == (src, dst)]
+            assert len(job) == 1
+            fwd = [m.nbytes for m in sends[src] if m.dst == dst and m.nbytes >= 100]
+            want = [n for b in fwd for _, n, p in pieces(b, len(relays)) if p == k]
+            assert list(job[0].forward) == want
+            assert len(job[0].backward) == len(job[0].forward)
+
+
+def test_plan_spreads_relays_over_routes():
+    """Two routes of similar size both get detours (relays go one at a time to the route
+    whose direct link carries the most), not one route all of them."""
+    sends = _chain(8, [151, 10, 10, 10, 10, 10, 10], skips=[(1, 7, 150)])
+    stripes, _ = plan(sends, list(range(8)), min_bytes=100, max_relays=3)
+    assert stripes.get((0, 1)) and stripes.get((1, 7))
+
+
+def test_plan_is_deterministic_and_respects_thresholds():
+    sends = _chain(4, [50, 60, 70])
+    assert plan(sends, [0, 1, 2, 3], min_bytes=100) == ({}, {})
+    a = plan(sends, [0, 1, 2, 3], min_bytes=1)
+    b = plan({k: list(v) for k, v in reversed(list(sends.items()))}, [0, 1, 2, 3], 1)
+    assert a == b
+
+
+def test_plan_skips_routes_with_other_traffic():
+    sends = _chain(4, [500, 10, 10])
+    sends[0].append(Send(1, 'other', 500))
+    stripes, _ = plan(sends, [0, 1, 2, 3], min_bytes=100)
+    assert (0, 1) not in stripes

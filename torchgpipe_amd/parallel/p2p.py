@@ -28,18 +28,25 @@ control payloads, host-staged tensors) take ``timeout`` and raise
 stream-ordered, so a missing peer is caught by the process group's watchdog
 (``init_process_group(timeout=...)``), which aborts the rank instead of
 hanging the job.
+
+Multi-path transfers.  With a stripe plan (``parallel/stripes.py``, set per step by the
+pipeline stage) a large message leaves as pieces over the direct link and over detours
+through idle ranks, which forward them (:meth:`P2P.begin_relays`).
 """
-from dataclasses import dataclass
+import contextlib
+from dataclasses import dataclass, field
 import datetime
-from typing import Dict, Hashable, List, Optional, Sequence, Tuple
+import threading
+from typing import Any, Dict, FrozenSet, Hashable, List, Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor
 import torch.distributed as dist
 
 from torchgpipe_amd.ops import misc
+from torchgpipe_amd.parallel.stripes import RelayJob, Send, message_kind, pieces
 
-__all__ = ['TensorMeta', 'P2P', 'Message', 'PipelineTimeout']
+__all__ = ['TensorMeta', 'P2P', 'Message', 'PipelineTimeout', 'StripePlan']
 
 _DTYPES = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64,
            torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool]
@@ -113,6 +120,11 @@ def _align16(n: int) -> int:
     return (n + 15) // 16 * 16
 
 
+def _bytes_of(t: Tensor) -> Tensor:
+    """Flat byte view of a contiguous tensor (its pieces travel as slices of it)."""
+    return t.reshape(-1).view(torch.uint8)
+
+
 class Message:
     """Handle of a posted receive: ``wait()`` returns the received tensors."""
 
@@ -180,6 +192,30 @@ class Message:
         return out
 
 
+@dataclass
+class StripePlan:
+    """One step signature's multi-path transfers as seen by one rank."""
+    # (src, dst) -> relays (global ranks), for every striped route of the pipeline
+    stripes: Dict[Tuple[int, int], List[int]]
+    # (src, dst) -> bytes of each message on the route, in order (the recorded step)
+    sizes: Dict[Tuple[int, int], List[int]]
+    # the routes this rank relays
+    jobs: List[RelayJob] = field(default_factory=list)
+    min_bytes: int = 0  # smaller messages of a striped route go direct
+    sub: int = 4
+
+
+class _Relay:
+    """A relay's state for one route: a staging ring, the sends still reading it, and the
+    stream (RCCL) its chains run on."""
+
+    def __init__(self, slots: int) -> None:
+        self.bufs: List[Optional[Tensor]] = [None] * slots
+        self.pending: List[Optional[object]] = [None] * slots
+        self.next = 0
+        self.stream: Optional[torch.cuda.Stream] = None
+
+
 class P2P:
     """RCCL/gloo point-to-point with cached shape metadata.
 
@@ -219,6 +255,16 @@ class P2P:
         self._bufs: Dict[Hashable, List[Tensor]] = {}
         self._pending_sends: List[object] = []
         self._pending_meta: List[object] = []
+        # multi-path transfers: this step's plan, per-route message counters, relay links
+        # (one 2-rank group per detour pair) and relay states
+        self.me = dist.get_rank() if dist.is_initialized() else 0
+        self.plan: Optional[StripePlan] = None
+        self._route_pos: Dict[Tuple[int, int], int] = {}
+        self.relay_links: Dict[FrozenSet[int], Any] = {}
+        self._relays: Dict[Tuple[int, int], _Relay] = {}
+        self._relay_threads: List[threading.Thread] = []
+        self._relay_errors: List[BaseException] = []
+        self._recording: Optional[List[Send]] = None
 
     # -- metadata ---------------------------------------------------------------------------
 
@@ -272,17 +318,28 @@ class P2P:
                 f'message {key!r} changed shape/dtype under the same step signature '
                 f'({cached} -> {metas}); the receiver would misinterpret it')
         self._prune()
-        if len(tensors) == 1 or not self.pack:
+        single = len(tensors) == 1
+        if self._recording is not None:
+            kind = message_kind(key) if single or self.pack else 'unpacked'
+            nbytes = metas[0].nbytes if single else self._packed_nbytes(metas)
+            self._recording.append(Send(dst, kind or 'other', nbytes))
+        if single or not self.pack:
             for t in tensors:
                 t = t.detach().contiguous()
                 if self.stage_host:
                     t = t.cpu()
+                if single and self._striped(self.me, dst, t.numel() * t.element_size(), key):
+                    self._send_pieces(_bytes_of(t), dst)
+                    return
                 self._pending_sends.append(dist.isend(t, dst, group=self._link(dst)))
             return
         buf = torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=tensors[0].device)
         misc.pack([t.detach() for t in tensors], buf)
         if self.stage_host:
             buf = buf.cpu()
+        if self._striped(self.me, dst, buf.numel(), key):
+            self._send_pieces(buf, dst)
+            return
         self._pending_sends.append(dist.isend(buf, dst, group=self._link(dst)))
 
     def recv(self, src: int, key: Hashable, cache: bool = True,
@@ -312,13 +369,158 @@ class P2P:
         if split:
             out = ([torch.empty(m.shape, dtype=m.dtype, device=where) for m in metas]
                    if keep is None or self.stage_host else list(keep))
-            works = [dist.irecv(t, src, group=self._link(src)) for t in out]
+            if len(out) == 1 and self._striped(src, self.me, metas[0].nbytes, key):
+                works = self._recv_pieces(_bytes_of(out[0]), src)
+            else:
+                works = [dist.irecv(t, src, group=self._link(src)) for t in out]
             return Message(works, out, None, metas, atomic, late, timeout, what,
                            keep if self.stage_host else None)
         buf = (torch.empty(self._packed_nbytes(metas), dtype=torch.uint8, device=where)
                if keep is None or self.stage_host else keep[0])
-        return Message([dist.irecv(buf, src, group=self._link(src))], None, buf, metas, atomic,
-                       late, timeout, what, keep if self.stage_host else None)
+        works = (self._recv_pieces(buf, src) if self._striped(src, self.me, buf.numel(), key)
+                 else [dist.irecv(buf, src, group=self._link(src))])
+        return Message(works, None, buf, metas, atomic, late, timeout, what,
+                       keep if self.stage_host else None)
+
+    # -- multi-path transfers ---------------------------------------------------------------
+
+    def start_recording(self) -> None:
+        """Record every message sent from now on (destination, kind, bytes)."""
+        self._recording = []
+
+    def stop_recording(self) -> List[Send]:
+        sends, self._recording = self._recording or [], None
+        return sends
+
+    def use_plan(self, plan: Optional[StripePlan]) -> None:
+        """The stripe plan of the step about to run (``None``: every message direct)."""
+        self.plan = plan
+        self._route_pos = {}
+
+    def _striped(self, src: int, dst: int, nbytes: int, key: Hashable) -> bool:
+        """Whether this message of route ``src -> dst`` travels in pieces (checks it is the
+        message the plan expects next on the route)."""
+        plan = self.plan
+        if plan is None or (src, dst) not in plan.stripes or nbytes < plan.min_bytes:
+            return False
+        sizes = plan.sizes[(src, dst)]
+        pos = self._route_pos.get((src, dst), 0)
+        if pos >= len(sizes) or sizes[pos] != nbytes:
+            want = sizes[pos] if pos < len(sizes) else 'no message'
+            raise RuntimeError(
+                f'striped route {src} -> {dst}: message #{pos} ({key!r}) has {nbytes} bytes '
+                f'but the stripe plan (recorded in the first step of this signature) expects '
+                f'{want}; the step sends differently from the step it was planned on')
+        self._route_pos[(src, dst)] = pos + 1
+        return True
+
+    def _pieces(self, peer: int, nbytes: int, src: int, dst: int
+                ) -> List[Tuple[int, int, int, Optional[Any]]]:
+        assert self.plan is not None
+        relays = self.plan.stripes[(src, dst)]
+        out = []
+        for off, n, path in pieces(nbytes, len(relays), self.plan.sub):
+            if path == 0:
+                out.append((off, n, peer, self._link(peer)))
+            else:
+                r = relays[path - 1]
+                out.append((off, n, r, self.relay_links[frozenset((self.me, r))]))
+        return out
+
+    def _send_pieces(self, flat: Tensor, dst: int) -> None:
+        for off, n, peer, group in self._pieces(dst, flat.numel(), self.me, dst):
+            self._pending_sends.append(dist.isend(flat[off:off + n], peer, group=group))
+
+    def _recv_pieces(self, flat: Tensor, src: int) -> List[object]:
+        return [dist.irecv(flat[off:off + n], peer, group=group)
+                for off, n, peer, group in self._pieces(src, flat.numel(), src, self.me)]
+
+    def begin_relays(self) -> None:
+        """Post this step's relay chains: for every route this rank relays, each piece of
+        every forward message is received from the source and sent on to the destination,
+        then each piece of the gradients the other way.  RCCL: stream-ordered on one stream
+        per route (the host returns at once); gloo: one thread per route."""
+        if self.plan is None:
+            return
+        self._join_relays()
+        for job in self.plan.jobs:
+            ops = ([(job.src, job.dst, n) for n in job.forward]
+                   + [(job.dst, job.src, n) for n in job.backward])
+            state = self._relays.get((job.src, job.dst))
+            if state is None:
+                state = self._relays[(job.src, job.dst)] = _Relay(4)
+            size = max((n for _, _, n in ops), default=0)
+            if self._host_waits:
+                where = torch.device('cpu')
+            else:
+                where = self.device
+                if state.stream is None:
+                    state.stream = torch.cuda.Stream(self.device)
+            # (re)allocate the ring on the route's stream, after the sends still reading it
+            with (torch.cuda.stream(state.stream) if state.stream is not None
+                  else contextlib.nullcontext()):
+                for k, b in enumerate(state.bufs):
+                    if b is None or b.numel() < size:
+                        if state.pending[k] is not None:
+                            _wait(state.pending[k], self.timeout if self._host_waits else None,
+                                  'relay send')
+                            state.pending[k] = None
+                        state.bufs[k] = torch.empty(size, dtype=torch.uint8, device=where)
+            if self._host_waits:
+                t = threading.Thread(target=self._relay_chain, args=(ops, state),
+                                     name=f'relay {job.src}->{job.dst}', daemon=True)
+                t.start()
+                self._relay_threads.append(t)
+            else:
+                with torch.cuda.stream(state.stream):
+                    self._relay_chain(ops, state)
+
+    def _relay_chain(self, ops: List[Tuple[int, int, int]], state: _Relay) -> None:
+        host = self._host_waits
+        timeout = self.timeout if host else None
+        try:
+            for src, dst, n in ops:
+                slot = state.next
+                state.next = (slot + 1) % len(state.bufs)
+                prev = state.pending[slot]
+                if prev is not None:  # the slot's previous send has left (RCCL: stream wait)
+                    _wait(prev, timeout, 'relay send')
+                buf = state.bufs[slot][:n]  # type: ignore[index]
+                _wait(dist.irecv(buf, src, group=self.relay_links[frozenset((self.me, src))]),
+                      timeout, f'relayed piece from rank {src} to rank {dst}')
+                state.pending[slot] = dist.isend(
+                    buf, dst, group=self.relay_links[frozenset((self.me, dst))])
+            if host:
+                for k, w in enumerate(state.pending):
+                    if w is not None:
+                        _wait(w, timeout, 'relay send')
+                        state.pending[k] = None
+        except BaseException as exc:  # surfaced by end_relays on the main thread
+            if not host:
+                raise
+            self._relay_errors.append(exc)
+
+    def _join_relays(self) -> None:
+        threads, self._relay_threads = self._relay_threads, []
+        for t in threads:
+            t.join()
+        errors, self._relay_errors = self._relay_errors, []
+        if errors:
+            raise errors[0]
+
+    def end_relays(self) -> None:
+        """Join the gloo relay threads of the step (re-raising their errors) and check that
+        every striped route sent as many messages as planned."""
+        self._join_relays()
+        plan = self.plan
+        if plan is not None:
+            for (src, dst), sizes in plan.sizes.items():
+                if src == self.me and (src, dst) in plan.stripes and \
+                        self._route_pos.get((src, dst), 0) != len(sizes):
+                    raise RuntimeError(
+                        f'striped route {src} -> {dst} sent {self._route_pos.get((src, dst), 0)} '
+                        f'messages this step, the stripe plan {len(sizes)}')
+            self._route_pos = {}
 
     def _persistent(self, key: Hashable, metas: Sequence[TensorMeta],
                     split: bool) -> List[Tensor]:

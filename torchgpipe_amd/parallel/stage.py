@@ -217,6 +217,14 @@ class PipelineStage:
             timeout of the groups this stage creates.  ``None`` = the default
             group's timeout.  RCCL transfers are bounded by the RCCL process
             group's own watchdog timeout (``init_process_group(timeout=...)``).
+        stripes: multi-path transfers (``parallel/stripes.py``): messages of at least this
+            many bytes on a route that carries one kind of message also travel through up
+            to ``stripe_relays`` idle ranks, over links no pipeline traffic uses.  Planned
+            from the first training step of each step signature (recorded) at the start
+            of the second (collective on the control group); ``None`` = off.  Needs a
+            third rank and the pipeline group spanning WORLD (relay links are created with
+            ``new_group``); otherwise a no-op.
+        stripe_relays: the most relays one route takes.
     """
 
     def __init__(self, module: nn.Sequential, balance: Sequence[int], *,
@@ -234,7 +242,9 @@ class PipelineStage:
                  philox_dropout: bool = False,
                  graph_cells: bool = False,
                  graph_warmup: int = 2,
-                 transport: Optional[Any] = None) -> None:
+                 transport: Optional[Any] = None,
+                 stripes: Optional[int] = None,
+                 stripe_relays: int = 3) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
         if checkpoint not in ('always', 'except_last', 'never'):
@@ -355,6 +365,15 @@ class PipelineStage:
         # derived-weight cache budget: None = not sized yet, 'measuring' = first step ran
         # uncached (ops/conv.py size_cache_budget), 'sized'
         self._cache_state: Optional[str] = None
+        # multi-path transfers: per step signature 'record' (first training step records
+        # its sends), the recorded sends, then the plan
+        whole = distributed and self.n == dist.get_world_size()
+        self._stripe_min = int(stripes or 0) if whole and self.n > 2 else 0
+        self._stripe_relays = stripe_relays
+        self._stripe_plans: Dict[Any, Any] = {}
+        self._stripe_on = False  # this step runs a plan (or records)
+        self._stripe_sig: Optional[Signature] = None
+        self._group_kwargs = group_kwargs
         if distributed and self.n > 1:
             self.connect()
 
@@ -555,6 +574,7 @@ class PipelineStage:
                 self._cache_state = 'measuring'
             # derived weights recomputed in place, on this stream, before any lane reads them
             refresh_step_caches(self.partition)
+        self._stripe_begin(sig)
         seg = self._segments_for(sig, stop)
         phase = seg.begin_step() if seg is not None else 'eager'
         self._seg_phase = phase
@@ -672,6 +692,109 @@ class PipelineStage:
             self.p2p.flush()
             self._cells = []
         return outputs
+
+    # -- multi-path transfers ---------------------------------------------------------------
+
+    @property
+    def stripes_ready(self) -> bool:
+        """Whether the last step's signature runs its stripe plan (or striping is off)."""
+        if not self._stripe_min:
+            return True
+        from torchgpipe_amd.parallel.p2p import StripePlan
+        return isinstance(self._stripe_plans.get(self._sig), StripePlan)
+
+    @property
+    def striped_routes(self) -> Dict[str, List[int]]:
+        """The last step signature's striped routes, ``'src->dst': relays`` (global ranks)."""
+        from torchgpipe_amd.parallel.p2p import StripePlan
+        plan = self._stripe_plans.get(self._sig)
+        if not isinstance(plan, StripePlan):
+            return {}
+        return {f'{a}->{b}': list(r) for (a, b), r in sorted(plan.stripes.items())}
+
+    def _stripe_begin(self, sig: Signature) -> None:
+        """Start this step's multi-path transfers (``parallel/stripes.py``)."""
+        if not self._stripe_min:
+            return
+        p2p = self.p2p
+        self._stripe_end()
+        if not (self.training and torch.is_grad_enabled()):
+            p2p.use_plan(None)
+            return
+        state = self._stripe_plans.get(sig)
+        if state is None or state == 'record':
+            # first training step of this signature: every rank records what it sends
+            self._stripe_plans[sig] = 'record'
+            self._stripe_sig = sig
+            p2p.use_plan(None)
+            p2p.start_recording()
+            self._stripe_on = True
+            return
+        if isinstance(state, list):  # recorded last step: plan now, on every rank alike
+            state = self._stripe_plans[sig] = self._make_stripe_plan(state)
+        p2p.use_plan(state)
+        p2p.begin_relays()
+        self._stripe_on = True
+
+    def _stripe_end(self) -> None:
+        """End the step's multi-path transfers: keep the recording, join the relays."""
+        if not self._stripe_on:
+            return
+        self._stripe_on = False
+        p2p = self.p2p
+        if p2p._recording is not None:
+            self._stripe_plans[self._stripe_sig] = p2p.stop_recording()
+        else:
+            p2p.end_relays()
+        p2p.use_plan(None)
+
+    def _make_stripe_plan(self, mine: List[Any]) -> Any:
+        from torchgpipe_amd.parallel import stripes as stripes_mod
+        from torchgpipe_amd.parallel.p2p import StripePlan
+        me = self.ranks[self.rank]
+        gathered: List[Any] = [None] * self.n
+        dist.all_gather_object(gathered, (me, [tuple(s) for s in mine]),
+                               group=self.ctrl_group)
+        sends = {r: [stripes_mod.Send(*s) for s in lst] for r, lst in gathered}
+        routes, jobs = stripes_mod.plan(sends, self.ranks, self._stripe_min,
+                                        self._stripe_relays)
+        sizes: Dict[Tuple[int, int], List[int]] = {}
+        for src, lst in sends.items():
+            for s in lst:
+                if (src, s.dst) in routes and s.nbytes >= self._stripe_min:
+                    sizes.setdefault((src, s.dst), []).append(s.nbytes)
+        pairs = sorted({tuple(sorted((end, r))) for (src, dst), relays in routes.items()
+                        for r in relays for end in (src, dst)})
+        self._open_relay_links(pairs)
+        return StripePlan(routes, sizes, jobs.get(me, []), self._stripe_min)
+
+    def _open_relay_links(self, pairs: List[Tuple[int, int]]) -> None:
+        """One 2-rank group per detour pair (``new_group`` is collective: every rank creates
+        every pair, in one sorted order), each opened with a one-element exchange in that
+        order, like :meth:`connect`."""
+        links = self.p2p.relay_links
+        me = self.ranks[self.rank]
+        for a, b in pairs:
+            if frozenset((a, b)) not in links:
+                pg = dist.new_group(ranks=[a, b], **self._group_kwargs)
+                links[frozenset((a, b))] = pg
+        staged = self.p2p.stage_host or self.device.type != 'cuda'
+        where = torch.device('cpu') if staged else self.device
+        works = []
+        for a, b in pairs:
+            if me not in (a, b):
+                continue
+            pg = links[frozenset((a, b))]
+            buf = torch.zeros(1, device=where)
+            if me == a:
+                works.append(dist.isend(buf, b, group=pg))
+            else:
+                _wait(dist.irecv(buf, a, group=pg), self.p2p.timeout if staged else None,
+                      f'relay link handshake with rank {a}')
+        for w in works:
+            _wait(w, self.p2p.timeout if staged else None, 'relay link handshake')
+        if where.type == 'cuda':
+            torch.cuda.synchronize(where)
 
     # -- backward ---------------------------------------------------------------------------
 
@@ -844,6 +967,7 @@ class PipelineStage:
             self._cache_state = 'sized'
         self._cells = []
         self.p2p.flush()
+        self._stripe_end()
 
     def _recompute_lanes(self) -> Optional[List[torch.cuda.Stream]]:
         if not self.overlap_recompute or self.device.type != 'cuda':
