@@ -186,12 +186,13 @@ def test_graph_cells_accumulate_over_train_steps_like_eager(graph_warmup):
     no backward reaches keeps ``.grad`` None."""
     dev = torch.device('cuda', 0)
     base, shape, classes = _models('unet')
-    unused = nn.Parameter(torch.ones(3, device=dev))
     a, b = copy.deepcopy(base), copy.deepcopy(base)
-    b.register_parameter('unused_weight', nn.Parameter(unused.detach().clone()))
+    # a parameter of a partition's layer that no forward uses
+    b[0].register_parameter('unused_weight', nn.Parameter(torch.ones(3, device=dev)))
     sa = PipelineStage(a, [len(a)], device=dev, chunks=4)
     sb = PipelineStage(b, [len(b)], device=dev, chunks=4, graph_cells=True,
                        graph_warmup=graph_warmup)
+    pbs = dict(b.named_parameters())
     gen = torch.Generator(device=dev).manual_seed(7)
     phases = []
     for step in range(5):
@@ -201,16 +202,17 @@ def test_graph_cells_accumulate_over_train_steps_like_eager(graph_warmup):
             sb.train_step(x, y, loss_fn)
             phases.append(sb.graph_phase)
         torch.cuda.synchronize()
-        for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        for name, pa in a.named_parameters():
+            pb = pbs[name]
             scale = pa.grad.abs().max().item() + 1e-12
             torch.testing.assert_close(pb.grad, pa.grad, rtol=1e-4, atol=1e-5 * scale,
                                        msg=lambda m: f'step {step} {name}: {m}')
         if 'replay' in phases:
-            assert b.unused_weight.grad is None
+            assert b[0].unused_weight.grad is None
         with torch.no_grad():
-            for pa, pb in zip(a.parameters(), b.parameters()):
+            for name, pa in a.named_parameters():
                 pa.sub_(0.05 * pa.grad)
-                pb.copy_(pa)
+                pbs[name].copy_(pa)
         for p in a.parameters():
             p.grad = None
         for p in b.parameters():
