@@ -72,3 +72,40 @@ def test_lib_dgrad_table_round_trips():
     assert (a, b, same) == ('1', '0', 'True')
     # the shipped table's lines all load (minus the one already imported above, if listed)
     assert int(c) >= int(n) - 1
+
+
+def test_f4_split_models_match_the_sweep():
+    """The F(4x4) split-K models (winograd_f4.hip) pick the measured-best split count, or
+    one within 5 % of it, on the shapes of profiles/r5/split_sweep.json: ResNet-101's 3x3
+    layers at 15 / 22 / 36-image micro-batches (where the old ">= 32 steps per split"
+    rule ran the 14^2 x 256 weight gradient at 22 images on 2 splits, 2.4x slower) and
+    U-Net's."""
+    if not any(f.startswith('_C') and f.endswith('.so')
+               for f in os.listdir(os.path.join(ROOT, 'torchgpipe_amd'))):
+        pytest.skip('extension not built')
+    sweep = os.path.join(ROOT, 'profiles', 'r5', 'split_sweep.json')
+    code = ('import json, torch, torchgpipe_amd._C; ops = torch.ops.tgpipe; '
+            f'rows = json.load(open({sweep!r})); out = []\n'
+            'for r in rows:\n'
+            '    n, c, k, h = r["shape"]\n'
+            '    for key, var in (("wgrad_v0", 0), ("fwd_v6", 6), ("fwd_v7", 7)):\n'
+            '        if key in r:\n'
+            '            out.append([r["shape"], key, ops.wino4_splits(n, c, k, h, h, var)])\n'
+            'print(json.dumps(out))')
+    res = subprocess.run([sys.executable, '-c', code], cwd=ROOT, capture_output=True,
+                         text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-2000:]
+    import json
+    picks = json.loads(res.stdout.strip().splitlines()[-1])
+    with open(sweep) as f:
+        rows = {tuple(r['shape']): r for r in json.load(f)}
+    checked = 0
+    for shape, key, s in picks:
+        times = rows[tuple(shape)][key]
+        best = times[str(times['best'])]
+        if str(s) in times:  # the model may pick a count the sweep did not time
+            assert times[str(s)] <= 1.05 * best + 2e-3, (shape, key, s, times)
+            checked += 1
+    assert checked >= 40
+    # the case that motivated it
+    assert dict(((tuple(sh), k), s) for sh, k, s in picks)[((22, 256, 256, 14), 'wgrad_v0')] == 8

@@ -373,6 +373,16 @@ at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
   return y;
 }
 
+// Split-K count of the F(4x4) kernels for one convolution: variant 0 = the weight gradient,
+// otherwise that forward / backward-data variant (wino4_plan).
+int64_t wino4_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int64_t variant) {
+  if (variant == 0) {
+    const int64_t steps = (n * ((h + 3) / 4) * ((w + 3) / 4) + 3) / 4;
+    return std::min<int64_t>(wino4_wgrad_splits(n, c, k, h, w), steps);
+  }
+  return wino4_plan(n, c, h, w, k, static_cast<int>(variant), 0).splits;
+}
+
 }  // namespace
 }  // namespace tgpipe
 
@@ -394,6 +404,9 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("wino4_conv(Tensor x, Tensor u, Tensor? bias, int out_channels, int variant=-1, "
         "int splits=0) -> Tensor");
   m.def("bg_weight(Tensor w, bool flip, int kind=4, Tensor? out=None, int emu=-1) -> Tensor");
+  // split-K counts the F(4x4) host heuristics pick (host only, CPU-testable)
+  m.def("wino4_splits(int n, int c, int k, int h, int w, int variant) -> int",
+        &tgpipe::wino4_splits);
   m.def("bg_conv(Tensor x, Tensor a, Tensor? bias, int out_channels, int bn=0, int splits=0, "
         "int kind=4, int waves=0, int sub=0, int emu=-1) -> Tensor");
 }

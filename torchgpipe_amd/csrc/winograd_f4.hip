@@ -2053,12 +2053,26 @@ WinoPlan wino4_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64
   if (splits > 0) {
     plan.splits = static_cast<int>(std::min<int64_t>(splits, steps));
   } else {
-    // >= 2 rounds of workgroups over the 256 CUs (4 - og... one or two per CU), >= 16
-    // steps per split to amortise the pipeline prologue and the output transform
-    const int64_t target = og == 4 ? 512 : 1024;
-    int64_t s = 1;
-    while (blocks * s < target && steps / (s * 2) >= 16) s *= 2;
-    plan.splits = static_cast<int>(s);
+    // Split-K by a cost model fitted to benchmarks/split_sweep.py (profiles/r5/
+    // split_sweep.json): ~2.1 us per 4-channel step of a 64-channel workgroup (one per CU;
+    // 32-channel workgroups ~1.9 us, two per CU), and per extra split ~0.23 us per MB of
+    // output partials plus ~11.6 us for the reduce pass.  (The old ">= 16 steps per split"
+    // rule kept ResNet's 28^2 x 128 layers at 22 images on 2 splits: 49 -> 41 us at 3.)
+    const int64_t cap = og == 4 ? 256 : 512;
+    const double step_us = og == 4 ? 2.1 : 1.9;
+    const double mb = static_cast<double>(n) * out_channels * h * w * 4 / 1e6;
+    int64_t best = 1;
+    double best_cost = 0;
+    for (int64_t s = 1; s <= std::min<int64_t>(64, steps); ++s) {
+      const int64_t rounds = (blocks * s + cap - 1) / cap;
+      const double cost = rounds * ((steps + s - 1) / s) * step_us +
+                          (s > 1 ? 11.6 + 0.23 * s * mb : 0.0);
+      if (s == 1 || cost < best_cost) {
+        best = s;
+        best_cost = cost;
+      }
+    }
+    plan.splits = static_cast<int>(best);
   }
   plan.workspace = plan.splits > 1 ? plan.splits * n * out_channels * h * w : 0;
   if (plan.variant >= 14) {  // + the transformed input V4[P/32][Rp/4][4][32][36], first
@@ -2146,13 +2160,27 @@ bool wino4_wgrad_supported(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w
 }
 
 int wino4_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
-  // one 8-wave workgroup per CU: >= 2 rounds of 256, >= 32 steps of 4 tiles per split
+  // Split-K by a cost model fitted to benchmarks/split_sweep.py (profiles/r5/
+  // split_sweep.json): one 8-wave workgroup per CU, ~2.5 us per 4-tile step, and per extra
+  // split ~0.8 us per MB of k x c x 36 partials (written, then summed by the reduce pass)
+  // plus ~5 us for that pass.  The old ">= 32 steps per split" rule left 3/4 of the CUs
+  // idle at ResNet's 15-36-image micro-batches (14^2 x 256 channels at 22 images: 139 ->
+  // 57 us).
   const int64_t blocks = ((c + 31) / 32) * ((k + 63) / 64);
   const int64_t steps = (n * ((h + 3) / 4) * ((w + 3) / 4) + 3) / 4;
-  int64_t s = (512 + blocks - 1) / blocks;
-  s = std::min<int64_t>(s, std::max<int64_t>(1, steps / 32));
-  s = std::min<int64_t>(s, 512);
-  return static_cast<int>(std::max<int64_t>(s, 1));
+  const double mb = static_cast<double>(((c + 31) / 32) * 32) * (((k + 63) / 64) * 64) * 9 * 4 /
+                    1e6;
+  int best = 1;
+  double best_cost = 0;
+  for (int64_t s = 1; s <= std::min<int64_t>(512, steps); ++s) {
+    const int64_t rounds = (blocks * s + 255) / 256;
+    const double cost = rounds * ((steps + s - 1) / s) * 2.5 + (s > 1 ? 5.0 + 0.8 * s * mb : 0.0);
+    if (s == 1 || cost < best_cost) {
+      best = static_cast<int>(s);
+      best_cost = cost;
+    }
+  }
+  return best;
 }
 
 int64_t wino4_wgrad_workspace(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int splits,

@@ -32,7 +32,8 @@ import contextlib
 import datetime
 import threading
 import time
-from typing import Any, Callable, Dict, Hashable, List, Optional, Sequence, Tuple, Union
+from typing import (Any, Callable, Dict, FrozenSet, Hashable, List, Optional, Sequence, Tuple,
+                    Union)
 
 import torch
 from torch import Tensor, nn
@@ -173,6 +174,10 @@ class _Cell:
         self.chk: Optional[Checkpointing] = None
         self.n_act_out = 0
         self.lane: Optional[torch.cuda.Stream] = None  # stream it was recomputed on
+
+
+# 2-rank relay communicators of multi-path transfers, per WORLD group, per GPU pair
+_RELAY_LINKS: Dict[int, Dict[FrozenSet[int], Any]] = {}
 
 
 class PipelineStage:
@@ -774,10 +779,14 @@ class PipelineStage:
         order, like :meth:`connect`."""
         links = self.p2p.relay_links
         me = self.ranks[self.rank]
+        # shared by every stage of this process (bench.py builds several): every rank
+        # creates the same pairs in the same order, so the cache stays in step across ranks
+        shared = _RELAY_LINKS.setdefault(id(dist.group.WORLD), {})
         for a, b in pairs:
-            if frozenset((a, b)) not in links:
-                pg = dist.new_group(ranks=[a, b], **self._group_kwargs)
-                links[frozenset((a, b))] = pg
+            key = frozenset((a, b))
+            if key not in shared:
+                shared[key] = dist.new_group(ranks=[a, b], **self._group_kwargs)
+            links[key] = shared[key]
         staged = self.p2p.stage_host or self.device.type != 'cuda'
         where = torch.device('cpu') if staged else self.device
         works = []
