@@ -28,6 +28,12 @@ SHAPES = [(n, c, c, h) for n in (15, 22, 36)
     (16, 1024, 1024, 12), (40, 1024, 1024, 12), (40, 128, 32, 192), (40, 32, 32, 192),
 ]
 SPLITS = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256)
+# batched-GEMM Winograd (bg_conv, split-bf16): ResNet's 14^2 / 7^2 layers and U-Net's deep ones
+BG_SHAPES = [(n, c, c, h) for n in (15, 22, 36) for c, h in ((256, 14), (512, 7))] + [
+    (40, 256, 256, 48), (40, 512, 512, 24), (40, 1024, 1024, 12), (16, 256, 256, 48),
+    (16, 512, 512, 24), (16, 1024, 1024, 12), (16, 2048, 2048, 6), (110, 256, 256, 14),
+    (110, 512, 512, 7)]
+BG_SPLITS = (1, 2, 3, 4, 6, 8)
 
 
 def timed(fn, iters):  # type: ignore[no-untyped-def]
@@ -42,17 +48,48 @@ def timed(fn, iters):  # type: ignore[no-untyped-def]
     return s.elapsed_time(e) / iters
 
 
+def bg_row(ops, n, c, k, h, iters):  # type: ignore[no-untyped-def]
+    """Every (tile width, split count) of the batched-GEMM forward at one shape."""
+    torch.manual_seed(0)
+    kind = 2 if h < 8 else 4
+    x = torch.randn(n, c, h, h, device='cuda')
+    w = torch.randn(k, c, 3, 3, device='cuda') * 0.05
+    a = ops.bg_weight(w, False, kind)
+    ref = ops.bg_conv(x, a, None, k, 128, 1, kind, 4).double()
+    res = {'auto': round(timed(lambda: ops.bg_conv(x, a, None, k, 0, 0, kind), iters), 4)}
+    best = None
+    for bn in (64, 96, 128):
+        for s in BG_SPLITS:
+            if s > -(-c // 16):
+                break
+            got = ops.bg_conv(x, a, None, k, bn, s, kind, 4).double()
+            err = ((got - ref).abs().max() / ref.abs().max()).item()
+            assert err < 1e-3, (n, c, k, h, bn, s, err)
+            ms = timed(lambda: ops.bg_conv(x, a, None, k, bn, s, kind, 4), iters)
+            res[f'{bn}/{s}'] = round(ms, 4)
+            if best is None or ms < res[best]:
+                best = f'{bn}/{s}'
+    res['best'] = best
+    return {'shape': [n, c, k, h], 'bg': res}
+
+
 def main() -> None:
     p = argparse.ArgumentParser()
     p.add_argument('--iters', type=int, default=20)
     p.add_argument('--out', default=None)
-    p.add_argument('--ops', default='wgrad,fwd')
+    p.add_argument('--ops', default='wgrad,fwd', help="any of wgrad, fwd, bg")
     p.add_argument('--shape', type=int, nargs=4, action='append', default=None,
                    help='N C K H (repeatable; default: the built-in table)')
     a = p.parse_args()
     ops = _ext.require()
     rows = []
+    if 'bg' in a.ops:
+        for n, c, k, h in BG_SHAPES:
+            rows.append(bg_row(ops, n, c, k, h, a.iters))
+            print(json.dumps(rows[-1]), flush=True)
     for n, c, k, h in (a.shape or SHAPES):
+        if 'wgrad' not in a.ops and 'fwd' not in a.ops:
+            break
         torch.manual_seed(0)
         x = torch.randn(n, c, h, h, device='cuda')
         dy = torch.randn(n, k, h, h, device='cuda')

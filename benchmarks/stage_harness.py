@@ -90,7 +90,8 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
 
     lanes = {'auto': args.model == 'unet', 'on': True, 'off': False}[args.lanes]
     # placeholder transport until the stage knows its skip routes
-    transport = LoopbackP2P(dev, acts, atomic, {})
+    sizes = [len(c) for c in torch.empty(args.batch, 0).chunk(args.chunks)]
+    transport = LoopbackP2P(dev, acts, atomic, {}, sizes)
     # (as bench.py: ResNet-101 recomputes on a lane too, forward lanes are U-Net's only)
     recompute_lane = lanes or (args.lanes == 'auto' and args.model == 'resnet101')
     stage = PipelineStage(model, args.balance, rank=k, device=dev, chunks=args.chunks,

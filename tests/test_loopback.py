@@ -96,3 +96,26 @@ def test_first_rank_gradients_match_its_layers():
         torch.autograd.backward(ys, grads)
     for (name, pa), pb in zip(ref.named_parameters(), stage.parameters()):
         torch.testing.assert_close(pb.grad, pa.grad, rtol=1e-5, atol=1e-6, msg=name)
+
+
+def test_uneven_micro_batches_on_the_last_rank():
+    """A mini-batch that does not split evenly (7 images in 3 micro-batches: 3, 3, 1, as
+    ResNet-101's B=25000 in 1667): with the micro-batch sizes the loopback trims its
+    templates, so the last rank's outputs line up with the target's chunks."""
+    kind, balance = 'amoebanet', [3, 6]
+    model, shape = _model(kind)
+    balance[-1] = len(model) - balance[0]
+    layers = list(model)
+    tracker = SkipTracker()
+    with torch.no_grad(), use_skip_tracker(tracker):
+        b = Batch(torch.rand(3, *shape))
+        for layer in layers[:balance[0]]:
+            b = b.call(layer)
+    sizes = [len(c) for c in torch.empty(7, 0).chunk(3)]
+    assert sizes == [3, 3, 1]
+    transport = LoopbackP2P(torch.device('cpu'), list(b), b.atomic, {}, sizes)
+    stage = PipelineStage(model, balance, rank=1, chunks=3, transport=transport)
+    loss = stage.train_step(None, torch.randint(10, (7,)), F.cross_entropy,
+                            signature=signature_of(torch.empty(7, *shape)))
+    assert loss is not None and torch.isfinite(loss)
+    assert all(p.grad is not None for p in stage.parameters())

@@ -32,13 +32,18 @@ class LoopbackP2P:
         acts_atomic: whether the activation message is a single tensor.
         skips: per source stage, the skip tensors this stage pops from it, in the stage's
             canonical route order.
+        sizes: the batch size of each micro-batch when they differ (a mini-batch that does
+            not split evenly: the last micro-batch is smaller); the templates are trimmed
+            to it along dim 0.
     """
 
     stage_host = False
 
     def __init__(self, device: torch.device, acts: Sequence[Tensor], acts_atomic: bool,
-                 skips: Dict[int, List[Tensor]]) -> None:
+                 skips: Dict[int, List[Tensor]],
+                 sizes: Optional[Sequence[int]] = None) -> None:
         self.device = device
+        self.sizes = list(sizes) if sizes is not None else None
         self.acts = [t.detach() for t in acts]
         self.acts_atomic = acts_atomic
         self.skips = {src: [t.detach() for t in ts] for src, ts in skips.items()}
@@ -59,10 +64,11 @@ class LoopbackP2P:
 
     def _source(self, kind: str, i: int, src: int, me: int) -> List[Tuple[Tensor, bool]]:
         """(template tensor, requires_grad) of every tensor of the message."""
-        if kind == 'act':
-            return [(t, t.is_floating_point()) for t in self.acts]
-        if kind == 'skip':
-            return [(t, t.is_floating_point()) for t in self.skips.get(src, [])]
+        if kind in ('act', 'skip'):
+            ts = self.acts if kind == 'act' else self.skips.get(src, [])
+            if self.sizes is not None and i < len(self.sizes):
+                ts = [t[:self.sizes[i]] if t.dim() else t for t in ts]
+            return [(t, t.is_floating_point()) for t in ts]
         # gradients of what this stage sent to ``src`` for micro-batch i
         # (activation gradients: only for tensors that require grad; skip gradients: one
         # per skip, zeros where none flows -- PipelineStage._backward_cells)
