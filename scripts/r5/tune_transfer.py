@@ -8,7 +8,8 @@ cross-stage skip travels on its own link (``torchgpipe_amd.balance.simulate``). 
 reference balance, the balance given with ``--current`` and the searched one, each
 simulated at free links and at ``--gbps``.
 
-    python scripts/r5/tune_transfer.py --model unet --profile profiles/unet_layer_profile_f4w.json \\
+    python scripts/r5/tune_transfer.py --model unet \\
+        --profile profiles/unet_layer_profile_f4w.json \\
         --harness profiles/r5/harness/stage_harness_unet_p8.json --gbps 100 \\
         --current 18 26 27 30 22 44 40 34
 """

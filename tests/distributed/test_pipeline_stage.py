@@ -280,17 +280,28 @@ def _dead_peer_worker(rank, world):
     from torchgpipe_amd.parallel import PipelineStage
     from torchgpipe_amd.parallel.p2p import PipelineTimeout
     stage = PipelineStage(build(), BALANCE, chunks=2, timeout=2.0)
+    # (the rendezvous store, not the gloo pairs, orders the exits: rank 0 hosts it and
+    # leaves last; the others stay until rank 1 has timed out)
+    store = torch.distributed.distributed_c10d._get_default_store()
+    deadline = time.monotonic() + 60
+
+    def leave() -> None:
+        while store.add('dead_timed_out', 0) < 1 and time.monotonic() < deadline:
+            time.sleep(0.05)
+        store.add('dead_left', 1)
+        while rank == 0 and store.add('dead_left', 0) < world and time.monotonic() < deadline:
+            time.sleep(0.05)
+
     if rank != 1:
-        time.sleep(5.0)  # rank 0 never sends; rank 2 idles too
+        leave()  # rank 0 never sends; rank 2 idles too
         return {'raised': None, 'elapsed': 0.0}
     start = time.monotonic()
     try:
         stage.forward(None)
     except PipelineTimeout as exc:
         elapsed = time.monotonic() - start
-        # stay connected until the peer has timed out too: exiting first would close the
-        # gloo pair and turn the peer's timeout into a connection error
-        time.sleep(2.0)
+        store.add('dead_timed_out', 1)
+        leave()
         return {'raised': type(exc).__name__, 'elapsed': elapsed, 'msg': str(exc)}
     return {'raised': None, 'elapsed': time.monotonic() - start}
 
@@ -313,9 +324,19 @@ def _misordered_worker(rank, world):
         p2p.recv(1 - rank, ('act', 0)).wait()
     except PipelineTimeout as exc:
         elapsed = time.monotonic() - start
-        # stay connected until the peer has timed out too: exiting first would close the
-        # gloo pair and turn the peer's timeout into a connection error
-        time.sleep(2.0)
+        # stay connected until the peer has timed out too (counted on the rendezvous
+        # store, not the gloo pair): exiting first would close the pair and turn the
+        # peer's timeout into a connection error.  Rank 0 hosts the store, so it leaves
+        # last.
+        store = torch.distributed.distributed_c10d._get_default_store()
+        store.add('misordered_timed_out', 1)
+        deadline = time.monotonic() + 60
+        while store.add('misordered_timed_out', 0) < world and time.monotonic() < deadline:
+            time.sleep(0.05)
+        store.add('misordered_left', 1)
+        while rank == 0 and store.add('misordered_left', 0) < world and \
+                time.monotonic() < deadline:
+            time.sleep(0.05)
         return {'raised': type(exc).__name__, 'elapsed': elapsed, 'msg': str(exc)}
     return {'raised': None, 'elapsed': time.monotonic() - start}
 

@@ -113,6 +113,11 @@ def _wait(work: object, timeout: Optional[datetime.timedelta], what: str) -> Non
         if 'imeout' in msg or 'imed out' in msg:
             raise PipelineTimeout(f'{what}: no matching peer operation within {timeout} '
                                   f'(peer dead or messages out of order): {msg}') from exc
+        if 'onnection closed' in msg or 'onnection reset' in msg:
+            # gloo closes a pair when one side's wait times out: the peer gave up (its own
+            # timeout on a mis-ordered exchange) or died
+            raise PipelineTimeout(f'{what}: the peer closed the connection (it died, or '
+                                  f'timed out waiting on this rank): {msg}') from exc
         raise
 
 
