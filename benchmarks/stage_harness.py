@@ -97,7 +97,8 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
     stage = PipelineStage(model, args.balance, rank=k, device=dev, chunks=args.chunks,
                           checkpoint=args.checkpoint, transport=transport,
                           overlap_recompute=recompute_lane, overlap_forward=lanes,
-                          graph_cells=args.graph_cells)
+                          graph_cells=args.graph_cells,
+                          backward_thread=args.backward_thread)
     skips: Dict[int, List[torch.Tensor]] = {}
     for src, key in stage.in_skips:
         skips.setdefault(src, []).append(pending[key])
@@ -150,6 +151,7 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
         idle_launch_ms = (time.perf_counter() - t1) * 1e3
         torch.cuda.synchronize(dev)
     row = {'stage': k, 'layers': [lo, hi], 'graph_cells': args.graph_cells,
+           'backward_thread': args.backward_thread,
            'graph_phase': stage.graph_phase, 'lanes': lanes,
            'host_ms': round(host_ms, 2), 'wall_ms': round(wall_ms, 2),
            'device_ms': round(dev_ms, 2), 'host_share': round(host_ms / dev_ms, 3),
@@ -183,6 +185,8 @@ def main() -> None:
     p.add_argument('--checkpoint', default='except_last')
     p.add_argument('--graph-cells', action='store_true',
                    help='captured cells (PipelineStage(graph_cells=True))')
+    p.add_argument('--backward-thread', action='store_true',
+                   help='backward issued from a helper thread (PipelineStage(backward_thread))')
     p.add_argument('--lanes', choices=['auto', 'on', 'off'], default='auto',
                    help='forward / recompute lanes (auto: on for U-Net, as bench.py)')
     p.add_argument('--cell-streams', type=int, default=3,

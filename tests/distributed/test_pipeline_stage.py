@@ -273,6 +273,23 @@ def test_striped_transfers_match_one_process(tmp_path, kind):
             assert rank in plans[0][(src, dst)]
 
 
+@pytest.mark.parametrize('kind,world,options', [
+    ('unet', 2, dict(backward_thread=True, steps=3)),
+    ('amoebanet', 2, dict(backward_thread=True, checkpoint_mode='always', steps=3)),
+    ('unet-p8', 8, dict(backward_thread=True, dtype=torch.float64, stripes=1, steps=3)),
+])
+def test_backward_thread_matches_one_process(tmp_path, kind, world, options):
+    """``backward_thread``: each micro-batch's backward issued from a helper thread while
+    the main thread recomputes the next one and posts its receives; gradients and loss
+    equal one process (with multi-path transfers too at 8 ranks)."""
+    options = dict(options)
+    checkpoint = options.pop('checkpoint_mode', 'except_last')
+    results = run(parity.stage_worker, world, tmp_path, kind, 3, checkpoint, 'cpu', options)
+    dtype = options.get('dtype')
+    grads, loss = parity.reference(kind, torch.device('cpu'), 3, dtype=dtype)
+    parity.assert_parity(results, grads, loss, rel=1e-9 if dtype == torch.float64 else 1e-5)
+
+
 # -- failure detection: a dead or mis-ordered peer raises within the timeout --------------
 
 def _dead_peer_worker(rank, world):

@@ -32,6 +32,10 @@ CASES = [
     ('unet', 'always', dict(graph_cells=True, steps=5)),
     ('amoebanet', 'except_last', dict(cell_streams=True, graph_cells=True, steps=5)),
     ('amoebanet', 'always', dict(overlap_recompute=True, graph_cells=True, steps=5)),
+    # backward issued from a helper thread while the next micro-batch recomputes
+    ('unet', 'except_last', dict(overlap_recompute=True, overlap_forward=True,
+                                 backward_thread=True, steps=3)),
+    ('amoebanet', 'always', dict(cell_streams=True, backward_thread=True, steps=3)),
 ]
 
 
@@ -59,9 +63,9 @@ def test_overlapped_stage_matches_one_gpu(tmp_path, kind, checkpoint, options):
 def test_striped_stage_matches_one_gpu(tmp_path, kind, options):
     """Multi-path transfers (``parallel/stripes.py``) with device tensors: four ranks on
     ``cuda:0``, the 0 -> 1 boundary striped (1-byte threshold) through rank 3 (the one
-    idle detour of a 4-stage chain), whose relay threads forward host-staged pieces; record, plan, two striped
-    steps.  (RCCL relays run the same chains stream-ordered; one GPU cannot host two RCCL
-    ranks.)"""
+    idle detour of a 4-stage chain), whose relay threads forward host-staged pieces;
+    record, plan, two striped steps.  (RCCL relays run the same chains stream-ordered;
+    one GPU cannot host two RCCL ranks.)"""
     if not torch.cuda.is_available():
         pytest.skip('needs a GPU')
     chunks = 3

@@ -38,6 +38,7 @@ the transform runs once per optimizer step instead of once per call.
   these.  A transform that would exceed the budget is used for the call and dropped.
 """
 import os
+import threading
 from typing import Any, Dict, Optional, Sequence, Tuple
 
 import torch
@@ -144,6 +145,10 @@ def _await(t: Tensor, ready: Optional[Any]) -> None:
         torch.cuda.current_stream(t.device).wait_event(ready)
 
 
+# guards the miss path of every _TransformCache (derive + insert + byte accounting)
+_CACHE_LOCK = threading.RLock()
+
+
 class _TransformCache:
     """Derived weights keyed by (storage, version, device, step) of the parameter.
 
@@ -176,16 +181,21 @@ class _TransformCache:
             # stage with one warm-up step captures before any cached step).  The graph
             # derives its own copy on every replay instead.
             return _derive(weight, slot)
-        if hit is not None:  # stale: release before transforming again
-            _CACHE_BYTES[dev] -= hit[1].numel() * hit[1].element_size()
-            del self._entries[slot]
-        u = _derive(weight, slot)
-        size = u.numel() * u.element_size()
-        if _CACHE_BYTES.get(dev, 0) + size <= _budget(dev):
-            self._entries[slot] = (key, u, _ready_event(u))
-            self._weight = weight.detach()
-            _CACHE_BYTES[dev] = _CACHE_BYTES.get(dev, 0) + size
-        return u
+        with _CACHE_LOCK:  # (PipelineStage(backward_thread=True): two host threads)
+            hit = self._entries.get(slot)
+            if hit is not None and hit[0] == key:
+                _await(hit[1], hit[2])
+                return hit[1]
+            if hit is not None:  # stale: release before transforming again
+                _CACHE_BYTES[dev] -= hit[1].numel() * hit[1].element_size()
+                del self._entries[slot]
+            u = _derive(weight, slot)
+            size = u.numel() * u.element_size()
+            if _CACHE_BYTES.get(dev, 0) + size <= _budget(dev):
+                self._entries[slot] = (key, u, _ready_event(u))
+                self._weight = weight.detach()
+                _CACHE_BYTES[dev] = _CACHE_BYTES.get(dev, 0) + size
+            return u
 
     def get(self, weight: Tensor, flip: bool, f4: bool = False, bg: int = 0) -> Tensor:
         """The transformed weight for ``flip`` (backward-data) and the kernel family:
