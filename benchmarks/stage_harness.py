@@ -150,6 +150,16 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
         seg.cells[0].fwd.replay()
         idle_launch_ms = (time.perf_counter() - t1) * 1e3
         torch.cuda.synchronize(dev)
+    if args.torch_profile:
+        # one more step under torch.profiler (CPU activities of every thread, the autograd
+        # engine's included): where the host time of a launch-bound stage goes
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU]) as prof:
+            step()
+            torch.cuda.synchronize(dev)
+        with open(f'{args.torch_profile}_stage{k}.txt', 'w') as f:
+            f.write(prof.key_averages().table(sort_by='self_cpu_time_total', row_limit=60,
+                                              max_name_column_width=70))
     row = {'stage': k, 'layers': [lo, hi], 'graph_cells': args.graph_cells,
            'backward_thread': args.backward_thread,
            'graph_phase': stage.graph_phase, 'lanes': lanes,
@@ -185,6 +195,8 @@ def main() -> None:
     p.add_argument('--checkpoint', default='except_last')
     p.add_argument('--graph-cells', action='store_true',
                    help='captured cells (PipelineStage(graph_cells=True))')
+    p.add_argument('--torch-profile', default=None,
+                   help='path prefix: one extra step under torch.profiler, op table per stage')
     p.add_argument('--backward-thread', action='store_true',
                    help='backward issued from a helper thread (PipelineStage(backward_thread))')
     p.add_argument('--lanes', choices=['auto', 'on', 'off'], default='auto',

@@ -233,9 +233,10 @@ class PipelineStage:
         backward_thread: issue each micro-batch's backward from a helper thread, so the
             host enqueues the next micro-batch's recomputation (and posts its receives)
             while the autograd engine enqueues this backward: the two host streams of
-            kernel launches overlap where they release the GIL.  For launch-bound stages
-            (AmoebaNet and ResNet-101 at 22-40-image micro-batches: host enqueue 0.9-1.0
-            of the step).  Eager cells only.
+            kernel launches overlap where they release the GIL.  Measured on the
+            launch-bound stages (AmoebaNet and ResNet-101 at 22-40-image micro-batches):
+            no gain, the host time is GIL-held Python (profiles/r5/backward_thread.md);
+            off by default.  Eager cells only.
     """
 
     def __init__(self, module: nn.Sequential, balance: Sequence[int], *,
