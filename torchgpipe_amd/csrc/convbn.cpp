@@ -429,17 +429,21 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
   const int width = split ? static_cast<int>(s) : plans[0].col_width;
   const int blocks = split ? static_cast<int>(n) : plans[0].col_blocks;
   auto part = at::empty({2, blocks, c}, x.options());
+  // the two halves by pointer: part[k] would be an aten::select per use (host time of a
+  // launch-bound stage, profiles/r5/host_profile.md)
+  float* const part0 = part.data_ptr<float>();
+  float* const part1 = part0 + static_cast<int64_t>(blocks) * c;
   const bool epilogue_stats = !split || fused_stats;
   for (size_t i = 0; i < p.geo.size(); ++i) {
     const auto wt = weights[i];
     const ConvGemmPlan& pl = plans[i];
     run_gemm(0, wt.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
-             epilogue_stats ? part[0].data_ptr<float>() : nullptr,
-             epilogue_stats ? part[1].data_ptr<float>() : nullptr, p.geo[i], pl, false,
+             epilogue_stats ? part0 : nullptr,
+             epilogue_stats ? part1 : nullptr, p.geo[i], pl, false,
              wt.numel() * 4, x.numel() * 4, x);
   }
   if (split && !fused_stats)
-    launch_bn_stats(z.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n,
+    launch_bn_stats(z.data_ptr<float>(), part0, part1, n,
                     c, s, stream);
   auto mean = at::empty({c}, x.options());
   auto invstd = at::empty({c}, x.options());
@@ -468,7 +472,7 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
   // relu_out with a node sum: relu(bn(z) + add) (ResNet's residual join); the caller masks
   // the gradient with the saved output (the backward's re-derived mask cannot see `add`)
   auto y = at::empty_like(z);
-  launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, n,
+  launch_bn_finalize_apply(part0, part1, blocks, width, n,
                            c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), const_cast<float*>(rm),
                            const_cast<float*>(rv), tracked, nullptr, sums.data_ptr<float>(),
@@ -869,12 +873,16 @@ std::vector<at::Tensor> convbn_group_forward(
   const int width = split ? static_cast<int>(s) : plan.col_width;
   const int blocks = split ? static_cast<int>(n) : plan.col_blocks;
   auto part = at::empty({2, blocks, c}, x.options());
+  // the two halves by pointer: part[k] would be an aten::select per use (host time of a
+  // launch-bound stage, profiles/r5/host_profile.md)
+  float* const part0 = part.data_ptr<float>();
+  float* const part1 = part0 + static_cast<int64_t>(blocks) * c;
   run_gemm(0, w_cat.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
-           part[0].data_ptr<float>(), part[1].data_ptr<float>(), p.geo[0], plan, false,
+           part0, part1, p.geo[0], plan, false,
            w_cat.numel() * 4, x.numel() * 4, x);
   auto mean = at::empty({c}, x.options());
   auto invstd = at::empty({c}, x.options());
-  launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(), blocks, width, n,
+  launch_bn_finalize_apply(part0, part1, blocks, width, n,
                            c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr,
                            z.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, stream, false,
@@ -1163,6 +1171,8 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
   const int64_t n = x.size(0), c = x.size(1), s = n * c == 0 ? 0 : x.numel() / (n * c);
   const auto stream = cur_stream(x);
   auto part = at::empty({2, n, c}, x.options());
+  float* const part0 = part.data_ptr<float>();
+  float* const part1 = part0 + n * c;
   auto mean = at::empty({c}, x.options());
   auto invstd = at::empty({c}, x.options());
   auto y = at::empty_like(x);
@@ -1185,10 +1195,10 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
                 "num_batches_tracked must be a 1-element int64 tensor on the input's device");
     tracked = num_batches_tracked->data_ptr<int64_t>();
   }
-  launch_bn_stats(x.data_ptr<float>(), part[0].data_ptr<float>(), part[1].data_ptr<float>(), n, c,
+  launch_bn_stats(x.data_ptr<float>(), part0, part1, n, c,
                   s, stream);
   auto sums = at::empty({2, c}, x.options());  // zeroed by the finalize, for the backward
-  launch_bn_finalize_apply(part[0].data_ptr<float>(), part[1].data_ptr<float>(),
+  launch_bn_finalize_apply(part0, part1,
                            static_cast<int>(n), static_cast<int>(s), n, c, s,
                            static_cast<float>(eps), rm != nullptr ? momentum : 0.0,
                            mean.data_ptr<float>(), invstd.data_ptr<float>(),

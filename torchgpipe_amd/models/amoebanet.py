@@ -284,6 +284,17 @@ class Stem(nn.Module):
         return self.bn(self.conv(self.relu(x)))
 
 
+class _EventPool(dict):
+    """Per-device HIP events of a cell's stream schedule; a copy or a pickle of the cell
+    starts with none (events belong to the process and device that made them)."""
+
+    def __deepcopy__(self, memo: Dict[int, object]) -> '_EventPool':
+        return _EventPool()
+
+    def __reduce__(self) -> Tuple[object, ...]:
+        return (_EventPool, ())
+
+
 class Cell(nn.Module):
     def __init__(self, c_prev_prev: int, c_prev: int, c: int, reduction: bool,
                  reduction_prev: bool) -> None:
@@ -305,6 +316,9 @@ class Cell(nn.Module):
         self._group_cache = _GroupCache()
         self._shared = self._shared_plan()
         self._plans: Dict[int, List[int]] = {}
+        self._event_flags: Dict[int, List[bool]] = {}
+        # per device: the cross-stream events of _forward_streams, reused call after call
+        self._events = _EventPool()
 
     @property
     def _plan(self) -> List[int]:
@@ -410,7 +424,7 @@ class Cell(nn.Module):
         if node < 0 or node >= len(nodes):
             return {}
         x = nodes[node]
-        triplets = [fused_triplets(self.operations[k].module)[0] for k in ops]  # type: ignore[index]
+        triplets = [self.operations[k].module._triplets()[0] for k in ops]  # type: ignore[index]
         if not groupable(x, triplets):
             return {}
         outs = group_relu_conv_bn(x, triplets, self._group_cache)
@@ -488,10 +502,25 @@ class Cell(nn.Module):
         pre: Dict[int, Tensor] = {}
         shared: Dict[int, Tensor] = {}
         special: Dict[str, Tuple[int, torch.cuda.Event]] = {}  # 'group' / 'shared' -> (stream, ev)
+        # which nodes need an event (an input of a node on another stream, or a concat input
+        # off the current stream): fixed per plan
+        flags = self._event_flags.get(count)
+        if flags is None:
+            flags = [any(plan[j] != plan[k] for j in range(k + 1, len(plan))) or
+                     (plan[k] != 0 and k in self.concat) for k in range(len(plan))]
+            self._event_flags[count] = flags
+        # events are re-recorded call after call (every wait on one is issued within the
+        # call that recorded it); fresh ones inside a capture
+        capturing = torch.cuda.is_current_stream_capturing()
+        pool = self._events.setdefault(s1.device, {}) if not capturing else None
 
-        def needs_event(k: int, s: int) -> bool:
-            return any(plan[j] != s for j in range(k + 1, len(plan))) or \
-                (s != 0 and k in self.concat)
+        def event(key: object) -> torch.cuda.Event:
+            if pool is None:
+                return torch.cuda.Event()
+            ev = pool.get(key)
+            if ev is None:
+                ev = pool[key] = torch.cuda.Event()
+            return ev
 
         def run(k: int, fn: Callable[[], Tensor], inputs: List[int],
                 external: List[Tensor], waits: List[str]) -> None:
@@ -515,8 +544,8 @@ class Cell(nn.Module):
             with torch.cuda.stream(stream):
                 out = fn()
             ev = None
-            if needs_event(k, s):
-                ev = torch.cuda.Event()
+            if flags[k]:
+                ev = event(k)
                 ev.record(stream)
             nodes.append(out)
             events.append(ev)
@@ -541,7 +570,7 @@ class Cell(nn.Module):
                 stream = streams[plan[node]]
                 if first_group:
                     pre.update(self._grouped(nodes))
-                    ev = torch.cuda.Event()
+                    ev = event('group')
                     ev.record(stream)
                     special['group'] = (plan[node], ev)
                 if first_shared:
@@ -549,7 +578,7 @@ class Cell(nn.Module):
                     out = self.operations[a](nodes[self.indices[a]])
                     for j in self._shared:
                         shared[j] = out
-                    ev = torch.cuda.Event()
+                    ev = event('shared')
                     ev.record(stream)
                     special['shared'] = (plan[node], ev)
                 return self._node(k, nodes, pre, shared)

@@ -249,14 +249,27 @@ def _weight_cache(conv: nn.Module) -> _TransformCache:
     return cache
 
 
+_LIMIT = (1 << 31) - 64  # 32-bit buffer offsets of the kernels
+
+
 def fusable(x: Tensor, convs: Sequence[nn.Conv2d], bn: nn.Module) -> bool:
-    limit = (1 << 31) - 64  # 32-bit buffer offsets of the kernels
-    co = sum(c.out_channels for c in convs)
-    return (_ENABLED and _bn_ok(bn, x) and all(conv_supported(c) for c in convs)
-            and x.numel() * 4 < limit and x.numel() // max(1, x.shape[1]) * co * 4 < limit
-            and all(c.weight.numel() * 4 < limit for c in convs)
-            and _ext.available()
-            and all(c.weight.dtype == torch.float32 and c.weight.is_cuda for c in convs))
+    if not (_ENABLED and _bn_ok(bn, x)):
+        return False
+    numel = x.numel()
+    if numel * 4 >= _LIMIT:
+        return False
+    co = 0
+    for c in convs:
+        # the module's own configuration, checked once (every micro-batch asks)
+        ok = c.__dict__.get('_fusable_conv')
+        if ok is None:
+            ok = c.__dict__['_fusable_conv'] = (conv_supported(c)
+                                                and c.weight.numel() * 4 < _LIMIT)
+        w = c.weight
+        if not ok or w.dtype != torch.float32 or not w.is_cuda:
+            return False
+        co += c.out_channels
+    return numel // max(1, x.shape[1]) * co * 4 < _LIMIT and _ext.available()
 
 
 def fused_triplets(seq: nn.Sequential) -> Optional[List[Tuple[bool, nn.Conv2d, nn.BatchNorm2d]]]:
@@ -288,7 +301,7 @@ class FusedChain(nn.Sequential):
                 start: int = 0) -> Tensor:
         """The chain from triplet ``start`` on (``start`` > 0: ``x`` is the output of
         triplet ``start - 1``, e.g. computed by :func:`group_relu_conv_bn`)."""
-        triplets = fused_triplets(self)
+        triplets = self._triplets()
         if triplets is None:
             assert start == 0, 'start > 0 needs a chain of (ReLU, Conv2d, BatchNorm2d) triplets'
             out = super().forward(x)
@@ -305,6 +318,19 @@ class FusedChain(nn.Sequential):
                 if extra is not None:
                     x = x + extra
         return x
+
+
+    def _triplets(self) -> Optional[List[Tuple[bool, nn.Conv2d, nn.BatchNorm2d]]]:
+        """:func:`fused_triplets` of this chain, cached while its children stay the same
+        objects (every forward of every micro-batch asks)."""
+        mods = tuple(self._modules.values())
+        hit = self.__dict__.get('_triplet_cache')
+        if hit is not None and len(hit[0]) == len(mods) and \
+                all(a is b for a, b in zip(hit[0], mods)):
+            return hit[1]
+        triplets = fused_triplets(self)
+        self.__dict__['_triplet_cache'] = (mods, triplets)
+        return triplets
 
 
 class ReLUConvBN(FusedChain):
