@@ -206,6 +206,14 @@ class Checkpointing:
         if not self.shared.recomputed:
             self.shared.run_recompute(tuple(self.batch))
 
+    def take_recomputed(self) -> Tuple[Tuple[Tensor, ...], Tuple[Tensor, ...]]:
+        """The recomputation's ``(outputs, input leaves)``, for a caller that back-propagates
+        through the recomputed graph itself (``PipelineStage``: one backward call per
+        micro-batch instead of the Checkpoint node's reentrant one); the Checkpoint node
+        then never runs."""
+        output, leaves = self.shared.recomputed.pop()
+        return (output if isinstance(output, tuple) else (output,)), leaves
+
 
 def checkpoint(function: Any, input: TensorOrTensors) -> TensorOrTensors:
     """Drop-in ``torch.utils.checkpoint``-like helper (tests / debugging)."""

@@ -230,6 +230,10 @@ class PipelineStage:
             third rank and the pipeline group spanning WORLD (relay links are created with
             ``new_group``); otherwise a no-op.
         stripe_relays: the most relays one route takes.
+        direct_backward: back-propagate a recomputed micro-batch straight through its
+            recomputed graph (one autograd engine call) instead of through its Checkpoint
+            node, whose backward re-enters the engine for the same work (default on; off
+            restores the reference's Checkpoint/Recompute choreography exactly).
         backward_thread: issue each micro-batch's backward from a helper thread, so the
             host enqueues the next micro-batch's recomputation (and posts its receives)
             while the autograd engine enqueues this backward: the two host streams of
@@ -257,7 +261,8 @@ class PipelineStage:
                  transport: Optional[Any] = None,
                  stripes: Optional[int] = None,
                  stripe_relays: int = 3,
-                 backward_thread: bool = False) -> None:
+                 backward_thread: bool = False,
+                 direct_backward: bool = True) -> None:
         if chunks <= 0:
             raise ValueError('number of chunks must be positive integer')
         if checkpoint not in ('always', 'except_last', 'never'):
@@ -388,6 +393,7 @@ class PipelineStage:
         self._stripe_sig: Optional[Signature] = None
         self._group_kwargs = group_kwargs
         self.backward_thread = backward_thread
+        self.direct_backward = direct_backward
         self._bwd_pool: Optional[Any] = None
         if distributed and self.n > 1:
             self.connect()
@@ -869,8 +875,7 @@ class PipelineStage:
             self._drain_pool()  # no backward left running into the next step
             raise
         if pending is not None:
-            pending[0].result()
-            self._ship_input_grads(pending[1], pending[2], None, me, prev)
+            self._finish_pending(pending, me, prev)
         if on_gpu:
             # fused kernels on the lanes wrote .grad without autograd knowing
             cur = torch.cuda.current_stream(self.device)
@@ -885,6 +890,19 @@ class PipelineStage:
         self.p2p.flush()
         self._stripe_end()
 
+    def _finish_pending(self, pending: Tuple[Any, _Cell, Optional[torch.cuda.Stream],
+                                             Optional[Tuple[Tensor, ...]]],
+                        me: int, prev: Optional[int]) -> None:
+        """Join a helper-thread backward and ship its input gradients (on the recomputed
+        leaves when it back-propagated through the recomputed graph)."""
+        fut, cell, run, leaves = pending
+        fut.result()
+        if leaves is None:
+            self._ship_input_grads(cell, run, None, me, prev)
+        else:
+            self._ship_input_grads(cell, run, [self._grad_of(x) for x in leaves], me, prev,
+                                   on_run=False)
+
     def _drain_pool(self) -> None:
         if self._bwd_pool is not None:
             self._bwd_pool.shutdown(wait=True)
@@ -895,11 +913,13 @@ class PipelineStage:
                        main: Optional[torch.cuda.Stream], seg: Optional[Any], ahead: bool,
                        persistent: bool, threaded: bool, nxt: Optional[int],
                        prev: Optional[int], me: int
-                       ) -> Optional[Tuple[Any, _Cell, Optional[torch.cuda.Stream]]]:
+                       ) -> Optional[Tuple[Any, _Cell, Optional[torch.cuda.Stream],
+                                           Optional[Tuple[Tensor, ...]]]]:
         """Steps 1-4 of every micro-batch's backward (``_backward_cells``); returns the
         last micro-batch's backward when the helper thread still owns it."""
         prev_run: Optional[torch.cuda.Stream] = None
-        pending: Optional[Tuple[Any, _Cell, Optional[torch.cuda.Stream]]] = None
+        pending: Optional[Tuple[Any, _Cell, Optional[torch.cuda.Stream],
+                                Optional[Tuple[Tensor, ...]]]] = None
         for j, cell in enumerate(cells):
             i = cell.index
             # 1. post the gradient receives first ...
@@ -933,13 +953,21 @@ class PipelineStage:
 
             if pending is not None:
                 # the previous micro-batch's backward has been enqueued: ship its gradients
-                pending[0].result()
-                self._ship_input_grads(pending[1], pending[2], None, me, prev)
+                self._finish_pending(pending, me, prev)
                 pending = None
 
-            # 3. backward through this cell
+            # 3. backward through this cell -- a recomputed one straight through the
+            #    recomputed graph (its Checkpoint node's reentrant backward would wrap the
+            #    same work in a second engine call: 0.7 ms of host per AmoebaNet micro-batch)
             tensors: List[Tensor] = []
             grads: List[Tensor] = []
+            direct = bool(self.direct_backward and cell.chk is not None and not cell.seg
+                      and not self.is_last and cell.chk.shared.recomputed)
+            rec_out: Tuple[Tensor, ...] = ()
+            leaves: Tuple[Tensor, ...] = ()
+            if direct:
+                assert cell.chk is not None
+                rec_out, leaves = cell.chk.take_recomputed()
             # captured cells: the gradient of each output (None: none), and whether it sits
             # in a persistent receive buffer
             seg_grads: List[Optional[Tensor]] = [None] * len(cell.outputs)
@@ -959,8 +987,14 @@ class PipelineStage:
                 received = iter(grad_msg.wait())
                 for k, t in enumerate(act_out):
                     if t.requires_grad:
+                        g = next(received)
+                        if direct:
+                            if rec_out[k].requires_grad:
+                                tensors.append(rec_out[k])
+                                grads.append(g)
+                            continue
                         tensors.append(t)
-                        grads.append(next(received))
+                        grads.append(g)
                         seg_grads[k], seg_kept[k] = grads[-1], persistent
             skip_out = cell.outputs[cell.n_act_out:]
             dst_of = [d for d, _ in self.out_skips]
@@ -969,6 +1003,12 @@ class PipelineStage:
                 for k, (d, t) in enumerate(zip(dst_of, skip_out)):
                     if d == dst:
                         g = next(received)
+                        if direct:
+                            r = rec_out[cell.n_act_out + k]
+                            if t.requires_grad and r.requires_grad:
+                                tensors.append(r)
+                                grads.append(g)
+                            continue
                         if t.requires_grad:
                             tensors.append(t)
                             grads.append(g)
@@ -996,7 +1036,8 @@ class PipelineStage:
                 # micro-batch's receives and recomputation (joined there, before its
                 # backward: the fused ops add into the same .grad buffers)
                 pending = (self._backward_pool().submit(
-                    self._threaded_backward, tensors, grads, main, i), cell, run)
+                    self._threaded_backward, tensors, grads, main, i), cell, run,
+                    leaves if direct else None)
                 prev_run = run
                 continue
             else:
@@ -1004,22 +1045,30 @@ class PipelineStage:
                     if tensors:
                         torch.autograd.backward(tensors, grads)
             prev_run = run
+            if direct:
+                # the input gradients sit on the recomputation's leaves
+                gins = [self._grad_of(x) for x in leaves]
+                del rec_out, leaves, tensors, grads
 
             # 4. ship input gradients upstream
-            self._ship_input_grads(cell, run, gins, me, prev)
+            self._ship_input_grads(cell, run, gins, me, prev, on_run=not direct)
         return pending
 
     def _ship_input_grads(self, cell: _Cell, run: Optional[torch.cuda.Stream],
-                          gins: Optional[List[Tensor]], me: int, prev: Optional[int]) -> None:
+                          gins: Optional[List[Tensor]], me: int, prev: Optional[int],
+                          on_run: bool = True) -> None:
         """Send a micro-batch's input gradients upstream (a replayed backward ran no
-        autograd, so its sends leave from the stream that ran it) and release the cell."""
+        autograd, so its sends leave from the stream that ran it; gradients ``gins`` that
+        autograd accumulated leave from the current stream, which the engine synced) and
+        release the cell."""
         i = cell.index
         n_in_act = len(cell.inputs) - len(self.in_skips)
 
         def grad_in(k: int) -> Tensor:
             return gins[k] if gins is not None else self._grad_of(cell.inputs[k])
 
-        with torch.cuda.stream(run) if gins is not None else contextlib.nullcontext():
+        with torch.cuda.stream(run) if gins is not None and on_run and run is not None \
+                else contextlib.nullcontext():
             if prev is not None:
                 gin = [grad_in(k) for k in range(n_in_act) if cell.inputs[k].requires_grad]
                 self.p2p.send(gin, prev, self._key('gact', i, me, prev))
