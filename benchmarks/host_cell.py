@@ -42,6 +42,28 @@ def main() -> None:
     dev = torch.device('cuda')
     rows = {}
 
+    # stream / event primitives the multi-stream cells use per node
+    side = torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+    t = torch.randn(16, device=dev)
+    ev = torch.cuda.Event()
+
+    def ctx():  # type: ignore[no-untyped-def]
+        with torch.cuda.stream(side):
+            pass
+
+    def setstream():  # type: ignore[no-untyped-def]
+        torch.cuda.set_stream(side)
+        torch.cuda.set_stream(main)
+
+    rows['stream_context_us'] = host_us(ctx, 2000)
+    rows['set_stream_pair_us'] = host_us(setstream, 2000)
+    rows['event_new_record_us'] = host_us(lambda: torch.cuda.Event().record(side), 2000)
+    rows['event_record_us'] = host_us(lambda: ev.record(side), 2000)
+    rows['wait_event_us'] = host_us(lambda: main.wait_event(ev), 2000)
+    rows['record_stream_us'] = host_us(lambda: t.record_stream(side), 2000)
+    rows['current_stream_us'] = host_us(lambda: torch.cuda.current_stream(dev), 2000)
+
     from torchgpipe_amd.models.amoebanet import amoebanetd, set_cell_streams
     model = amoebanetd(num_classes=10, num_layers=6, num_filters=32).to(dev).train()
     layers = list(model)

@@ -233,7 +233,11 @@ def relu_conv_bn(x: Tensor, convs: Sequence[Tuple[nn.Conv2d, int]], bn: nn.Batch
     """
     geo: List[int] = []
     for conv, offset in convs:
-        geo += _geo(conv, offset)
+        # (the module's geometry, built once per offset: every micro-batch asks)
+        cached = conv.__dict__.get('_convbn_geo')
+        if cached is None or cached[0] != offset:
+            cached = conv.__dict__['_convbn_geo'] = (offset, _geo(conv, offset))
+        geo += cached[1]
     weights = [conv.weight for conv, _ in convs]
     return _ConvBN.apply(x, add, bn.weight, bn.bias, bn, geo, relu, relu_out,
                          [_weight_cache(conv) for conv, _ in convs], (sink_in, sink_out),
