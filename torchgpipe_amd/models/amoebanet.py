@@ -284,17 +284,6 @@ class Stem(nn.Module):
         return self.bn(self.conv(self.relu(x)))
 
 
-class _EventPool(dict):
-    """Per-device HIP events of a cell's stream schedule; a copy or a pickle of the cell
-    starts with none (events belong to the process and device that made them)."""
-
-    def __deepcopy__(self, memo: Dict[int, object]) -> '_EventPool':
-        return _EventPool()
-
-    def __reduce__(self) -> Tuple[object, ...]:
-        return (_EventPool, ())
-
-
 class Cell(nn.Module):
     def __init__(self, c_prev_prev: int, c_prev: int, c: int, reduction: bool,
                  reduction_prev: bool) -> None:
@@ -317,8 +306,6 @@ class Cell(nn.Module):
         self._shared = self._shared_plan()
         self._plans: Dict[int, List[int]] = {}
         self._event_flags: Dict[int, List[bool]] = {}
-        # per device: the cross-stream events of _forward_streams, reused call after call
-        self._events = _EventPool()
 
     @property
     def _plan(self) -> List[int]:
@@ -509,18 +496,11 @@ class Cell(nn.Module):
             flags = [any(plan[j] != plan[k] for j in range(k + 1, len(plan))) or
                      (plan[k] != 0 and k in self.concat) for k in range(len(plan))]
             self._event_flags[count] = flags
-        # events are re-recorded call after call (every wait on one is issued within the
-        # call that recorded it); fresh ones inside a capture
-        capturing = torch.cuda.is_current_stream_capturing()
-        pool = self._events.setdefault(s1.device, {}) if not capturing else None
 
         def event(key: object) -> torch.cuda.Event:
-            if pool is None:
-                return torch.cuda.Event()
-            ev = pool.get(key)
-            if ev is None:
-                ev = pool[key] = torch.cuda.Event()
-            return ev
+            # a fresh event: recording a new one costs 2.3 us of host, re-recording a
+            # pending one 5.6 (benchmarks/host_cell.py)
+            return torch.cuda.Event()
 
         def run(k: int, fn: Callable[[], Tensor], inputs: List[int],
                 external: List[Tensor], waits: List[str]) -> None:
@@ -541,7 +521,14 @@ class Cell(nn.Module):
             if s != 0:
                 for t in external:
                     t.record_stream(stream)
-            with torch.cuda.stream(stream):
+                # set / restore the current stream directly: a torch.cuda.stream block
+                # costs 6.1 us of host, the two switches 0.9 (benchmarks/host_cell.py)
+                torch.cuda.set_stream(stream)
+                try:
+                    out = fn()
+                finally:
+                    torch.cuda.set_stream(current)
+            else:
                 out = fn()
             ev = None
             if flags[k]:
