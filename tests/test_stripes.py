@@ -104,3 +104,29 @@ def test_plan_skips_routes_with_other_traffic():
     sends[0].append(Send(1, 'other', 500))
     stripes, _ = plan(sends, [0, 1, 2, 3], min_bytes=100)
     assert (0, 1) not in stripes
+
+
+def test_p2p_refuses_a_step_that_sends_differently_from_its_plan():
+    """A striped route checks every message against the plan recorded for its signature:
+    a different size (or one message too many) raises instead of mis-delivering pieces,
+    and a step that sends fewer messages than planned raises at its end."""
+    import torch
+
+    from torchgpipe_amd.parallel.p2p import P2P, StripePlan
+    p2p = P2P(torch.device('cpu'))
+    p2p.me = 0
+    plan = StripePlan({(0, 1): [2], (1, 0): [2]}, {(0, 1): [1024, 1024]}, [], min_bytes=1)
+    p2p.use_plan(plan)
+    assert p2p._striped(0, 1, 1024, 'k0')
+    with pytest.raises(RuntimeError, match='expects 1024'):
+        p2p._striped(0, 1, 512, 'k1')
+    p2p.use_plan(plan)
+    assert p2p._striped(0, 1, 1024, 'k0') and p2p._striped(0, 1, 1024, 'k1')
+    with pytest.raises(RuntimeError, match='no message'):
+        p2p._striped(0, 1, 1024, 'k2')
+    # messages under the threshold and unplanned routes go direct
+    p2p.use_plan(StripePlan({(0, 1): [2]}, {(0, 1): [4096]}, [], min_bytes=2048))
+    assert not p2p._striped(0, 1, 100, 'small')
+    assert not p2p._striped(0, 3, 1 << 20, 'other route')
+    with pytest.raises(RuntimeError, match='sent 0 messages this step, the stripe plan 1'):
+        p2p.end_relays()
