@@ -65,7 +65,7 @@ def main() -> None:
             row[f'v{v}'] = {'ms': round(ms, 4), 'direct_tflops': round(flops / ms / 1e9, 1),
                             'rel_err': err}
         if h >= 8 or a.all_f4:
-            for name, var in (('f4', 0), ('f4nf', 1)):
+            for name, var in (('f4', 0), ('f4nf', 1), ('f4emu', 2)):
                 got = ops.wino4_wgrad(x, dy, 0, var)
                 err = ((got.double() - ref).abs().max() / ref.abs().max()).item()
                 ms = timed(lambda: ops.wino4_wgrad(x, dy, 0, var), a.iters)

@@ -147,16 +147,36 @@ def test_f4_forward_and_flip(shape, splits, variant):
                                    (1, 16, 8, 1, 1), (4, 32, 32, 33, 2), (2, 256, 128, 12, 12),
                                    (5, 64, 33, 20, 36)])
 @pytest.mark.parametrize('splits', [0, 1, 3, 1000])
-@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('variant', [0, 1, 2])
 def test_f4_wgrad(shape, splits, variant):
     # F(4x4,3x3) weight gradient: edge tiles, channel blocks past C / K, split tiles
-    # (1000 is capped at the step count)
+    # (1000 is capped at the step count); variant 2 = the split-bf16 batched GEMM (rows
+    # past K, columns past C, 16-tile steps past the last tile)
     n, c, k, h, w = shape
     torch.manual_seed(5)
     x = torch.randn(n, c, h, w, device=cuda)
     dy = torch.randn(n, k, h, w, device=cuda)
     got = _ext.require(x).wino4_wgrad(x, dy, splits, variant)
     want = torch.ops.aten.convolution_backward(
+        dy.double(), x.double(), torch.zeros(k, c, 3, 3, device=cuda, dtype=torch.double), None,
+        [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    torch.testing.assert_close(got.double(), want, rtol=1e-4,
+                               atol=5e-5 * (want.abs().max().item() + 1))
+
+
+@pytest.mark.parametrize('variant', [0, 1, 2])
+def test_f4_wgrad_accumulates_into_existing_gradient(variant):
+    """``into``: the weight gradient is added to an existing ``.grad`` (gradient-accumulation
+    fusion), split partials included."""
+    n, c, k, h, w = 3, 70, 130, 13, 13
+    torch.manual_seed(6)
+    x = torch.randn(n, c, h, w, device=cuda)
+    dy = torch.randn(n, k, h, w, device=cuda)
+    base = torch.randn(k, c, 3, 3, device=cuda)
+    into = base.clone()
+    got = _ext.require(x).wino4_wgrad(x, dy, 2, variant, into)
+    assert got.data_ptr() == into.data_ptr()
+    want = base.double() + torch.ops.aten.convolution_backward(
         dy.double(), x.double(), torch.zeros(k, c, 3, 3, device=cuda, dtype=torch.double), None,
         [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
     torch.testing.assert_close(got.double(), want, rtol=1e-4,
@@ -325,3 +345,21 @@ def test_cache_budget_sizing_modes(monkeypatch):
         min(cap, (1 << 30) // 2)
     assert convmod.size_cache_budget(dev, 1 << 30, fraction=0.15) == int(0.15 * (1 << 30))
     assert convmod.size_cache_budget(dev, total // 2, fraction=None) == cap
+
+
+def test_module_weight_gradient_picks_split_bf16_gemm_for_deep_layers():
+    """``WinogradConv2d``'s weight gradient at 512 channels on >= 320 tiles runs the
+    split-bf16 batched GEMM (variant 2) and matches float64."""
+    from torchgpipe_amd.ops import conv as conv_mod
+    torch.manual_seed(9)
+    m = conv_mod.WinogradConv2d(512, 512, 3, padding=1, bias=False).to(cuda)
+    x = torch.randn(3, 512, 48, 48, device=cuda, requires_grad=True)
+    assert conv_mod._wgrad_f4_variant(x, m.weight) == 2
+    y = m(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    want = torch.ops.aten.convolution_backward(
+        g.double(), x.detach().double(), m.weight.detach().double(), None, [1, 1], [1, 1],
+        [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    torch.testing.assert_close(m.weight.grad.double(), want, rtol=1e-4,
+                               atol=5e-5 * (want.abs().max().item() + 1))

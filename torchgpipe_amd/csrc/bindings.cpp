@@ -302,11 +302,16 @@ at::Tensor wino4_wgrad(const at::Tensor& x_in, const at::Tensor& dy_in, int64_t 
   TORCH_CHECK(wino4_wgrad_supported(n, c, k, h, w),
               "input too large for the F(4x4) weight-gradient kernel (needs < 1 GiB); "
               "use wino_wgrad");
-  // every split owns >= 1 step of 4 tiles
-  const int64_t steps = (n * ((h + 3) / 4) * ((w + 3) / 4) + 3) / 4;
+  TORCH_CHECK(variant >= 0 && variant <= 2,
+              "variant must be 0 (fused), 1 (non-fused) or 2 (split-bf16 batched GEMM)");
+  // every split owns >= 1 step (of 4 tiles; of 16 for the split-bf16 GEMM)
+  const int64_t tiles = n * ((h + 3) / 4) * ((w + 3) / 4);
+  const int64_t steps = variant == 2 ? (tiles + 15) / 16 : (tiles + 3) / 4;
   const int s = static_cast<int>(std::min<int64_t>(
-      splits > 0 ? splits : wino4_wgrad_splits(n, c, k, h, w), steps));
-  TORCH_CHECK(variant == 0 || variant == 1, "variant must be 0 (fused) or 1 (non-fused)");
+      splits > 0 ? splits
+                 : (variant == 2 ? wino4_wgrad_emu_splits(n, c, k, h, w)
+                                 : wino4_wgrad_splits(n, c, k, h, w)),
+      steps));
   const int64_t wsize = wino4_wgrad_workspace(n, c, k, h, w, s, static_cast<int>(variant));
   at::Tensor ws;
   if (wsize > 0) ws = at::empty({wsize}, x.options());

@@ -122,6 +122,13 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
 // over `splits` workgroups (> 1 needs a workspace of splits*K*C*9 floats).
 bool wino4_wgrad_supported(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
 int wino4_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
+// variant 2: the split-bf16 batched-GEMM weight gradient (its own split count / workspace)
+int wino4_wgrad_emu_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w);
+int64_t wino4_wgrad_emu_workspace(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w,
+                                  int splits);
+void launch_wino4_wgrad_emu(const float* x, const float* dy, float* dw, float* ws, int64_t n,
+                            int64_t c, int64_t k, int64_t h, int64_t w, int splits, bool accum,
+                            hipStream_t stream);
 // variant 0: fused (patch / gradient-tile staging inside the GEMM kernel); 1: non-fused
 // (transform passes into the GEMM's LDS image order, then an LDS-DMA GEMM).  The workspace
 // holds the split-K partials (splits > 1) and, for variant 1, the transformed operands.

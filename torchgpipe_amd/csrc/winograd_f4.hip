@@ -932,9 +932,9 @@ __device__ __forceinline__ void f4_load_dy(float (&g)[16], __amdgpu_buffer_rsrc_
   }
 }
 
-// M' = A g A^T into the lane's 36 contiguous LDS floats (both passes on pairs, packed
-// fp32 VALU, like f4_transform_store).
-__device__ __forceinline__ void f4_dy_transform_store(const float (&g)[16], float* mdst) {
+// M' = A g A^T (36 values, row-major 6x6) of one 4x4 gradient tile (both passes on pairs,
+// packed fp32 VALU, like f4_transform).
+__device__ __forceinline__ void f4_dy_transform(const float (&g)[16], float (&m)[kP]) {
   float t[6][4];
 #pragma unroll
   for (int jp = 0; jp < 2; ++jp) {
@@ -949,7 +949,6 @@ __device__ __forceinline__ void f4_dy_transform_store(const float (&g)[16], floa
       t[i][2 * jp + 1] = col[i][1];
     }
   }
-  float m[kP];
 #pragma unroll
   for (int ip = 0; ip < 3; ++ip) {
     floatx2 row[6];
@@ -961,6 +960,12 @@ __device__ __forceinline__ void f4_dy_transform_store(const float (&g)[16], floa
       m[(2 * ip + 1) * 6 + j] = row[j][1];
     }
   }
+}
+
+// M' into the lane's 36 contiguous LDS floats.
+__device__ __forceinline__ void f4_dy_transform_store(const float (&g)[16], float* mdst) {
+  float m[kP];
+  f4_dy_transform(g, m);
 #pragma unroll
   for (int q = 0; q < kP / 4; ++q)
     reinterpret_cast<floatx4*>(mdst)[q] = floatx4{m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]};
@@ -1870,6 +1875,121 @@ __device__ __forceinline__ void f2_weight_tile(const float* __restrict__ w, int 
   }
 }
 
+// ---- split-bf16 F(4x4) weight gradient (variant 2) ----------------------------------------
+// The non-fused weight gradient as one batched split-bf16 GEMM per position, on the
+// batched-GEMM machinery: dU[b][k][c] = sum_t M'[b][k][t] V[b][c][t], the 36 positions b,
+// output channels k as GEMM rows (A image, the gradient tiles' M' = A g A^T), input channels
+// c as columns (B image, the input patches' V = B^T d B), the tiles t as the reduction in
+// 16-deep steps -- the same [b][step][plane, half][rows][8] images bg_gemm_emu_kernel reads,
+// with tiles where the forward has channels.  Then dW = G^T (sum of the split partials) G.
+
+// V image of (channel row c, tiles st*16 + 4g .. +3); zeros past the tiles or channels.
+template <bool kVec>
+__global__ __launch_bounds__(256) void wg_x_emu_kernel(const float* __restrict__ x,
+                                                      float* __restrict__ v, int C, int H, int W,
+                                                      int TW, int tpi, int P, int Np, int ksteps,
+                                                      uint32_t x_bytes) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 4 * Np) return;
+  const int g = static_cast<int>(idx & 3);
+  const int64_t rest = idx >> 2;
+  const int c = static_cast<int>(rest % Np);
+  const int st = static_cast<int>(rest / Np);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
+                                        static_cast<int>(x_bytes), 0x00020000);
+  float out[4][kP];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int t = st * 16 + 4 * g + e;
+    F4Patch p;
+    if (t < P && c < C) {
+      f4_fwd_offsets(p, t, c, P, tpi, TW, C, H, W);
+      f4_load_patch<kVec>(p, xr, 0);
+      f4_transform(p);
+    } else {
+#pragma unroll
+      for (int b = 0; b < kP; ++b) p.d[b] = 0.f;
+    }
+#pragma unroll
+    for (int b = 0; b < kP; ++b) out[e][b] = p.d[b];
+  }
+  bg_emu_store<kP>(v, out, st, c, g, Np, ksteps);
+}
+
+// M' image of (gradient channel row k, tiles st*16 + 4g .. +3); zeros past the tiles or
+// channels.
+template <bool kVec>
+__global__ __launch_bounds__(256) void wg_dy_emu_kernel(const float* __restrict__ dy,
+                                                       float* __restrict__ m, int N, int K,
+                                                       int H, int W, int TH, int TW, int Mp,
+                                                       int ksteps, uint32_t dy_bytes) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(ksteps) * 4 * Mp) return;
+  const int g = static_cast<int>(idx & 3);
+  const int64_t rest = idx >> 2;
+  const int k = static_cast<int>(rest % Mp);
+  const int st = static_cast<int>(rest / Mp);
+  const __amdgpu_buffer_rsrc_t dyr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), static_cast<short>(0),
+                                        static_cast<int>(dy_bytes), 0x00020000);
+  const int tpi = TH * TW;
+  float out[4][kP];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int t = st * 16 + 4 * g + e;
+    F4TileCursor cur;
+    cur.n = t / tpi;  // t past the last tile: n >= N, f4_load_dy reads zeros
+    const int rem = t - cur.n * tpi;
+    cur.ty = rem / TW;
+    cur.tx = rem - cur.ty * TW;
+    float gt[16];
+    f4_load_dy<kVec>(gt, dyr, cur, k, N, K, H, W);
+    f4_dy_transform(gt, out[e]);
+  }
+  bg_emu_store<kP>(m, out, st, k, g, Mp, ksteps);
+}
+
+// dW[k][c] (+)= G^T (sum_z dU[z][b][k][c] over b as 6x6) G: one thread per (k, c),
+// consecutive threads on consecutive c (coalesced reads of each position's row).
+__global__ __launch_bounds__(256) void wg_output_emu_kernel(const float* __restrict__ cbuf,
+                                                           float* __restrict__ dw, int K, int C,
+                                                           int Mp, int Np, int splits,
+                                                           bool accum) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= static_cast<int64_t>(K) * C) return;
+  const int c = static_cast<int>(idx % C);
+  const int k = static_cast<int>(idx / C);
+  const int64_t pos = static_cast<int64_t>(Mp) * Np;
+  float u[kP];
+#pragma unroll
+  for (int b = 0; b < kP; ++b) {
+    const float* src = cbuf + b * pos + static_cast<int64_t>(k) * Np + c;
+    float acc = 0.f;
+    for (int z = 0; z < splits; ++z) acc += src[static_cast<int64_t>(z) * kP * pos];
+    u[b] = acc;
+  }
+  float t[3][6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float col[6], w3[3];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) col[i] = u[i * 6 + j];
+    gt6(col, w3);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) t[a][j] = w3[a];
+  }
+  float* o = dw + (static_cast<int64_t>(k) * C + c) * 9;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float w3[3];
+    gt6(t[a], w3);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) o[a * 3 + e] = accum ? o[a * 3 + e] + w3[e] : w3[e];
+  }
+}
+
+
 __global__ __launch_bounds__(256) void bg_weight_f2_kernel(const float* __restrict__ w,
                                                           float* __restrict__ a, int O, int R,
                                                           int Mp, int ksteps, bool flip) {
@@ -2185,6 +2305,7 @@ int wino4_wgrad_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
 
 int64_t wino4_wgrad_workspace(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w, int splits,
                               int variant) {
+  if (variant == 2) return wino4_wgrad_emu_workspace(n, c, k, h, w, splits);
   int64_t total = splits > 1 ? splits * k * c * 9 : 0;
   if (variant == 1) {
     const int64_t ppad = ((n * ((h + 3) / 4) * ((w + 3) / 4) + 3) / 4) * 4;
@@ -2203,6 +2324,10 @@ void launch_wino4_wgrad(const float* x, const float* dy, float* dw, float* ws, i
   const int64_t nwg = static_cast<int64_t>(cblocks) * kblocks * splits;
   const uint32_t x_bytes = static_cast<uint32_t>(n * c * h * w * 4);
   const uint32_t dy_bytes = static_cast<uint32_t>(n * k * h * w * 4);
+  if (variant == 2) {
+    launch_wino4_wgrad_emu(x, dy, dw, ws, n, c, k, h, w, splits, accum, stream);
+    return;
+  }
   float* partial = ws;
   if (variant == 1) {
     const int64_t nsteps = (P + 3) / 4;
@@ -2434,6 +2559,79 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
                      static_cast<int>(plan.mp), static_cast<int>(plan.np), static_cast<int>(P),
                      static_cast<int>(th * tw), static_cast<int>(tw), static_cast<int>(h),
                      static_cast<int>(w), plan.splits);
+}
+
+
+// ---- split-bf16 weight gradient host side (variant 2) -------------------------------------
+
+namespace {
+struct WgEmuPlan {
+  int64_t ksteps, mp, np;
+  int bn;
+};
+
+WgEmuPlan wg_emu_plan(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
+  WgEmuPlan p;
+  const int64_t P = n * ((h + 3) / 4) * ((w + 3) / 4);
+  p.ksteps = (P + 15) / 16;
+  p.bn = bg_pick_bn(c, 4, true);  // columns: the input channels
+  p.mp = bg_round(k, 128);        // rows: the gradient channels (128-row tiles)
+  p.np = bg_round(c, p.bn);
+  return p;
+}
+}  // namespace
+
+int wino4_wgrad_emu_splits(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w) {
+  // two workgroups per CU: >= 2 rounds over the 256 CUs, >= 8 sixteen-tile steps per split
+  const WgEmuPlan p = wg_emu_plan(n, c, k, h, w);
+  const int64_t tiles = (p.mp / 128) * (p.np / p.bn) * kP;
+  int64_t s = 1;
+  while (tiles * s < 1024 && p.ksteps / (s * 2) >= 8) s *= 2;
+  return static_cast<int>(s);
+}
+
+int64_t wino4_wgrad_emu_workspace(int64_t n, int64_t c, int64_t k, int64_t h, int64_t w,
+                                  int splits) {
+  const WgEmuPlan p = wg_emu_plan(n, c, k, h, w);
+  // M' and V images (96 bytes = 24 floats per row and step), then the split partials
+  return kP * p.ksteps * 24 * (p.mp + p.np) + static_cast<int64_t>(splits) * kP * p.mp * p.np;
+}
+
+void launch_wino4_wgrad_emu(const float* x, const float* dy, float* dw, float* ws, int64_t n,
+                            int64_t c, int64_t k, int64_t h, int64_t w, int splits, bool accum,
+                            hipStream_t stream) {
+  const WgEmuPlan p = wg_emu_plan(n, c, k, h, w);
+  const int64_t th = (h + 3) / 4, tw = (w + 3) / 4;
+  const int64_t P = n * th * tw;
+  float* am = ws;
+  float* bv = am + kP * p.ksteps * 24 * p.mp;
+  float* cb = bv + kP * p.ksteps * 24 * p.np;
+  const bool vec = (w & 3) == 0;
+  const int64_t mt = p.ksteps * 4 * p.mp, vt = p.ksteps * 4 * p.np;
+  hipLaunchKernelGGL(vec ? wg_dy_emu_kernel<true> : wg_dy_emu_kernel<false>,
+                     dim3(static_cast<unsigned>((mt + 255) / 256)), dim3(256), 0, stream, dy, am,
+                     static_cast<int>(n), static_cast<int>(k), static_cast<int>(h),
+                     static_cast<int>(w), static_cast<int>(th), static_cast<int>(tw),
+                     static_cast<int>(p.mp), static_cast<int>(p.ksteps),
+                     static_cast<uint32_t>(n * k * h * w * 4));
+  hipLaunchKernelGGL(vec ? wg_x_emu_kernel<true> : wg_x_emu_kernel<false>,
+                     dim3(static_cast<unsigned>((vt + 255) / 256)), dim3(256), 0, stream, x, bv,
+                     static_cast<int>(c), static_cast<int>(h), static_cast<int>(w),
+                     static_cast<int>(tw), static_cast<int>(th * tw), static_cast<int>(P),
+                     static_cast<int>(p.np), static_cast<int>(p.ksteps),
+                     static_cast<uint32_t>(n * c * h * w * 4));
+  const int mtiles = static_cast<int>(p.mp / 128);
+  const int ntiles = static_cast<int>(p.np / p.bn);
+  const int64_t nwg = static_cast<int64_t>(mtiles) * ntiles * kP * splits;
+  auto gemm = p.bn == 64 ? bg_gemm_emu_kernel<64>
+              : p.bn == 96 ? bg_gemm_emu_kernel<96> : bg_gemm_emu_kernel<128>;
+  hipLaunchKernelGGL(gemm, dim3(static_cast<unsigned>(nwg)), dim3(256), 0, stream, am, bv, cb,
+                     static_cast<int>(p.mp), static_cast<int>(p.np), static_cast<int>(p.ksteps),
+                     mtiles, ntiles, static_cast<int>(kP), splits);
+  const int64_t ot = k * c;
+  hipLaunchKernelGGL(wg_output_emu_kernel, dim3(static_cast<unsigned>((ot + 255) / 256)),
+                     dim3(256), 0, stream, cb, dw, static_cast<int>(k), static_cast<int>(c),
+                     static_cast<int>(p.mp), static_cast<int>(p.np), splits, accum);
 }
 
 }  // namespace tgpipe

@@ -408,11 +408,7 @@ def _conv_grads(x: Tensor, weight: Tensor, dy: Tensor, cache: _TransformCache, n
         # node shared by micro-batches of different streams would otherwise sync them
         fuse, into = gradacc.target(param) if param is not None else (False, None)
         if f4:
-            # non-fused (transform passes + LDS-DMA GEMM) from 512 channels on both
-            # sides: 11-23 % faster there, 1.2-3.6x slower on the wide shallow planes
-            # (profiles/wgrad_f4_variants.json)
-            nonfused = min(weight.shape[0], weight.shape[1]) >= 512
-            dw = ops.wino4_wgrad(x, dy, 0, 1 if nonfused else 0, into)
+            dw = ops.wino4_wgrad(x, dy, 0, _wgrad_f4_variant(x, weight), into)
         elif mfma:
             dw = ops.wino_wgrad(x, dy, 0, -1, into)
         else:
@@ -427,6 +423,27 @@ def _conv_grads(x: Tensor, weight: Tensor, dy: Tensor, cache: _TransformCache, n
                 into.add_(dw)
             dw = None
     return dx, dw
+
+
+# TGPIPE_WGRAD_EMU=0 keeps the F(4x4) weight gradients on the f32 matrix pipes.
+WGRAD_EMU = os.environ.get('TGPIPE_WGRAD_EMU', '1') != '0'
+# the split-bf16 batched GEMM (variant 2) from this many 4x4 tiles on: its [36][K][C]
+# products go through HBM once, which only the longer tile reductions amortise
+WGRAD_EMU_MIN_TILES = 320
+
+
+def _wgrad_f4_variant(x: Tensor, weight: Tensor) -> int:
+    """F(4x4) weight-gradient kernel (benchmarks/wgrad_variants.py,
+    profiles/r5/wgrad_variants_emu.json): from 512 channels on both sides the non-fused
+    kernels (transform passes + GEMM; 11-23 % faster than the fused one there, 1.2-3.6x
+    slower on the wide shallow planes, profiles/wgrad_f4_variants.json) -- the split-bf16
+    batched GEMM (2) once the tile count amortises its products' trip through HBM
+    (40 x 512^2 at 24^2: 0.321 vs 0.401 ms; 40 x 1024^2 at 12^2: 0.286 vs 0.334), the f32
+    one (1) below (16 x 2048^2 at 6^2: 0.294 vs 0.474)."""
+    if min(weight.shape[0], weight.shape[1]) < 512:
+        return 0
+    tiles = x.shape[0] * -(-x.shape[2] // 4) * -(-x.shape[3] // 4)
+    return 2 if WGRAD_EMU and tiles >= WGRAD_EMU_MIN_TILES else 1
 
 
 def _wgrad_f4(x: Tensor, dy: Tensor, weight: Tensor) -> bool:
