@@ -123,11 +123,16 @@ class RNGSnapshot:
 class _Shared:
     """State shared by one Checkpoint/Recompute pair (the reference uses deques)."""
 
-    __slots__ = ('function', 'input_atomic', 'recomputed', 'rng', 'tape')
+    __slots__ = ('function', 'input_atomic', 'recomputed', 'rng', 'tape', 'inputs')
 
     def __init__(self, function: Any, input_atomic: bool) -> None:
         self.function = function
         self.input_atomic = input_atomic
+        # the Checkpoint node's inputs, for a recomputation its backward has to run itself;
+        # held here rather than in the node's saved tensors so a pipeline that recomputes
+        # ahead and back-propagates through the recomputed graph can release them while a
+        # loss still references the node (PipelineStage's last stage)
+        self.inputs: Optional[Tensors] = None
         self.recomputed: Deque[Recomputed] = deque(maxlen=1)
         self.rng: Deque[RNGSnapshot] = deque(maxlen=1)
         self.tape = RngTape()
@@ -146,7 +151,7 @@ class Checkpoint(torch.autograd.Function):
     def forward(ctx, phony: Tensor, shared: _Shared,  # type: ignore[override]
                 *input: Tensor) -> TensorOrTensors:
         ctx.shared = shared
-        ctx.save_for_backward(*input)
+        shared.inputs = input
         shared.rng.append(RNGSnapshot(input[0].device))
         with torch.no_grad(), enable_checkpointing(), shared.tape.recording():
             return shared.function(input[0] if shared.input_atomic else input)
@@ -156,7 +161,9 @@ class Checkpoint(torch.autograd.Function):
         shared: _Shared = ctx.shared
         if not shared.recomputed:
             # Nobody scheduled the recomputation ahead of time: do it now.
-            shared.run_recompute(ctx.saved_tensors)
+            assert shared.inputs is not None, 'checkpoint inputs already released'
+            shared.run_recompute(shared.inputs)
+        shared.inputs = None
         output, leaves = shared.recomputed.pop()
         outputs = output if isinstance(output, tuple) else (output,)
         pairs = [(y, g) for y, g in zip(outputs, grad_output) if y.requires_grad]
@@ -212,6 +219,7 @@ class Checkpointing:
         micro-batch instead of the Checkpoint node's reentrant one); the Checkpoint node
         then never runs."""
         output, leaves = self.shared.recomputed.pop()
+        self.shared.inputs = None  # the Checkpoint node will not run
         return (output if isinstance(output, tuple) else (output,)), leaves
 
 

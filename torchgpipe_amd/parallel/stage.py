@@ -962,7 +962,7 @@ class PipelineStage:
             tensors: List[Tensor] = []
             grads: List[Tensor] = []
             direct = bool(self.direct_backward and cell.chk is not None and not cell.seg
-                      and not self.is_last and cell.chk.shared.recomputed)
+                          and cell.chk.shared.recomputed)
             rec_out: Tuple[Tensor, ...] = ()
             leaves: Tuple[Tensor, ...] = ()
             if direct:
@@ -980,6 +980,16 @@ class PipelineStage:
                     torch.autograd.backward([losses[i]], [torch.ones_like(losses[i])])
                     for k, t in enumerate(act_out):
                         seg_grads[k] = t.grad
+                elif direct:
+                    # the loss's gradient w.r.t. the cell's outputs (a backward through the
+                    # loss alone), then on into the recomputed graph
+                    ks = [k for k, t in enumerate(act_out) if t.requires_grad]
+                    gouts = torch.autograd.grad([losses[i]], [act_out[k] for k in ks],
+                                                [torch.ones_like(losses[i])], allow_unused=True)
+                    for k, g in zip(ks, gouts):
+                        if g is not None and rec_out[k].requires_grad:
+                            tensors.append(rec_out[k])
+                            grads.append(g)
                 else:
                     tensors.append(losses[i])
                     grads.append(torch.ones_like(losses[i]))
