@@ -124,9 +124,14 @@ def measure_stage(kind, layers, lo, hi, batch_size, chunks, shape, checkpoint, d
             else:
                 chk, out = None, list(fn(tuple(acts)))
             cells.append((chk, out))
-        for chk, out in reversed(cells):
+        for k in reversed(range(len(cells))):
+            chk, out = cells[k]
             if chk is not None:
+                # as PipelineStage(direct_backward=True): recompute, then back-propagate
+                # through the recomputed graph (the Checkpoint node never runs)
                 chk.recompute_now()
+                out, _ = chk.take_recomputed()
+            cells[k] = (None, [])
             ys = [y for y in out if y.requires_grad]
             if last and kind == 'unet':
                 loss = F.binary_cross_entropy_with_logits(ys[0], torch.ones_like(ys[0]))
