@@ -141,6 +141,103 @@ def test_strided_1x1_backward_data_fill_overwrites_stale_memory(hw):
         assert rel_err(dx, x64.grad) < 2e-6
 
 
+def _presplit_runs(case, cfg, splits):
+    n, ci, h, w, co, kh, kw, stride, pad, offset = case
+    torch.manual_seed(0)
+    x = torch.randn(n, ci, h, w, device='cuda')
+    wt = torch.randn(co, ci, kh, kw, device='cuda') / (ci * kh * kw) ** 0.5
+    geo = _geo(kh, kw, stride, pad, offset)
+    dz = None
+    outs = {}
+    ops().conv_gemm_force_cfg(cfg, splits)
+    try:
+        for budget in (0, -1):  # in-kernel split, then pre-split weights
+            ops().conv_gemm_presplit(budget)
+            z = ops().conv_gemm_forward(x, wt, geo, True)
+            if dz is None:
+                dz = torch.randn_like(z)
+            dx = ops().conv_gemm_backward_data(dz, x, wt, geo, True)
+            outs[budget] = (z, dx)
+        held = ops().conv_gemm_presplit(-1)
+    finally:
+        ops().conv_gemm_force_cfg(-1)
+        ops().conv_gemm_presplit(-1)
+    return outs, held
+
+
+@pytest.mark.parametrize('splits', [1, 4])
+@pytest.mark.parametrize('cfg', [7, 8, 9])
+@pytest.mark.parametrize('case', CASES, ids=[f'{c[5]}x{c[6]}s{c[7]}o{c[9]}_{c[0]}x{c[1]}x{c[2]}'
+                                            for c in CASES])
+def test_presplit_weights_are_bit_identical(case, cfg, splits):
+    """Weights split into bf16 planes once (conv_gemm_presplit_kernel) give exactly the
+    products of the split-bf16 kernels splitting them as they stage them -- forward and
+    backward-data, every geometry (K not a multiple of 8: the zero-padded last octet; the
+    stride-phase backward-data keeps the in-kernel split)."""
+    outs, held = _presplit_runs(case, cfg, splits)
+    assert held > 0  # the forward at least ran on the cached planes
+    for a, b in zip(outs[0], outs[-1]):
+        assert torch.equal(a, b)
+
+
+def test_presplit_follows_weight_updates_and_drops_dead_weights():
+    ops().conv_gemm_force_cfg(9)
+    ops().conv_gemm_presplit(-1)
+    try:
+        torch.manual_seed(0)
+        x = torch.randn(4, 64, 14, 14, device='cuda')
+        w = torch.randn(96, 64, 1, 1, device='cuda') * 0.1
+        geo = [1, 1, 1, 1, 0, 0, 0, 0]
+        z1 = ops().conv_gemm_forward(x, w, geo, True)
+        with torch.no_grad():
+            w.mul_(2)  # version bump: the next launch re-derives (powers of 2 split exactly)
+        assert torch.equal(ops().conv_gemm_forward(x, w, geo, True), 2 * z1)
+        with torch.no_grad():
+            w.mul_(0.5)
+        assert ops().conv_gemm_presplit_refresh() == 1  # re-derived in place
+        assert torch.equal(ops().conv_gemm_forward(x, w, geo, True), z1)
+        del w
+        assert ops().conv_gemm_presplit_refresh() == 0  # the dead weight's entry is dropped
+    finally:
+        ops().conv_gemm_force_cfg(-1)
+        ops().conv_gemm_presplit(-1)
+
+
+def test_presplit_in_a_captured_graph_follows_the_step_refresh():
+    """A hipGraph bakes the cached planes' address in: the step-start refresh
+    (ops/conv.py refresh_step_caches) re-derives them in place, so a replay after an
+    optimizer update reads the new weights."""
+    ops().conv_gemm_force_cfg(7)
+    ops().conv_gemm_presplit(-1)
+    try:
+        torch.manual_seed(0)
+        x = torch.randn(4, 32, 14, 14, device='cuda')
+        w = torch.randn(48, 32, 1, 7, device='cuda') * 0.1
+        geo = [1, 7, 1, 1, 0, 3, 0, 0]
+        want = ops().conv_gemm_forward(x, w, geo, True)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ops().conv_gemm_forward(x, w, geo, True)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = ops().conv_gemm_forward(x, w, geo, True)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, want)
+        with torch.no_grad():
+            w.mul_(2)
+        from torchgpipe_amd.ops.conv import refresh_step_caches
+        refresh_step_caches(nn.Module())
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, 2 * want)
+    finally:
+        ops().conv_gemm_force_cfg(-1)
+        ops().conv_gemm_presplit(-1)
+
+
 def _block(kind, ci, co):
     if kind == '1x1':
         conv = nn.Conv2d(ci, co, 1, bias=False)

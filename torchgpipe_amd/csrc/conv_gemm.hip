@@ -47,6 +47,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 #include <type_traits>
 #include <vector>
 
@@ -254,15 +255,23 @@ __device__ __forceinline__ void store_nmajor(float* img, const floatx4 (&v)[Q], 
 // MFMA's rate per product: six of them cost 3/8 of the f32 MFMA time of the same tile.
 // Accumulation stays f32 in the MFMA accumulators; the fp64 tests hold these
 // configurations to the same error bounds as the f32 ones (tests/ops/test_convbn_gpu.py).
+__device__ __forceinline__ void split1(float v, __bf16& hi, __bf16& mid, __bf16& lo) {
+  const __bf16 h = static_cast<__bf16>(v);
+  const float r = v - static_cast<float>(h);
+  const __bf16 m = static_cast<__bf16>(r);
+  hi = h;
+  mid = m;
+  lo = static_cast<__bf16>(r - static_cast<float>(m));
+}
+
 __device__ __forceinline__ void split3(const floatx4& v, bf16x4& hi, bf16x4& mid, bf16x4& lo) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const __bf16 h = static_cast<__bf16>(v[e]);
-    const float r = v[e] - static_cast<float>(h);
-    const __bf16 m = static_cast<__bf16>(r);
+    __bf16 h, m, l;
+    split1(v[e], h, m, l);
     hi[e] = h;
     mid[e] = m;
-    lo[e] = static_cast<__bf16>(r - static_cast<float>(m));
+    lo[e] = l;
   }
 }
 
@@ -457,7 +466,11 @@ __device__ __forceinline__ Col make_col(const Geo& g, int j, int N) {
   return c;
 }
 
-template <int MODE, int CFG, bool kPlain>
+// kPreA (EMU forward / backward-data): A arrives pre-split ([M][ceil(K/8)][hi, mid, lo][8]
+// bf16, conv_gemm_presplit_kernel) -- the weights, split once per step instead of by every
+// column block of every micro-batch; each thread stages whole k octets of it (three 16-byte
+// loads and three ds_write_b128 per octet, no split arithmetic).
+template <int MODE, int CFG, bool kPlain, bool kPreA>
 __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void conv_gemm_kernel(
     const float* __restrict__ a_src, const float* __restrict__ b_src,
     const float* __restrict__ x_mask, float* __restrict__ out, float* __restrict__ part_mean,
@@ -521,7 +534,11 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
   const bool quads = kPlain && (hw_out & 3) == 0;
 
   constexpr int kRB = kBK_major ? C::kBQuadsK : C::kBQuadsN;
+  static_assert(!kPreA || (kEmu && MODE != kWgrad), "pre-split A: EMU forward / bwd-data");
+  constexpr int kAOct = kBK * C::BM / 8 / kThreads;  // pre-split A octets per thread
+  constexpr int kAU = kPreA ? kAOct : C::kAQuads;    // A load units
   floatx4 ra[SUB][C::kAQuads], rb[SUB][kRB];
+  floatx4 rs[SUB][kPreA ? kAOct : 1][3];  // pre-split A: the three planes of one octet
 
   // N-major B columns of this thread (forward / bwd-data): a quad of adjacent columns when
   // the operand is read as 16-byte quads (1x1, planes of 4k pixels), else columns BN/4
@@ -603,6 +620,19 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
       }
       return v;
     }
+  };
+
+  // pre-split A: row (tid >> 2) + (threads / 4) i, k octet (tid & 3) -- 48 bytes at
+  // (row * ceil(K/8) + k/8) * 48 (k0 and k_end are multiples of 8 within K; the octet past
+  // a K that is not is zero-padded)
+  auto load_a_split = [&](int k0, int i, floatx4 (&v)[3]) {
+    const int k = k0 + 8 * (tid & 3);
+    const int row = m0 + (tid >> 2) + (kThreads / 4) * i;
+    const uint32_t off = row < M && k < k_end
+                             ? static_cast<uint32_t>((row * ((K + 7) >> 3) + (k >> 3)) * 48)
+                             : kOOB;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) v[p] = bload4(ar, off + 16 * p);
   };
 
   auto load_b = [&](int k0, int i) -> floatx4 {
@@ -764,14 +794,18 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
   };
 
   // load unit q of sub-stage u (A quads first, then B quads) for the stage at k0
-  constexpr int kUnits = C::kAQuads + kRB;
+  constexpr int kUnits = kAU + kRB;
   auto load_unit = [&](int k0, int u, int q) {
-    if (q < C::kAQuads)
-      ra[u][q] = load_a(k0 + u * kBK, q);
-    else if constexpr (kEmu && !kBK_major)
-      rb[u][q - C::kAQuads] = load_b_emu(k0 + u * kBK, q - C::kAQuads);
-    else
-      rb[u][q - C::kAQuads] = load_b(k0 + u * kBK, q - C::kAQuads);
+    if (q < kAU) {
+      if constexpr (kPreA)
+        load_a_split(k0 + u * kBK, q, rs[u][q]);
+      else
+        ra[u][q] = load_a(k0 + u * kBK, q);
+    } else if constexpr (kEmu && !kBK_major) {
+      rb[u][q - kAU] = load_b_emu(k0 + u * kBK, q - kAU);
+    } else {
+      rb[u][q - kAU] = load_b(k0 + u * kBK, q - kAU);
+    }
   };
   // The forward / weight-gradient ReLU of X is applied here, after the stage's MFMAs:
   // applied in load_b it made every prefetch wait for its own loads (vmcnt(0) right
@@ -790,10 +824,21 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
     if constexpr (kEmu) {
 #pragma unroll
       for (int u = 0; u < SUB; ++u) {
+        if constexpr (kPreA) {
 #pragma unroll
-        for (int i = 0; i < C::kAQuads; ++i)
-          store_emu_quad<C::BM>(aimg(buf, u), ra[u][i], (tid >> 3) + (kThreads / 8) * i,
-                                tid & 7);
+          for (int i = 0; i < kAOct; ++i) {
+            __bf16* p = reinterpret_cast<__bf16*>(aimg(buf, u)) +
+                        emu_off<C::BM>(tid & 3, (tid >> 2) + (kThreads / 4) * i);
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+              *reinterpret_cast<floatx4*>(p + pl * kBK * C::BM) = rs[u][i][pl];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < C::kAQuads; ++i)
+            store_emu_quad<C::BM>(aimg(buf, u), ra[u][i], (tid >> 3) + (kThreads / 8) * i,
+                                  tid & 7);
+        }
 #pragma unroll
         for (int i = 0; i < kRB; ++i) {
           if constexpr (kBK_major)
@@ -1017,7 +1062,7 @@ template <int MODE, int CFG>
 void launch_cfg(const float* a, const float* b, const float* xm, float* out, float* pmean,
                 float* pm2, const Geo& g, int M, int N, int K, int splits, int64_t split_stride,
                 bool accumulate, int64_t a_bytes, int64_t b_bytes, hipStream_t stream,
-                const PhaseSet& ps = PhaseSet{}) {
+                const PhaseSet& ps = PhaseSet{}, bool pre_a = false) {
   using C = Cfg<CFG>;
   const int mb = (M + C::BM - 1) / C::BM, nb = (N + C::BN - 1) / C::BN;
   int k_chunk = (K + splits - 1) / splits;
@@ -1026,14 +1071,55 @@ void launch_cfg(const float* a, const float* b, const float* xm, float* out, flo
   const bool plain = g.taps == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 &&
                      g.oh == 0 && g.ow == 0;
   const dim3 grid(mb * nb, zs, ps.count > 0 ? ps.count : 1), block(C::kThreads);
-  if (plain)
-    hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, true>), grid, block, 0, stream, a, b, xm,
-                       out, pmean, pm2, g, M, N, K, k_chunk, split_stride, accumulate ? 1 : 0,
-                       a_bytes, b_bytes, ps);
-  else
-    hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, false>), grid, block, 0, stream, a, b, xm,
-                       out, pmean, pm2, g, M, N, K, k_chunk, split_stride, accumulate ? 1 : 0,
-                       a_bytes, b_bytes, ps);
+  auto go = [&](auto plain_c, auto pre_c) {
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, CFG, decltype(plain_c)::value,
+                                         decltype(pre_c)::value>),
+                       grid, block, 0, stream, a, b, xm, out, pmean, pm2, g, M, N, K, k_chunk,
+                       split_stride, accumulate ? 1 : 0, a_bytes, b_bytes, ps);
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  if constexpr (C::EMU && MODE != kWgrad) {
+    if (pre_a) {
+      if (plain) go(T{}, T{}); else go(F{}, T{});
+      return;
+    }
+  }
+  if (plain) go(T{}, F{}); else go(F{}, F{});
+}
+
+// A operand of a forward / backward-data GEMM split into bf16 planes once (see
+// launch_conv_gemm_presplit): one thread per (row, k octet), split1 as the GEMM kernels
+// would split it (bit-identical products).
+__global__ __launch_bounds__(256) void conv_gemm_presplit_kernel(const float* __restrict__ w,
+                                                                 bf16x8* __restrict__ out,
+                                                                 int M, int K, int ko, int taps,
+                                                                 int transposed) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= static_cast<int64_t>(M) * ko) return;
+  const int row = static_cast<int>(idx / ko), j = static_cast<int>(idx - static_cast<int64_t>(row) * ko);
+  bf16x8 hi, mid, lo;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * j + e;
+    float v = 0.f;
+    if (k < K) {
+      if (transposed) {  // A[ci = row][co * T + t] = W[co][ci][t]
+        const int co = k / taps, t = k - co * taps;
+        v = w[(static_cast<int64_t>(co) * M + row) * taps + t];
+      } else {
+        v = w[static_cast<int64_t>(row) * K + k];
+      }
+    }
+    __bf16 h, m, l;
+    split1(v, h, m, l);
+    hi[e] = h;
+    mid[e] = m;
+    lo[e] = l;
+  }
+  out[3 * idx] = hi;
+  out[3 * idx + 1] = mid;
+  out[3 * idx + 2] = lo;
 }
 
 // Sum of the split partials: ws[s][plane][c][hw] -> out[plane][c_off + c][hw] (c_total
@@ -1378,6 +1464,18 @@ int env_int(const char* name, int fallback) {
   return v != nullptr && *v != 0 ? std::atoi(v) : fallback;
 }
 
+bool conv_gemm_emu_cfg(int cfg) { return cfg >= kFirstEmuCfg && cfg < kConvGemmCfgs; }
+
+void launch_conv_gemm_presplit(const float* w, void* out, int M, int K, int taps,
+                               bool transposed, hipStream_t stream) {
+  const int ko = (K + 7) / 8;
+  const int64_t total = static_cast<int64_t>(M) * ko;
+  if (total == 0) return;
+  hipLaunchKernelGGL(conv_gemm_presplit_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
+                     dim3(256), 0, stream, w, static_cast<bf16x8*>(out), M, K, ko,
+                     std::max(1, taps), transposed ? 1 : 0);
+}
+
 bool conv_gemm_phased(const ConvGemmGeo& g) {
   return !g.phase && (g.kh > 1 || g.kw > 1) && (g.sh > 1 || g.sw > 1) && g.oh == 0 &&
          g.ow == 0;
@@ -1534,10 +1632,13 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
   float* pm = split ? nullptr : part_mean;
   float* pm2 = split ? nullptr : part_m2;
   const bool acc = accumulate && !split;
+  if (cg.a_split && (mode == kWgrad || !conv_gemm_emu_cfg(plan.cfg) || cg.phase))
+    throw std::runtime_error("conv_gemm: a pre-split A needs a split-bf16 forward / "
+                             "backward-data plan");
   auto go = [&](auto mode_c, auto cfg_c, float* p1, float* p2, const float* mask) {
     launch_cfg<decltype(mode_c)::value, decltype(cfg_c)::value>(
         a, b, mask, dst, p1, p2, gk, M, N, K, plan.splits, stride, acc, a_bytes, b_bytes,
-        stream);
+        stream, PhaseSet{}, cg.a_split);
   };
   using F = std::integral_constant<int, kFwd>;
   using D = std::integral_constant<int, kBwdData>;

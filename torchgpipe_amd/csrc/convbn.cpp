@@ -226,10 +226,192 @@ int64_t conv_gemm_plans_import(const std::string& text) {
   return taken;
 }
 
-// One implicit-GEMM launch with its split-reduction workspace.
+// ---- pre-split A operands -------------------------------------------------------------------
+// A split-bf16 plan (conv_gemm.hip, tile configs 7-9) splits every A element into three bf16
+// planes as it stages them -- the same weights again in every column block of every
+// micro-batch, half of the kernel's split arithmetic.  Here the weights of forward /
+// backward-data GEMMs are split once per weight version instead ([M][ceil(K/8)][3][8] bf16,
+// 1.5x the weight's bytes) and the kernel loads the planes.  Entries are keyed by the
+// source tensor's storage, held by weak reference (a dead weight's entry is dropped), and
+// re-derived when its version counter moves: lazily by the next launch (readers on other
+// streams wait for that derive's event), or in place for the whole step by
+// conv_gemm_presplit_refresh (PipelineStage's step start, ops/conv.py
+// refresh_step_caches) -- which is what keeps a captured hipGraph, that baked the buffer in,
+// reading the current weights.  Inside a capture a stale or missing entry is derived into
+// the graph's own buffer on every replay (the cache is not written).
+// TGPIPE_CG_PRESPLIT_MB: the bytes all entries may hold (default 512; 0 = off).
+struct PreDims {
+  int M = 0, K = 0, taps = 1;
+  bool transposed = false;
+  bool operator==(const PreDims& o) const {
+    return M == o.M && K == o.K && taps == o.taps && transposed == o.transposed;
+  }
+};
+using WeakImpl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>;
+struct PreSplit {
+  PreSplit(WeakImpl s, PreDims dims) : src(std::move(s)), d(dims) {}
+  WeakImpl src;
+  PreDims d;
+  int64_t version = -1;
+  at::Tensor split;
+  hipEvent_t ready = nullptr;
+  hipStream_t stream = nullptr;  // derived lazily on this stream (null: ordered by the caller)
+};
+using PreKey = std::tuple<const void*, bool, int>;
+std::mutex pre_mutex;
+std::map<PreKey, PreSplit> pre_cache;
+int64_t pre_bytes = 0;
+std::atomic<int64_t> pre_budget{-1};
+
+int64_t presplit_budget() {
+  int64_t b = pre_budget.load();
+  if (b < 0) {
+    b = static_cast<int64_t>(std::max(0, env_int("TGPIPE_CG_PRESPLIT_MB", 512))) << 20;
+    pre_budget.store(b);
+  }
+  return b;
+}
+
+int64_t presplit_numel(int M, int K) { return static_cast<int64_t>(M) * ((K + 7) / 8) * 24; }
+
+void presplit_derive(const at::Tensor& src, at::Tensor& out, const PreDims& d,
+                     hipStream_t stream) {
+  launch_conv_gemm_presplit(src.data_ptr<float>(), out.data_ptr(), d.M, d.K, d.taps,
+                            d.transposed, stream);
+}
+
+void presplit_erase(std::map<PreKey, PreSplit>::iterator it) {
+  pre_bytes -= it->second.split.numel() * 2;
+  if (it->second.ready != nullptr) hipEventDestroy(it->second.ready);
+  pre_cache.erase(it);
+}
+
+// The pre-split A of `src` (row-major [M][K], or with `transposed` W[co][ci][T] read as
+// A[ci][co*T + t]) for a launch on the current stream, or undefined (no budget).
+at::Tensor presplit_of(const at::Tensor& src, bool transposed, int M, int K, int taps,
+                       const at::Tensor& like) {
+  const int64_t budget = presplit_budget();
+  const int64_t numel = presplit_numel(M, K);
+  if (budget <= 0 || numel * 2 > kMaxBytes || !src.is_contiguous() ||
+      src.scalar_type() != at::kFloat || src.numel() != static_cast<int64_t>(M) * K)
+    return {};
+  const hipStream_t stream = cur_stream(like);
+  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(stream, &capture) == hipSuccess &&
+                         capture != hipStreamCaptureStatusNone;
+  const int64_t version = static_cast<int64_t>(src._version());
+  const PreKey key{src.data_ptr(), transposed, src.device().index()};
+  const PreDims probe{M, K, taps, transposed};
+  std::lock_guard<std::mutex> lock(pre_mutex);
+  auto it = pre_cache.find(key);
+  if (it != pre_cache.end()) {
+    PreSplit& e = it->second;
+    auto alive = e.src.lock();
+    const bool same = alive.get() == src.unsafeGetTensorImpl() && e.d == probe;
+    if (same && e.version == version) {
+      if (e.stream != nullptr && e.stream != stream && !capturing)
+        hipStreamWaitEvent(stream, e.ready, 0);
+      return e.split;
+    }
+    if (capturing) {  // derived into the graph's own buffer (see above)
+      at::Tensor tmp = at::empty({numel}, like.options().dtype(at::kBFloat16));
+      presplit_derive(src, tmp, probe, stream);
+      return tmp;
+    }
+    if (same) {  // stale: in place, on this stream
+      presplit_derive(src, e.split, e.d, stream);
+      e.version = version;
+      hipEventRecord(e.ready, stream);
+      e.stream = stream;
+      return e.split;
+    }
+    presplit_erase(it);  // another tensor at the same address (or a reshaped use)
+  }
+  if (capturing) {
+    at::Tensor tmp = at::empty({numel}, like.options().dtype(at::kBFloat16));
+    presplit_derive(src, tmp, probe, stream);
+    return tmp;
+  }
+  // drop the entries of dead tensors before charging the budget
+  for (auto j = pre_cache.begin(); j != pre_cache.end();) {
+    auto nxt = std::next(j);
+    if (j->second.src.expired()) presplit_erase(j);
+    j = nxt;
+  }
+  if (pre_bytes + numel * 2 > budget) return {};
+  PreSplit e(WeakImpl(src.getIntrusivePtr()), probe);
+  e.version = version;
+  e.split = at::empty({numel}, like.options().dtype(at::kBFloat16));
+  presplit_derive(src, e.split, e.d, stream);
+  hipEventCreateWithFlags(&e.ready, hipEventDisableTiming);
+  hipEventRecord(e.ready, stream);
+  e.stream = stream;
+  pre_bytes += numel * 2;
+  at::Tensor out = e.split;
+  pre_cache.emplace(key, std::move(e));
+  return out;
+}
+
+// Re-derive every stale entry in place on its device's current stream; drop dead ones.
+// Returns the entries kept.
+int64_t conv_gemm_presplit_refresh() {
+  std::lock_guard<std::mutex> lock(pre_mutex);
+  for (auto it = pre_cache.begin(); it != pre_cache.end();) {
+    auto nxt = std::next(it);
+    PreSplit& e = it->second;
+    auto alive = e.src.lock();
+    if (!alive) {
+      presplit_erase(it);
+    } else {
+      const at::Tensor src(alive);
+      if (static_cast<int64_t>(src._version()) != e.version) {
+        c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+        presplit_derive(src, e.split, e.d, cur_stream(src));
+        e.version = static_cast<int64_t>(src._version());
+      }
+      e.stream = nullptr;  // ordered before the step by the caller
+    }
+    it = nxt;
+  }
+  return static_cast<int64_t>(pre_cache.size());
+}
+
+// Test / benchmark hook: set the pre-split budget (MiB; 0 = off, < 0 = the environment's)
+// and drop every entry.  Returns the bytes the entries held.
+int64_t conv_gemm_presplit(int64_t budget_mb) {
+  std::lock_guard<std::mutex> lock(pre_mutex);
+  const int64_t held = pre_bytes;
+  while (!pre_cache.empty()) presplit_erase(pre_cache.begin());
+  pre_budget.store(budget_mb < 0 ? -1 : budget_mb << 20);
+  return held;
+}
+
+// The weight a forward / backward-data GEMM's A operand comes from, for a pre-split A:
+// `t` row-major [M][K] (transposed = false) or W[co][ci][T] read transposed.
+struct ASource {
+  const at::Tensor* t = nullptr;
+  bool transposed = false;
+};
+
+// One implicit-GEMM launch with its split-reduction workspace (a pre-split A when the plan
+// is a split-bf16 one and `src` names the A operand's weight).
 void run_gemm(int mode, const float* a, const float* b, const float* mask, float* out,
               float* pm, float* pm2, const ConvGemmGeo& g, const ConvGemmPlan& plan,
-              bool accumulate, int64_t a_bytes, int64_t b_bytes, const at::Tensor& like) {
+              bool accumulate, int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
+              ASource src = {}) {
+  if (src.t != nullptr && mode != 2 && conv_gemm_emu_cfg(plan.cfg) && !g.phase) {
+    const int taps = g.kh * g.kw;
+    const int M = mode == 0 ? g.co : g.ci;
+    const int K = (mode == 0 ? g.ci : g.co) * taps;
+    const at::Tensor split = presplit_of(*src.t, src.transposed, M, K, taps, like);
+    if (split.defined()) {
+      ConvGemmGeo gs = g;
+      gs.a_split = true;
+      launch_one(mode, static_cast<const float*>(split.data_ptr()), b, mask, out, pm, pm2, gs,
+                 plan, accumulate, split.numel() * 2, b_bytes, like);
+      return;
+    }
+  }
   launch_one(mode, a, b, mask, out, pm, pm2, g, plan, accumulate, a_bytes, b_bytes, like);
 }
 
@@ -310,7 +492,7 @@ void backward_data_into(const at::Tensor& wt, const at::Tensor& dz, const at::Te
                  dz.numel() * 4, x, x.numel());
   run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
            dx.data_ptr<float>(), nullptr, nullptr, g, plan, accumulate, wt.numel() * 4,
-           dz.numel() * 4, x);
+           dz.numel() * 4, x, ASource{&wt, false});
 }
 
 // A channel slice of a dense NCHW tensor (e.g. the gradient of one input of a
@@ -440,7 +622,7 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     run_gemm(0, wt.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
              epilogue_stats ? part0 : nullptr,
              epilogue_stats ? part1 : nullptr, p.geo[i], pl, false,
-             wt.numel() * 4, x.numel() * 4, x);
+             wt.numel() * 4, x.numel() * 4, x, ASource{&weights[i], false});
   }
   if (split && !fused_stats)
     launch_bn_stats(z.data_ptr<float>(), part0, part1, n,
@@ -879,7 +1061,7 @@ std::vector<at::Tensor> convbn_group_forward(
   float* const part1 = part0 + static_cast<int64_t>(blocks) * c;
   run_gemm(0, w_cat.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
            part0, part1, p.geo[0], plan, false,
-           w_cat.numel() * 4, x.numel() * 4, x);
+           w_cat.numel() * 4, x.numel() * 4, x, ASource{&w_cat, false});
   auto mean = at::empty({c}, x.options());
   auto invstd = at::empty({c}, x.options());
   launch_bn_finalize_apply(part0, part1, blocks, width, n,
@@ -1094,7 +1276,8 @@ at::Tensor conv_gemm_forward(const at::Tensor& x_in, const at::Tensor& weight,
                  nullptr, nullptr, p.geo[0], false, weight.numel() * 4, x.numel() * 4, x,
                  z.numel());
   run_gemm(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
-           nullptr, nullptr, p.geo[0], plan, false, weight.numel() * 4, x.numel() * 4, x);
+           nullptr, nullptr, p.geo[0], plan, false, weight.numel() * 4, x.numel() * 4, x,
+           ASource{&weight, false});
   return z;
 }
 
@@ -1431,6 +1614,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("lib_dgrad_import(str text) -> int", &tgpipe::lib_dgrad_import);
   m.def("lib_dgrad_force(int mode) -> ()", &tgpipe::lib_dgrad_force);
   m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
+  m.def("conv_gemm_presplit(int budget_mb) -> int", &tgpipe::conv_gemm_presplit);
+  m.def("conv_gemm_presplit_refresh() -> int", &tgpipe::conv_gemm_presplit_refresh);
   m.def("conv_gemm_sweep(int mode, Tensor x, Tensor weight, int[] geo, int reps) -> float[]");
   m.def("conv_gemm_plans_import(str text) -> int", &tgpipe::conv_gemm_plans_import);
   m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "

@@ -168,6 +168,10 @@ struct ConvGemmGeo {
   // strided 1x1 backward-data (stride 2, no padding / offset, even width): also write the
   // zeros of the other three pixels of each 2x2 block, so dX needs no memset first
   bool fill = false;
+  // forward / backward-data on a split-bf16 tile config (conv_gemm_emu_cfg): `a` is the A
+  // operand pre-split into bf16 planes ([M][ceil(K/8)][hi, mid, lo][8], conv_gemm_presplit),
+  // a_bytes its size -- the kernel stages it without splitting
+  bool a_split = false;
 };
 // Sub-pixel decomposition of a strided convolution's backward-data: input pixels of one
 // residue (a, b) modulo the stride receive exactly the taps th = th0 + sh*i, tw = tw0 + sw*j,
@@ -221,6 +225,14 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
 // sized slices that persists across the micro-batches of a step: split s stores
 // (accumulate = false) or adds (true) its partial into slice s, with no reduction pass;
 // launch_slab_flush sums the slices into the gradient once per step.
+// Whether a plan's tile config runs on the split-bf16 MFMA (and so can take a pre-split A).
+bool conv_gemm_emu_cfg(int cfg);
+// The A operand of a forward / backward-data GEMM (M x K row-major: W[co][ci*T], or with
+// `transposed` A[ci][co*T + t] = W[co][ci][t], T = taps) split into three bf16 planes,
+// [M][ceil(K/8)][3][8] (k octets, zero past K): 6 bytes per element, into `out`
+// (M * ceil(K/8) * 24 bf16).
+void launch_conv_gemm_presplit(const float* w, void* out, int M, int K, int taps,
+                               bool transposed, hipStream_t stream);
 void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
                                  const ConvGemmGeo& g, const ConvGemmPlan& plan, bool accumulate,
                                  int64_t a_bytes, int64_t b_bytes, hipStream_t stream);

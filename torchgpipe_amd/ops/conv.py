@@ -244,12 +244,17 @@ class _TransformCache:
 
 def refresh_step_caches(module: nn.Module) -> None:
     """Refresh every step-scoped derived-weight cache in ``module`` in place (current
-    stream): Winograd transforms, transposed weights and grouped-GEMM concatenations."""
+    stream): Winograd transforms, transposed weights, grouped-GEMM concatenations and the
+    split-bf16 GEMMs' pre-split weights."""
     from torchgpipe_amd.ops.convbn import _GroupCache
     for m in module.modules():
         for v in list(vars(m).values()):
             if isinstance(v, (_TransformCache, _GroupCache)):
                 v.refresh()
+    if _ext._loaded:
+        # then the implicit-GEMM kernels' pre-split weights (csrc/convbn.cpp presplit_of;
+        # every entry of the process, after the transposes above they may be derived from)
+        torch.ops.tgpipe.conv_gemm_presplit_refresh()
 
 
 def clear_winograd_caches(module: torch.nn.Module) -> None:
