@@ -254,6 +254,57 @@ def _block(kind, ci, co):
 @pytest.mark.parametrize('channels', [(32, 48, 14), (512, 256, 7)], ids=['epilogue-stats',
                                                                        'split-stats'])
 def test_fused_relu_conv_bn_matches_fp64_training_step(kind, with_add, channels, tile_cfg):
+    _check_fused_training_step(kind, with_add, channels)
+
+
+@pytest.fixture(params=[(7, 4), (9, 3), (0, 8)], ids=['cfg7-split4', 'cfg9-split3', 'cfg0-split8'])
+def split_cfg(request):
+    """Split-K forward plans (the small-plane ones reduce, normalise and take their
+    statistics in one launch: launch_split_bn_small)."""
+    ops().conv_gemm_force_cfg(*request.param)
+    yield request.param
+    ops().conv_gemm_force_cfg(-1)
+
+
+@pytest.mark.parametrize('kind', ['1x1', '1x7'])
+@pytest.mark.parametrize('with_add', [False, True])
+@pytest.mark.parametrize('channels', [(256, 192, 7), (256, 64, 8), (384, 48, 5)],
+                         ids=['7x7', '8x8', '5x5'])
+def test_fused_split_small_plane_matches_fp64(kind, with_add, channels, split_cfg):
+    _check_fused_training_step(kind, with_add, channels, n=20)
+
+
+@pytest.mark.parametrize('with_add', [False, True])
+def test_fused_split_small_plane_relu_out_matches_fp64(with_add, split_cfg):
+    """ResNet's Conv-BN-ReLU (and with `add` its residual join) on the fused split path."""
+    from torchgpipe_amd.ops.convbn import relu_conv_bn
+    torch.manual_seed(3)
+    conv = nn.Conv2d(128, 96, 1, bias=False).cuda()
+    bn = nn.BatchNorm2d(96).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    c64, b64 = copy.deepcopy(conv).double(), copy.deepcopy(bn).double()
+    x = torch.randn(12, 128, 7, 7, device='cuda', requires_grad=True)
+    add = torch.randn(12, 96, 7, 7, device='cuda', requires_grad=True) if with_add else None
+    y = relu_conv_bn(x, [(conv, 0)], bn, relu=False, add=add, relu_out=True)
+    x64 = x.detach().double().requires_grad_(True)
+    add64 = add.detach().double().requires_grad_(True) if with_add else None
+    y64 = b64(c64(x64))
+    y64 = F.relu(y64 + add64 if with_add else y64)
+    assert rel_err(y, y64) < 1e-5
+    g = torch.randn_like(y)
+    y.backward(g)
+    y64.backward(g.double())
+    assert rel_err(x.grad, x64.grad) < 1e-5
+    if with_add:
+        assert rel_err(add.grad, add64.grad) < 1e-5
+    assert rel_err(conv.weight.grad, c64.weight.grad) < 1e-5
+    assert rel_err(bn.weight.grad, b64.weight.grad) < 1e-5
+    assert rel_err(bn.running_var, b64.running_var) < 1e-6
+
+
+def _check_fused_training_step(kind, with_add, channels, n=6):
     torch.manual_seed(1)
     ci, co, hw = channels
     block = _block(kind, ci, co).cuda()
@@ -261,8 +312,8 @@ def test_fused_relu_conv_bn_matches_fp64_training_step(kind, with_add, channels,
         block[2].weight.uniform_(0.5, 1.5)
         block[2].bias.uniform_(-0.5, 0.5)
     ref = copy.deepcopy(block).double()
-    x = torch.randn(6, ci, hw, hw, device='cuda', requires_grad=True)
-    add = torch.randn(6, co, hw, hw, device='cuda', requires_grad=True) if with_add else None
+    x = torch.randn(n, ci, hw, hw, device='cuda', requires_grad=True)
+    add = torch.randn(n, co, hw, hw, device='cuda', requires_grad=True) if with_add else None
     y = block(x, add)
     x64 = x.detach().double().requires_grad_(True)
     add64 = add.detach().double().requires_grad_(True) if with_add else None

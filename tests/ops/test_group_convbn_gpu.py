@@ -24,10 +24,20 @@ def rel_err(a, b):
     return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
 
 
+@pytest.fixture(params=[None, (9, 4)], ids=['tuned', 'cfg9-split4'])
+def plan(request):
+    """Tuned plans, and a forced split-K plan (on 7^2 planes: the partials reduced,
+    normalised and their statistics taken by one launch, launch_split_bn_small)."""
+    if request.param is not None:
+        torch.ops.tgpipe.conv_gemm_force_cfg(*request.param)
+    yield request.param
+    torch.ops.tgpipe.conv_gemm_force_cfg(-1)
+
+
 @pytest.mark.parametrize('shape', [(6, 64, 14, (16, 64, 16)), (4, 256, 7, (64, 256, 64)),
                                    (3, 32, 28, (8, 48))], ids=['14x14', '7x7-split', 'two'])
 @pytest.mark.parametrize('unused', [False, True], ids=['all-used', 'one-unused'])
-def test_grouped_ops_match_fp64(shape, unused):
+def test_grouped_ops_match_fp64(shape, unused, plan):
     n, ci, hw, cos = shape
     torch.manual_seed(0)
     triplets = []

@@ -219,6 +219,123 @@ __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
   }
 }
 
+// A split-K forward of a small-plane convolution (s <= 64 pixels) and its BatchNorm, after
+// the GEMM left its split partials in `ws` ([split][n][c][s]): one workgroup per channel
+// sums the partials of every image (z, kept for the backward), takes the channel's
+// statistics in fp64 over the values it holds (two passes, mean then M2: no partials to
+// merge, no cancellation), finalizes (as bn_finalize_apply: running statistics, counter,
+// DeferredBatchNorm accumulators, the backward's zeroed sums) and normalises -- one launch
+// instead of split_reduce_stats + bn_finalize_apply, and z read back from registers.
+constexpr int kSplitBnPer = 16;  // values per thread: n * s <= 16 * 256
+
+template <bool kAdd, bool kRelu>
+__global__ __launch_bounds__(256) void split_bn_small_kernel(
+    const float* __restrict__ ws, int splits, int64_t stride, float* __restrict__ z, int n,
+    int c, int s, float eps, double momentum, float* __restrict__ mean,
+    float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv,
+    int64_t* __restrict__ tracked, double* __restrict__ acc, float* __restrict__ zero2c,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ add, float* __restrict__ y, BnParts parts) {
+  const int ch = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int yc = c, ych = ch;
+  if (parts.count > 0) {  // (as bn_finalize_apply_kernel)
+    int pi = 0;
+    while (pi + 1 < parts.count && ch >= parts.c_end[pi]) ++pi;
+    const int begin = pi == 0 ? 0 : parts.c_end[pi - 1];
+    yc = parts.c_end[pi] - begin;
+    ych = ch - begin;
+    gamma = parts.gamma[pi] ? parts.gamma[pi] - begin : nullptr;
+    beta = parts.beta[pi] ? parts.beta[pi] - begin : nullptr;
+    rm = parts.rm[pi] ? parts.rm[pi] - begin : nullptr;
+    rv = parts.rv[pi] ? parts.rv[pi] - begin : nullptr;
+    tracked = ych == 0 ? parts.tracked[pi] : nullptr;
+    y = parts.y[pi];
+  }
+  const int total = n * s;
+  float v[kSplitBnPer];
+  double sum = 0.0;
+#pragma unroll
+  for (int r = 0; r < kSplitBnPer; ++r) {
+    const int e = tid + 256 * r;
+    v[r] = 0.f;
+    if (e < total) {
+      const int img = e / s, p = e - img * s;
+      const int64_t o = (static_cast<int64_t>(img) * c + ch) * s + p;
+      float a = 0.f, b = 0.f;
+      int k = 0;
+      for (; k + 1 < splits; k += 2) {
+        a += ws[k * stride + o];
+        b += ws[(k + 1) * stride + o];
+      }
+      if (k < splits) a += ws[k * stride + o];
+      v[r] = a + b;
+      z[o] = v[r];
+      sum += static_cast<double>(v[r]);
+    }
+  }
+  __shared__ double red[4];
+  __shared__ float kb[3];
+  auto block_sum = [&](double t) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    __syncthreads();  // (red reused by the second pass)
+    if (lane == 0) red[wave] = t;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+  };
+  const double na = static_cast<double>(total);
+  const double ma = block_sum(sum) / na;
+  double sq = 0.0;
+#pragma unroll
+  for (int r = 0; r < kSplitBnPer; ++r) {
+    if (tid + 256 * r < total) {
+      const double d = static_cast<double>(v[r]) - ma;
+      sq += d * d;
+    }
+  }
+  const double m2a = block_sum(sq);
+  if (tid == 0) {
+    const double var = m2a / na;
+    const float mu = static_cast<float>(ma);
+    const float is = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+    kb[0] = mu;
+    kb[1] = is * (gamma ? gamma[ch] : 1.f);  // (part pointers shifted by its first channel)
+    kb[2] = beta ? beta[ch] : 0.f;
+    if (tracked != nullptr && (ch == 0 || parts.count > 0)) *tracked += 1;
+    if (zero2c != nullptr) {
+      zero2c[ch] = 0.f;
+      zero2c[c + ch] = 0.f;
+    }
+    mean[ch] = mu;
+    invstd[ch] = is;
+    if (acc != nullptr) {
+      double n0 = acc[ch], m0 = acc[c + ch], q0 = acc[2 * c + ch];
+      chan_merge(n0, m0, q0, na, ma, m2a);
+      acc[ch] = n0;
+      acc[c + ch] = m0;
+      acc[2 * c + ch] = q0;
+    }
+    if (rm != nullptr) {
+      const double unbiased = na > 1.0 ? m2a / (na - 1.0) : var;
+      rm[ch] = static_cast<float>((1.0 - momentum) * rm[ch] + momentum * ma);
+      rv[ch] = static_cast<float>((1.0 - momentum) * rv[ch] + momentum * unbiased);
+    }
+  }
+  __syncthreads();
+  const float mu = kb[0], k = kb[1], bb = kb[2];
+#pragma unroll
+  for (int r = 0; r < kSplitBnPer; ++r) {
+    const int e = tid + 256 * r;
+    if (e >= total) break;
+    const int img = e / s, p = e - img * s;
+    float o = __builtin_fmaf(v[r] - mu, k, bb);  // (bn_finalize_apply's rounding)
+    if constexpr (kAdd) o += add[(static_cast<int64_t>(img) * c + ch) * s + p];
+    if constexpr (kRelu) o = o > 0.f ? o : 0.f;
+    y[(static_cast<int64_t>(img) * yc + ych) * s + p] = o;
+  }
+}
+
 // The ReLU after a BatchNorm (relu_out), re-derived in the backward from the saved
 // convolution output: the forward's normalised value > 0, computed with the same fma.
 __device__ __forceinline__ bool bn_relu_mask(float z, float mu, float k, float b) {
@@ -621,6 +738,32 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
   else if (vec) go(bn_finalize_apply_kernel<true, false, false>);
   else if (add) go(bn_finalize_apply_kernel<false, true, false>);
   else go(bn_finalize_apply_kernel<false, false, false>);
+}
+
+bool split_bn_small_ok(int64_t n, int64_t s) {
+  static const bool on = env_int("TGPIPE_SPLIT_BN", 1) != 0;
+  return on && s <= 64 && n * s <= kSplitBnPer * 256;
+}
+
+void launch_split_bn_small(const float* ws, int splits, int64_t stride, float* z, int64_t n,
+                           int64_t c, int64_t s, float eps, double momentum, float* mean,
+                           float* invstd, float* running_mean, float* running_var,
+                           int64_t* tracked, double* acc, float* zero2c, const float* gamma,
+                           const float* beta, const float* add, float* y, hipStream_t stream,
+                           bool relu, const BnParts* parts) {
+  if (c == 0 || n * s == 0) return;
+  BnParts none{};
+  const BnParts& pt = parts != nullptr ? *parts : none;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(c)), dim3(256), 0, stream, ws, splits,
+                       stride, z, static_cast<int>(n), static_cast<int>(c), static_cast<int>(s),
+                       eps, momentum, mean, invstd, running_mean, running_var, tracked, acc,
+                       zero2c, gamma, beta, add, y, pt);
+  };
+  if (add != nullptr && relu) go(split_bn_small_kernel<true, true>);
+  else if (add != nullptr) go(split_bn_small_kernel<true, false>);
+  else if (relu) go(split_bn_small_kernel<false, true>);
+  else go(split_bn_small_kernel<false, false>);
 }
 
 void launch_dbn_commit64(double* acc, float* running_mean, float* running_var, int64_t c,

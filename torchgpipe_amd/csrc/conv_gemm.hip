@@ -1673,6 +1673,27 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
                       accumulate, planes, c, hw, c_total, c_off, stream);
 }
 
+void launch_conv_gemm_partials(const float* a, const float* b, float* ws, const ConvGemmGeo& cg,
+                               const ConvGemmPlan& plan, int64_t a_bytes, int64_t b_bytes,
+                               hipStream_t stream) {
+  Geo g = make_geo(cg);
+  int M, N, K;
+  gemm_dims(kFwd, g, M, N, K);
+  if (M == 0 || N == 0) return;
+  if (plan.splits <= 1 || cg.phase)
+    throw std::runtime_error("conv_gemm: partials need a split forward plan");
+  if (cg.a_split && !conv_gemm_emu_cfg(plan.cfg))
+    throw std::runtime_error("conv_gemm: a pre-split A needs a split-bf16 plan");
+  g.co_total = g.co;  // (each split's slice holds this convolution's channels only)
+  g.co_off = 0;
+  const int64_t stride = static_cast<int64_t>(M) * N;
+  with_cfg(plan.cfg, [&](auto cfg_c) {
+    launch_cfg<kFwd, decltype(cfg_c)::value>(a, b, nullptr, ws, nullptr, nullptr, g, M, N, K,
+                                             plan.splits, stride, false, a_bytes, b_bytes,
+                                             stream, PhaseSet{}, cg.a_split);
+  });
+}
+
 void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
                                  const ConvGemmGeo& cg, const ConvGemmPlan& plan, bool accumulate,
                                  int64_t a_bytes, int64_t b_bytes, hipStream_t stream) {

@@ -394,25 +394,32 @@ struct ASource {
 };
 
 // One implicit-GEMM launch with its split-reduction workspace (a pre-split A when the plan
-// is a split-bf16 one and `src` names the A operand's weight).
+// is a split-bf16 one and `src` names the A operand's weight).  `partials` (split forward
+// plans): the GEMM alone, its split partials left in that workspace
+// (launch_conv_gemm_partials) for the caller's own reduction.
 void run_gemm(int mode, const float* a, const float* b, const float* mask, float* out,
               float* pm, float* pm2, const ConvGemmGeo& g, const ConvGemmPlan& plan,
               bool accumulate, int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
-              ASource src = {}) {
+              ASource src = {}, float* partials = nullptr) {
+  ConvGemmGeo gs = g;
+  at::Tensor split;
   if (src.t != nullptr && mode != 2 && conv_gemm_emu_cfg(plan.cfg) && !g.phase) {
     const int taps = g.kh * g.kw;
     const int M = mode == 0 ? g.co : g.ci;
     const int K = (mode == 0 ? g.ci : g.co) * taps;
-    const at::Tensor split = presplit_of(*src.t, src.transposed, M, K, taps, like);
+    split = presplit_of(*src.t, src.transposed, M, K, taps, like);
     if (split.defined()) {
-      ConvGemmGeo gs = g;
       gs.a_split = true;
-      launch_one(mode, static_cast<const float*>(split.data_ptr()), b, mask, out, pm, pm2, gs,
-                 plan, accumulate, split.numel() * 2, b_bytes, like);
-      return;
+      a = static_cast<const float*>(split.data_ptr());
+      a_bytes = split.numel() * 2;
     }
   }
-  launch_one(mode, a, b, mask, out, pm, pm2, g, plan, accumulate, a_bytes, b_bytes, like);
+  if (partials != nullptr) {
+    TORCH_CHECK(mode == 0, "split partials: forward only");
+    launch_conv_gemm_partials(a, b, partials, gs, plan, a_bytes, b_bytes, cur_stream(like));
+    return;
+  }
+  launch_one(mode, a, b, mask, out, pm, pm2, gs, plan, accumulate, a_bytes, b_bytes, like);
 }
 
 // Whether a backward-data into `dx` leaves pixels unwritten (stride holes of a strided 1x1,
@@ -608,27 +615,6 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
   for (const auto& pl : plans)
     split = split || pl.col_width != plans[0].col_width;
   const bool fused_stats = split && p.geo.size() == 1;
-  const int width = split ? static_cast<int>(s) : plans[0].col_width;
-  const int blocks = split ? static_cast<int>(n) : plans[0].col_blocks;
-  auto part = at::empty({2, blocks, c}, x.options());
-  // the two halves by pointer: part[k] would be an aten::select per use (host time of a
-  // launch-bound stage, profiles/r5/host_profile.md)
-  float* const part0 = part.data_ptr<float>();
-  float* const part1 = part0 + static_cast<int64_t>(blocks) * c;
-  const bool epilogue_stats = !split || fused_stats;
-  for (size_t i = 0; i < p.geo.size(); ++i) {
-    const auto wt = weights[i];
-    const ConvGemmPlan& pl = plans[i];
-    run_gemm(0, wt.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
-             epilogue_stats ? part0 : nullptr,
-             epilogue_stats ? part1 : nullptr, p.geo[i], pl, false,
-             wt.numel() * 4, x.numel() * 4, x, ASource{&weights[i], false});
-  }
-  if (split && !fused_stats)
-    launch_bn_stats(z.data_ptr<float>(), part0, part1, n,
-                    c, s, stream);
-  auto mean = at::empty({c}, x.options());
-  auto invstd = at::empty({c}, x.options());
   const float* rm = opt_ptr(running_mean, "running_mean", x, c);
   const float* rv = opt_ptr(running_var, "running_var", x, c);
   TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean and running_var go together");
@@ -654,6 +640,42 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
   // relu_out with a node sum: relu(bn(z) + add) (ResNet's residual join); the caller masks
   // the gradient with the saved output (the backward's re-derived mask cannot see `add`)
   auto y = at::empty_like(z);
+  auto mean = at::empty({c}, x.options());
+  auto invstd = at::empty({c}, x.options());
+  if (fused_stats && split_bn_small_ok(n, s)) {
+    // small planes: the split partials reduced, normalised and their statistics taken by
+    // one per-channel launch (launch_split_bn_small) instead of two
+    const ConvGemmPlan& pl = plans[0];
+    auto ws = at::empty({conv_gemm_workspace(0, p.geo[0], pl)}, x.options());
+    run_gemm(0, weights[0].data_ptr<float>(), x.data_ptr<float>(), nullptr, nullptr, nullptr,
+             nullptr, p.geo[0], pl, false, weights[0].numel() * 4, x.numel() * 4, x,
+             ASource{&weights[0], false}, ws.data_ptr<float>());
+    launch_split_bn_small(ws.data_ptr<float>(), pl.splits, c * cols, z.data_ptr<float>(), n, c,
+                          s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), const_cast<float*>(rm),
+                          const_cast<float*>(rv), tracked, nullptr, sums.data_ptr<float>(), ga,
+                          be, ad, y.data_ptr<float>(), stream, relu_out);
+    return {y, z, mean, invstd, sums};
+  }
+  const int width = split ? static_cast<int>(s) : plans[0].col_width;
+  const int blocks = split ? static_cast<int>(n) : plans[0].col_blocks;
+  auto part = at::empty({2, blocks, c}, x.options());
+  // the two halves by pointer: part[k] would be an aten::select per use (host time of a
+  // launch-bound stage, profiles/r5/host_profile.md)
+  float* const part0 = part.data_ptr<float>();
+  float* const part1 = part0 + static_cast<int64_t>(blocks) * c;
+  const bool epilogue_stats = !split || fused_stats;
+  for (size_t i = 0; i < p.geo.size(); ++i) {
+    const auto wt = weights[i];
+    const ConvGemmPlan& pl = plans[i];
+    run_gemm(0, wt.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
+             epilogue_stats ? part0 : nullptr,
+             epilogue_stats ? part1 : nullptr, p.geo[i], pl, false,
+             wt.numel() * 4, x.numel() * 4, x, ASource{&weights[i], false});
+  }
+  if (split && !fused_stats)
+    launch_bn_stats(z.data_ptr<float>(), part0, part1, n,
+                    c, s, stream);
   launch_bn_finalize_apply(part0, part1, blocks, width, n,
                            c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), const_cast<float*>(rm),
@@ -1052,6 +1074,22 @@ std::vector<at::Tensor> convbn_group_forward(
                  nullptr, nullptr, p.geo[0], false, w_cat.numel() * 4, x.numel() * 4, x,
                  z.numel());
   const bool split = plan.splits > 1;
+  auto mean = at::empty({c}, x.options());
+  auto invstd = at::empty({c}, x.options());
+  if (split && split_bn_small_ok(n, s)) {  // (as convbn_forward)
+    auto ws = at::empty({conv_gemm_workspace(0, p.geo[0], plan)}, x.options());
+    run_gemm(0, w_cat.data_ptr<float>(), x.data_ptr<float>(), nullptr, nullptr, nullptr,
+             nullptr, p.geo[0], plan, false, w_cat.numel() * 4, x.numel() * 4, x,
+             ASource{&w_cat, false}, ws.data_ptr<float>());
+    launch_split_bn_small(ws.data_ptr<float>(), plan.splits, c * n * s, z.data_ptr<float>(), n,
+                          c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr,
+                          nullptr, nullptr, nullptr, nullptr, stream, false, &pt);
+    out.push_back(z);
+    out.push_back(mean);
+    out.push_back(invstd);
+    return out;
+  }
   const int width = split ? static_cast<int>(s) : plan.col_width;
   const int blocks = split ? static_cast<int>(n) : plan.col_blocks;
   auto part = at::empty({2, blocks, c}, x.options());
@@ -1062,8 +1100,6 @@ std::vector<at::Tensor> convbn_group_forward(
   run_gemm(0, w_cat.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
            part0, part1, p.geo[0], plan, false,
            w_cat.numel() * 4, x.numel() * 4, x, ASource{&w_cat, false});
-  auto mean = at::empty({c}, x.options());
-  auto invstd = at::empty({c}, x.options());
   launch_bn_finalize_apply(part0, part1, blocks, width, n,
                            c, s, static_cast<float>(eps), momentum, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr,

@@ -236,6 +236,11 @@ void launch_conv_gemm_presplit(const float* w, void* out, int M, int K, int taps
 void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
                                  const ConvGemmGeo& g, const ConvGemmPlan& plan, bool accumulate,
                                  int64_t a_bytes, int64_t b_bytes, hipStream_t stream);
+// The GEMM of a split forward plan (plan.splits > 1) alone: partial sums of split s into
+// ws[s][n][co][ho*wo] (conv_gemm_workspace floats), no reduction, no statistics.
+void launch_conv_gemm_partials(const float* a, const float* b, float* ws, const ConvGemmGeo& g,
+                               const ConvGemmPlan& plan, int64_t a_bytes, int64_t b_bytes,
+                               hipStream_t stream);
 constexpr int kSlabFlushMax = 24;  // table entries per flush launch (kernel argument bytes)
 struct SlabFlushEntry {
   const float* slab;
@@ -303,6 +308,17 @@ void launch_bn_finalize_apply(const float* part_mean, const float* part_m2, int 
                               const float* z, const float* gamma, const float* beta,
                               const float* add, float* y, hipStream_t stream, bool relu = false,
                               const BnParts* parts = nullptr);
+// A split-K forward's partials (ws[split][n][c][s], launch_conv_gemm_partials) summed into z
+// and its BatchNorm finalized and applied in one launch of per-channel workgroups (the
+// arguments as launch_bn_finalize_apply's); for planes of s <= 64 pixels and n * s <= 4096
+// (split_bn_small_ok; TGPIPE_SPLIT_BN=0: never).
+bool split_bn_small_ok(int64_t n, int64_t s);
+void launch_split_bn_small(const float* ws, int splits, int64_t stride, float* z, int64_t n,
+                           int64_t c, int64_t s, float eps, double momentum, float* mean,
+                           float* invstd, float* running_mean, float* running_var,
+                           int64_t* tracked, double* acc, float* zero2c, const float* gamma,
+                           const float* beta, const float* add, float* y, hipStream_t stream,
+                           bool relu = false, const BnParts* parts = nullptr);
 // Backward of a grouped BatchNorm (one workgroup per channel, both passes): dz [n][c][s].
 bool bn_backward_parts_ok(int64_t n, int64_t c, int64_t s);
 void launch_bn_backward_parts(const BnParts& parts, const float* z, const float* mean,
