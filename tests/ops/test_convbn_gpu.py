@@ -194,10 +194,13 @@ def test_presplit_follows_weight_updates_and_drops_dead_weights():
         assert torch.equal(ops().conv_gemm_forward(x, w, geo, True), 2 * z1)
         with torch.no_grad():
             w.mul_(0.5)
-        assert ops().conv_gemm_presplit_refresh() == 1  # re-derived in place
+        other = torch.randn(8, device='cuda')
+        assert ops().conv_gemm_presplit_refresh([other]) == 0  # another stage's sources
+        assert ops().conv_gemm_presplit_refresh([w]) == 1  # re-derived in place
         assert torch.equal(ops().conv_gemm_forward(x, w, geo, True), z1)
         del w
-        assert ops().conv_gemm_presplit_refresh() == 0  # the dead weight's entry is dropped
+        assert ops().conv_gemm_presplit_refresh([other]) == 0
+        assert ops().conv_gemm_presplit(-1) == 0  # the dead weight's entry was dropped
     finally:
         ops().conv_gemm_force_cfg(-1)
         ops().conv_gemm_presplit(-1)
@@ -229,10 +232,44 @@ def test_presplit_in_a_captured_graph_follows_the_step_refresh():
         with torch.no_grad():
             w.mul_(2)
         from torchgpipe_amd.ops.conv import refresh_step_caches
-        refresh_step_caches(nn.Module())
+        holder = nn.Module()
+        holder.w = nn.Parameter(w, requires_grad=False)  # (the same tensor storage)
+        refresh_step_caches(holder)
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(out, 2 * want)
+    finally:
+        ops().conv_gemm_force_cfg(-1)
+        ops().conv_gemm_presplit(-1)
+
+
+def test_presplit_refresh_inside_a_capture_rederives_fresh_entries():
+    """A whole-step graph (parallel/graph.py StepGraph) captures the step-start refresh and
+    the optimizer's update: the captured refresh derives every entry of the stage, even one
+    that was fresh at the capture, or the replays after the captured update would read the
+    planes of the weights as they were when captured."""
+    ops().conv_gemm_force_cfg(9)
+    ops().conv_gemm_presplit(-1)
+    try:
+        torch.manual_seed(0)
+        x = torch.randn(4, 64, 14, 14, device='cuda')
+        w = torch.randn(96, 64, 1, 1, device='cuda') * 0.1
+        geo = [1, 1, 1, 1, 0, 0, 0, 0]
+        want = ops().conv_gemm_forward(x, w, geo, True)  # the entry: fresh from here on
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ops().conv_gemm_forward(x, w, geo, True)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ops().conv_gemm_presplit_refresh([w])
+            out = ops().conv_gemm_forward(x, w, geo, True)
+            w.mul_(2)  # the captured "optimizer"
+        for k in range(3):
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, (2 ** k) * want), k
     finally:
         ops().conv_gemm_force_cfg(-1)
         ops().conv_gemm_presplit(-1)

@@ -74,10 +74,9 @@ ConvGemmPlan tuned_plan_raw(int mode, const float* a, const float* b, const floa
     const char* v = std::getenv("TGPIPE_CG_TUNE");
     return v != nullptr && std::string(v) == "1";
   }();
-  const ConvGemmPlan heuristic = conv_gemm_plan(mode, g);
   const int forced = forced_cfg.load();
   if (forced >= 0) {  // test hook: that tile config's candidate with the most splits <= N
-    ConvGemmPlan pick = heuristic;
+    ConvGemmPlan pick = conv_gemm_plan(mode, g);
     bool found = false;
     for (const auto& cand : conv_gemm_candidates(mode, g))
       if (cand.cfg == forced && cand.splits <= std::max(1, forced_splits.load()) &&
@@ -101,6 +100,8 @@ ConvGemmPlan tuned_plan_raw(int mode, const float* a, const float* b, const floa
     p.splits = 1;
     return p;
   }
+  // (the heuristic only on a miss: every launch of a launch-bound stage asks)
+  const ConvGemmPlan heuristic = conv_gemm_plan(mode, g);
   if (!tune) return heuristic;
   // A stream capture (hipGraph) records launches, it cannot time them: a shape first met
   // inside a capture runs the heuristic plan (warm-up steps before capturing tune it).
@@ -234,7 +235,7 @@ int64_t conv_gemm_plans_import(const std::string& text) {
 // 1.5x the weight's bytes) and the kernel loads the planes.  Entries are keyed by the
 // source tensor's storage, held by weak reference (a dead weight's entry is dropped), and
 // re-derived when its version counter moves: lazily by the next launch (readers on other
-// streams wait for that derive's event), or in place for the whole step by
+// streams wait for that derive's event), or in place for a whole stage by
 // conv_gemm_presplit_refresh (PipelineStage's step start, ops/conv.py
 // refresh_step_caches) -- which is what keeps a captured hipGraph, that baked the buffer in,
 // reading the current weights.  Inside a capture a stale or missing entry is derived into
@@ -352,28 +353,48 @@ at::Tensor presplit_of(const at::Tensor& src, bool transposed, int M, int K, int
   return out;
 }
 
-// Re-derive every stale entry in place on its device's current stream; drop dead ones.
-// Returns the entries kept.
-int64_t conv_gemm_presplit_refresh() {
+// The step-start refresh of one stage (ops/conv.py refresh_step_caches): the entries derived
+// from `sources` (the stage's parameters and its transposed / concatenated weights) are
+// re-derived in place on the device's current stream when stale -- and every one of them
+// when that stream is capturing: a whole-step graph (parallel/graph.py) captures this
+// refresh and the optimizer, and its replays must re-derive even the entries that were
+// fresh at the capture.  Other stages' entries are left alone; dead ones are dropped.
+// Returns the entries refreshed or checked.
+int64_t conv_gemm_presplit_refresh(at::TensorList sources) {
   std::lock_guard<std::mutex> lock(pre_mutex);
   for (auto it = pre_cache.begin(); it != pre_cache.end();) {
     auto nxt = std::next(it);
-    PreSplit& e = it->second;
-    auto alive = e.src.lock();
-    if (!alive) {
-      presplit_erase(it);
-    } else {
-      const at::Tensor src(alive);
-      if (static_cast<int64_t>(src._version()) != e.version) {
-        c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
-        presplit_derive(src, e.split, e.d, cur_stream(src));
-        e.version = static_cast<int64_t>(src._version());
-      }
-      e.stream = nullptr;  // ordered before the step by the caller
-    }
+    if (it->second.src.expired()) presplit_erase(it);
     it = nxt;
   }
-  return static_cast<int64_t>(pre_cache.size());
+  int64_t count = 0;
+  for (const at::Tensor& t : sources) {
+    if (!t.defined() || !t.is_cuda()) continue;
+    for (const bool transposed : {false, true}) {
+      auto it = pre_cache.find(PreKey{t.data_ptr(), transposed, t.device().index()});
+      if (it == pre_cache.end()) continue;
+      PreSplit& e = it->second;
+      auto alive = e.src.lock();
+      if (!alive) {
+        presplit_erase(it);
+        continue;
+      }
+      const at::Tensor src(alive);
+      c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+      const hipStream_t stream = cur_stream(src);
+      hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+      const bool capturing = hipStreamIsCapturing(stream, &capture) == hipSuccess &&
+                             capture != hipStreamCaptureStatusNone;
+      const int64_t version = static_cast<int64_t>(src._version());
+      if (capturing || version != e.version) {
+        presplit_derive(src, e.split, e.d, stream);
+        e.version = version;
+      }
+      e.stream = nullptr;  // ordered before the step by the caller
+      ++count;
+    }
+  }
+  return count;
 }
 
 // Test / benchmark hook: set the pre-split budget (MiB; 0 = off, < 0 = the environment's)
@@ -1651,7 +1672,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("lib_dgrad_force(int mode) -> ()", &tgpipe::lib_dgrad_force);
   m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
   m.def("conv_gemm_presplit(int budget_mb) -> int", &tgpipe::conv_gemm_presplit);
-  m.def("conv_gemm_presplit_refresh() -> int", &tgpipe::conv_gemm_presplit_refresh);
+  m.def("conv_gemm_presplit_refresh(Tensor[] sources) -> int",
+        &tgpipe::conv_gemm_presplit_refresh);
   m.def("conv_gemm_sweep(int mode, Tensor x, Tensor weight, int[] geo, int reps) -> float[]");
   m.def("conv_gemm_plans_import(str text) -> int", &tgpipe::conv_gemm_plans_import);
   m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "

@@ -39,7 +39,7 @@ the transform runs once per optimizer step instead of once per call.
 """
 import os
 import threading
-from typing import Any, Dict, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -221,6 +221,10 @@ class _TransformCache:
                 _derive(weight, slot, out=u)
             self._entries[slot] = (key, u, None)
 
+    def derived(self) -> List[Tensor]:
+        """The cached derived weights (the tensors other caches may be keyed on)."""
+        return [u for _, u, _ in self._entries.values()]
+
     def clear(self) -> None:
         for _, u, _ in self._entries.values():
             _CACHE_BYTES[u.device] -= u.numel() * u.element_size()
@@ -247,14 +251,21 @@ def refresh_step_caches(module: nn.Module) -> None:
     stream): Winograd transforms, transposed weights, grouped-GEMM concatenations and the
     split-bf16 GEMMs' pre-split weights."""
     from torchgpipe_amd.ops.convbn import _GroupCache
+    sources: List[Tensor] = []
     for m in module.modules():
         for v in list(vars(m).values()):
-            if isinstance(v, (_TransformCache, _GroupCache)):
+            if isinstance(v, _TransformCache):
                 v.refresh()
+                sources += v.derived()
+            elif isinstance(v, _GroupCache):
+                v.refresh()
+                sources += [t for t in (v.cat, v.cat_t) if t is not None]
     if _ext._loaded:
-        # then the implicit-GEMM kernels' pre-split weights (csrc/convbn.cpp presplit_of;
-        # every entry of the process, after the transposes above they may be derived from)
-        torch.ops.tgpipe.conv_gemm_presplit_refresh()
+        # then the implicit-GEMM kernels' pre-split weights (csrc/convbn.cpp presplit_of)
+        # derived from this module's parameters and the transposes / concatenations above
+        sources += [p for p in module.parameters() if p.is_cuda]
+        if sources:
+            torch.ops.tgpipe.conv_gemm_presplit_refresh(sources)
 
 
 def clear_winograd_caches(module: torch.nn.Module) -> None:
