@@ -243,6 +243,35 @@ def test_presplit_in_a_captured_graph_follows_the_step_refresh():
         ops().conv_gemm_presplit(-1)
 
 
+def test_presplit_capture_miss_keeps_the_in_kernel_split():
+    """A weight first met inside a capture: the launch splits A in the kernel (no cache
+    entry written from inside the capture, no derive node per replay)."""
+    ops().conv_gemm_force_cfg(9)
+    ops().conv_gemm_presplit(-1)
+    try:
+        torch.manual_seed(0)
+        x = torch.randn(4, 64, 14, 14, device='cuda')
+        w = torch.randn(96, 64, 1, 1, device='cuda') * 0.1
+        geo = [1, 1, 1, 1, 0, 0, 0, 0]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # (warm-up without the cache)
+            ops().conv_gemm_presplit(0, False)
+            ops().conv_gemm_forward(x, w, geo, True)
+            ops().conv_gemm_presplit(-1, False)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = ops().conv_gemm_forward(x, w, geo, True)
+        assert ops().conv_gemm_presplit(-1, False) == 0
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ops().conv_gemm_forward(x, w, geo, True))
+    finally:
+        ops().conv_gemm_force_cfg(-1)
+        ops().conv_gemm_presplit(-1)
+
+
 def test_presplit_refresh_inside_a_capture_rederives_fresh_entries():
     """A whole-step graph (parallel/graph.py StepGraph) captures the step-start refresh and
     the optimizer's update: the captured refresh derives every entry of the stage, even one

@@ -238,9 +238,11 @@ int64_t conv_gemm_plans_import(const std::string& text) {
 // streams wait for that derive's event), or in place for a whole stage by
 // conv_gemm_presplit_refresh (PipelineStage's step start, ops/conv.py
 // refresh_step_caches) -- which is what keeps a captured hipGraph, that baked the buffer in,
-// reading the current weights.  Inside a capture a stale or missing entry is derived into
-// the graph's own buffer on every replay (the cache is not written).
-// TGPIPE_CG_PRESPLIT_MB: the bytes all entries may hold (default 512; 0 = off).
+// reading the current weights.  Inside a capture a stale or missing entry leaves that launch
+// on the in-kernel split (the cache is not written, and a derive per replay would cost a
+// graph node per launch).  TGPIPE_CG_PRESPLIT_MB: the bytes all entries may hold (default
+// 2048; 0 = off); a pipeline stage's first, measuring step and the memory-lean cache mode
+// set it to 0 (ops/conv.py hold_cache / size_cache_budget).
 struct PreDims {
   int M = 0, K = 0, taps = 1;
   bool transposed = false;
@@ -267,7 +269,7 @@ std::atomic<int64_t> pre_budget{-1};
 int64_t presplit_budget() {
   int64_t b = pre_budget.load();
   if (b < 0) {
-    b = static_cast<int64_t>(std::max(0, env_int("TGPIPE_CG_PRESPLIT_MB", 512))) << 20;
+    b = static_cast<int64_t>(std::max(0, env_int("TGPIPE_CG_PRESPLIT_MB", 2048))) << 20;
     pre_budget.store(b);
   }
   return b;
@@ -314,11 +316,7 @@ at::Tensor presplit_of(const at::Tensor& src, bool transposed, int M, int K, int
         hipStreamWaitEvent(stream, e.ready, 0);
       return e.split;
     }
-    if (capturing) {  // derived into the graph's own buffer (see above)
-      at::Tensor tmp = at::empty({numel}, like.options().dtype(at::kBFloat16));
-      presplit_derive(src, tmp, probe, stream);
-      return tmp;
-    }
+    if (capturing) return {};  // (see above)
     if (same) {  // stale: in place, on this stream
       presplit_derive(src, e.split, e.d, stream);
       e.version = version;
@@ -328,11 +326,7 @@ at::Tensor presplit_of(const at::Tensor& src, bool transposed, int M, int K, int
     }
     presplit_erase(it);  // another tensor at the same address (or a reshaped use)
   }
-  if (capturing) {
-    at::Tensor tmp = at::empty({numel}, like.options().dtype(at::kBFloat16));
-    presplit_derive(src, tmp, probe, stream);
-    return tmp;
-  }
+  if (capturing) return {};
   // drop the entries of dead tensors before charging the budget
   for (auto j = pre_cache.begin(); j != pre_cache.end();) {
     auto nxt = std::next(j);
@@ -397,12 +391,13 @@ int64_t conv_gemm_presplit_refresh(at::TensorList sources) {
   return count;
 }
 
-// Test / benchmark hook: set the pre-split budget (MiB; 0 = off, < 0 = the environment's)
-// and drop every entry.  Returns the bytes the entries held.
-int64_t conv_gemm_presplit(int64_t budget_mb) {
+// Set the pre-split budget (MiB; 0 = off, < 0 = the environment's) and, with `clear`, drop
+// every entry (test / benchmark hook).  Returns the bytes the entries held.
+int64_t conv_gemm_presplit(int64_t budget_mb, bool clear) {
   std::lock_guard<std::mutex> lock(pre_mutex);
   const int64_t held = pre_bytes;
-  while (!pre_cache.empty()) presplit_erase(pre_cache.begin());
+  if (clear)
+    while (!pre_cache.empty()) presplit_erase(pre_cache.begin());
   pre_budget.store(budget_mb < 0 ? -1 : budget_mb << 20);
   return held;
 }
@@ -1671,7 +1666,7 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("lib_dgrad_import(str text) -> int", &tgpipe::lib_dgrad_import);
   m.def("lib_dgrad_force(int mode) -> ()", &tgpipe::lib_dgrad_force);
   m.def("conv_gemm_force_cfg(int cfg, int splits=1) -> ()", &tgpipe::conv_gemm_force_cfg);
-  m.def("conv_gemm_presplit(int budget_mb) -> int", &tgpipe::conv_gemm_presplit);
+  m.def("conv_gemm_presplit(int budget_mb, bool clear=True) -> int", &tgpipe::conv_gemm_presplit);
   m.def("conv_gemm_presplit_refresh(Tensor[] sources) -> int",
         &tgpipe::conv_gemm_presplit_refresh);
   m.def("conv_gemm_sweep(int mode, Tensor x, Tensor weight, int[] geo, int reps) -> float[]");

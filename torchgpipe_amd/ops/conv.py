@@ -91,8 +91,16 @@ def _budget(device: torch.device) -> int:
 
 
 def hold_cache(device: torch.device) -> None:
-    """Cache nothing on ``device`` (a stage's first step, which measures its footprint)."""
+    """Cache nothing on ``device`` (a stage's first step, which measures its footprint) --
+    nor pre-split implicit-GEMM weights (csrc/convbn.cpp presplit_of)."""
     _DEVICE_BUDGET[device] = 0
+    _presplit_budget(0)
+
+
+def _presplit_budget(mb: int) -> None:
+    """The implicit-GEMM pre-split weights' budget (MiB; -1: ``TGPIPE_CG_PRESPLIT_MB``)."""
+    if _ext.available():
+        torch.ops.tgpipe.conv_gemm_presplit(mb, False)
 
 
 def size_cache_budget(device: torch.device, peak_bytes: int,
@@ -108,6 +116,9 @@ def size_cache_budget(device: torch.device, peak_bytes: int,
         budget = max(0, total - peak_bytes) // 2
     budget = min(_device_cap(device), budget)
     _DEVICE_BUDGET[device] = budget
+    # pre-split implicit-GEMM weights (1.5x the weights they split): off in the memory-lean
+    # mode (a fraction of the peak, e.g. benchmarks/memory.py), else their own budget
+    _presplit_budget(0 if fraction is not None else -1)
     return budget
 
 
