@@ -62,10 +62,21 @@ void conv_gemm_force_cfg(int64_t cfg, int64_t splits) {
   forced_splits.store(static_cast<int>(splits));
 }
 
+// The weight a forward / backward-data GEMM's A operand comes from, for a pre-split A:
+// `t` row-major [M][K] (transposed = false) or W[co][ci][T] read transposed.
+struct ASource {
+  const at::Tensor* t = nullptr;
+  bool transposed = false;
+};
+void run_gemm(int mode, const float* a, const float* b, const float* mask, float* out,
+              float* pm, float* pm2, const ConvGemmGeo& g, const ConvGemmPlan& plan,
+              bool accumulate, int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
+              ASource src = {}, float* partials = nullptr);
+
 ConvGemmPlan tuned_plan_raw(int mode, const float* a, const float* b, const float* mask,
                             float* out, float* pm, float* pm2, const ConvGemmGeo& g,
                             bool accumulate, int64_t a_bytes, int64_t b_bytes,
-                            const at::Tensor& like, int64_t out_numel) {
+                            const at::Tensor& like, int64_t out_numel, ASource src) {
   // Timing trials only when asked for (TGPIPE_CG_TUNE=1: benchmarks/tune_plans.py, the
   // offline tuner): a training step never synchronises the host to time candidates, and
   // every rank of a pipeline picks the same plan for the same shape.  A shape missing from
@@ -124,7 +135,8 @@ ConvGemmPlan tuned_plan_raw(int mode, const float* a, const float* b, const floa
     float ms = 0.f;
     for (int rep = 0; rep < 2; ++rep) {  // first run: warm-up (code object, caches)
       hipEventRecord(t0, stream);
-      launch_one(mode, a, b, mask, out, pm, pm2, g, cand, false, a_bytes, b_bytes, like);
+      // (as the launch will run: split-bf16 candidates on the pre-split weights)
+      run_gemm(mode, a, b, mask, out, pm, pm2, g, cand, false, a_bytes, b_bytes, like, src);
       hipEventRecord(t1, stream);
       hipEventSynchronize(t1);
       hipEventElapsedTime(&ms, t0, t1);
@@ -147,10 +159,10 @@ ConvGemmPlan tuned_plan_raw(int mode, const float* a, const float* b, const floa
 ConvGemmPlan tuned_plan(int mode, const float* a, const float* b, const float* mask, float* out,
                         float* pm, float* pm2, const ConvGemmGeo& g, bool accumulate,
                         int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
-                        int64_t out_numel) {
+                        int64_t out_numel, ASource src = {}) {
   static const int cap = env_int("TGPIPE_CG_SPLIT_CAP", 0);
   ConvGemmPlan p = tuned_plan_raw(mode, a, b, mask, out, pm, pm2, g, accumulate, a_bytes,
-                                  b_bytes, like, out_numel);
+                                  b_bytes, like, out_numel, src);
   if (cap <= 0 || mode == 2 || p.splits <= cap) return p;
   ConvGemmPlan pick = p;
   bool found = false;
@@ -402,13 +414,6 @@ int64_t conv_gemm_presplit(int64_t budget_mb, bool clear) {
   return held;
 }
 
-// The weight a forward / backward-data GEMM's A operand comes from, for a pre-split A:
-// `t` row-major [M][K] (transposed = false) or W[co][ci][T] read transposed.
-struct ASource {
-  const at::Tensor* t = nullptr;
-  bool transposed = false;
-};
-
 // One implicit-GEMM launch with its split-reduction workspace (a pre-split A when the plan
 // is a split-bf16 one and `src` names the A operand's weight).  `partials` (split forward
 // plans): the GEMM alone, its split partials left in that workspace
@@ -416,7 +421,7 @@ struct ASource {
 void run_gemm(int mode, const float* a, const float* b, const float* mask, float* out,
               float* pm, float* pm2, const ConvGemmGeo& g, const ConvGemmPlan& plan,
               bool accumulate, int64_t a_bytes, int64_t b_bytes, const at::Tensor& like,
-              ASource src = {}, float* partials = nullptr) {
+              ASource src, float* partials) {
   ConvGemmGeo gs = g;
   at::Tensor split;
   if (src.t != nullptr && mode != 2 && conv_gemm_emu_cfg(plan.cfg) && !g.phase) {
@@ -512,7 +517,7 @@ void backward_data_into(const at::Tensor& wt, const at::Tensor& dz, const at::Te
   const ConvGemmPlan plan =
       tuned_plan(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
                  dx.data_ptr<float>(), nullptr, nullptr, g, accumulate, wt.numel() * 4,
-                 dz.numel() * 4, x, x.numel());
+                 dz.numel() * 4, x, x.numel(), ASource{&wt, false});
   run_gemm(1, wt.data_ptr<float>(), dz.data_ptr<float>(), x.data_ptr<float>(),
            dx.data_ptr<float>(), nullptr, nullptr, g, plan, accumulate, wt.numel() * 4,
            dz.numel() * 4, x, ASource{&wt, false});
@@ -622,7 +627,8 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
     // (tuning candidates write z without statistics; the real launches follow)
     plans.push_back(tuned_plan(0, weights[i].data_ptr<float>(), x.data_ptr<float>(), nullptr,
                                z.data_ptr<float>(), nullptr, nullptr, p.geo[i], false,
-                               weights[i].numel() * 4, x.numel() * 4, x, z.numel()));
+                               weights[i].numel() * 4, x.numel() * 4, x, z.numel(),
+                               ASource{&weights[i], false}));
     split = split || plans.back().splits > 1;
   }
   // statistics partials: from the GEMM epilogue (all parts share one column tiling), or
@@ -1088,7 +1094,7 @@ std::vector<at::Tensor> convbn_group_forward(
   const ConvGemmPlan plan =
       tuned_plan(0, w_cat.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
                  nullptr, nullptr, p.geo[0], false, w_cat.numel() * 4, x.numel() * 4, x,
-                 z.numel());
+                 z.numel(), ASource{&w_cat, false});
   const bool split = plan.splits > 1;
   auto mean = at::empty({c}, x.options());
   auto invstd = at::empty({c}, x.options());
@@ -1326,7 +1332,7 @@ at::Tensor conv_gemm_forward(const at::Tensor& x_in, const at::Tensor& weight,
   const ConvGemmPlan plan =
       tuned_plan(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
                  nullptr, nullptr, p.geo[0], false, weight.numel() * 4, x.numel() * 4, x,
-                 z.numel());
+                 z.numel(), ASource{&weight, false});
   run_gemm(0, weight.data_ptr<float>(), x.data_ptr<float>(), nullptr, z.data_ptr<float>(),
            nullptr, nullptr, p.geo[0], plan, false, weight.numel() * 4, x.numel() * 4, x,
            ASource{&weight, false});
