@@ -75,3 +75,34 @@ def test_pack_unpack_cpu():
     misc.unpack(buf, outs)
     for a, b in zip(ts, outs):
         assert torch.equal(a, b)
+
+
+def test_refresh_step_caches_names_the_stage_sources(monkeypatch):
+    """The pre-split refresh (csrc/convbn.cpp conv_gemm_presplit_refresh) gets exactly this
+    module's device parameters plus its cached derived weights -- another stage's entries
+    stay untouched (a whole-step graph must capture the derives of its own stage)."""
+    from types import SimpleNamespace
+
+    from torch import nn
+
+    from torchgpipe_amd.ops import _ext, conv, convbn
+
+    class FakeCuda:  # a parameter stand-in that reports is_cuda
+        def __init__(self, t):
+            self.t, self.is_cuda = t, True
+
+    seen = []
+    monkeypatch.setattr(_ext, '_loaded', True)
+    monkeypatch.setattr(torch, 'ops', SimpleNamespace(tgpipe=SimpleNamespace(
+        conv_gemm_presplit_refresh=lambda sources: seen.append(list(sources)) or len(sources))))
+    m = nn.Sequential(nn.Conv2d(4, 8, 1, bias=False), nn.Conv2d(8, 8, 1, bias=False))
+    derived = torch.zeros(3)
+    cache = convbn._weight_cache(m[0])
+    cache._entries[(True, True, 'T')] = ((0, 0, torch.device('cpu'), 0), derived, None)
+    monkeypatch.setattr(conv._TransformCache, 'refresh', lambda self: None)
+    fakes = [FakeCuda(p) for p in m.parameters()]
+    monkeypatch.setattr(nn.Module, 'parameters', lambda self, recurse=True: iter(fakes))
+    conv.refresh_step_caches(m)
+    assert len(seen) == 1
+    assert seen[0][0] is derived
+    assert seen[0][1:] == fakes
