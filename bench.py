@@ -11,23 +11,30 @@ partitions, using the reference's experiment tables
     N=4  U-Net pipeline-4  B=512, chunks=16, balance [30, 66, 84, 61]
     N=8  U-Net pipeline-8  B=640, chunks=40, balance [16, 27, 31, 44, 22, 57, 27, 17]
 
-The top-level ``value`` is the U-Net headline.  After it, every run also times
-(``--sections``):
+The top-level ``value`` is the U-Net headline: the reference balance on the plain eager
+engine.  After it, every run also times (``--sections``), in this order:
 
 * ``baseline``: the reference's speed-up denominator, U-Net(5,64) *without* GPipe
   (plain model, B=40, no checkpointing) on rank 0's GPU, so ``speedup_vs_baseline``
   is measured on the same box as the headline;
+* ``gpipe`` (N=1): the headline experiment through the public single-process ``GPipe``
+  API (the reference's own benchmark path), ``vs_pipeline_stage`` its ratio;
 * ``amoebanet``: AmoebaNet-D(18,256), n{N}m32 at the reference balance (n1m32, B=640
   at N=1), and at N=2 the reference's own denominator n2m1 (B=96, ``always``);
 * ``resnet``: ResNet-101 pipeline-1 (B=220, m=2) at N=1, BASELINE.json's config #2
   (pipeline-2, chunks=32, ``always``) at N=2, the reference's pipeline-4 / -8 (B=5632,
   m=256 / B=5400, m=150) at N=4 / 8, and the reference's ResNet denominator (no GPipe,
   B=118) on rank 0's GPU;
+* at N > 1, the opt-in engine variants, each under its own key: ``tuned`` (the
+  MI355X-tuned balances of U-Net and AmoebaNet), ``striped`` (N >= 3: the headline with
+  multi-path transfers) and ``amoebanet_graph_cells`` (captured cells);
 * for N > 1, one extra *diagnostic* step (not timed) in which every rank measures
   how long its streams waited for activations / gradients (``per_rank``).
 
 One process per GPU (``torch.distributed.run``), RCCL point-to-point between
-stages; fp32 like the reference.  Rank 0 prints one JSON line.
+stages; fp32 like the reference.  Rank 0 prints the JSON record right after the headline
+and re-prints it, augmented, after every section (each line complete; the last one the
+most complete), so a late section that fails cannot lose the headline.
 
     python bench.py --gpus 1 --steps 5 --warmup 2
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
@@ -42,13 +49,16 @@ import sys
 import time
 from typing import Any, Callable, Dict, List, Optional
 
+# Hardware queues of a multi-rank run: every stream a rank queues work on -- compute,
+# lanes, AmoebaNet cell streams, relay routes -- and one stream per RCCL communicator
+# (parallel/stage.py stream_census, HW_QUEUES; tests/test_stream_census.py checks the
+# 8-rank pipelines, multi-path transfers included, against it).  HIP's default is 4:
+# streams beyond that share a queue, whose work then runs in order, so a spinning RCCL
+# receive could hold up unrelated compute.  Set before the HIP runtime initialises (first
+# CUDA call); 32 is the most this pool's runtime is given.
+HW_QUEUES = 32
 if int(os.environ.get('WORLD_SIZE', '1')) > 1:
-    # One HIP hardware queue per stream: a rank runs its compute stream and lanes plus
-    # one RCCL stream per pipeline link (up to 6 on U-Net p8 with long skips).  With
-    # HIP's default of 4 queues, streams beyond that share a queue and their kernels
-    # serialise, so a spinning RCCL receive could hold up unrelated work.  Set before
-    # the HIP runtime initialises (first CUDA call).
-    os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
+    os.environ.setdefault('GPU_MAX_HW_QUEUES', str(HW_QUEUES))
 
 import torch
 import torch.distributed as dist
@@ -132,11 +142,15 @@ def parse() -> argparse.Namespace:
                    help="after the headline timing, time the MI355X-tuned balance too and "
                         "report it as the 'tuned' field (auto: when N > 1 and it differs)")
     p.add_argument('--sections', default='auto',
-                   help="comma-separated extra timings after the headline: 'baseline' "
-                        "(U-Net without GPipe, B=40, rank 0), 'amoebanet' (AmoebaNet-D n{N}m32 "
-                        "and, at N=2, n2m1), 'resnet' (ResNet-101 pipeline-1 at N=1, "
-                        "BASELINE config #2 at N=2); 'auto' = all of them when the headline is "
-                        "U-Net (resnet at N <= 2); 'none'")
+                   help="comma-separated extra timings after the headline, in this order: "
+                        "'baseline' (U-Net without GPipe, B=40, rank 0), 'gpipe' (N=1: the "
+                        "headline through single-process GPipe), 'amoebanet' (AmoebaNet-D "
+                        "n{N}m32 and, at N=2, n2m1), 'resnet' (ResNet-101 pipeline-{N} and its "
+                        "no-GPipe baseline), then at N > 1 the MI355X-tuned balances "
+                        "(--also-tuned), 'striped' (N >= 3: the headline with multi-path "
+                        "transfers) and 'graph_cells' (AmoebaNet with captured cells); "
+                        "'auto' = all that apply when the headline is U-Net; 'none'.  The JSON "
+                        'record is printed after the headline and re-printed after each section')
     p.add_argument('--section-steps', type=int, default=None,
                    help='timed steps of each extra section (default: --steps)')
     p.add_argument('--probe', choices=['auto', 'on', 'off'], default='auto',
@@ -169,20 +183,17 @@ def parse() -> argparse.Namespace:
     p.add_argument('--overlap-forward', choices=['auto', 'on', 'off'], default='auto',
                    help='alternate the forward micro-batches of a stateless partition (no '
                         'running statistics: U-Net) between two streams (auto: on for U-Net)')
-    p.add_argument('--wgrad-stream', choices=['auto', 'on', 'off'], default='auto',
-                   help='run the fused ops\' weight-gradient GEMMs on a side stream '
-                        '(PipelineStage(wgrad_stream=True); auto: off)')
     p.add_argument('--graph-cells', choices=['auto', 'on', 'off'], default='auto',
                    help='replay each micro-batch of a stage as captured hipGraphs, transfers '
                         'issued between them (PipelineStage(graph_cells=True), '
                         'parallel/segments.py; instead of the one-GPU whole-step graph; '
                         'auto: on for one-GPU AmoebaNet)')
     p.add_argument('--stripes', choices=['auto', 'on', 'off'], default='auto',
-                   help='multi-path transfers: messages of at least --stripe-mb also travel '
-                        'through up to 3 idle ranks over otherwise unused links '
-                        '(PipelineStage(stripes=...), parallel/stripes.py; planned from the '
-                        'first step, so the warm-up runs until the plan exists; auto: on at '
-                        'N >= 3)')
+                   help='multi-path transfers in the headline: messages of at least '
+                        '--stripe-mb also travel through up to 3 idle ranks over otherwise '
+                        'unused links (PipelineStage(stripes=...), parallel/stripes.py; '
+                        'planned from the first step, so the warm-up runs until the plan '
+                        "exists; auto: off -- the 'striped' section times them at N >= 3)")
     p.add_argument('--stripe-mb', type=float, default=16.0,
                    help='smallest striped message, MB')
     p.add_argument('--profile-steps', type=int, default=0,
@@ -320,7 +331,8 @@ class Bench:
         return {'elapsed': elapsed, 'warm_s': warm_s, 'first_step_s': first_s}
 
     def pipeline(self, kind: str, exp: Dict[str, Any], balance: List[int], checkpoint: str,
-                 steps: int, tag: str, probe: bool = False) -> Dict[str, Any]:
+                 steps: int, tag: str, probe: bool = False, stripes: Optional[bool] = None,
+                 graph_cells: Optional[bool] = None) -> Dict[str, Any]:
         """Build the PipelineStage for ``balance``, warm up, time ``steps`` SGD steps."""
         from torchgpipe_amd.parallel import PipelineStage
         from torchgpipe_amd.parallel.stage import signature_of
@@ -338,9 +350,6 @@ class Bench:
         overlap = choice(args.overlap_recompute, self.gpu and kind in ('unet', 'resnet'))
         overlap_fwd = choice(args.overlap_forward, self.gpu and unet)
         cell_streams = kind == 'amoebanet' and choice(args.cell_streams, self.gpu)
-        # (auto: off -- with the two-stream cells it measured 280.3 vs 328.6 samples/s on one
-        # box, profiles/r2/bench_amoeba_s13.md)
-        wgrad_stream = choice(args.wgrad_stream, False)
         # captured cells (parallel/segments.py): one GPU, AmoebaNet -- three-stream cells in
         # per-pass captures, 392.0 vs 389.4 samples/s for the two-stream whole-step graph
         # (profiles/r4/amoeba_n1_graph_modes.md).  Multi-rank runs stay eager by default: in
@@ -349,15 +358,19 @@ class Bench:
         # n8m32 stage 6 494.1 vs 506.6 ms: profiles/r4/stage_harness_*_ref_{eager,
         # graph_cells}.jsonl), which does not pay for running RCCL receives into captured
         # graphs' buffers before any multi-GPU node has (--graph-cells on to opt in).
-        graph_cells = choice(args.graph_cells, self.world == 1 and kind == 'amoebanet') \
-            and self.gpu
+        if graph_cells is None:
+            graph_cells = choice(args.graph_cells, self.world == 1 and kind == 'amoebanet')
+        graph_cells = graph_cells and self.gpu
         # multi-path transfers (parallel/stripes.py): U-Net p8's 226 MB skip and AmoebaNet
-        # n8's 321 MB boundary outrun one xGMI link (profiles/r5/speedup_prediction.md)
-        stripes = choice(args.stripes, self.world >= 3)
+        # n8's 321 MB boundary outrun one xGMI link (profiles/r5/speedup_prediction.md);
+        # opt-in (the 'striped' section times them at N >= 3) until a multi-GPU node has
+        # run their RCCL relay chains
+        if stripes is None:
+            stripes = choice(args.stripes, False)
         stage = PipelineStage(self.build(kind), balance, device=self.device, chunks=chunks,
                               checkpoint=checkpoint, timeout=args.timeout,
                               overlap_recompute=overlap, overlap_forward=overlap_fwd,
-                              wgrad_stream=wgrad_stream, graph_cells=graph_cells,
+                              graph_cells=graph_cells,
                               stripes=max(1, int(args.stripe_mb * 1e6)) if stripes else None)
         if args.channels_last and not unet:
             stage.partition.to(memory_format=torch.channels_last)
@@ -407,7 +420,7 @@ class Bench:
                    # (a captured step keeps at most CAPTURE_CELL_STREAMS per cell)
                    cell_streams=min(int(cell_streams), _capture_streams())
                    if graph is not None and cell_streams else int(cell_streams),
-                   overlap_forward=overlap_fwd, wgrad_stream=wgrad_stream,
+                   overlap_forward=overlap_fwd,
                    hipgraph=graph is not None, graph_cells=graph_cells,
                    striped_routes=stage.striped_routes)
         if probe and graph is None:
@@ -432,6 +445,35 @@ class Bench:
                 file=sys.stderr)
         res['mem'] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30 if self.gpu else 0.0
         del stage, optimizer, x, target, graph, step, settle
+        self.release()
+        return res
+
+    def gpipe_api(self, exp: Dict[str, Any], balance: List[int], checkpoint: str,
+                  steps: int) -> Dict[str, Any]:
+        """The U-Net experiment through the public single-process ``GPipe`` API on this
+        rank's GPU (the reference's speed benchmark path, ``benchmarks/unet-speed/main.py:
+        37-67``): ``model(x)``, the loss on the gathered output, ``loss.backward()``, SGD."""
+        from torchgpipe_amd import GPipe
+        batch, chunks = exp['batch'], exp['chunks']
+        model = GPipe(self.build('unet'), balance=balance, devices=[self.device] * len(balance),
+                      chunks=chunks, checkpoint=checkpoint)
+        optimizer = torch.optim.SGD(model.parameters(), lr=0.1)
+        x, target, loss_fn, _ = self.data('unet', batch, True, True)
+
+        def step() -> None:
+            loss = loss_fn(model(x), target)
+            loss.backward()
+            optimizer.step()
+            optimizer.zero_grad(set_to_none=True)
+
+        world, self.world = self.world, 1  # one process drives it: no collective
+        try:
+            res: Dict[str, Any] = self.timed(step, steps, self.args.warmup, 'gpipe')
+        finally:
+            self.world = world
+        res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
+                   steps=steps)
+        del model, optimizer, x, target, step
         self.release()
         return res
 
@@ -490,10 +532,9 @@ def summary(res: Dict[str, Any], ref: Optional[float]) -> Dict[str, Any]:
 
 def main() -> None:
     args = parse()
-    # stdout carries exactly one JSON line (rank 0).  Libraries print to fd 1
-    # from native code (gloo's "[Gloo] Rank r is connected to ..." banner, RCCL
-    # info): point fd 1 at stderr for the whole run and keep a private handle
-    # on the real stdout for the result.
+    # stdout carries the JSON lines (rank 0).  Libraries print to fd 1 from native code
+    # (gloo's "[Gloo] Rank r is connected to ..." banner, RCCL info): point fd 1 at stderr
+    # for the whole run and keep a private handle on the real stdout for the result.
     sys.stdout.flush()
     result_out = os.fdopen(os.dup(1), 'w')
     os.dup2(2, 1)
@@ -552,59 +593,136 @@ def main() -> None:
         b.log(f'section {name}: {section_s[name]} s')
         t_sec = time.time()
 
+    record: Dict[str, Any] = {}
+
+    def emit() -> None:
+        """Rank 0 prints the record as it stands: right after the headline, then again,
+        augmented, after every section -- a later section that fails or hangs cannot take
+        the lines already printed with it.  Each line is a complete record; the last one
+        printed is the most complete."""
+        if b.rank == 0:
+            record['section_s'] = dict(section_s)
+            print(json.dumps(record), file=result_out, flush=True)
+
+    # 1. the headline: the reference balance on the plain eager engine (no multi-path
+    #    transfers, no captured cells at N > 1 -- those have their own sections below)
     main_run = b.pipeline(kind, exp, balance, checkpoint, args.steps, 'headline', probe=probe)
     lap('headline')
     elapsed = main_run['elapsed']
-    tuned = None
-    also = args.also_tuned == 'yes' or (args.also_tuned == 'auto' and world > 1
-                                         and args.balance == 'ref' and tuned_balance != balance)
-    if also:
-        t = b.pipeline(kind, exp, tuned_balance, checkpoint, args.steps, 'tuned')
-        tuned = {'balance': tuned_balance,
-                 'value': round(batch * args.steps / t['elapsed'], 3),
-                 'ms_per_step': round(1000 * t['elapsed'] / args.steps, 3)}
-        lap('tuned')
-
-    sections = ({'baseline', 'amoebanet'} | ({'resnet'} if world in RESNET_EXPERIMENTS else set())
-                if kind == 'unet' else set()) \
-        if args.sections == 'auto' else \
-        (set() if args.sections == 'none' else set(args.sections.split(',')))
-    sec_steps = args.section_steps or args.steps
     samples_per_s = batch * args.steps / elapsed
+    ref = None if args.tiny else exp.get('ref')
+    if args.tiny:
+        model_name += ' TINY smoke-test variant (not a measurement)'
+    record.update({
+        'metric': f'{model_name} GPipe training throughput (samples/sec)',
+        'value': round(samples_per_s, 3),
+        'unit': 'samples/sec',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(1000 * elapsed / args.steps, 3),
+        'higher_is_better': True,
+        'scaling': 'strong',
+        'vs_baseline': round(samples_per_s / ref, 3) if ref else None,
+        'dtype': 'fp32',
+        'data': 'synthetic (torch.rand inputs, constant targets), random-init weights',
+        'config': {
+            'model': model_name,
+            'experiment': exp['name'],
+            'global_batch': batch,
+            'seq_len': None,
+            'input': in_shape,
+            'chunks': chunks,
+            'balance': balance,
+            'balance_source': args.balance,
+            'checkpoint': checkpoint,
+            'parallelism': f'pp{world}',
+            'transport': 'gloo-host-staged (rehearsal)' if b.rehearsal else
+                         ('rccl' if b.gpu and world > 1 else 'none'),
+            'fused_cells': kind == 'unet' and not args.unfused,
+            'baseline_samples_per_sec_p40': ref,
+            'rank0_peak_mem_gib': round(main_run['mem'], 2),
+            'warmup_s': round(main_run['warm_s'], 1),
+            'first_step_s': round(main_run['first_step_s'], 2),
+            'timeout_s': args.timeout,
+            'hipgraph': main_run['hipgraph'],
+            'cell_streams': main_run['cell_streams'],
+            'overlap_recompute': main_run['overlap_recompute'],
+            'overlap_forward': main_run['overlap_forward'],
+            'graph_cells': main_run['graph_cells'],
+            'striped_routes': main_run['striped_routes'],
+            'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'),
+        },
+        'tuned': None,
+    })
+    if 'per_rank' in main_run:
+        record['per_rank'] = main_run['per_rank']
+    emit()
 
-    baseline = None
+    if args.sections == 'auto':
+        sections = set()
+        if kind == 'unet':
+            sections = {'baseline', 'amoebanet'}
+            if world in RESNET_EXPERIMENTS:
+                sections.add('resnet')
+            if world == 1:
+                sections.add('gpipe')
+            if world >= 3:
+                sections.add('striped')
+            if world > 1:
+                sections.add('graph_cells')
+    elif args.sections == 'none':
+        sections = set()
+    else:
+        sections = set(args.sections.split(','))
+    sec_steps = args.section_steps or args.steps
+    # the opt-in engine variants at N > 1 (striped transfers, captured cells, tuned
+    # balances): fewer timed steps, they are comparisons against the sections above
+    extra_steps = min(sec_steps, 10)
+
     if 'baseline' in sections and kind == 'unet':
         bl = b.plain('unet', 4 if args.tiny else UNET_BASELINE['batch'], sec_steps, 'baseline')
         if bl is not None:
             baseline = summary(bl, None if args.tiny else UNET_BASELINE['ref'])
             baseline['experiment'] = 'baseline (no GPipe, rank 0 GPU)'
+            # same-box speed-up over the reference's own denominator (no GPipe, B=40)
+            record['baseline_samples_per_sec'] = baseline['value']
+            record['speedup_vs_baseline'] = round(samples_per_s / baseline['value'], 3)
+            record['baseline'] = baseline
         lap('baseline')
+        emit()
 
-    amoeba = None
-    if 'amoebanet' in sections and kind == 'unet':
+    if 'gpipe' in sections and kind == 'unet' and world == 1:
+        # the reference's own API on its own benchmark path: single-process GPipe
+        gr = b.gpipe_api(exp, balance, checkpoint, sec_steps)
+        g = summary(gr, None if args.tiny else exp.get('ref'))
+        g['experiment'] = f"{exp['name']} through GPipe(balance={balance}, chunks={chunks})"
+        g['vs_pipeline_stage'] = round(g['value'] / samples_per_s, 3)
+        record['gpipe'] = g
+        lap('gpipe')
+        emit()
+
+    a_layers = None
+    aexp: Dict[str, Any] = {}
+    if ('amoebanet' in sections or 'graph_cells' in sections) and kind == 'unet':
         a_layers = len(b.build('amoebanet'))
         aexp = dict(AMOEBA_EXPERIMENTS.get(world) or dict(
             name=f'n{world}m32', batch=160 * world, chunks=32,
             balance=even_balance(a_layers, world), ref=None))
         if args.tiny:
             aexp.update(batch=4, chunks=2, balance=even_balance(a_layers, world))
-        ar = b.pipeline('amoebanet', aexp, aexp['balance'],
-                        'except_last' if aexp['chunks'] > 1 else 'always', sec_steps,
-                        'amoebanet')
+    a_ckpt = 'except_last' if aexp.get('chunks', 2) > 1 else 'always'
+
+    if 'amoebanet' in sections and kind == 'unet':
+        assert a_layers is not None
+        ar = b.pipeline('amoebanet', aexp, aexp['balance'], a_ckpt, sec_steps, 'amoebanet')
         amoeba = summary(ar, None if args.tiny else aexp['ref'])
         amoeba['experiment'] = aexp['name']
         amoeba['cell_streams'] = ar['cell_streams']
         amoeba['hipgraph'] = ar['hipgraph']
         amoeba['graph_cells'] = ar['graph_cells']
         amoeba['striped_routes'] = ar['striped_routes']
-        a_tuned = list(aexp.get('tuned', aexp['balance']))
-        if world > 1 and not args.tiny and a_tuned != list(aexp['balance']):
-            # the MI355X-searched balance too (AMOEBA_EXPERIMENTS 'tuned')
-            at = b.pipeline('amoebanet', aexp, a_tuned, 'except_last', sec_steps,
-                            'amoebanet-tuned')
-            amoeba['tuned'] = {'balance': a_tuned,
-                               'value': round(aexp['batch'] * sec_steps / at['elapsed'], 3),
-                               'ms_per_step': round(1000 * at['elapsed'] / sec_steps, 3)}
+        record['amoebanet'] = amoeba
         if world == 2:
             d = dict(AMOEBA_N2M1)
             if args.tiny:
@@ -613,8 +731,8 @@ def main() -> None:
             amoeba['n2m1'] = summary(dr, None if args.tiny else d['ref'])
             amoeba['speedup_vs_n2m1'] = round(amoeba['value'] / amoeba['n2m1']['value'], 3)
         lap('amoebanet')
+        emit()
 
-    resnet = None
     if 'resnet' in sections and kind == 'unet' and world in RESNET_EXPERIMENTS:
         rexp = dict(RESNET_EXPERIMENTS[world])
         if args.tiny:
@@ -626,6 +744,7 @@ def main() -> None:
         resnet['hipgraph'] = rr['hipgraph']
         resnet['graph_cells'] = rr['graph_cells']
         resnet['striped_routes'] = rr['striped_routes']
+        record['resnet101'] = resnet
         rb = b.plain('resnet', 4 if args.tiny else RESNET_BASELINE['batch'], sec_steps,
                      'resnet-baseline')
         if rb is not None:
@@ -633,66 +752,53 @@ def main() -> None:
             resnet['speedup_vs_baseline'] = round(resnet['value'] / resnet['baseline']['value'],
                                                   3)
         lap('resnet')
+        emit()
 
-    if b.rank == 0:
-        ref = None if args.tiny else exp.get('ref')
-        if args.tiny:
-            model_name += ' TINY smoke-test variant (not a measurement)'
-        record = {
-            'metric': f'{model_name} GPipe training throughput (samples/sec)',
-            'value': round(samples_per_s, 3),
-            'unit': 'samples/sec',
-            'n_gpus': world,
-            'steps': args.steps,
-            'warmup': args.warmup,
-            'ms_per_step': round(1000 * elapsed / args.steps, 3),
-            'higher_is_better': True,
-            'scaling': 'strong',
-            'vs_baseline': round(samples_per_s / ref, 3) if ref else None,
-            'dtype': 'fp32',
-            'data': 'synthetic (torch.rand inputs, constant targets), random-init weights',
-            'config': {
-                'model': model_name,
-                'experiment': exp['name'],
-                'global_batch': batch,
-                'seq_len': None,
-                'input': in_shape,
-                'chunks': chunks,
-                'balance': balance,
-                'balance_source': args.balance,
-                'checkpoint': checkpoint,
-                'parallelism': f'pp{world}',
-                'transport': 'gloo-host-staged (rehearsal)' if b.rehearsal else
-                             ('rccl' if b.gpu and world > 1 else 'none'),
-                'fused_cells': kind == 'unet' and not args.unfused,
-                'baseline_samples_per_sec_p40': ref,
-                'rank0_peak_mem_gib': round(main_run['mem'], 2),
-                'warmup_s': round(main_run['warm_s'], 1),
-                'first_step_s': round(main_run['first_step_s'], 2),
-                'timeout_s': args.timeout,
-                'hipgraph': main_run['hipgraph'],
-                'cell_streams': main_run['cell_streams'],
-                'overlap_recompute': main_run['overlap_recompute'],
-                'wgrad_stream': main_run['wgrad_stream'],
-                'overlap_forward': main_run['overlap_forward'],
-                'graph_cells': main_run['graph_cells'],
-                'striped_routes': main_run['striped_routes'],
-            },
-            'tuned': tuned,
-        }
-        if baseline is not None:
-            # same-box speed-up over the reference's own denominator (no GPipe, B=40)
-            record['baseline_samples_per_sec'] = baseline['value']
-            record['speedup_vs_baseline'] = round(samples_per_s / baseline['value'], 3)
-            record['baseline'] = baseline
-        if amoeba is not None:
-            record['amoebanet'] = amoeba
-        if resnet is not None:
-            record['resnet101'] = resnet
-        if 'per_rank' in main_run:
-            record['per_rank'] = main_run['per_rank']
-        record['section_s'] = section_s
-        print(json.dumps(record), file=result_out, flush=True)
+    also = args.also_tuned == 'yes' or (args.also_tuned == 'auto' and world > 1
+                                         and args.balance == 'ref' and tuned_balance != balance)
+    if also:
+        t = b.pipeline(kind, exp, tuned_balance, checkpoint, extra_steps, 'tuned')
+        record['tuned'] = {'balance': tuned_balance,
+                           'value': round(batch * extra_steps / t['elapsed'], 3),
+                           'ms_per_step': round(1000 * t['elapsed'] / extra_steps, 3),
+                           'steps': extra_steps}
+        if 'amoebanet' in record and world > 1 and not args.tiny:
+            a_tuned = list(aexp.get('tuned', aexp['balance']))
+            if a_tuned != list(aexp['balance']):
+                # the MI355X-searched balance too (AMOEBA_EXPERIMENTS 'tuned')
+                at = b.pipeline('amoebanet', aexp, a_tuned, a_ckpt, extra_steps,
+                                'amoebanet-tuned')
+                record['amoebanet']['tuned'] = {
+                    'balance': a_tuned,
+                    'value': round(aexp['batch'] * extra_steps / at['elapsed'], 3),
+                    'ms_per_step': round(1000 * at['elapsed'] / extra_steps, 3),
+                    'steps': extra_steps}
+        lap('tuned')
+        emit()
+
+    if 'striped' in sections and world >= 3:
+        # multi-path transfers (parallel/stripes.py) on the headline configuration: opt-in
+        # until a multi-GPU node has run their RCCL relay chains
+        sr = b.pipeline(kind, exp, balance, checkpoint, extra_steps, 'striped', stripes=True)
+        st = summary(sr, None if args.tiny else exp.get('ref'))
+        st['striped_routes'] = sr['striped_routes']
+        st['stripe_mb'] = args.stripe_mb
+        record['striped'] = st
+        lap('striped')
+        emit()
+
+    if 'graph_cells' in sections and kind == 'unet' and world > 1:
+        # captured cells at N > 1 (parallel/segments.py: RCCL receives into the captured
+        # graphs' persistent buffers) on the AmoebaNet experiment, opt-in like the stripes
+        gc_run = b.pipeline('amoebanet', aexp, aexp['balance'], a_ckpt, extra_steps,
+                            'amoebanet-graph-cells', graph_cells=True)
+        gcs = summary(gc_run, None if args.tiny else aexp['ref'])
+        gcs['experiment'] = aexp['name']
+        gcs['graph_cells'] = gc_run['graph_cells']
+        record['amoebanet_graph_cells'] = gcs
+        lap('graph_cells')
+        emit()
+
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -492,6 +492,33 @@ def test_gemm_conv2d_module_matches_conv2d():
     assert rel_err(conv.weight.grad, ref.weight.grad) < 5e-6
 
 
+def test_presplit_follows_data_updates_across_steps():
+    """An update through ``param.data`` moves no version counter: the pre-split planes of a
+    1x1 implicit-GEMM weight (forward) are still re-derived on the next training step
+    (ops/conv.py new_step), so forward and backward-data read the same weights."""
+    from torchgpipe_amd.ops.conv import new_step
+    from torchgpipe_amd.ops.convbn import GemmConv2d
+    ops().conv_gemm_force_cfg(9)
+    ops().conv_gemm_presplit(-1)
+    try:
+        torch.manual_seed(0)
+        conv = GemmConv2d(64, 96, 1, bias=False).cuda()
+        x = torch.randn(4, 64, 14, 14, device='cuda')
+        new_step()
+        y1 = conv(x)
+        assert ops().conv_gemm_presplit(-1, False) > 0  # the planes are cached
+        fresh = torch.randn_like(conv.weight) * 0.1
+        conv.weight.data.copy_(fresh)  # no version bump on the parameter
+        new_step()
+        y2 = conv(x)
+        ref = F.conv2d(x.double(), fresh.double())
+        assert rel_err(y2, ref) < 2e-6
+        assert not torch.equal(y1, y2)
+    finally:
+        ops().conv_gemm_force_cfg(-1)
+        ops().conv_gemm_presplit(-1)
+
+
 @pytest.mark.parametrize('stride', [1, 2])
 @pytest.mark.parametrize('hw', [(7, 7), (12, 9), (1, 1), (2, 3), (120, 121)])
 @pytest.mark.parametrize('with_add', [False, True])

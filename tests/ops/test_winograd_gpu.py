@@ -343,8 +343,13 @@ def test_cache_budget_sizing_modes(monkeypatch):
     cap = total // 20
     assert convmod.size_cache_budget(dev, total - (1 << 30), fraction=None) == \
         min(cap, (1 << 30) // 2)
+    # the pre-split weights get at most half of what the step and the cache left free
+    assert convmod.presplit_budget_mb == min(convmod.PRESPLIT_MB, 256)
     assert convmod.size_cache_budget(dev, 1 << 30, fraction=0.15) == int(0.15 * (1 << 30))
+    assert convmod.presplit_budget_mb == 0
     assert convmod.size_cache_budget(dev, total // 2, fraction=None) == cap
+    assert convmod.presplit_budget_mb == convmod.PRESPLIT_MB
+    convmod._presplit_budget(-1)
 
 
 def test_module_weight_gradient_picks_split_bf16_gemm_for_deep_layers():

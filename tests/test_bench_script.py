@@ -1,4 +1,7 @@
-"""The bench.py driver contract: one JSON line from rank 0, MAX-over-ranks timing.
+"""The bench.py driver contract: JSON records from rank 0, MAX-over-ranks timing.
+
+Rank 0 prints the complete record right after the headline and re-prints it, augmented,
+after every section; every line is a complete record and the last one the most complete.
 
 Runs the script end to end on CPU (gloo) with the ``--tiny`` model variant, at
 one rank and under ``torch.distributed.run`` with two ranks.
@@ -23,6 +26,10 @@ def _free_port() -> int:
 
 
 def _run(nproc: int, *extra: str) -> dict:
+    return _run_lines(nproc, *extra)[-1]
+
+
+def _run_lines(nproc: int, *extra: str) -> list:
     env = dict(os.environ, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='', OMP_NUM_THREADS='2')
     args = ['bench.py', '--gpus', str(nproc), '--steps', '1', '--warmup', '1', '--tiny',
             '--batch', '4', '--chunks', '2', *extra]
@@ -35,8 +42,12 @@ def _run(nproc: int, *extra: str) -> dict:
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
-    assert len(lines) == 1, out.stdout  # nothing but the JSON line on stdout
-    return json.loads(lines[0])
+    assert lines, out.stderr[-3000:]
+    records = [json.loads(ln) for ln in lines]  # nothing but JSON records on stdout
+    for rec in records:
+        assert KEYS <= set(rec)
+        assert rec['value'] == records[0]['value']  # every line carries the same headline
+    return records
 
 
 @pytest.mark.parametrize('nproc,model', [(1, 'unet'), (2, 'unet'), (2, 'amoebanet'),
@@ -58,6 +69,11 @@ def test_bench_json_contract(nproc, model):
         assert rec['config']['checkpoint'] == 'except_last'
     # value is the whole-job aggregate: batch * steps / elapsed
     assert rec['value'] == pytest.approx(4 * 1000 / rec['ms_per_step'], rel=1e-2)
+    if model == 'unet' and nproc == 1:
+        # the public single-process GPipe API on the headline experiment
+        assert rec['gpipe']['value'] > 0 and rec['gpipe']['chunks'] == 2
+        assert rec['gpipe']['vs_pipeline_stage'] == pytest.approx(
+            rec['gpipe']['value'] / rec['value'], rel=1e-2)
     if model == 'unet':
         # same-box speed-up denominator and the AmoebaNet section ride along
         assert rec['baseline']['value'] > 0 and rec['speedup_vs_baseline'] > 0
@@ -72,7 +88,11 @@ def test_bench_json_contract(nproc, model):
         res = rec['resnet101']
         assert res['value'] > 0 and res['checkpoint'] == ('always' if nproc == 2
                                                            else 'except_last')
-        assert set(rec['section_s']) == {'headline', 'baseline', 'amoebanet', 'resnet'}
+        want = {'headline', 'baseline', 'amoebanet', 'resnet'}
+        # (the tiny variant's tuned balance is its reference one: no 'tuned' section)
+        want |= {'gpipe'} if nproc == 1 else {'graph_cells'}
+        want |= {'striped'} if nproc >= 3 else set()
+        assert set(rec['section_s']) == want
         # with its own no-GPipe denominator (the reference's ResNet baseline, B=118)
         assert res['baseline']['value'] > 0
         assert res['speedup_vs_baseline'] == pytest.approx(
@@ -88,17 +108,33 @@ def test_bench_json_contract(nproc, model):
         assert ranks[1]['fwd_wait_ms'] > 0 and ranks[0]['bwd_wait_ms'] > 0
 
 
+def test_bench_headline_printed_before_the_sections_eight_ranks():
+    """At N=8 the first line is the headline alone (the reference balance on the plain
+    eager engine: no stripes, no captured cells), printed before any section runs; each
+    later line adds one section."""
+    records = _run_lines(8, '--model', 'unet', '--sections', 'baseline,amoebanet,striped')
+    first = records[0]
+    assert set(first['section_s']) == {'headline'}
+    assert 'baseline' not in first and 'amoebanet' not in first and 'striped' not in first
+    assert first['config']['striped_routes'] == {} and first['config']['graph_cells'] is False
+    assert first['config']['balance_source'] == 'ref'
+    assert [set(r['section_s']) for r in records[1:]] == [
+        {'headline', 'baseline'}, {'headline', 'baseline', 'amoebanet'},
+        {'headline', 'baseline', 'amoebanet', 'striped'}]
+
+
 def test_bench_striped_eight_ranks():
-    """``--stripes`` at 8 ranks with a threshold every tiny message clears: the headline
-    U-Net's routes are planned after the first warm-up step (an extra untimed step), relayed
-    in the timed step, and reported."""
-    rec = _run(8, '--model', 'unet', '--stripe-mb', '0.000001', '--sections', 'none')
-    routes = rec['config']['striped_routes']
-    assert routes, rec['config']
+    """The ``striped`` section at 8 ranks with a threshold every tiny message clears: the
+    headline U-Net's routes are planned after the first warm-up step (an extra untimed
+    step), relayed in the timed step, and reported under their own key."""
+    rec = _run(8, '--model', 'unet', '--stripe-mb', '0.000001', '--sections', 'striped')
+    assert rec['config']['striped_routes'] == {}  # the headline stays direct
+    routes = rec['striped']['striped_routes']
+    assert routes, rec['striped']
     for route, relays in routes.items():
         src, dst = map(int, route.split('->'))
         assert relays and not {src, dst} & set(relays)
-    assert rec['value'] > 0
+    assert rec['striped']['value'] > 0
 
 
 def test_bench_headline_uses_reference_balance_and_reports_tuned():

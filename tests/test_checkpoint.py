@@ -227,3 +227,18 @@ def test_user_dropout_on_the_philox_tape(where):
         grads[mode] = [p.grad.clone() for p in gpipe.parameters()]
     for a, b in zip(grads['never'], grads['always']):
         assert torch.equal(a, b)
+
+
+def test_inplace_change_of_a_checkpointed_input_is_an_error():
+    """The Checkpoint node keeps its inputs outside autograd's saved tensors (so a pipeline
+    can release them early): the recomputation checks their version counters itself, so
+    an in-place change between forward and recomputation fails loudly instead of
+    recomputing from the changed value."""
+    x = torch.randn(4, 3)
+    lin = nn.Linear(3, 2)
+    chk = Checkpointing(lin, Batch(x))
+    out = chk.checkpoint()
+    x.add_(1.0)
+    with pytest.raises(RuntimeError, match='inplace'):
+        chk.recompute_now()
+    del out

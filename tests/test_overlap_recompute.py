@@ -114,20 +114,22 @@ def test_overlap_with_two_stream_cells_matches_plain():
 
 @pytest.mark.gpu
 def test_weight_gradient_stream_matches_plain():
-    """The fused ops' weight-gradient GEMMs on a side stream (with the recompute lanes):
+    """The fused ops' weight-gradient GEMMs on a side stream (``ops.convbn.
+    wgrad_stream_scope`` around the training step, with the recompute lanes):
     the same kernels in the same per-stream order as the plain schedule, so losses,
     gradients and SGD-updated parameters agree over several steps
     (profiles/r2/wgrad_stream_steps.log: bit-identical).  Two-stream cells are left out
     here: autograd sums a node's gradient contributions from the two streams in another
     order (~1e-6), which the tiny model's SGD trajectory then amplifies."""
     from torchgpipe_amd.models import amoebanetd
+    from torchgpipe_amd.ops.convbn import wgrad_stream_scope
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
     base = amoebanetd(num_classes=10, num_layers=3, num_filters=16)
     a, b = copy.deepcopy(base), copy.deepcopy(base)
     sa = PipelineStage(a, [len(a)], device=dev, chunks=4, checkpoint='except_last')
     sb = PipelineStage(b, [len(b)], device=dev, chunks=4, checkpoint='except_last',
-                       overlap_recompute=True, wgrad_stream=True)
+                       overlap_recompute=True)
     oa = torch.optim.SGD(sa.parameters(), lr=0.05)
     ob = torch.optim.SGD(sb.parameters(), lr=0.05)
     gen = torch.Generator(device=dev).manual_seed(13)
@@ -135,7 +137,8 @@ def test_weight_gradient_stream_matches_plain():
         x = torch.rand(8, 3, 224, 224, device=dev, generator=gen)
         y = torch.randint(10, (8,), device=dev, generator=gen)
         la = sa.train_step(x, y, F.cross_entropy)
-        lb = sb.train_step(x, y, F.cross_entropy)
+        with wgrad_stream_scope(dev):
+            lb = sb.train_step(x, y, F.cross_entropy)
         _close_grads(a, b)
         oa.step()
         ob.step()
@@ -145,3 +148,25 @@ def test_weight_gradient_stream_matches_plain():
         ob.zero_grad(set_to_none=True)
     for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pb, pa, rtol=1e-5, atol=1e-6, msg=name)
+
+
+@pytest.mark.parametrize('checkpoint', ['always', 'except_last'])
+def test_direct_backward_reaches_a_learnable_loss_head(checkpoint):
+    """The last stage's direct backward (through the recomputed graph, not the Checkpoint
+    node) still gives a parameter the loss reaches around the stage outputs its gradient,
+    as ``direct_backward=False`` and the reference's ``loss.backward()`` do."""
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(4, 8), nn.ReLU(), nn.Linear(8, 2))
+    a, b = copy.deepcopy(model), copy.deepcopy(model)
+    head_a = nn.Parameter(torch.tensor([1.5, -0.5]))
+    head_b = nn.Parameter(head_a.detach().clone())
+    sa = PipelineStage(a, [3], chunks=4, checkpoint=checkpoint, direct_backward=False)
+    sb = PipelineStage(b, [3], chunks=4, checkpoint=checkpoint, direct_backward=True)
+    x, y = torch.randn(8, 4), torch.randn(8, 2)
+    la = sa.train_step(x, y, lambda o, t: F.mse_loss(o * head_a, t))
+    lb = sb.train_step(x, y, lambda o, t: F.mse_loss(o * head_b, t))
+    torch.testing.assert_close(la, lb)
+    assert head_b.grad is not None
+    torch.testing.assert_close(head_b.grad, head_a.grad)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pb.grad, pa.grad)

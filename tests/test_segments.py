@@ -32,8 +32,6 @@ def test_cpu_stage_ignores_graph_cells():
 
 def test_graph_cells_option_checks():
     model = nn.Sequential(nn.Linear(4, 4))
-    with pytest.raises(ValueError, match='wgrad_stream'):
-        PipelineStage(model, [1], graph_cells=True, wgrad_stream=True)
     with pytest.raises(ValueError, match='warm-up'):
         PipelineStage(model, [1], graph_cells=True, graph_warmup=0)
 

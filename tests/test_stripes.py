@@ -53,20 +53,23 @@ def _chain(n, sizes, skips=()):
     return sends
 
 
-def test_plan_relays_only_over_idle_links():
+def test_plan_relays_only_over_idle_link_directions():
     sends = _chain(8, [300, 200, 10, 10, 10, 10, 10], skips=[(1, 6, 250)])
     stripes, jobs = plan(sends, list(range(8)), min_bytes=100)
-    busy = {frozenset((j, j + 1)) for j in range(7)} | {frozenset((1, 6))}
+    forward = {(j, j + 1) for j in range(7)} | {(1, 6)}
     assert set(stripes) >= {(0, 1), (1, 0), (1, 2), (2, 1), (1, 6), (6, 1)}
     seen = set()
     for (src, dst), relays in stripes.items():
         assert relays == stripes[(dst, src)]  # gradients come back the same way
         for r in relays:
             assert r not in (src, dst)
-            for pair in (frozenset((src, r)), frozenset((r, dst))):
-                assert pair not in busy
-                if src < dst:
-                    assert pair not in seen  # a detour link carries one route
+            if src < dst:
+                # no (large) forward message uses a detour's direction (nor, mirrored, a
+                # gradient the backward detour's): only the 10-byte ones may
+                for link in ((src, r), (r, dst)):
+                    assert link not in forward or link not in {(0, 1), (1, 2), (1, 6)}
+                for pair in (frozenset((src, r)), frozenset((r, dst))):
+                    assert pair not in seen  # a GPU pair carries one route's detour
                     seen.add(pair)
     # small routes stay direct
     assert (3, 4) not in stripes
@@ -130,3 +133,27 @@ def test_p2p_refuses_a_step_that_sends_differently_from_its_plan():
     assert not p2p._striped(0, 3, 1 << 20, 'other route')
     with pytest.raises(RuntimeError, match='sent 0 messages this step, the stripe plan 1'):
         p2p.end_relays()
+
+
+def test_plan_uses_the_reverse_direction_of_busy_links():
+    """U-Net p4 at the reference balance (routes 0->1, 1->2, 2->3 and skips 0->3, 1->2,
+    1->3) has no detour whose links are idle in both directions, so an undirected planner
+    finds none; the forward phase leaves 2 -> 1 and 3 -> 1 free (only gradients use them,
+    later), so the large first boundary goes 0 -> 2 -> 1 and 0 -> 3 -> 1 too (0 -> 3
+    carries a small skip only)."""
+    sends = _chain(4, [500, 10, 10], skips=[(0, 3, 10), (1, 2, 10), (1, 3, 10)])
+    stripes, jobs = plan(sends, [0, 1, 2, 3], min_bytes=100)
+    assert stripes == {(0, 1): [2, 3], (1, 0): [2, 3]}
+    assert [(j.src, j.dst) for j in jobs[2]] == [(0, 1)]
+
+
+def test_plan_shares_a_lightly_loaded_link_direction():
+    """U-Net p4's 302 MB skip 0 -> 3: every link into stage 3 carries forward traffic, so no
+    idle detour exists; 2 -> 3 carries only the 38 MB activation (1/8 of the skip), so the
+    skip still takes 0 -> 2 -> 3.  A busier link (half the message) is not shared."""
+    sends = _chain(4, [151, 75, 37], skips=[(0, 3, 302), (1, 2, 10), (1, 3, 151)])
+    stripes, _ = plan(sends, [0, 1, 2, 3], min_bytes=100)
+    assert 2 in stripes[(0, 3)]
+    sends = _chain(4, [151, 75, 151], skips=[(0, 3, 302), (1, 2, 10), (1, 3, 151)])
+    stripes, _ = plan(sends, [0, 1, 2, 3], min_bytes=100)
+    assert (0, 3) not in stripes

@@ -123,7 +123,8 @@ class RNGSnapshot:
 class _Shared:
     """State shared by one Checkpoint/Recompute pair (the reference uses deques)."""
 
-    __slots__ = ('function', 'input_atomic', 'recomputed', 'rng', 'tape', 'inputs')
+    __slots__ = ('function', 'input_atomic', 'recomputed', 'rng', 'tape', 'inputs',
+                 'versions')
 
     def __init__(self, function: Any, input_atomic: bool) -> None:
         self.function = function
@@ -133,11 +134,22 @@ class _Shared:
         # ahead and back-propagates through the recomputed graph can release them while a
         # loss still references the node (PipelineStage's last stage)
         self.inputs: Optional[Tensors] = None
+        # the inputs' version counters at the checkpointed forward: with the inputs held
+        # here instead of in saved tensors, autograd's own check is gone, so the
+        # recomputation checks them itself (an in-place change in between would recompute
+        # from the changed value and give wrong gradients silently)
+        self.versions: Optional[Tuple[int, ...]] = None
         self.recomputed: Deque[Recomputed] = deque(maxlen=1)
         self.rng: Deque[RNGSnapshot] = deque(maxlen=1)
         self.tape = RngTape()
 
     def run_recompute(self, inputs: Tensors) -> None:
+        if self.versions is not None and \
+                tuple(x._version for x in inputs) != self.versions:
+            raise RuntimeError('one of the inputs of a checkpointed micro-batch has been '
+                               'modified by an inplace operation before its recomputation '
+                               f'(versions {self.versions} at the forward, '
+                               f'{tuple(x._version for x in inputs)} now)')
         leaves = tuple(x.detach().requires_grad_(x.requires_grad) for x in inputs)
         snapshot = self.rng.pop()
         with snapshot.restored(), self.tape.replaying():
@@ -154,7 +166,11 @@ class Checkpoint(torch.autograd.Function):
         shared.inputs = input
         shared.rng.append(RNGSnapshot(input[0].device))
         with torch.no_grad(), enable_checkpointing(), shared.tape.recording():
-            return shared.function(input[0] if shared.input_atomic else input)
+            output = shared.function(input[0] if shared.input_atomic else input)
+        # (after the function: its own in-place ops on its inputs are the recomputation's
+        # business, as in the reference; what must not happen is a change in between)
+        shared.versions = tuple(x._version for x in input)
+        return output
 
     @staticmethod
     def backward(ctx, *grad_output: Tensor) -> Tuple[Optional[Tensor], ...]:  # type: ignore[override]

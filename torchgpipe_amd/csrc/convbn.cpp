@@ -246,7 +246,8 @@ int64_t conv_gemm_plans_import(const std::string& text) {
 // backward-data GEMMs are split once per weight version instead ([M][ceil(K/8)][3][8] bf16,
 // 1.5x the weight's bytes) and the kernel loads the planes.  Entries are keyed by the
 // source tensor's storage, held by weak reference (a dead weight's entry is dropped), and
-// re-derived when its version counter moves: lazily by the next launch (readers on other
+// re-derived when its version counter moves or a new training step starts (updates through
+// `.data` move no version counter): lazily by the next launch (readers on other
 // streams wait for that derive's event), or in place for a whole stage by
 // conv_gemm_presplit_refresh (PipelineStage's step start, ops/conv.py
 // refresh_step_caches) -- which is what keeps a captured hipGraph, that baked the buffer in,
@@ -268,6 +269,7 @@ struct PreSplit {
   WeakImpl src;
   PreDims d;
   int64_t version = -1;
+  int64_t step = -1;  // the training step it was derived in (conv_gemm_presplit_step)
   at::Tensor split;
   hipEvent_t ready = nullptr;
   hipStream_t stream = nullptr;  // derived lazily on this stream (null: ordered by the caller)
@@ -277,6 +279,11 @@ std::mutex pre_mutex;
 std::map<PreKey, PreSplit> pre_cache;
 int64_t pre_bytes = 0;
 std::atomic<int64_t> pre_budget{-1};
+// The current training step (ops/conv.py new_step).  An update through `param.data`
+// (copy_, EMA swaps) moves no version counter, so an entry is fresh only for the version
+// AND the step it was derived in: the first launch (or the step-start refresh) of every
+// step re-derives it, like the Winograd transform caches keyed on ops/conv.py _STEP.
+std::atomic<int64_t> pre_step{0};
 
 int64_t presplit_budget() {
   int64_t b = pre_budget.load();
@@ -323,7 +330,8 @@ at::Tensor presplit_of(const at::Tensor& src, bool transposed, int M, int K, int
     PreSplit& e = it->second;
     auto alive = e.src.lock();
     const bool same = alive.get() == src.unsafeGetTensorImpl() && e.d == probe;
-    if (same && e.version == version) {
+    const int64_t step = pre_step.load();
+    if (same && e.version == version && e.step == step) {
       if (e.stream != nullptr && e.stream != stream && !capturing)
         hipStreamWaitEvent(stream, e.ready, 0);
       return e.split;
@@ -332,6 +340,7 @@ at::Tensor presplit_of(const at::Tensor& src, bool transposed, int M, int K, int
     if (same) {  // stale: in place, on this stream
       presplit_derive(src, e.split, e.d, stream);
       e.version = version;
+      e.step = step;
       hipEventRecord(e.ready, stream);
       e.stream = stream;
       return e.split;
@@ -348,6 +357,7 @@ at::Tensor presplit_of(const at::Tensor& src, bool transposed, int M, int K, int
   if (pre_bytes + numel * 2 > budget) return {};
   PreSplit e(WeakImpl(src.getIntrusivePtr()), probe);
   e.version = version;
+  e.step = pre_step.load();
   e.split = at::empty({numel}, like.options().dtype(at::kBFloat16));
   presplit_derive(src, e.split, e.d, stream);
   hipEventCreateWithFlags(&e.ready, hipEventDisableTiming);
@@ -392,9 +402,11 @@ int64_t conv_gemm_presplit_refresh(at::TensorList sources) {
       const bool capturing = hipStreamIsCapturing(stream, &capture) == hipSuccess &&
                              capture != hipStreamCaptureStatusNone;
       const int64_t version = static_cast<int64_t>(src._version());
-      if (capturing || version != e.version) {
+      const int64_t step = pre_step.load();
+      if (capturing || version != e.version || step != e.step) {
         presplit_derive(src, e.split, e.d, stream);
         e.version = version;
+        e.step = step;
       }
       e.stream = nullptr;  // ordered before the step by the caller
       ++count;
@@ -402,6 +414,9 @@ int64_t conv_gemm_presplit_refresh(at::TensorList sources) {
   }
   return count;
 }
+
+// A new training step: every entry is re-derived before its next use.
+void conv_gemm_presplit_step(int64_t step) { pre_step.store(step); }
 
 // Set the pre-split budget (MiB; 0 = off, < 0 = the environment's) and, with `clear`, drop
 // every entry (test / benchmark hook).  Returns the bytes the entries held.
@@ -1675,6 +1690,7 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("conv_gemm_presplit(int budget_mb, bool clear=True) -> int", &tgpipe::conv_gemm_presplit);
   m.def("conv_gemm_presplit_refresh(Tensor[] sources) -> int",
         &tgpipe::conv_gemm_presplit_refresh);
+  m.def("conv_gemm_presplit_step(int step) -> ()", &tgpipe::conv_gemm_presplit_step);
   m.def("conv_gemm_sweep(int mode, Tensor x, Tensor weight, int[] geo, int reps) -> float[]");
   m.def("conv_gemm_plans_import(str text) -> int", &tgpipe::conv_gemm_plans_import);
   m.def("conv_gemm_backward_data(Tensor dz, Tensor x, Tensor weight, int[] geo, bool relu, "

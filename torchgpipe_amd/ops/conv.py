@@ -58,6 +58,8 @@ _BUDGET: Optional[int] = None
 _DEVICE_BUDGET: Dict[torch.device, int] = {}
 _FRACTION = os.environ.get('TGPIPE_WINOGRAD_CACHE_FRACTION')
 CACHE_PEAK_FRACTION: Optional[float] = float(_FRACTION) if _FRACTION else None
+# the implicit-GEMM pre-split weights' budget cap, MiB (csrc/convbn.cpp presplit_budget)
+PRESPLIT_MB = max(0, int(os.environ.get('TGPIPE_CG_PRESPLIT_MB', '2048')))
 
 
 def new_step() -> None:
@@ -66,6 +68,10 @@ def new_step() -> None:
     (``ops/gradacc.py``), so this step's graph gets nodes bound to its own streams."""
     global _STEP
     _STEP += 1
+    if _ext._loaded:
+        # the implicit GEMMs' pre-split weights too (csrc/convbn.cpp presplit_of): an
+        # update through ``param.data`` moves no version counter
+        torch.ops.tgpipe.conv_gemm_presplit_step(_STEP)
     from torchgpipe_amd.ops import gradacc
     gradacc.release()
 
@@ -99,8 +105,14 @@ def hold_cache(device: torch.device) -> None:
 
 def _presplit_budget(mb: int) -> None:
     """The implicit-GEMM pre-split weights' budget (MiB; -1: ``TGPIPE_CG_PRESPLIT_MB``)."""
+    global presplit_budget_mb
+    presplit_budget_mb = mb
     if _ext.available():
         torch.ops.tgpipe.conv_gemm_presplit(mb, False)
+
+
+# the last pre-split budget set from here (MiB; -1 = the environment's default)
+presplit_budget_mb = -1
 
 
 def size_cache_budget(device: torch.device, peak_bytes: int,
@@ -117,8 +129,15 @@ def size_cache_budget(device: torch.device, peak_bytes: int,
     budget = min(_device_cap(device), budget)
     _DEVICE_BUDGET[device] = budget
     # pre-split implicit-GEMM weights (1.5x the weights they split): off in the memory-lean
-    # mode (a fraction of the peak, e.g. benchmarks/memory.py), else their own budget
-    _presplit_budget(0 if fraction is not None else -1)
+    # mode (a fraction of the peak, e.g. benchmarks/memory.py); else their own budget
+    # (TGPIPE_CG_PRESPLIT_MB), capped by half of what the measuring step and the transform
+    # cache leave free -- like the transform cache, memory the stage did not need
+    if fraction is not None:
+        _presplit_budget(0)
+    else:
+        total = torch.cuda.get_device_properties(device).total_memory
+        left = max(0, total - peak_bytes - budget) // 2
+        _presplit_budget(min(PRESPLIT_MB, left >> 20))
     return budget
 
 

@@ -107,6 +107,15 @@ def wgrad_stream_scope(device: torch.device, enabled: bool = True) -> Iterator[N
             torch.cuda.current_stream(device).wait_stream(stream)
 
 
+def join_wgrad_stream(device: torch.device) -> None:
+    """Order the current stream on ``device`` after the weight-gradient side stream of an
+    active :func:`wgrad_stream_scope` (before gradients written there are read: the
+    deferred split-gradient flush at the end of a pipeline stage's backward)."""
+    stream = _WGRAD_STREAMS.get(device)
+    if stream is not None and device in _WGRAD:
+        torch.cuda.current_stream(device).wait_stream(stream)
+
+
 def _wgrad_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     if device not in _WGRAD or device.type != 'cuda' or torch.cuda.is_current_stream_capturing():
         return None

@@ -448,7 +448,7 @@ class P2P:
         if self.plan is None:
             return
         self._join_relays()
-        for job in self.plan.jobs:
+        for index, job in enumerate(self.plan.jobs):
             ops = ([(job.src, job.dst, n) for n in job.forward]
                    + [(job.dst, job.src, n) for n in job.backward])
             state = self._relays.get((job.src, job.dst))
@@ -459,8 +459,9 @@ class P2P:
                 where = torch.device('cpu')
             else:
                 where = self.device
-                if state.stream is None:
-                    state.stream = torch.cuda.Stream(self.device)
+                if state.stream is None:  # (named: a fixed stream set per process)
+                    from torchgpipe_amd.stream import named_stream
+                    state.stream = named_stream(self.device, f'relay-route{index}')
             # (re)allocate the ring on the route's stream, after the sends still reading it
             with (torch.cuda.stream(state.stream) if state.stream is not None
                   else contextlib.nullcontext()):

@@ -63,6 +63,7 @@ from torch import Tensor, nn
 
 from torchgpipe_amd.checkpoint import enable_checkpointing, enable_recomputing
 from torchgpipe_amd.ops import gradacc
+from torchgpipe_amd.stream import named_stream
 from torchgpipe_amd.utils import rng
 
 __all__ = ['Segments', 'SegmentCell']
@@ -136,7 +137,7 @@ class Segments:
         self.steps = 0
         self.captured = False
         self.pools = [torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()]
-        self.streams = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
+        self.streams = [named_stream(device, 'capture0'), named_stream(device, 'capture1')]
         from torchgpipe_amd.models.amoebanet import prepare_side_streams
         for s in self.streams:  # cell side streams paired with the capture streams
             prepare_side_streams(device, s)

@@ -53,11 +53,12 @@ from torchgpipe_amd.skip.layout import SkipLayout, inspect_skip_layout
 from torchgpipe_amd.skip.namespace import Namespace
 from torchgpipe_amd.skip.skippable import Skippable, verify_skippables
 from torchgpipe_amd.skip.tracker import SkipTracker, use_skip_tracker
+from torchgpipe_amd.stream import named_stream
 from torchgpipe_amd.utils import trace
 from torchgpipe_amd.utils.meta import is_meta
 from torchgpipe_amd.utils.meta import materialize as meta_materialize
 
-__all__ = ['PipelineStage', 'signature_of']
+__all__ = ['PipelineStage', 'signature_of', 'stream_census', 'link_pairs', 'HW_QUEUES']
 
 Tensors = Tuple[Tensor, ...]
 TensorOrTensors = Union[Tensor, Tensors]
@@ -134,6 +135,28 @@ _accumulator_holders = 0
 _accumulator_saved = True
 
 
+def _loss_leaves(loss: Tensor, outputs: Sequence[Tensor]) -> List[Tensor]:
+    """The leaves (e.g. a loss head's parameters) whose gradient ``loss`` reaches without
+    passing through ``outputs``: the last stage's direct backward stops at the outputs,
+    so these need their own share of the pass.  Walks the loss's graph up to the
+    outputs' nodes (a few nodes for the usual loss functions)."""
+    stop = {t.grad_fn for t in outputs if t.grad_fn is not None}
+    leaves: List[Tensor] = []
+    seen = set()
+    todo = [loss.grad_fn]
+    while todo:
+        node = todo.pop()
+        if node is None or node in seen or node in stop:
+            continue
+        seen.add(node)
+        var = getattr(node, 'variable', None)
+        if var is not None and var.requires_grad:
+            leaves.append(var)
+            continue
+        todo.extend(nxt for nxt, _ in node.next_functions)
+    return leaves
+
+
 class _RemoteSkipTracker(SkipTracker):
     """Skip tracker of one cell: local skips in a dict, cross-rank ones captured."""
 
@@ -176,6 +199,41 @@ class _Cell:
         self.lane: Optional[torch.cuda.Stream] = None  # stream it was recomputed on
 
 
+def link_pairs(layout: SkipLayout, n: int) -> List[Tuple[int, int]]:
+    """Stage pairs of an ``n``-stage pipeline that exchange messages: neighbours plus the
+    cross-stage skip routes of ``layout`` (each pair: one link, one RCCL communicator)."""
+    pairs = {(j, j + 1) for j in range(n - 1)}
+    for (src, dst) in layout.by_ns_name.values():
+        if src != dst:
+            pairs.add((min(src, dst), max(src, dst)))
+    return sorted(pairs)
+
+
+# GPU_MAX_HW_QUEUES that bench.py sets for multi-rank runs (the most the runtime is given
+# on this pool).  A rank's own streams and its RCCL communicators' streams must fit with
+# room to spare -- CENSUS_LIMIT, for the default stream and library streams -- or a spinning
+# receive shares a hardware queue with (and blocks) unrelated work
+# (tests/test_stream_census.py).
+HW_QUEUES = 32
+CENSUS_LIMIT = 24
+
+
+def stream_census(rank: int, pairs: Sequence[Tuple[int, int]], *, forward_lanes: bool,
+                  recompute_lanes: bool, cell_streams: int = 0, graph_cells: bool = False,
+                  relay_routes: int = 0, relay_links: int = 0) -> Dict[str, int]:
+    """Streams a pipeline rank queues work on: the compute stream, two forward lanes, two
+    recompute lanes, an AmoebaNet cell's side streams (``cell_streams - 1``), the captured
+    cells' two streams, one stream per relayed route (``parallel/p2p.py`` begin_relays),
+    and one RCCL communicator stream per link and per relay link it is part of."""
+    links = sum(1 for a, b in pairs if rank in (a, b))
+    out = {'compute': 1, 'forward_lanes': 2 if forward_lanes else 0,
+           'recompute_lanes': 2 if recompute_lanes else 0,
+           'cell_side_streams': max(0, cell_streams - 1), 'graph_cells': 2 if graph_cells else 0,
+           'relay_routes': relay_routes, 'link_comms': links, 'relay_comms': relay_links}
+    out['total'] = sum(out.values())
+    return out
+
+
 # 2-rank relay communicators of multi-path transfers, per WORLD group, per GPU pair
 _RELAY_LINKS: Dict[int, Dict[FrozenSet[int], Any]] = {}
 
@@ -207,8 +265,9 @@ class PipelineStage:
             backward as captured hipGraphs, with the transfers issued eagerly in between
             (``parallel/segments.py``): after ``graph_warmup`` eager steps and one capture
             step, the host launches three graphs per cell instead of every kernel.  GPU
-            stages only; gradients are zeroed at the start of each step (each step computes
-            them from scratch, like ``StepGraph``).
+            stages only; gradients accumulate across steps as in eager mode (the captured
+            backward adds into ``.grad``, which is zeroed only where the user released it:
+            ``parallel/segments.py``).
         graph_warmup: eager steps before the capture step (the first runs without cached
             weight transforms and sizes their budget, the second fills the caches, so the
             capture reads them instead of recomputing transforms in its graphs).
@@ -254,7 +313,6 @@ class PipelineStage:
                  timeout: Optional[float] = None,
                  overlap_recompute: bool = False,
                  overlap_forward: bool = False,
-                 wgrad_stream: bool = False,
                  philox_dropout: bool = False,
                  graph_cells: bool = False,
                  graph_warmup: int = 2,
@@ -352,7 +410,6 @@ class PipelineStage:
         self._cells: List[_Cell] = []
         self.overlap_recompute = overlap_recompute
         self.overlap_forward = overlap_forward
-        self.wgrad_stream = wgrad_stream
         self._lanes: Optional[List[torch.cuda.Stream]] = None
         self._fwd_lanes: Optional[List[torch.cuda.Stream]] = None
         # modules whose forward carries state across micro-batches (running statistics):
@@ -362,8 +419,6 @@ class PipelineStage:
         self._sig: Optional[Signature] = None
         self._m = 0
         self._probe: Optional[List[Tuple[str, Any, Any]]] = None
-        if graph_cells and wgrad_stream:
-            raise ValueError('graph_cells does not combine with wgrad_stream')
         if graph_warmup < 1:
             raise ValueError('graph_cells needs at least one eager warm-up step')
         self.graph_cells = graph_cells and device.type == 'cuda'
@@ -419,11 +474,25 @@ class PipelineStage:
 
     def _link_pairs(self) -> List[Tuple[int, int]]:
         """Stage pairs that exchange messages: neighbours plus cross-rank skip routes."""
-        pairs = {(j, j + 1) for j in range(self.n - 1)}
-        for (src, dst) in self.layout.by_ns_name.values():
-            if src != dst:
-                pairs.add((min(src, dst), max(src, dst)))
-        return sorted(pairs)
+        return link_pairs(self.layout, self.n)
+
+    def stream_census(self) -> Dict[str, int]:
+        """The HIP streams this rank's engine runs work on, and the RCCL communicators
+        (each with a stream of its own) it is part of: :func:`stream_census` of this
+        stage's options, links and (once planned) relay routes."""
+        from torchgpipe_amd.parallel.p2p import StripePlan
+        plan = self._stripe_plans.get(self._sig)
+        me = self.ranks[self.rank]
+        jobs = len(plan.jobs) if isinstance(plan, StripePlan) else 0
+        relay_links = sum(1 for k in self.p2p.relay_links if me in k) \
+            if hasattr(self.p2p, 'relay_links') else 0
+        cells = [getattr(m, 'streams', 0) for m in self.partition.modules()]
+        return stream_census(self.rank, link_pairs(self.layout, self.n),
+                             forward_lanes=self.overlap_forward and not self._stateful,
+                             recompute_lanes=self.overlap_recompute,
+                             cell_streams=max([c for c in cells if isinstance(c, int)] + [0]),
+                             graph_cells=self.graph_cells, relay_routes=jobs,
+                             relay_links=relay_links)
 
     def connect(self) -> None:
         """Open every link this stage uses, in one global order.
@@ -827,20 +896,18 @@ class PipelineStage:
         """Back-propagate every micro-batch (reverse order) and ship input gradients.
 
         The last stage passes one scalar loss per micro-batch; the others pass
-        ``None``.  With ``wgrad_stream`` the fused ops' weight-gradient GEMMs run on a side
-        stream (``ops.convbn.wgrad_stream_scope``), joined before this returns.
+        ``None``.
         """
         # split weight-gradient reductions of the fused ops are deferred to one flush after
         # the last micro-batch (ops/gradacc.py deferred_wgrad), issued once every stream
         # that wrote a slab has been joined to the current one
         from torchgpipe_amd.ops.gradacc import deferred_wgrad
         with deferred_wgrad(self.device, self.device.type == 'cuda'):
-            if self.wgrad_stream and self.device.type == 'cuda':
-                from torchgpipe_amd.ops.convbn import wgrad_stream_scope
-                with wgrad_stream_scope(self.device):
-                    self._backward(losses)
-            else:
-                self._backward(losses)
+            self._backward(losses)
+            if self.device.type == 'cuda':
+                # a caller's ops.convbn.wgrad_stream_scope: its side stream wrote slabs
+                from torchgpipe_amd.ops.convbn import join_wgrad_stream
+                join_wgrad_stream(self.device)
 
     def _backward(self, losses: Optional[Sequence[Tensor]] = None) -> None:
         if self._recompute_lanes() is not None or self._fwd_lanes is not None:
@@ -982,10 +1049,23 @@ class PipelineStage:
                         seg_grads[k] = t.grad
                 elif direct:
                     # the loss's gradient w.r.t. the cell's outputs (a backward through the
-                    # loss alone), then on into the recomputed graph
+                    # loss alone), then on into the recomputed graph; leaves the loss reaches
+                    # around the outputs (a learnable loss head) get theirs in the same pass
                     ks = [k for k, t in enumerate(act_out) if t.requires_grad]
-                    gouts = torch.autograd.grad([losses[i]], [act_out[k] for k in ks],
-                                                [torch.ones_like(losses[i])], allow_unused=True)
+                    outs = [act_out[k] for k in ks]
+                    extra = _loss_leaves(losses[i], outs)
+                    grads_all = torch.autograd.grad([losses[i]], outs + extra,
+                                                    [torch.ones_like(losses[i])],
+                                                    allow_unused=True)
+                    gouts = grads_all[:len(outs)]
+                    with torch.no_grad():
+                        for leaf, g in zip(extra, grads_all[len(outs):]):
+                            if g is None:
+                                continue
+                            if leaf.grad is None:
+                                leaf.grad = g.detach().clone()
+                            else:
+                                leaf.grad += g
                     for k, g in zip(ks, gouts):
                         if g is not None and rec_out[k].requires_grad:
                             tensors.append(rec_out[k])
@@ -1119,7 +1199,8 @@ class PipelineStage:
             # two-stream cells are verified inside captures (profiles/r3/capture_crash.md)
             return None
         if self._lanes is None:
-            self._lanes = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
+            self._lanes = [named_stream(self.device, 'recompute-lane0'),
+                           named_stream(self.device, 'recompute-lane1')]
         return self._lanes
 
     def _forward_lanes(self) -> Optional[List[torch.cuda.Stream]]:
@@ -1137,7 +1218,8 @@ class PipelineStage:
         if self.device.type != 'cuda' or torch.cuda.is_current_stream_capturing():
             return None
         if self._fwd_lanes is None:
-            self._fwd_lanes = [torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)]
+            self._fwd_lanes = [named_stream(self.device, 'forward-lane0'),
+                               named_stream(self.device, 'forward-lane1')]
         return self._fwd_lanes
 
     def _recompute_on_lane(self, cell: _Cell, lane: torch.cuda.Stream,

@@ -7,15 +7,20 @@ its first boundaries carry more bytes per micro-batch than one link moves in a f
 cell (U-Net(5,64) p8: 226 MB of skips from stage 1 to stage 6 per micro-batch, AmoebaNet
 n8m32: 321 MB from stage 0 to 1; ``profiles/r5/speedup_prediction.md``).  Striping sends
 chunk 0 of such a message over the direct link and chunk k over ``src -> relay_k ->
-dst``, where both links of the detour carry no pipeline traffic, so a route gets up to
-``1 + max_relays`` links' bandwidth.
+dst``, where both link directions of the detour carry no forward pipeline traffic, so a
+route gets up to ``1 + max_relays`` links' bandwidth.  xGMI links are full duplex, and a
+GPipe step's forward transfers (upward in rank order) and gradient transfers (downward)
+happen in two phases that never overlap: a detour may run against the direction of a busy
+pipeline link (U-Net p4 has no fully idle detour; ``tests/test_stripes.py``).
 
 Plan.  Every rank records the messages it sends in one training step (destination, kind,
 bytes, in order); at the start of the next step of the same signature the ranks exchange
 those lists on the control group and compute the same plan: forward routes (src, dst)
 (activations and skips; gradients only the other way) with a message of at least
-``min_bytes``, largest first, each taking relays whose two links are idle and not yet
-used by another route; the route's gradients (``dst -> src``) take the same relays back.
+``min_bytes``, largest first, each taking relays whose two link directions carry no
+forward message and whose GPU pairs no other route's detour uses yet; the route's
+gradients (``dst -> src``) take the same relays back, over the mirrored directions, which
+the backward phase leaves free for the same reason.
 Every message of at least ``min_bytes`` on a striped route travels in pieces (both ends
 know its size from the shape metadata); smaller ones stay on the direct link.  A relay
 link therefore carries one route, forward pieces then gradient pieces, exactly in the
@@ -34,6 +39,9 @@ from typing import Dict, Hashable, List, NamedTuple, Optional, Sequence, Tuple
 __all__ = ['Send', 'RelayJob', 'pieces', 'message_kind', 'plan']
 
 STRIPED_KINDS = ('act', 'skip')
+# a detour may share a link direction with forward traffic of at most this fraction of
+# the striped message (see plan)
+SHARE_RATIO = 8
 GRAD_KINDS = ('gact', 'gskip')
 
 
@@ -105,7 +113,18 @@ def plan(sends: Dict[int, Sequence[Send]], ranks: Sequence[int], min_bytes: int,
     for src in sorted(sends):
         for s in sends[src]:
             routes.setdefault((src, s.dst), []).append(s)
-    busy = {frozenset(r) for r in routes}
+    # Forward-phase directed links: every forward message travels upward-ordered routes
+    # (activations j -> j+1, skips stash -> pop) and its gradient the reverse direction in
+    # the backward phase, which starts only after the last stage's last forward -- so the
+    # two phases never overlap in time, and a detour link direction is free when no forward
+    # route uses it (the mirrored gradient detour is then free in the backward phase).
+    # A GPU pair carries at most one route's detour: its relay communicator orders that
+    # route's forward then backward pieces, and a second route on it would queue behind.
+    # A direction that carries a small forward route (at most 1/SHARE_RATIO of the striped
+    # message: U-Net p4's 38 MB activation 2 -> 3 beside its 302 MB skip 0 -> 3, whose
+    # destination has no other way in) still takes a detour: the link has the room.
+    fwd_load = {r: max(m.nbytes for m in msgs) for r, msgs in routes.items()
+                if not {m.kind for m in msgs} <= set(GRAD_KINDS)}
     candidates = []
     for (src, dst), msgs in routes.items():
         if not {m.kind for m in msgs} <= set(STRIPED_KINDS):
@@ -117,7 +136,7 @@ def plan(sends: Dict[int, Sequence[Send]], ranks: Sequence[int], min_bytes: int,
         if size < min_bytes:
             continue
         candidates.append((-size, src, dst))
-    used = set(busy)
+    relay_pairs: set = set()
     # relays one at a time, each to the route whose direct link then still carries the
     # most bytes (size * w0 / (w0 + R)): a large route does not take every free detour
     # while another one of nearly its size gets none
@@ -132,13 +151,16 @@ def plan(sends: Dict[int, Sequence[Send]], ranks: Sequence[int], min_bytes: int,
         # relays nearest the route's midpoint first (any order works; this one is fixed)
         order = sorted((r for r in ranks if r not in (src, dst)),
                        key=lambda r: (abs(2 * r - src - dst), r))
-        pick = next((r for r in order if frozenset((src, r)) not in used
-                     and frozenset((r, dst)) not in used), None)
+        room = size_of[(src, dst)] / SHARE_RATIO
+        pick = next((r for r in order if fwd_load.get((src, r), 0) <= room
+                     and fwd_load.get((r, dst), 0) <= room
+                     and frozenset((src, r)) not in relay_pairs
+                     and frozenset((r, dst)) not in relay_pairs), None)
         if pick is None:
             open_routes.discard((src, dst))
             continue
-        used.add(frozenset((src, pick)))
-        used.add(frozenset((pick, dst)))
+        relay_pairs.add(frozenset((src, pick)))
+        relay_pairs.add(frozenset((pick, dst)))
         relays.append(pick)
         if len(relays) >= max_relays:
             open_routes.discard((src, dst))

@@ -154,6 +154,29 @@ class StreamPool:
         return [[self.get(d, i) for i in range(chunks)] for d in devices]
 
 
+_NAMED: Dict[Tuple[torch.device, str], torch.cuda.Stream] = {}
+_NAMED_LOCK = threading.Lock()
+
+
+def named_stream(device: torch.device, name: str) -> torch.cuda.Stream:
+    """The process's stream ``name`` on ``device`` (created once, then reused).
+
+    The engine's side streams -- a stage's forward / recompute lanes, relay routes,
+    capture streams -- are named rather than created per stage object, so a process that
+    builds many stages (``bench.py`` times several in a row) keeps a fixed set of streams,
+    which is what the hardware-queue count of a multi-rank run is sized for
+    (``parallel/stage.py`` ``stream_census``): ``torch.cuda.Stream()`` hands out a small
+    pool round-robin, and ever new lanes would come to share pool streams, and with them
+    hardware queues, with the RCCL communicators' streams.
+    """
+    key = (normalize_device(device), name)
+    with _NAMED_LOCK:
+        stream = _NAMED.get(key)
+        if stream is None:
+            stream = _NAMED[key] = torch.cuda.Stream(key[0])
+    return stream
+
+
 def normalize_device(device: torch.device) -> torch.device:
     """cuda → cuda:<current>, cpu:N → cpu.  Used to dedupe worker threads."""
     if device.type == 'cuda' and device.index is None:
