@@ -455,8 +455,10 @@ class Bench:
         37-67``): ``model(x)``, the loss on the gathered output, ``loss.backward()``, SGD."""
         from torchgpipe_amd import GPipe
         batch, chunks = exp['batch'], exp['chunks']
+        # the headline's forward lanes where the headline has them (--overlap-forward)
+        lanes = choice(self.args.overlap_forward, self.gpu)
         model = GPipe(self.build('unet'), balance=balance, devices=[self.device] * len(balance),
-                      chunks=chunks, checkpoint=checkpoint)
+                      chunks=chunks, checkpoint=checkpoint, overlap_forward=lanes)
         optimizer = torch.optim.SGD(model.parameters(), lr=0.1)
         x, target, loss_fn, _ = self.data('unet', batch, True, True)
 
@@ -472,7 +474,10 @@ class Bench:
         finally:
             self.world = world
         res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
-                   steps=steps)
+                   steps=steps, overlap_forward=lanes)
+        model._workers.close()  # (its device thread, before the next section's stage)
+        from torchgpipe_amd.ops.conv import clear_winograd_caches
+        clear_winograd_caches(model)
         del model, optimizer, x, target, step
         self.release()
         return res
@@ -696,7 +701,8 @@ def main() -> None:
         # the reference's own API on its own benchmark path: single-process GPipe
         gr = b.gpipe_api(exp, balance, checkpoint, sec_steps)
         g = summary(gr, None if args.tiny else exp.get('ref'))
-        g['experiment'] = f"{exp['name']} through GPipe(balance={balance}, chunks={chunks})"
+        g['experiment'] = (f"{exp['name']} through GPipe(balance={balance}, chunks={chunks}, "
+                           f"overlap_forward={gr['overlap_forward']})")
         g['vs_pipeline_stage'] = round(g['value'] / samples_per_s, 3)
         record['gpipe'] = g
         lap('gpipe')

@@ -32,6 +32,7 @@ from torchgpipe_amd.checkpoint import Checkpointing  # noqa: E402
 from torchgpipe_amd.microbatch import Batch  # noqa: E402
 from torchgpipe_amd.models import amoebanetd, unet  # noqa: E402
 from torchgpipe_amd.ops import conv as wino  # noqa: E402
+from torchgpipe_amd.ops import gradacc  # noqa: E402
 from torchgpipe_amd.skip.tracker import SkipTracker, use_skip_tracker  # noqa: E402
 from torchgpipe_amd.utils.meta import materialize  # noqa: E402
 
@@ -124,6 +125,10 @@ def measure_stage(kind, layers, lo, hi, batch_size, chunks, shape, checkpoint, d
             else:
                 chk, out = None, list(fn(tuple(acts)))
             cells.append((chk, out))
+        # as PipelineStage.backward: split weight gradients deferred into per-parameter
+        # slabs, flushed once after the last micro-batch (ops/gradacc.py)
+        scope = gradacc.deferred_wgrad(device)
+        scope.__enter__()
         for k in reversed(range(len(cells))):
             chk, out = cells[k]
             if chk is not None:
@@ -142,18 +147,39 @@ def measure_stage(kind, layers, lo, hi, batch_size, chunks, shape, checkpoint, d
                 loss.backward()
             else:
                 torch.autograd.backward(ys, [torch.ones_like(y) for y in ys])
+        scope.__exit__(None, None, None)
         del cells
         opt.step()
+        if step == 1:  # the model state at its largest: parameters, gradients, optimizer
+            grad_bytes = sum(q.grad.numel() * q.grad.element_size() for q in part.parameters()
+                             if q.grad is not None)
+            opt_bytes = sum(t.numel() * t.element_size() for st in opt.state.values()
+                            for t in st.values() if torch.is_tensor(t) and t.is_cuda)
+            slab_bytes = 0
+            for q in part.parameters():
+                entry = getattr(q, '_tgpipe_wgrad_slab', None)  # [slab, step]
+                if entry and torch.is_tensor(entry[0]):
+                    slab_bytes += entry[0].numel() * entry[0].element_size()
         opt.zero_grad(set_to_none=True)
     torch.cuda.synchronize(device)
     peak = torch.cuda.max_memory_reserved(device)
+    peak_alloc = torch.cuda.max_memory_allocated(device)
     cached = wino.cache_bytes()
+    param_bytes = sum(q.numel() * q.element_size() for q in part.parameters())
+    # what the peak is made of: the reference reports model memory (parameters + gradients +
+    # optimizer state) and peak activation memory (benchmarks/amoebanetd-memory/README.md)
+    parts = {'param_gib': param_bytes, 'grad_gib': grad_bytes, 'optimizer_state_gib': opt_bytes,
+             'transform_cache_gib': cached, 'wgrad_slab_gib': slab_bytes,
+             'activations_and_workspace_gib': max(0, peak_alloc - param_bytes - grad_bytes
+                                                  - opt_bytes - cached - slab_bytes),
+             'allocator_reserve_gib': max(0, peak - peak_alloc)}
+    parts = {k: round(v / 2 ** 30, 3) for k, v in parts.items()}
     del opt
     wino.clear_winograd_caches(part)
     part.to_empty(device='meta')  # release this stage before measuring the next one
     del part
     torch.cuda.empty_cache()
-    return params, peak, cache_budget, cached
+    return params, peak, cache_budget, cached, parts
 
 
 def main() -> None:
@@ -201,13 +227,13 @@ def main() -> None:
     rows = []
     t0 = time.time()
     for k in stages:
-        params, peak, budget, cached = measure_stage(args.model, layers, bounds[k], bounds[k + 1],
-                                                     batch, chunks, shape, args.checkpoint,
-                                                     device)
+        params, peak, budget, cached, parts = measure_stage(
+            args.model, layers, bounds[k], bounds[k + 1], batch, chunks, shape,
+            args.checkpoint, device)
         row = {'stage': k, 'layers': [bounds[k], bounds[k + 1]], 'params': params,
                'peak_reserved_gib': round(peak / 2 ** 30, 2),
                'transform_cache_budget_gib': round(budget / 2 ** 30, 2),
-               'transform_cache_gib': round(cached / 2 ** 30, 2)}
+               'transform_cache_gib': round(cached / 2 ** 30, 2), 'breakdown': parts}
         rows.append(row)
         print(json.dumps(row), f'({time.time() - t0:.0f}s)', flush=True)
     summary = {'model': args.model, 'depth': depth, 'channels': channels, 'balance': balance,
@@ -215,6 +241,8 @@ def main() -> None:
                'total_params_billion': round(total_params / 1e9, 3),
                'sum_peak_reserved_gib': round(sum(r['peak_reserved_gib'] for r in rows), 2),
                'max_stage_peak_gib': max(r['peak_reserved_gib'] for r in rows),
+               'sum_breakdown_gib': {key: round(sum(r['breakdown'][key] for r in rows), 2)
+                                     for key in rows[0]['breakdown']},
                'device': torch.cuda.get_device_name(device),
                'device_total_gib': round(torch.cuda.get_device_properties(device).total_memory
                                          / 2 ** 30, 1),

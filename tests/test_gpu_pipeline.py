@@ -55,6 +55,44 @@ def test_gpipe_training_gradients_match_reference_with_dropout(checkpoint):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.filterwarnings('ignore:The AccumulateGrad node')
+@pytest.mark.parametrize('balance,devices', [(None, [0]), ('half', [0, 0])])
+def test_gpipe_forward_lanes_train_like_one_stream(balance, devices):
+    """``GPipe(overlap_forward=True)``: the forward micro-batches of the (stateless) U-Net
+    partitions alternate between two lanes; losses and gradients over three SGD steps match
+    the one-stream schedule (same Philox dropout masks: the tape is consumed in the same
+    host order)."""
+    results = []
+    for lanes in (False, True):
+        model = small_unet()
+        n = len(model)
+        bal = [n] if balance is None else [n // 2, n - n // 2]
+        gpipe = GPipe(model, bal, devices=devices, chunks=4, checkpoint='except_last',
+                      overlap_forward=lanes)
+        opt = torch.optim.SGD(gpipe.parameters(), lr=0.05)
+        gen = torch.Generator(device='cuda').manual_seed(7)
+        torch.manual_seed(123)
+        torch.cuda.manual_seed(123)
+        losses = []
+        for _ in range(3):
+            x = torch.rand(8, 3, 32, 32, device='cuda', generator=gen)
+            out = gpipe(x)
+            loss = F.binary_cross_entropy_with_logits(out, torch.ones_like(out))
+            loss.backward()
+            losses.append(loss.detach())
+            grads = [p.grad.clone() for p in gpipe.parameters()]
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        assert (gpipe._lanes is not None) == lanes
+        results.append((losses, grads))
+    (la, ga), (lb, gb) = results
+    for a, b in zip(la, lb):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+    for a, b in zip(ga, gb):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
+
+
 def test_fused_unet_matches_unfused_training_without_dropout():
     # Both fp32 models are judged against an fp64 copy of the plain model: the fused one
     # runs Winograd F(4x4,3x3) / F(2x2,3x3) whose fp32 rounding (~1e-5 relative per conv)

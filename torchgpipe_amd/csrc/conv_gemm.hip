@@ -66,7 +66,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kBK = 32;
-constexpr int kConvGemmCfgs = 10;  // tile configurations (Cfg<0..9>; 7..9 split-bf16)
+constexpr int kConvGemmCfgs = 11;  // tile configurations (Cfg<0..10>; 7..10 split-bf16)
 constexpr int kFirstEmuCfg = 7;
 // mfma_stage: all of a stage's LDS fragment reads ahead of its MFMAs (see there)
 constexpr bool kMfmaReadsFirst = true;
@@ -157,9 +157,17 @@ struct PhaseSet {
 // CFG 7 / 8 / 9: the tiles of CFG 0 / 2 / 1 on the bf16 matrix pipes (EMU, see
 // "split-bf16 products" below): 64 x 64 (3 x 48 KiB per CU), 128 x 128 / 4 waves and
 // 128 x 128 / 8 waves (96 KiB).
+// CFG 10: CFG 9 with ONE operand buffer (48 KiB; the epilogue's 68 KiB C tile sets the
+// footprint): two workgroups per CU, four waves per SIMD.  CFG 9's double buffer holds one
+// workgroup per CU, and its waves sat in waits for 35-47 % of their cycles (PMC,
+// profiles/KERNELS.md "Pre-split weights"): here the stage's loads still go to registers
+// during its MFMAs, the store into the one buffer waits for a barrier behind the last
+// reader, and the other workgroup's waves fill that barrier and the waits.  Fragments are
+// read per 16-deep step (a 128-register budget) rather than a whole stage ahead.
 template <int CFG>
 struct Cfg {
   static constexpr bool EMU = CFG >= kFirstEmuCfg;
+  static constexpr bool SINGLE = CFG == 10;  // one operand buffer (see above)
   static constexpr int TILE = !EMU ? CFG % 3 : (CFG == 7 ? 0 : (CFG == 8 ? 2 : 1));
   static constexpr int SUB = EMU || CFG < 3 ? 1 : (CFG == 3 ? 4 : 2);  // (CFG 6: 2 x 80 KiB)
   static constexpr int WVM = 2;
@@ -170,8 +178,8 @@ struct Cfg {
   // waves per SIMD when the LDS footprint's workgroups per CU are resident (4 x 40 KiB /
   // 2 x 72 KiB / 1 x 147-160 KiB): the register budget __launch_bounds__ holds them to
   static constexpr int kWavesPerSimd =
-      CFG == 0 || CFG == 1 ? 4
-      : CFG == 7           ? 3
+      CFG == 0 || CFG == 1 || CFG == 10 ? 4
+      : CFG == 7                        ? 3
       : (CFG == 2 || CFG == 4 || CFG == 6 || CFG == 9 ? 2 : 1);
   static constexpr int BM = WVM * 32 * TM;
   static constexpr int BN = WVN * 32 * TN;
@@ -185,7 +193,7 @@ struct Cfg {
   // register) land 32 banks apart
   static constexpr int kCStride = BN + 8;
   static constexpr int kOpFloats(bool k_major) {
-    return 2 * SUB * (kAImg + (k_major || EMU ? kBImgK : kBImgN));
+    return (SINGLE ? 1 : 2) * SUB * (kAImg + (k_major || EMU ? kBImgK : kBImgN));
   }
   // operand images (double-buffered), reused by the epilogue's C tile (forward /
   // bwd-data); 128 x 128: 72 KiB -> two workgroups per CU
@@ -311,6 +319,37 @@ __device__ __forceinline__ void mfma_stage_emu(floatx16 (&acc)[Cfg<CFG>::TM][Cfg
   const int h = lane >> 5, l32 = lane & 31;
   const __bf16* ab = reinterpret_cast<const __bf16*>(aimg);
   const __bf16* bb = reinterpret_cast<const __bf16*>(bimg);
+  constexpr int kPairs[6][2] = {{2, 0}, {0, 2}, {1, 1}, {1, 0}, {0, 1}, {0, 0}};
+  if constexpr (C::SINGLE) {
+    // per 16-deep step: its fragments, then its MFMAs (the other workgroup's waves cover
+    // the read latency; a whole stage of fragments would not fit 128 registers)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      bf16x8 a[3][WM], b[3][WN];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+          a[p][i] = *reinterpret_cast<const bf16x8*>(
+              ab + p * kBK * C::BM + emu_off<C::BM>(2 * s + h, wm * 32 * WM + i * 32 + l32));
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          b[p][j] = *reinterpret_cast<const bf16x8*>(
+              bb + p * kBK * C::BN + emu_off<C::BN>(2 * s + h, wn * 32 * WN + j * 32 + l32));
+      }
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                a[kPairs[t][0]][i], b[kPairs[t][1]][j], acc[i][j], 0, 0, 0);
+        if (s == 0 && t < 4) between(t);
+      }
+    }
+    return;
+  }
   bf16x8 a[S][3][WM], b[S][3][WN];
 #pragma unroll
   for (int s = 0; s < S; ++s)
@@ -326,7 +365,6 @@ __device__ __forceinline__ void mfma_stage_emu(floatx16 (&acc)[Cfg<CFG>::TM][Cfg
             bb + p * kBK * C::BN + emu_off<C::BN>(2 * s + h, wn * 32 * WN + j * 32 + l32));
     }
   __builtin_amdgcn_sched_barrier(0);
-  constexpr int kPairs[6][2] = {{2, 0}, {0, 2}, {1, 1}, {1, 0}, {0, 1}, {0, 0}};
 #pragma unroll
   for (int s = 0; s < S; ++s) {
 #pragma unroll
@@ -509,8 +547,11 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
   constexpr int SUB = C::SUB;
   __shared__ __attribute__((aligned(16))) float lds[C::kLdsFloats(MODE)];
   // buffer b, sub-stage u
-  auto aimg = [&](int b, int u) { return lds + (b * SUB + u) * C::kAImg; };
-  auto bimg = [&](int b, int u) { return lds + 2 * SUB * C::kAImg + (b * SUB + u) * kBImg; };
+  constexpr int kBufs = C::SINGLE ? 1 : 2;
+  auto aimg = [&](int b, int u) { return lds + ((C::SINGLE ? 0 : b) * SUB + u) * C::kAImg; };
+  auto bimg = [&](int b, int u) {
+    return lds + kBufs * SUB * C::kAImg + ((C::SINGLE ? 0 : b) * SUB + u) * kBImg;
+  };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % C::WVM, wn = wave / C::WVM;
@@ -918,7 +959,12 @@ __global__ __launch_bounds__(Cfg<CFG>::kThreads, Cfg<CFG>::kWavesPerSimd) void c
                                          }
                                      }
                                    });
-      store_stage(buf ^ 1);
+      if constexpr (C::SINGLE) {
+        __syncthreads();  // every wave is done reading the one buffer
+        store_stage(0);
+      } else {
+        store_stage(buf ^ 1);
+      }
       __syncthreads();
     }
 #pragma unroll
@@ -1442,8 +1488,16 @@ void with_cfg(int cfg, F&& f) {
     case 7: f(std::integral_constant<int, 7>{}); break;
     case 8: f(std::integral_constant<int, 8>{}); break;
     case 9: f(std::integral_constant<int, 9>{}); break;
+    case 10: f(std::integral_constant<int, 10>{}); break;
     default: f(std::integral_constant<int, 0>{}); break;
   }
+}
+
+// TGPIPE_CG_SINGLE=1: plans naming CFG 9 (the double-buffered 8-wave split-bf16 tile) run
+// CFG 10, its single-buffered twin at two workgroups per CU (same tile, same products).
+int run_cfg(int cfg) {
+  static const bool single = env_int("TGPIPE_CG_SINGLE", 0) != 0;
+  return cfg == 9 && single ? 10 : cfg;
 }
 
 // TGPIPE_CG_EMU=0: the split-bf16 configurations are never candidates (exact f32 MFMA only;
@@ -1552,9 +1606,10 @@ ConvGemmPlan conv_gemm_plan(int mode, const ConvGemmGeo& cg) {
     }
   }
   if (plan.splits < 1 || g.scatter) plan.splits = 1;
-  // The split-bf16 tiles of the same shapes (7 / 9 for 0 / 1) won 628 of the 709 measured
-  // plans (tuned/conv_gemm_mi355x.txt): shapes missing from the table take them too.
-  if (emu_enabled()) plan.cfg = plan.cfg == 1 ? 9 : 7;
+  // The split-bf16 tiles of the same shapes won 628 of the 709 measured plans
+  // (tuned/conv_gemm_mi355x.txt): shapes missing from the table take them too -- 7 for 0,
+  // and for 1 the single-buffered 10 (two workgroups per CU; profiles/KERNELS.md "Round 6").
+  if (emu_enabled()) plan.cfg = plan.cfg == 1 ? 10 : 7;
   // the launch rounds each split to whole stages: report the number it really runs
   int k_chunk = (K + plan.splits - 1) / plan.splits;
   k_chunk = (k_chunk + kBK - 1) / kBK * kBK;
@@ -1644,7 +1699,7 @@ void launch_conv_gemm(int mode, const float* a, const float* b, const float* x_m
   using D = std::integral_constant<int, kBwdData>;
   using W = std::integral_constant<int, kWgrad>;
   auto by_cfg = [&](auto mode_c, float* p1, float* p2, const float* mask) {
-    with_cfg(plan.cfg, [&](auto cfg_c) { go(mode_c, cfg_c, p1, p2, mask); });
+    with_cfg(run_cfg(plan.cfg), [&](auto cfg_c) { go(mode_c, cfg_c, p1, p2, mask); });
   };
   if (mode == kFwd)
     by_cfg(F{}, pm, pm2, x_mask);
@@ -1687,7 +1742,7 @@ void launch_conv_gemm_partials(const float* a, const float* b, float* ws, const 
   g.co_total = g.co;  // (each split's slice holds this convolution's channels only)
   g.co_off = 0;
   const int64_t stride = static_cast<int64_t>(M) * N;
-  with_cfg(plan.cfg, [&](auto cfg_c) {
+  with_cfg(run_cfg(plan.cfg), [&](auto cfg_c) {
     launch_cfg<kFwd, decltype(cfg_c)::value>(a, b, nullptr, ws, nullptr, nullptr, g, M, N, K,
                                              plan.splits, stride, false, a_bytes, b_bytes,
                                              stream, PhaseSet{}, cg.a_split);
@@ -1708,7 +1763,7 @@ void launch_conv_gemm_wgrad_slab(const float* a, const float* b, float* slab,
                                                plan.splits, stride, accumulate, a_bytes, b_bytes,
                                                stream);
   };
-  with_cfg(plan.cfg, go);
+  with_cfg(run_cfg(plan.cfg), go);
 }
 
 void launch_conv_gemm_phases(const float* a, const int64_t* a_off, const float* b,
@@ -1745,7 +1800,7 @@ void launch_conv_gemm_phases(const float* a, const int64_t* a_off, const float* 
     launch_cfg<kBwdData, decltype(cfg_c)::value>(a, b, x_mask, out, nullptr, nullptr, g, M, N, K,
                                                  1, 0, accumulate, a_bytes, b_bytes, stream, ps);
   };
-  with_cfg(plan.cfg, go);
+  with_cfg(run_cfg(plan.cfg), go);
 }
 
 void launch_slab_flush(const SlabFlushEntry* entries, int count, hipStream_t stream) {

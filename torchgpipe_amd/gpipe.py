@@ -32,7 +32,7 @@ from torchgpipe_amd.ops.fusion import relink
 from torchgpipe_amd.pipeline import Pipeline
 from torchgpipe_amd.skip.layout import inspect_skip_layout
 from torchgpipe_amd.skip.skippable import verify_skippables
-from torchgpipe_amd.stream import AbstractStream, StreamPool
+from torchgpipe_amd.stream import AbstractStream, StreamPool, current_stream, named_stream
 from torchgpipe_amd.utils.meta import is_meta, materialize
 from torchgpipe_amd.worker import WorkerPool
 
@@ -172,6 +172,14 @@ class GPipe(nn.Module):
             forking and restoring the global generators during recomputation
             (``ops.dropout.convert_dropout``; default ``False``: the reference's
             behaviour, bitwise equal to the plain model under the same seed).
+        overlap_forward: compute the forward micro-batches of every partition without
+            running statistics (no BatchNorm buffers; e.g. U-Net) alternately on two
+            streams of its GPU ("lanes", like ``PipelineStage(overlap_forward=True)``), so
+            micro-batch ``i + 1`` can run beside micro-batch ``i`` where its input is ready:
+            on the first partition, and on any partition slower than its upstream.
+            Backward passes keep the reference's order (the ``depend`` edges, with the
+            autograd engine's cross-stream syncs).  Default ``False``: one stream per
+            device, as the reference.
     """
 
     balance: List[int] = []
@@ -182,7 +190,8 @@ class GPipe(nn.Module):
     def __init__(self, module: nn.Sequential, balance: Optional[Iterable[int]] = None, *,
                  devices: Optional[Devices] = None, chunks: int = chunks,
                  checkpoint: str = checkpoint, deferred_batch_norm: bool = False,
-                 copy_streams_per_device: int = 4, philox_dropout: bool = False) -> None:
+                 copy_streams_per_device: int = 4, philox_dropout: bool = False,
+                 overlap_forward: bool = False) -> None:
         super().__init__()
         chunks = int(chunks)
         checkpoint = str(checkpoint)
@@ -221,6 +230,8 @@ class GPipe(nn.Module):
         self._workers = WorkerPool()
         self._skip_layout = inspect_skip_layout(self.partitions)
         self._has_dbn = any(isinstance(m, DeferredBatchNorm) for m in self.modules())
+        self.overlap_forward = overlap_forward
+        self._lanes: Optional[List[Optional[List[AbstractStream]]]] = None
 
     # -- Sequential-like interface ------------------------------------------------------------
 
@@ -260,6 +271,21 @@ class GPipe(nn.Module):
             self._copy_streams = self._stream_pool.grid(self.devices, self.chunks)
         return self._copy_streams
 
+    def _forward_lanes(self) -> Optional[List[Optional[List[AbstractStream]]]]:
+        """Two named streams per stateless GPU partition (``overlap_forward``)."""
+        if not self.overlap_forward or torch.cuda.is_available() and \
+                torch.cuda.is_current_stream_capturing():
+            return None
+        if self._lanes is None:
+            lanes: List[Optional[List[AbstractStream]]] = []
+            for j, (part, dev) in enumerate(zip(self.partitions, self.devices)):
+                stateful = any(isinstance(m, nn.modules.batchnorm._BatchNorm)
+                               and m.track_running_stats for m in part.modules())
+                lanes.append(None if dev.type != 'cuda' or stateful else
+                             [named_stream(dev, f'gpipe-lane{j}-{k}') for k in (0, 1)])
+            self._lanes = lanes
+        return self._lanes
+
     def checkpoint_stop(self) -> int:
         if not self.training:
             return 0
@@ -284,11 +310,18 @@ class GPipe(nn.Module):
         # while later micro-batches still compute (no torch.cat after the pipeline)
         gatherer = microbatch.Gatherer([b[0].shape[0] if b[0].dim() else 1 for b in batches],
                                        copy_streams[-1])
+        lanes = self._forward_lanes()
         pipeline = Pipeline(batches, list(self.partitions), self.devices, copy_streams,
                             self._skip_layout, self.checkpoint_stop(),
                             queues=self._workers.queues(self.devices),
-                            on_output=gatherer.put)
+                            on_output=gatherer.put, lanes=lanes)
         pipeline.run()
+        if lanes is not None:
+            # (a fallback gather reads the last partition's outputs on the current stream)
+            for dev, lane in zip(self.devices, lanes):
+                if lane is not None:
+                    for stream in lane:
+                        current_stream(dev).wait_stream(stream)  # type: ignore[union-attr]
         return gatherer.result(batches)
 
     def __getstate__(self) -> Any:
@@ -296,4 +329,5 @@ class GPipe(nn.Module):
         state['_workers'] = WorkerPool()
         state['_stream_pool'] = StreamPool(self._stream_pool.size)
         state['_copy_streams'] = []
+        state['_lanes'] = None
         return state

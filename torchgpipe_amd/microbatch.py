@@ -177,7 +177,9 @@ class Gatherer:
         self.ok = True
         self.used: List[object] = []
 
-    def put(self, i: int, batch: Batch) -> None:
+    def put(self, i: int, batch: Batch, stream: Optional[object] = None) -> None:
+        """Copy micro-batch ``i``'s outputs into their slice, after ``stream`` (the stream
+        that computed them; default: the device's current stream)."""
         from torchgpipe_amd.stream import current_stream, record_stream, use_stream, wait_stream
         if not self.ok:
             return
@@ -197,7 +199,7 @@ class Gatherer:
                 or t.device != b.device for t, b in zip(tensors, self.buffers)):
             self.ok = False
             return
-        compute = current_stream(tensors[0].device)
+        compute = stream if stream is not None else current_stream(tensors[0].device)
         side = self.streams[i] if self.streams is not None else compute
         wait_stream(side, compute)  # type: ignore[arg-type]
         with use_stream(side):  # type: ignore[arg-type]

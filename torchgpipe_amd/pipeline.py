@@ -20,7 +20,7 @@ each partition micro-batch ``i-1`` back-propagates after micro-batch ``i``,
 and ``Recompute`` sits in front of the gradient ``Wait`` so recomputation
 overlaps the incoming gradient transfer.
 """
-from typing import Callable, Iterable, List, Optional, Tuple, Union
+from typing import Callable, Iterable, List, Optional, Sequence, Tuple, Union
 
 import torch
 from torch import Tensor, nn
@@ -84,7 +84,8 @@ class Pipeline:
                  skip_layout: Optional[SkipLayout] = None,
                  checkpoint_stop: int = 0,
                  queues: Optional[Tuple[List[InQueue], List[OutQueue]]] = None,
-                 on_output: Optional[Callable[[int, Batch], None]] = None,
+                 on_output: Optional[Callable[[int, Batch, AbstractStream], None]] = None,
+                 lanes: Optional[Sequence[Optional[Sequence[AbstractStream]]]] = None,
                  ) -> None:
         self.batches = batches
         self.partitions = partitions
@@ -99,8 +100,13 @@ class Pipeline:
         self.skip_layout = skip_layout
         self.checkpoint_stop = checkpoint_stop
         self._queues = queues
-        # called with (i, batch) as micro-batch i leaves the last partition (K11 gather)
+        # called with (i, batch, stream that computed it) as micro-batch i leaves the last
+        # partition (K11 gather)
         self.on_output = on_output
+        # forward lanes per partition (GPipe(overlap_forward=True)): cell (i, j) computes on
+        # lanes[j][i % 2] instead of device j's current stream, so consecutive micro-batches
+        # of a stateless partition overlap on the GPU wherever their inputs are ready
+        self.lanes = lanes
 
     def run(self) -> None:
         m = len(self.batches)
@@ -145,11 +151,18 @@ class Pipeline:
         n = len(partitions)
         streams = [current_stream(d) for d in devices]
 
+        run = {}
         for i, j in schedule:
             batch = batches[i]
+            lane = self.lanes[j] if self.lanes is not None else None
+            stream = run[(i, j)] = lane[i % 2] if lane else streams[j]
             if j != 0:
-                wait(batch, copy_streams[j][i], streams[j])
-            task = self._make_task(i, j, batch, partitions[j], skip_trackers[i], streams[j])
+                wait(batch, copy_streams[j][i], stream)
+            elif lane:
+                # the mini-batch was made on the device's current stream (and its gradient
+                # goes back there)
+                wait(batch, streams[j], stream)
+            task = self._make_task(i, j, batch, partitions[j], skip_trackers[i], stream)
             in_queues[j].put(task)
 
         exc_info = None
@@ -162,11 +175,11 @@ class Pipeline:
                 continue
             task, batch = payload
             if j != n - 1:
-                wait(batch, streams[j], copy_streams[j][i])
+                wait(batch, run[(i, j)], copy_streams[j][i])
             with use_device(devices[j]):
                 task.finalize(batch)
                 if j == n - 1 and self.on_output is not None:
-                    self.on_output(i, batch)
+                    self.on_output(i, batch, run[(i, j)])
             batches[i] = batch
 
         if exc_info is not None:

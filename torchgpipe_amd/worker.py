@@ -73,8 +73,12 @@ def worker(in_queue: InQueue, out_queue: OutQueue, device: torch.device,
                     batch = task.compute()
             except Exception:
                 out_queue.put((False, sys.exc_info()))
+                task = None
                 continue
             out_queue.put((True, (task, batch)))
+            # a parked persistent thread must not keep the last task (its closure holds the
+            # partition, and through it the module and its caches) alive until the next one
+            task = batch = None
     out_queue.put((False, None))
 
 
