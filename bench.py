@@ -169,10 +169,6 @@ def parse() -> argparse.Namespace:
                    help='tiny models of the same families (CI smoke test of this script only)')
     p.add_argument('--channels-last', action='store_true',
                    help='NHWC activations and weights (MIOpen NHWC kernels; AmoebaNet)')
-    p.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
-                   help='one-GPU runs: capture the whole step (forward, backward, SGD) into a '
-                        'hipGraph after the warm-up and replay it (RNG-free models only: '
-                        'AmoebaNet; parallel/graph.py; auto: off -- captured cells instead)')
     p.add_argument('--cell-streams', choices=['auto', 'on', 'off'], default='auto',
                    help="AmoebaNet: run each cell's independent nodes on several HIP streams "
                         '(TGPIPE_CELL_STREAMS, default 3; auto: on)')
@@ -186,7 +182,7 @@ def parse() -> argparse.Namespace:
     p.add_argument('--graph-cells', choices=['auto', 'on', 'off'], default='auto',
                    help='replay each micro-batch of a stage as captured hipGraphs, transfers '
                         'issued between them (PipelineStage(graph_cells=True), '
-                        'parallel/segments.py; instead of the one-GPU whole-step graph; '
+                        'parallel/segments.py; '
                         'auto: on for one-GPU AmoebaNet)')
     p.add_argument('--stripes', choices=['auto', 'on', 'off'], default='auto',
                    help='multi-path transfers in the headline: messages of at least '
@@ -204,11 +200,6 @@ def parse() -> argparse.Namespace:
 def even_balance(layers: int, parts: int) -> list:
     base, extra = divmod(layers, parts)
     return [base + (1 if i < extra else 0) for i in range(parts)]
-
-
-def _capture_streams() -> int:
-    from torchgpipe_amd.models.amoebanet import CAPTURE_CELL_STREAMS
-    return max(2, CAPTURE_CELL_STREAMS)
 
 
 def choice(value: str, auto: bool) -> bool:
@@ -385,21 +376,7 @@ class Bench:
         x, target, loss_fn, shape = self.data(kind, batch, stage.is_first, stage.is_last)
         signature = signature_of(torch.empty(batch, *shape, device='meta'))
 
-        graph = None
-        # whole-step hipGraph: AmoebaNet (no RNG) on one GPU (two-stream cells included,
-        # launched from a big-stack thread: profiles/r3/capture_crash.md)
-        use_graph = choice(args.graph, self.world == 1 and self.gpu and kind == 'amoebanet'
-                           and not graph_cells)
-        if use_graph:
-            if self.world != 1:
-                raise SystemExit('--graph captures one-rank runs only')
-            from torchgpipe_amd.parallel import StepGraph
-            graph = StepGraph(stage, loss_fn, optimizer, warmup=max(1, args.warmup - 1))
-
         def step() -> None:
-            if graph is not None:
-                graph.step(x, target)  # type: ignore[arg-type]
-                return
             stage.train_step(x, target, loss_fn, signature=signature)
             if optimizer is not None:
                 optimizer.step()
@@ -408,22 +385,16 @@ class Bench:
         if self.gpu:
             torch.cuda.reset_peak_memory_stats(self.device)
         settle = None
-        if graph is not None:
-            settle = lambda: graph.captured  # noqa: E731
-        elif graph_cells:
+        if graph_cells:
             settle = lambda: stage._segments is not None and stage._segments.captured  # noqa: E731
         elif stripes:  # the step that plans the stripes (and opens relay links) is untimed
             settle = lambda: stage.stripes_ready  # noqa: E731
         res: Dict[str, Any] = self.timed(step, steps, args.warmup, tag, settle=settle)
         res.update(batch=batch, chunks=chunks, balance=list(balance), checkpoint=checkpoint,
-                   steps=steps, overlap_recompute=overlap,
-                   # (a captured step keeps at most CAPTURE_CELL_STREAMS per cell)
-                   cell_streams=min(int(cell_streams), _capture_streams())
-                   if graph is not None and cell_streams else int(cell_streams),
-                   overlap_forward=overlap_fwd,
-                   hipgraph=graph is not None, graph_cells=graph_cells,
+                   steps=steps, overlap_recompute=overlap, cell_streams=int(cell_streams),
+                   overlap_forward=overlap_fwd, graph_cells=graph_cells,
                    striped_routes=stage.striped_routes)
-        if probe and graph is None:
+        if probe:
             # one untimed diagnostic step: per-rank receive waits and busy time
             mine = stage.probe_step(step)
             mine['rank'] = self.rank
@@ -444,7 +415,7 @@ class Bench:
                 sort_by='cuda_time_total' if self.gpu else 'cpu_time_total', row_limit=30),
                 file=sys.stderr)
         res['mem'] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30 if self.gpu else 0.0
-        del stage, optimizer, x, target, graph, step, settle
+        del stage, optimizer, x, target, step, settle
         self.release()
         return res
 
@@ -650,7 +621,6 @@ def main() -> None:
             'warmup_s': round(main_run['warm_s'], 1),
             'first_step_s': round(main_run['first_step_s'], 2),
             'timeout_s': args.timeout,
-            'hipgraph': main_run['hipgraph'],
             'cell_streams': main_run['cell_streams'],
             'overlap_recompute': main_run['overlap_recompute'],
             'overlap_forward': main_run['overlap_forward'],
@@ -725,7 +695,6 @@ def main() -> None:
         amoeba = summary(ar, None if args.tiny else aexp['ref'])
         amoeba['experiment'] = aexp['name']
         amoeba['cell_streams'] = ar['cell_streams']
-        amoeba['hipgraph'] = ar['hipgraph']
         amoeba['graph_cells'] = ar['graph_cells']
         amoeba['striped_routes'] = ar['striped_routes']
         record['amoebanet'] = amoeba
@@ -747,7 +716,6 @@ def main() -> None:
         rr = b.pipeline('resnet', rexp, rexp['balance'], rexp['checkpoint'], sec_steps, 'resnet')
         resnet = summary(rr, None if args.tiny else rexp['ref'])
         resnet['experiment'] = rexp['name']
-        resnet['hipgraph'] = rr['hipgraph']
         resnet['graph_cells'] = rr['graph_cells']
         resnet['striped_routes'] = rr['striped_routes']
         record['resnet101'] = resnet

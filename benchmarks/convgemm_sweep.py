@@ -21,7 +21,7 @@ SHAPES = [  # N, Ci, H, Co, kh, kw
 CFG = {0: '64x64/4w', 1: '128x128/8w', 2: '128x128/4w', 3: '64x64/4w/sub4',
        4: '128x128/8w/sub2', 5: '128x128/4w/sub2', 6: '64x64/4w/sub2',
        7: 'emu 64x64/4w', 8: 'emu 128x128/4w', 9: 'emu 128x128/8w',
-       10: 'emu 128x128/8w/single'}
+       10: 'emu 128x128/8w/single', 11: 'emu 64x64/4w/single'}
 # ResNet-101's 1x1 / 3x3 shapes at its micro-batches (--set resnet; N from --micro-batch)
 RESNET_SHAPES = [
     (22, 256, 56, 64, 1, 1), (22, 64, 56, 256, 1, 1), (22, 512, 28, 128, 1, 1),
@@ -54,7 +54,7 @@ def main() -> None:
                    'best_us': cands[0][2], 'best_tflops': round(gflop / cands[0][2] * 1e3, 1),
                    'top': cands[:6]}
             # the double- vs single-buffered 8-wave split-bf16 tile, each at its best split
-            for cfg in (9, 10):
+            for cfg in (7, 9, 10, 11):
                 mine = [c for c in cands if c[0] == CFG[cfg]]
                 if mine:
                     row[f'cfg{cfg}_us'] = mine[0][2]

@@ -41,6 +41,18 @@ CASES = [
 
 
 @pytest.mark.parametrize('relu', [True, False])
+@pytest.mark.parametrize('case', [(6, 64, 14, 64, 3, 1, 1), (4, 256, 7, 256, 3, 1, 1),
+                                  (3, 96, 13, 80, 3, 1, 1)],
+                         ids=['64@14', '256@7', '96to80@13'])
+def test_small_plane_3x3_on_the_implicit_gemm_matches_fp64(case, relu, monkeypatch):
+    """ResNet's small-plane 3x3 Conv-BN(-ReLU) on the fused implicit-GEMM op
+    (TGPIPE_GEMM3X3_MAX_PLANE) instead of Winograd + the native BatchNorm."""
+    from torchgpipe_amd.ops import fusion
+    monkeypatch.setattr(fusion, 'GEMM3X3_MAX_PLANE', 196)
+    test_conv_bn_relu_run_matches_fp64(case, relu)
+
+
+@pytest.mark.parametrize('relu', [True, False])
 @pytest.mark.parametrize('case', CASES, ids=[f'{c[4]}x{c[4]}s{c[5]}_{c[1]}to{c[3]}@{c[2]}'
                                             for c in CASES])
 def test_conv_bn_relu_run_matches_fp64(case, relu):

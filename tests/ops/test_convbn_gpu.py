@@ -69,10 +69,10 @@ def _geo(kh, kw, stride, pad, offset):
     return [kh, kw, stride, stride, ph, pw, offset, offset]
 
 
-@pytest.fixture(params=[-1] + list(range(11)), ids=['tuned'] + [f'cfg{i}' for i in range(11)])
+@pytest.fixture(params=[-1] + list(range(12)), ids=['tuned'] + [f'cfg{i}' for i in range(12)])
 def tile_cfg(request):
     """Every tile configuration of the implicit-GEMM kernel (7-10: split-bf16 products, held
-    to the same fp64 error bounds as the f32 ones; 10 single-buffered), then the tuned
+    to the same fp64 error bounds as the f32 ones; 10 / 11 single-buffered), then the tuned
     plans."""
     ops().conv_gemm_force_cfg(request.param)
     yield request.param
@@ -167,7 +167,7 @@ def _presplit_runs(case, cfg, splits):
 
 
 @pytest.mark.parametrize('splits', [1, 4])
-@pytest.mark.parametrize('cfg', [7, 8, 9, 10])
+@pytest.mark.parametrize('cfg', [7, 8, 9, 10, 11])
 @pytest.mark.parametrize('case', CASES, ids=[f'{c[5]}x{c[6]}s{c[7]}o{c[9]}_{c[0]}x{c[1]}x{c[2]}'
                                             for c in CASES])
 def test_presplit_weights_are_bit_identical(case, cfg, splits):
@@ -324,8 +324,8 @@ def test_fused_relu_conv_bn_matches_fp64_training_step(kind, with_add, channels,
     _check_fused_training_step(kind, with_add, channels)
 
 
-@pytest.fixture(params=[(7, 4), (9, 3), (10, 3), (0, 8)],
-                ids=['cfg7-split4', 'cfg9-split3', 'cfg10-split3', 'cfg0-split8'])
+@pytest.fixture(params=[(7, 4), (9, 3), (10, 3), (11, 4), (0, 8)],
+                ids=['cfg7-split4', 'cfg9-split3', 'cfg10-split3', 'cfg11-split4', 'cfg0-split8'])
 def split_cfg(request):
     """Split-K forward plans (the small-plane ones reduce, normalise and take their
     statistics in one launch: launch_split_bn_small)."""

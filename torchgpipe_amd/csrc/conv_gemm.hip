@@ -66,7 +66,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kBK = 32;
-constexpr int kConvGemmCfgs = 11;  // tile configurations (Cfg<0..10>; 7..10 split-bf16)
+constexpr int kConvGemmCfgs = 12;  // tile configurations (Cfg<0..11>; 7..11 split-bf16)
 constexpr int kFirstEmuCfg = 7;
 // mfma_stage: all of a stage's LDS fragment reads ahead of its MFMAs (see there)
 constexpr bool kMfmaReadsFirst = true;
@@ -164,11 +164,14 @@ struct PhaseSet {
 // during its MFMAs, the store into the one buffer waits for a barrier behind the last
 // reader, and the other workgroup's waves fill that barrier and the waits.  Fragments are
 // read per 16-deep step (a 128-register budget) rather than a whole stage ahead.
+// CFG 11: CFG 7 (64 x 64, 4 waves) single-buffered the same way: 24 KiB of operands, four
+// workgroups per CU at four waves per SIMD (CFG 7: three).
 template <int CFG>
 struct Cfg {
   static constexpr bool EMU = CFG >= kFirstEmuCfg;
-  static constexpr bool SINGLE = CFG == 10;  // one operand buffer (see above)
-  static constexpr int TILE = !EMU ? CFG % 3 : (CFG == 7 ? 0 : (CFG == 8 ? 2 : 1));
+  static constexpr bool SINGLE = CFG == 10 || CFG == 11;  // one operand buffer (see above)
+  static constexpr int TILE =
+      !EMU ? CFG % 3 : (CFG == 7 || CFG == 11 ? 0 : (CFG == 8 ? 2 : 1));
   static constexpr int SUB = EMU || CFG < 3 ? 1 : (CFG == 3 ? 4 : 2);  // (CFG 6: 2 x 80 KiB)
   static constexpr int WVM = 2;
   static constexpr int WVN = TILE == 1 ? 4 : 2;
@@ -178,7 +181,7 @@ struct Cfg {
   // waves per SIMD when the LDS footprint's workgroups per CU are resident (4 x 40 KiB /
   // 2 x 72 KiB / 1 x 147-160 KiB): the register budget __launch_bounds__ holds them to
   static constexpr int kWavesPerSimd =
-      CFG == 0 || CFG == 1 || CFG == 10 ? 4
+      CFG == 0 || CFG == 1 || CFG == 10 || CFG == 11 ? 4
       : CFG == 7                        ? 3
       : (CFG == 2 || CFG == 4 || CFG == 6 || CFG == 9 ? 2 : 1);
   static constexpr int BM = WVM * 32 * TM;
@@ -1474,7 +1477,9 @@ void gemm_dims(int mode, const Geo& g, int& M, int& N, int& K) {
 }
 
 // Block width (rows = columns) of a tile configuration, and the runtime -> template dispatch.
-int cfg_width(int cfg) { return cfg == 0 || cfg == 3 || cfg == 6 || cfg == 7 ? 64 : 128; }
+int cfg_width(int cfg) {
+  return cfg == 0 || cfg == 3 || cfg == 6 || cfg == 7 || cfg == 11 ? 64 : 128;
+}
 
 template <typename F>
 void with_cfg(int cfg, F&& f) {
@@ -1489,6 +1494,7 @@ void with_cfg(int cfg, F&& f) {
     case 8: f(std::integral_constant<int, 8>{}); break;
     case 9: f(std::integral_constant<int, 9>{}); break;
     case 10: f(std::integral_constant<int, 10>{}); break;
+    case 11: f(std::integral_constant<int, 11>{}); break;
     default: f(std::integral_constant<int, 0>{}); break;
   }
 }

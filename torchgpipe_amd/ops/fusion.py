@@ -187,6 +187,23 @@ STRIDED_FUSED = frozenset({
 })
 
 
+# 3x3 stride-1 Conv-BN(-ReLU) on planes of at most this many pixels with at most
+# GEMM3X3_MAX_IMAGES images per micro-batch: the fused implicit-GEMM op (2 launches forward,
+# BatchNorm statistics in the GEMM epilogue) instead of the Winograd kernels + the native
+# BatchNorm pass (4-5 launches: input transform, batched GEMM, output transform, statistics,
+# normalise) -- for the launch-bound ResNet stages at the reference's 22 / 36-image
+# micro-batches.  TGPIPE_GEMM3X3_MAX_PLANE=0 turns it off.
+GEMM3X3_MAX_PLANE = int(os.environ.get('TGPIPE_GEMM3X3_MAX_PLANE', '0'))
+GEMM3X3_MAX_IMAGES = int(os.environ.get('TGPIPE_GEMM3X3_MAX_IMAGES', '48'))
+
+
+def _gemm3x3(conv: nn.Conv2d, x: Tensor) -> bool:
+    return (GEMM3X3_MAX_PLANE > 0 and tuple(conv.kernel_size) == (3, 3)
+            and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
+            and x.dim() == 4 and x.shape[0] <= GEMM3X3_MAX_IMAGES
+            and x.shape[2] * x.shape[3] <= GEMM3X3_MAX_PLANE)
+
+
 def _strided_fused(conv: nn.Conv2d, bn: nn.BatchNorm2d, x: Tensor, relu: bool) -> bool:
     """Whether one strided Conv-BN(-ReLU) runs as the fused native op: the shipped measured
     set (``STRIDED_FUSED``), or with ``TGPIPE_STRIDED_CHOICE=1`` both ways timed on the first
@@ -256,6 +273,9 @@ class ConvBN2d(WinogradConv2d):
                 setattr(out, _DONE_BN, id(bn))
                 return out
             if self.bias is None and _native_bn_ok(bn, input):
+                if wino and _gemm3x3(self, input) and fusable(input, [self], bn):
+                    y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu)
+                    return _mark(y, bn, relu)
                 if wino:
                     z = WinogradConv2d.forward(self, input)
                     return _mark(bn_act(z, bn, relu), bn, relu)
