@@ -8,8 +8,9 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 out=gpurun_out/r6d
 mkdir -p $out
+timeout -k 10 120 python -u scripts/debug/gpipe_lanes_diag.py > $out/lanes_diag.log 2>&1; cat $out/lanes_diag.log | grep -v amdgpu.ids
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-    tests/test_gpu_pipeline.py tests/models/test_resnet_fused_gpu.py \
+    tests/models/test_resnet_fused_gpu.py \
     tests/ops/test_convbn_gpu.py -k "not cfg or cfg11" > $out/tests.log 2>&1 \
   && tail -1 $out/tests.log || { tail -30 $out/tests.log; exit 1; }
 TGPIPE_GEMM3X3_MAX_PLANE=196 timeout -k 10 1100 python -u benchmarks/tune_plans.py \

@@ -144,9 +144,16 @@ class Wait(torch.autograd.Function):
         ctx.prev_stream = prev_stream
         ctx.next_stream = next_stream
         wait_stream(next_stream, prev_stream)
+        # the consumer may be a lane (GPipe(overlap_forward=True)) rather than the stream the
+        # tensors were allocated on: keep their blocks from the allocator until it is done
+        for x in input:
+            record_stream(x, next_stream)
         return tuple(x.detach() for x in input)
 
     @staticmethod
     def backward(ctx, *grad_input: Tensor) -> Tuple[Optional[Tensor], ...]:  # type: ignore[override]
         wait_stream(ctx.prev_stream, ctx.next_stream)
+        for g in grad_input:
+            if g is not None:
+                record_stream(g, ctx.prev_stream)
         return (None, None) + grad_input
