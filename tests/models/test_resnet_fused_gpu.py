@@ -41,18 +41,6 @@ CASES = [
 
 
 @pytest.mark.parametrize('relu', [True, False])
-@pytest.mark.parametrize('case', [(6, 64, 14, 64, 3, 1, 1), (4, 256, 7, 256, 3, 1, 1),
-                                  (3, 96, 13, 80, 3, 1, 1)],
-                         ids=['64@14', '256@7', '96to80@13'])
-def test_small_plane_3x3_on_the_implicit_gemm_matches_fp64(case, relu, monkeypatch):
-    """ResNet's small-plane 3x3 Conv-BN(-ReLU) on the fused implicit-GEMM op
-    (TGPIPE_GEMM3X3_MAX_PLANE) instead of Winograd + the native BatchNorm."""
-    from torchgpipe_amd.ops import fusion
-    monkeypatch.setattr(fusion, 'GEMM3X3_MAX_PLANE', 196)
-    test_conv_bn_relu_run_matches_fp64(case, relu)
-
-
-@pytest.mark.parametrize('relu', [True, False])
 @pytest.mark.parametrize('case', CASES, ids=[f'{c[4]}x{c[4]}s{c[5]}_{c[1]}to{c[3]}@{c[2]}'
                                             for c in CASES])
 def test_conv_bn_relu_run_matches_fp64(case, relu):
@@ -202,3 +190,29 @@ def test_residual_join_runs_conv3_bn3_add_relu_as_one_op(shape):
                                plain32.parameters()):
         assert rel_err(p.grad, q.grad) < max(5e-5, 8 * rel_err(r.grad, q.grad)), name
     assert rel_err(fused.bn3.running_var, plain.bn3.running_var) < 2e-6
+
+
+def test_native_batchnorm_affine_gradients_accumulate_across_micro_batches():
+    """The native BatchNorm(+ReLU) after a Winograd 3x3 (``_BNAct``) adds its gamma / beta
+    gradients into ``.grad`` in the kernel (ops/gradacc.py) -- over several backward
+    passes (micro-batches) the same sums as autograd's accumulation of the plain layers."""
+    torch.manual_seed(0)
+    seq = nn.Sequential(ConvBN2d(32, 32, 3, padding=1, bias=False), BatchNormAct2d(32),
+                        ReLU()).cuda()
+    with torch.no_grad():
+        seq[1].weight.uniform_(0.5, 1.5)
+        seq[1].bias.uniform_(-0.5, 0.5)
+    ref = nn.Sequential(nn.Conv2d(32, 32, 3, padding=1, bias=False), nn.BatchNorm2d(32),
+                        nn.ReLU()).cuda().double()
+    ref.load_state_dict(seq.state_dict(), strict=False)
+    assert relink(seq) == 1
+    for k in range(3):
+        x = torch.randn(4, 32, 14, 14, device='cuda')
+        y = seq(x)
+        assert getattr(y, '_tgpipe_bn_done', None) == id(seq[1])
+        y64 = ref(x.double()) * (y > 0).double()
+        g = torch.randn_like(y)
+        y.backward(g)
+        y64.backward(g.double())
+        for (name, p), q in zip(seq.named_parameters(), ref.parameters()):
+            assert rel_err(p.grad, q.grad) < 2e-5, (k, name)

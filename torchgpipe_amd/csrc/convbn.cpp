@@ -1470,7 +1470,9 @@ std::vector<at::Tensor> bn_train_backward(const at::Tensor& dy_in, const at::Ten
                                           const at::Tensor& mean, const at::Tensor& invstd,
                                           at::Tensor& sums,
                                           const c10::optional<at::Tensor>& gamma,
-                                          const c10::optional<at::Tensor>& beta, bool relu) {
+                                          const c10::optional<at::Tensor>& beta, bool relu,
+                                          const c10::optional<at::Tensor>& accum_gamma,
+                                          const c10::optional<at::Tensor>& accum_beta) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   check_f32(x, "x", x);
@@ -1481,12 +1483,21 @@ std::vector<at::Tensor> bn_train_backward(const at::Tensor& dy_in, const at::Ten
   check_f32(sums, "sums", x);
   TORCH_CHECK(sums.numel() == 2 * c, "sums must be the forward's [2][C] buffer");
   auto dx = at::empty_like(x);
-  auto dgamma = at::empty({c}, x.options());
-  auto dbeta = at::empty({c}, x.options());
+  // gradient-accumulation fusion (ops/gradacc.py): the affine gradients added straight into
+  // the parameters' existing .grad instead of returned for autograd's add
+  const bool acc_g = accum_gamma.has_value() && accum_gamma->defined();
+  const bool acc_b = accum_beta.has_value() && accum_beta->defined();
+  auto dgamma = acc_g ? *accum_gamma : at::empty({c}, x.options());
+  auto dbeta = acc_b ? *accum_beta : at::empty({c}, x.options());
+  if (acc_g) check_f32(dgamma, "accum_gamma", x);
+  if (acc_b) check_f32(dbeta, "accum_beta", x);
+  TORCH_CHECK(dgamma.numel() == c && dbeta.numel() == c && dgamma.is_contiguous() &&
+                  dbeta.is_contiguous(),
+              "the affine gradients are contiguous [C]");
   launch_bn_backward(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), opt_ptr(gamma, "gamma", x, c),
                      sums.data_ptr<float>(), dx.data_ptr<float>(), dgamma.data_ptr<float>(),
-                     dbeta.data_ptr<float>(), false, false, n, c, s, 0, cur_stream(x), relu,
+                     dbeta.data_ptr<float>(), acc_g, acc_b, n, c, s, 0, cur_stream(x), relu,
                      opt_ptr(beta, "beta", x, c));
   return {dx, dgamma, dbeta};
 }
@@ -1658,7 +1669,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
         "Tensor(d!)? num_batches_tracked=None, float momentum=0.0, bool relu=False) "
         "-> Tensor[]");
   m.def("bn_train_backward(Tensor dy, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) sums, "
-        "Tensor? gamma, Tensor? beta=None, bool relu=False) -> Tensor[]");
+        "Tensor? gamma, Tensor? beta=None, bool relu=False, Tensor(b!)? accum_gamma=None, "
+        "Tensor(c!)? accum_beta=None) -> Tensor[]");
   m.def("dbn_commit64(Tensor(a!) acc, Tensor(b!) running_mean, Tensor(c!) running_var, "
         "float momentum) -> ()");
   m.def("convbn_forward(Tensor x, Tensor[] weights, int[] geo, bool relu, Tensor? gamma, "

@@ -40,7 +40,7 @@ import torch
 from torch import Tensor, nn
 import torch.nn.functional as F
 
-from torchgpipe_amd.ops import _ext
+from torchgpipe_amd.ops import _ext, gradacc
 from torchgpipe_amd.ops.conv import WinogradConv2d, wino_eligible
 from torchgpipe_amd.ops.convbn import (GradSink, _bn_ok, fusable, gemm_conv2d,
                                        gemm_conv_eligible, relu_conv_bn)
@@ -74,15 +74,28 @@ class _BNAct(torch.autograd.Function):
             float(bn.momentum) if track else 0.0, relu)
         ctx.save_for_backward(x, mean, invstd, sums, gamma, beta)
         ctx.relu = relu
+        ctx.params = (bn.weight, bn.bias)
         return y
 
     @staticmethod
     def backward(ctx, dy: Tensor):  # type: ignore[override]
         x, mean, invstd, sums, gamma, beta = ctx.saved_tensors
+        # the affine gradients accumulate into .grad in the kernel where autograd would add
+        # them (ops/gradacc.py): one launch per micro-batch and BatchNorm fewer
+        fused = [gradacc.target(p) if ctx.needs_input_grad[k + 1] else (False, None)
+                 for k, p in enumerate(ctx.params)]
         dx, dgamma, dbeta = _ext.require(dy).bn_train_backward(
-            dy.contiguous(), x, mean, invstd, sums, gamma, beta, ctx.relu)
-        return (dx, dgamma if ctx.needs_input_grad[1] else None,
-                dbeta if ctx.needs_input_grad[2] else None, None, None)
+            dy.contiguous(), x, mean, invstd, sums, gamma, beta, ctx.relu,
+            fused[0][1], fused[1][1])
+        grads = [dgamma if ctx.needs_input_grad[1] else None,
+                 dbeta if ctx.needs_input_grad[2] else None]
+        for k, ((fuse, into), p) in enumerate(zip(fused, ctx.params)):
+            if fuse:
+                if into is None:
+                    gradacc.commit(p, grads[k])
+                grads[k] = None
+        ctx.params = None
+        return (dx, grads[0], grads[1], None, None)
 
 
 def _native_bn_ok(bn: nn.BatchNorm2d, x: Tensor) -> bool:
@@ -187,23 +200,6 @@ STRIDED_FUSED = frozenset({
 })
 
 
-# 3x3 stride-1 Conv-BN(-ReLU) on planes of at most this many pixels with at most
-# GEMM3X3_MAX_IMAGES images per micro-batch: the fused implicit-GEMM op (2 launches forward,
-# BatchNorm statistics in the GEMM epilogue) instead of the Winograd kernels + the native
-# BatchNorm pass (4-5 launches: input transform, batched GEMM, output transform, statistics,
-# normalise) -- for the launch-bound ResNet stages at the reference's 22 / 36-image
-# micro-batches.  TGPIPE_GEMM3X3_MAX_PLANE=0 turns it off.
-GEMM3X3_MAX_PLANE = int(os.environ.get('TGPIPE_GEMM3X3_MAX_PLANE', '0'))
-GEMM3X3_MAX_IMAGES = int(os.environ.get('TGPIPE_GEMM3X3_MAX_IMAGES', '48'))
-
-
-def _gemm3x3(conv: nn.Conv2d, x: Tensor) -> bool:
-    return (GEMM3X3_MAX_PLANE > 0 and tuple(conv.kernel_size) == (3, 3)
-            and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
-            and x.dim() == 4 and x.shape[0] <= GEMM3X3_MAX_IMAGES
-            and x.shape[2] * x.shape[3] <= GEMM3X3_MAX_PLANE)
-
-
 def _strided_fused(conv: nn.Conv2d, bn: nn.BatchNorm2d, x: Tensor, relu: bool) -> bool:
     """Whether one strided Conv-BN(-ReLU) runs as the fused native op: the shipped measured
     set (``STRIDED_FUSED``), or with ``TGPIPE_STRIDED_CHOICE=1`` both ways timed on the first
@@ -273,9 +269,6 @@ class ConvBN2d(WinogradConv2d):
                 setattr(out, _DONE_BN, id(bn))
                 return out
             if self.bias is None and _native_bn_ok(bn, input):
-                if wino and _gemm3x3(self, input) and fusable(input, [self], bn):
-                    y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu)
-                    return _mark(y, bn, relu)
                 if wino:
                     z = WinogradConv2d.forward(self, input)
                     return _mark(bn_act(z, bn, relu), bn, relu)
