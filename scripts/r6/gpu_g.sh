@@ -23,3 +23,6 @@ hs() {  # name steps harness-args...
 }
 hs resnet_p4_s3 1 --model resnet101 --balance 44 92 124 110 --chunks 256 --batch 5632 --stages 3
 hs amoeba_n8m32_s6 2 --model amoebanet --balance 2 2 2 3 3 4 4 4 --chunks 32 --batch 1280 --stages 6
+# per-shape implicit GEMM (shipped plans) vs MIOpen over AmoebaNet-D(18,256) at micro-batch 40
+timeout -k 10 600 python3 benchmarks/convbn_bench.py --micro-batch 40 --out $out/convbn_bench_n40.json > $out/convbn_bench.log 2>&1 || { tail -20 $out/convbn_bench.log; exit 1; }
+tail -3 $out/convbn_bench.log

@@ -57,6 +57,9 @@ _SINK = '_tgpipe_grad_sink'  # tensor mark: a fused reader accepts this tensor's
 # TGPIPE_GRAD_SINK=0: the residual join returns the identity's gradient to autograd (which
 # sums it with conv1's) instead of handing it to conv1's backward-data GEMM
 GRAD_SINK = os.environ.get('TGPIPE_GRAD_SINK', '1') != '0'
+# TGPIPE_BN_GRAD_ACCUM=0: the native BatchNorm's gamma / beta gradients go back to autograd
+# (which adds them per micro-batch) instead of into .grad from the kernel
+BN_GRAD_ACCUM = os.environ.get('TGPIPE_BN_GRAD_ACCUM', '1') != '0'
 
 
 class _BNAct(torch.autograd.Function):
@@ -82,8 +85,8 @@ class _BNAct(torch.autograd.Function):
         x, mean, invstd, sums, gamma, beta = ctx.saved_tensors
         # the affine gradients accumulate into .grad in the kernel where autograd would add
         # them (ops/gradacc.py): one launch per micro-batch and BatchNorm fewer
-        fused = [gradacc.target(p) if ctx.needs_input_grad[k + 1] else (False, None)
-                 for k, p in enumerate(ctx.params)]
+        fused = [gradacc.target(p) if ctx.needs_input_grad[k + 1] and BN_GRAD_ACCUM
+                 else (False, None) for k, p in enumerate(ctx.params)]
         dx, dgamma, dbeta = _ext.require(dy).bn_train_backward(
             dy.contiguous(), x, mean, invstd, sums, gamma, beta, ctx.relu,
             fused[0][1], fused[1][1])

@@ -63,7 +63,6 @@ from torch import Tensor, nn
 
 from torchgpipe_amd.checkpoint import enable_checkpointing, enable_recomputing
 from torchgpipe_amd.ops import gradacc
-from torchgpipe_amd.stream import named_stream
 from torchgpipe_amd.utils import rng
 
 __all__ = ['Segments', 'SegmentCell']
@@ -137,7 +136,10 @@ class Segments:
         self.steps = 0
         self.captured = False
         self.pools = [torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()]
-        self.streams = [named_stream(device, 'capture0'), named_stream(device, 'capture1')]
+        # (fresh per instance, not named: a stage's captures must not share their streams
+        # -- and the cell side streams keyed on them -- with another stage's graphs in the
+        # same process)
+        self.streams = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
         from torchgpipe_amd.models.amoebanet import prepare_side_streams
         for s in self.streams:  # cell side streams paired with the capture streams
             prepare_side_streams(device, s)
