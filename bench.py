@@ -339,7 +339,7 @@ class Bench:
         # (ResNet-101 p1: 1459 vs 1411 samples/s with the recompute lane,
         # profiles/r4/resnet_p1_engine.md)
         overlap = choice(args.overlap_recompute, self.gpu and kind in ('unet', 'resnet'))
-        overlap_fwd = choice(args.overlap_forward, self.gpu and unet)
+        overlap_fwd = choice(args.overlap_forward, self.gpu and kind in ('unet', 'resnet'))
         cell_streams = kind == 'amoebanet' and choice(args.cell_streams, self.gpu)
         # captured cells (parallel/segments.py): one GPU, AmoebaNet -- three-stream cells in
         # per-pass captures, 392.0 vs 389.4 samples/s for the two-stream whole-step graph

@@ -88,11 +88,12 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
     pending = dict(tracker.tensors)
     del batch, tracker
 
-    lanes = {'auto': args.model == 'unet', 'on': True, 'off': False}[args.lanes]
+    lanes = {'auto': args.model in ('unet', 'resnet101'), 'on': True, 'off': False}[args.lanes]
     # placeholder transport until the stage knows its skip routes
     sizes = [len(c) for c in torch.empty(args.batch, 0).chunk(args.chunks)]
     transport = LoopbackP2P(dev, acts, atomic, {}, sizes)
-    # (as bench.py: ResNet-101 recomputes on a lane too, forward lanes are U-Net's only)
+    # (as bench.py: forward and recompute lanes for U-Net and ResNet-101; AmoebaNet runs
+    # its cells on several streams instead)
     recompute_lane = lanes or (args.lanes == 'auto' and args.model == 'resnet101')
     stage = PipelineStage(model, args.balance, rank=k, device=dev, chunks=args.chunks,
                           checkpoint=args.checkpoint, transport=transport,

@@ -170,3 +170,68 @@ def test_direct_backward_reaches_a_learnable_loss_head(checkpoint):
     torch.testing.assert_close(head_b.grad, head_a.grad)
     for pa, pb in zip(a.parameters(), b.parameters()):
         torch.testing.assert_close(pb.grad, pa.grad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('checkpoint', ['except_last', 'always'])
+def test_batchnorm_stage_on_lanes_matches_one_stream(checkpoint):
+    """A BatchNorm partition (ResNet) on forward and recompute lanes: its running-statistics
+    updates are slotted and folded in order (torchgpipe_amd/runstats.py), so losses,
+    gradients, running means / variances and counters agree with the one-stream schedule
+    over several steps, the recomputations' second updates included."""
+    from torchgpipe_amd.models.resnet import build_resnet
+    dev = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    base = build_resnet([1, 1, 1, 1], num_classes=10)
+    a, b = copy.deepcopy(base).to(dev), copy.deepcopy(base).to(dev)
+    sa = PipelineStage(a, [len(a)], device=dev, chunks=4, checkpoint=checkpoint,
+                       overlap_recompute=False, overlap_forward=False)
+    sb = PipelineStage(b, [len(b)], device=dev, chunks=4, checkpoint=checkpoint,
+                       overlap_recompute=True, overlap_forward=True)
+    assert sb._forward_lanes() is not None  # BatchNorms no longer pin it to one stream
+    gen = torch.Generator(device=dev).manual_seed(5)
+    for _ in range(3):
+        x = torch.rand(16, 3, 64, 64, device=dev, generator=gen)
+        y = torch.randint(10, (16,), device=dev, generator=gen)
+        for p in list(a.parameters()) + list(b.parameters()):
+            p.grad = None
+        la = sa.train_step(x, y, F.cross_entropy)
+        lb = sb.train_step(x, y, F.cross_entropy)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(lb, la, rtol=1e-5, atol=1e-6)
+        _close_grads(a, b)
+        # every gradient, the MIOpen stem's and the classifier's too, was accumulated by
+        # the ops on the lanes' own streams, none by an AccumulateGrad node shared across
+        # lanes (ops/gradacc.py library_conv2d / linear)
+        assert all(hasattr(p, '_tgpipe_grad_accumulator') for p in b.parameters())
+    for (name, ba), bb in zip(a.named_buffers(), b.buffers()):
+        if name.endswith('num_batches_tracked'):
+            assert torch.equal(bb, ba), name
+        else:
+            torch.testing.assert_close(bb, ba, rtol=1e-5, atol=1e-6, msg=name)
+
+
+@pytest.mark.gpu
+def test_library_layers_accumulate_like_autograd():
+    """ops.gradacc.library_conv2d / linear: two backward passes accumulate the same
+    gradients as autograd on the plain layers (strided conv with bias, Linear on 3-D input)."""
+    from torchgpipe_amd.ops import gradacc
+    dev = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    conv = nn.Conv2d(3, 8, 7, stride=2, padding=3).to(dev)
+    lin = nn.Linear(8, 5).to(dev)
+    c2, l2 = copy.deepcopy(conv), copy.deepcopy(lin)
+    for _ in range(2):
+        x = torch.randn(4, 3, 32, 32, device=dev, requires_grad=True)
+        x2 = x.detach().clone().requires_grad_(True)
+        y = gradacc.linear(gradacc.library_conv2d(x, conv).mean((2, 3))[:, None, :]
+                           .expand(4, 3, 8), lin)
+        y2 = l2(c2(x2).mean((2, 3))[:, None, :].expand(4, 3, 8))
+        g = torch.randn_like(y)
+        y.backward(g)
+        y2.backward(g)
+        torch.testing.assert_close(x.grad, x2.grad, rtol=1e-5, atol=1e-6)
+    for p, q in zip(list(conv.parameters()) + list(lin.parameters()),
+                    list(c2.parameters()) + list(l2.parameters())):
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-6)
+        assert hasattr(p, '_tgpipe_grad_accumulator')

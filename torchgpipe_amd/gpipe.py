@@ -147,6 +147,32 @@ MOVING_DENIED = TypeError('denied to move parameters and buffers, '
                           'because GPipe should manage device placement')
 
 
+class _JoinLanes(torch.autograd.Function):
+    """Identity on the pipeline's output whose backward (the first to run) schedules a
+    callback for the end of the backward pass: the caller's streams then wait for the
+    forward lanes.  The fused ops on the lanes add into ``.grad`` outside autograd
+    (``ops/gradacc.py``), so the engine's own end-of-backward sync, which covers only the
+    streams its ``AccumulateGrad`` nodes ran on, would let the optimizer read gradients the
+    last micro-batch's backward is still adding to."""
+
+    @staticmethod
+    def forward(ctx, lanes: List[AbstractStream], *outputs: Tensor):  # type: ignore[override]
+        ctx.lanes = lanes
+        views = tuple(t.view_as(t) for t in outputs)
+        return views if len(views) > 1 else views[0]
+
+    @staticmethod
+    def backward(ctx, *grads: Tensor):  # type: ignore[override]
+        lanes = ctx.lanes
+
+        def join() -> None:  # (runs with the caller's current streams current)
+            for lane in lanes:
+                cast(torch.cuda.Stream, current_stream(lane.device)).wait_stream(lane)
+
+        torch.autograd.Variable._execution_engine.queue_callback(join)  # type: ignore
+        return (None,) + grads
+
+
 class GPipe(nn.Module):
     """Wrap an ``nn.Sequential`` to train it with GPipe pipeline parallelism.
 
@@ -316,13 +342,19 @@ class GPipe(nn.Module):
                             queues=self._workers.queues(self.devices),
                             on_output=gatherer.put, lanes=lanes)
         pipeline.run()
+        output = gatherer.result(batches)
         if lanes is not None:
             # (a fallback gather reads the last partition's outputs on the current stream)
-            for dev, lane in zip(self.devices, lanes):
-                if lane is not None:
-                    for stream in lane:
-                        current_stream(dev).wait_stream(stream)  # type: ignore[union-attr]
-        return gatherer.result(batches)
+            used = [stream for lane in lanes if lane is not None for stream in lane]
+            for stream in used:
+                current_stream(stream.device).wait_stream(stream)  # type: ignore
+            if used and torch.is_grad_enabled():
+                outs = (output,) if isinstance(output, Tensor) else tuple(output)
+                if any(t.requires_grad for t in outs):
+                    joined = _JoinLanes.apply(used, *outs)
+                    output = joined if isinstance(output, Tensor) else \
+                        (tuple(joined) if isinstance(joined, tuple) else (joined,))
+        return output
 
     def __getstate__(self) -> Any:
         state = self.__dict__.copy()

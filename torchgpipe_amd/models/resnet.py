@@ -19,7 +19,7 @@ from typing import Any, Generator, List, Optional
 from torch import Tensor, nn
 
 from torchgpipe_amd.models.flatten import flatten_sequential
-from torchgpipe_amd.ops.fusion import (BatchNormAct2d, ConvBN2d, ReLU, add_relu,
+from torchgpipe_amd.ops.fusion import (BatchNormAct2d, ConvBN2d, Linear, ReLU, add_relu,
                                        pending_join, relink, relu_follows)
 from torchgpipe_amd.skip import Namespace, pop, skippable, stash
 
@@ -108,7 +108,7 @@ def build_resnet(layers: List[int], num_classes: int = 1000, inplace: bool = Fal
         ('layer4', make_layer(512, layers[3], stride=2)),
         ('avgpool', nn.AdaptiveAvgPool2d((1, 1))),
         ('flat', nn.Flatten()),
-        ('fc', nn.Linear(512 * 4, num_classes)),
+        ('fc', (Linear if fused else nn.Linear)(512 * 4, num_classes)),
     ]))
     model = flatten_sequential(model)
 

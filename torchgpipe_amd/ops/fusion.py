@@ -45,7 +45,7 @@ from torchgpipe_amd.ops.conv import WinogradConv2d, wino_eligible
 from torchgpipe_amd.ops.convbn import (GradSink, _bn_ok, fusable, gemm_conv2d,
                                        gemm_conv_eligible, relu_conv_bn)
 
-__all__ = ['ConvBN2d', 'BatchNormAct2d', 'ReLU', 'relink', 'bn_act', 'add_relu',
+__all__ = ['ConvBN2d', 'BatchNormAct2d', 'ReLU', 'Linear', 'relink', 'bn_act', 'add_relu',
            'pending_join']
 
 _LINK = '_tgpipe_link'       # ConvBN2d -> (BatchNormAct2d, relu?)
@@ -288,13 +288,22 @@ class ConvBN2d(WinogradConv2d):
                 if fusable(input, [self], bn) and _strided_fused(self, bn, input, relu):
                     y = relu_conv_bn(input, [(self, 0)], bn, relu=False, relu_out=relu)
                     return _mark(y, bn, relu)
-                z = nn.Conv2d.forward(self, input)  # strided: MIOpen
+                z = gradacc.library_conv2d(input, self)  # strided: MIOpen
                 return _mark(bn_act(z, bn, relu), bn, relu)
         if wino:
             return WinogradConv2d.forward(self, input)
         if _pointwise(self) and gemm_conv_eligible(input, self):
             return gemm_conv2d(input, self)
-        return nn.Conv2d.forward(self, input)
+        return gradacc.library_conv2d(input, self)
+
+
+class Linear(nn.Linear):
+    """``nn.Linear`` (same parameters) whose gradients are accumulated into ``.grad`` by its
+    own backward (``ops/gradacc.py`` ``linear``): no ``AccumulateGrad`` node shared by
+    micro-batches of different lanes."""
+
+    def forward(self, input: Tensor) -> Tensor:
+        return gradacc.linear(input, self)
 
 
 class BatchNormAct2d(nn.BatchNorm2d):

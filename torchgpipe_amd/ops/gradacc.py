@@ -48,7 +48,8 @@ import torch
 from torch import Tensor
 
 __all__ = ['target', 'commit', 'enabled', 'release', 'deferred_wgrad', 'slab', 'deferred',
-           'flush_pending', 'pending_snapshot', 'register_pending']
+           'flush_pending', 'pending_snapshot', 'register_pending', 'library_conv2d',
+           'linear']
 
 _ENABLED = os.environ.get('TGPIPE_FUSED_GRAD_ACCUM', '1') != '0'
 _DEFER_ENABLED = os.environ.get('TGPIPE_DEFERRED_WGRAD', '1') != '0'
@@ -257,3 +258,104 @@ def register_pending(device: torch.device,
         if entry is not None:
             entry[1] = state.step
         state.pending.setdefault(id(param), (ref, sb))
+
+
+# -- library layers with the accumulation fused ----------------------------------------------
+
+def _settle(param: Optional[Tensor], grad: Optional[Tensor], fuse: bool,
+            into: Optional[Tensor]) -> Optional[Tensor]:
+    """Hand a library-computed gradient to ``.grad`` (fused) or back to autograd."""
+    if not fuse or grad is None:
+        return grad
+    assert param is not None
+    if into is None:
+        commit(param, grad)
+    else:
+        into.add_(grad)
+    return None
+
+
+class _LibraryConv(torch.autograd.Function):
+    """``F.conv2d`` (MIOpen) whose weight / bias gradients are added into ``.grad`` by the
+    backward itself (:func:`target`).  Under forward / recompute lanes the micro-batches of
+    one step back-propagate on different streams; a parameter left to autograd has one
+    ``AccumulateGrad`` node shared by all of them, bound to one stream, and its gradients
+    came out wrong across micro-batches under PyTorch 2.10 (``tests/test_overlap_recompute.py``
+    ResNet case; ``profiles/KERNELS.md``).  Here the add runs on the backward's own stream,
+    which the engine orders micro-batch after micro-batch."""
+
+    @staticmethod
+    def forward(ctx, x: Tensor, weight: Tensor, bias: Optional[Tensor],  # type: ignore[override]
+                stride: Tuple[int, ...], padding: Tuple[int, ...], dilation: Tuple[int, ...],
+                groups: int) -> Tensor:
+        ctx.save_for_backward(x, weight)
+        ctx.conf = (list(stride), list(padding), list(dilation), groups)
+        ctx.params = (weight, bias)
+        return torch.nn.functional.conv2d(x, weight, bias, stride, padding, dilation, groups)
+
+    @staticmethod
+    def backward(ctx, dy: Tensor):  # type: ignore[override]
+        x, weight = ctx.saved_tensors
+        stride, padding, dilation, groups = ctx.conf
+        wparam, bparam = ctx.params
+        ctx.params = (None, None)  # a repeated backward (retain_graph) returns them instead
+        need = ctx.needs_input_grad
+        has_bias = need[2]
+        fw = target(wparam) if need[1] else (False, None)
+        fb = target(bparam) if has_bias else (False, None)
+        dx, dw, db = torch.ops.aten.convolution_backward(
+            dy, x, weight, [weight.shape[0]] if has_bias else None, stride, padding, dilation,
+            False, [0, 0], groups, [need[0], need[1], has_bias])
+        dw = _settle(wparam, dw if need[1] else None, *fw)
+        db = _settle(bparam, db if has_bias else None, *fb)
+        return dx if need[0] else None, dw, db, None, None, None, None
+
+
+def library_conv2d(x: Tensor, conv: torch.nn.Conv2d) -> Tensor:
+    """``conv(x)`` on the library convolution with the gradient accumulation fused (GPU,
+    zero padding); ``conv.forward`` otherwise."""
+    if not (_ENABLED and x.is_cuda and conv.padding_mode == 'zeros'
+            and isinstance(conv.padding, tuple)):
+        return torch.nn.Conv2d.forward(conv, x)
+    return _LibraryConv.apply(x, conv.weight, conv.bias, conv.stride, conv.padding,
+                              conv.dilation, conv.groups)
+
+
+class _Linear(torch.autograd.Function):
+    """``F.linear`` whose weight / bias gradients are accumulated by the backward: the
+    weight's as one GEMM with beta = 1 straight into ``.grad`` (``addmm_``), no separate
+    add.  See :class:`_LibraryConv` for why."""
+
+    @staticmethod
+    def forward(ctx, x: Tensor, weight: Tensor,  # type: ignore[override]
+                bias: Optional[Tensor]) -> Tensor:
+        ctx.save_for_backward(x, weight)
+        ctx.params = (weight, bias)
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy: Tensor):  # type: ignore[override]
+        x, weight = ctx.saved_tensors
+        wparam, bparam = ctx.params
+        ctx.params = (None, None)
+        need = ctx.needs_input_grad
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = dy.matmul(weight) if need[0] else None
+        dw = db = None
+        if need[1]:
+            fuse, into = target(wparam)
+            if fuse and into is not None:
+                into.addmm_(dy2.t(), x2)
+            else:
+                dw = _settle(wparam, dy2.t().mm(x2), fuse, into)
+        if need[2]:
+            db = _settle(bparam, dy2.sum(0), *target(bparam))
+        return dx, dw, db
+
+
+def linear(x: Tensor, layer: torch.nn.Linear) -> Tensor:
+    """``layer(x)`` with the gradient accumulation fused (GPU); ``layer.forward`` otherwise."""
+    if not (_ENABLED and x.is_cuda):
+        return torch.nn.Linear.forward(layer, x)
+    return _Linear.apply(x, layer.weight, layer.bias)

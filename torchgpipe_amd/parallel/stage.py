@@ -49,6 +49,7 @@ from torchgpipe_amd.ops.conv import hold_cache, refresh_step_caches, size_cache_
 from torchgpipe_amd.ops.dropout import convert_dropout
 from torchgpipe_amd.ops.fusion import relink
 from torchgpipe_amd.parallel.p2p import _DTYPE_CODE, P2P, _wait
+from torchgpipe_amd.runstats import OrderedRunningStats
 from torchgpipe_amd.skip.layout import SkipLayout, inspect_skip_layout
 from torchgpipe_amd.skip.namespace import Namespace
 from torchgpipe_amd.skip.skippable import Skippable, verify_skippables
@@ -416,6 +417,11 @@ class PipelineStage:
         # their micro-batches must run in order on one stream
         self._stateful = any(isinstance(m, nn.modules.batchnorm._BatchNorm)
                              and m.track_running_stats for m in self.partition.modules())
+        # ... unless their running statistics can be slotted per update and folded in order
+        # (runstats.py): then their forwards and recomputations may overlap on lanes too
+        self._stat_slots: Optional[OrderedRunningStats] = \
+            OrderedRunningStats.for_module(self.partition) if self._stateful else None
+        self._rec_slotted = False  # this step's recomputations are slotted
         self._sig: Optional[Signature] = None
         self._m = 0
         self._probe: Optional[List[Tuple[str, Any, Any]]] = None
@@ -488,7 +494,7 @@ class PipelineStage:
             if hasattr(self.p2p, 'relay_links') else 0
         cells = [getattr(m, 'streams', 0) for m in self.partition.modules()]
         return stream_census(self.rank, link_pairs(self.layout, self.n),
-                             forward_lanes=self.overlap_forward and not self._stateful,
+                             forward_lanes=self.overlap_forward and self._lanes_ok(),
                              recompute_lanes=self.overlap_recompute,
                              cell_streams=max([c for c in cells if isinstance(c, int)] + [0]),
                              graph_cells=self.graph_cells, relay_routes=jobs,
@@ -682,8 +688,11 @@ class PipelineStage:
         self._cells = []
         outputs: List[TensorOrTensors] = []
 
-        flanes = self._forward_lanes()
+        flanes = self._forward_lanes() if not (graphed and self._stateful) else None
         main = torch.cuda.current_stream(self.device) if flanes is not None else None
+        slots = self._stat_slots if self._stateful and flanes is not None else None
+        if slots is not None:
+            slots.begin(m)
         for i in range(m):
             cell = _Cell(i)
             # 1. inputs: activations + cross-rank skips (posted before waiting on any)
@@ -744,7 +753,8 @@ class PipelineStage:
                 for t in flat:
                     t.record_stream(lane)
             if not cell.seg:
-                with torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext():
+                with torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext(), \
+                        slots.update() if slots is not None else contextlib.nullcontext():
                     if i < stop:
                         cell.chk = Checkpointing(fn, Batch(tuple(flat)))
                         out = list(cell.chk.checkpoint())
@@ -777,6 +787,8 @@ class PipelineStage:
         if flanes is not None and main is not None:
             for lane in flanes:
                 main.wait_stream(lane)
+        if slots is not None:
+            slots.commit()  # the forwards' running-statistics updates, in micro-batch order
         if not torch.is_grad_enabled():
             # Inference: no backward will flush the sends; complete them now.
             self.p2p.flush()
@@ -928,6 +940,12 @@ class PipelineStage:
         on_gpu = self.device.type == 'cuda'
         main = torch.cuda.current_stream(self.device) if on_gpu else None
         seg = self._segments if self._seg_phase in ('capture', 'replay') else None
+        # recomputations on two lanes update running statistics concurrently: slotted, and
+        # folded in the order they were issued (the reference's backward order)
+        self._rec_slotted = lanes is not None and seg is None and self._stat_slots is not None
+        if self._rec_slotted:
+            assert self._stat_slots is not None
+            self._stat_slots.begin(len(cells))
         # the capture step recomputes no cell ahead: a graph captured while another cell's
         # autograd graph is alive would share its AccumulateGrad nodes (and their streams)
         ahead = seg is None or self._seg_phase == 'replay'
@@ -948,6 +966,10 @@ class PipelineStage:
             cur = torch.cuda.current_stream(self.device)
             for lane in (lanes or []) + (self._fwd_lanes or []):
                 cur.wait_stream(lane)
+        if self._rec_slotted:
+            assert self._stat_slots is not None
+            self._stat_slots.commit()
+            self._rec_slotted = False
         if seg is not None:
             seg.end_backward()
         if self._cache_state == 'measuring':
@@ -1210,10 +1232,10 @@ class PipelineStage:
         its outputs are sent from that lane, so consecutive micro-batches overlap whenever
         their inputs are already here: on the first stage, and on a stage slower than its
         upstream (the pipeline's bottleneck, where inputs queue).  Partitions with running
-        statistics (BatchNorm) keep one stream: their micro-batches update shared state
-        in order.
+        statistics (BatchNorm) take them when ``_lanes_ok``: their updates are slotted and
+        folded in micro-batch order (:class:`~torchgpipe_amd.runstats.OrderedRunningStats`).
         """
-        if not self.overlap_forward or self._stateful:
+        if not self.overlap_forward or not self._lanes_ok():
             return None
         if self.device.type != 'cuda' or torch.cuda.is_current_stream_capturing():
             return None
@@ -1221,6 +1243,17 @@ class PipelineStage:
             self._fwd_lanes = [named_stream(self.device, 'forward-lane0'),
                                named_stream(self.device, 'forward-lane1')]
         return self._fwd_lanes
+
+    def _lanes_ok(self) -> bool:
+        """Whether this partition's forwards may overlap: stateless, or running statistics
+        that can be slotted and no multi-stream cells (AmoebaNet's side streams are shared
+        process-wide, so two lanes' cells would interleave on them)."""
+        if not self._stateful:
+            return True
+        if self._stat_slots is None:
+            return False
+        return not any(isinstance(getattr(m, 'streams', 0), int) and getattr(m, 'streams', 0)
+                       for m in self.partition.modules())
 
     def _recompute_on_lane(self, cell: _Cell, lane: torch.cuda.Stream,
                            main: torch.cuda.Stream) -> None:
@@ -1237,7 +1270,9 @@ class PipelineStage:
         lane.wait_stream(main)
         for t in cell.inputs:
             t.record_stream(lane)
-        with torch.cuda.stream(lane), trace.range(f'recompute mb{cell.index} stage{self.rank}'):
+        slots = self._stat_slots if self._rec_slotted else None
+        with torch.cuda.stream(lane), trace.range(f'recompute mb{cell.index} stage{self.rank}'), \
+                slots.update() if slots is not None else contextlib.nullcontext():
             cell.chk.recompute_now()
         cell.lane = lane
 
