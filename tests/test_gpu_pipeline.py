@@ -63,7 +63,21 @@ def test_gpipe_forward_lanes_train_like_one_stream(balance, devices):
     the one-stream schedule (same Philox dropout masks: the tape is consumed in the same
     host order).  The kernels are not bitwise deterministic run to run (~1e-9 per step on
     one stream too, scripts/debug/gpipe_lanes_diag.py), and SGD carries that into later
-    steps, so the gradients are compared relative to their norms."""
+    steps, so the gradients are compared relative to their norms.  MIOpen's layers (the
+    3-channel input and 8-channel decoder convolutions) run their deterministic algorithms
+    here: its defaults differ by ~1e-6 run to run, which a ReLU mask can turn into much
+    more (scripts/debug/resnet_determinism.py).  The lanes' own ordering -- the optimizer
+    reads gradients the fused ops wrote on the lanes -- is what is under test
+    (gpipe.py ``_JoinLanes``)."""
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        _gpipe_lanes_vs_one_stream(balance, devices)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+
+
+def _gpipe_lanes_vs_one_stream(balance, devices):
     results = []
     for lanes in (False, True):
         model = small_unet()
