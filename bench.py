@@ -728,9 +728,34 @@ def main() -> None:
         lap('resnet')
         emit()
 
+    # The opt-in engine variants (tuned balances, multi-path transfers, captured cells) come
+    # last.  At N > 1 a variant that raises on every rank (a planner error, a PipelineTimeout
+    # of its own transfers) is recorded under its key and ends the optional sections; the
+    # lines already printed keep the headline and the sections before it.
+    failed: List[str] = []
+
+    def optional(name: str, fn: Callable[[], None]) -> None:
+        if failed:
+            return
+        if world == 1:
+            fn()
+            return
+        try:
+            if os.environ.get('TGPIPE_BENCH_FAIL') == name:  # (tests/test_bench_script.py)
+                raise RuntimeError(f'{name}: failure injected by TGPIPE_BENCH_FAIL')
+            fn()
+        except Exception as e:  # noqa: BLE001 - recorded, then the run winds down
+            import traceback
+            traceback.print_exc()
+            failed.append(name)
+            record[name] = {'error': f'{type(e).__name__}: {e}'[:500]}
+            lap(name)
+            emit()
+
     also = args.also_tuned == 'yes' or (args.also_tuned == 'auto' and world > 1
                                          and args.balance == 'ref' and tuned_balance != balance)
-    if also:
+
+    def tuned_section() -> None:
         t = b.pipeline(kind, exp, tuned_balance, checkpoint, extra_steps, 'tuned')
         record['tuned'] = {'balance': tuned_balance,
                            'value': round(batch * extra_steps / t['elapsed'], 3),
@@ -750,7 +775,7 @@ def main() -> None:
         lap('tuned')
         emit()
 
-    if 'striped' in sections and world >= 3:
+    def striped_section() -> None:
         # multi-path transfers (parallel/stripes.py) on the headline configuration: opt-in
         # until a multi-GPU node has run their RCCL relay chains
         sr = b.pipeline(kind, exp, balance, checkpoint, extra_steps, 'striped', stripes=True)
@@ -761,7 +786,7 @@ def main() -> None:
         lap('striped')
         emit()
 
-    if 'graph_cells' in sections and kind == 'unet' and world > 1:
+    def graph_cells_section() -> None:
         # captured cells at N > 1 (parallel/segments.py: RCCL receives into the captured
         # graphs' persistent buffers) on the AmoebaNet experiment, opt-in like the stripes
         gc_run = b.pipeline('amoebanet', aexp, aexp['balance'], a_ckpt, extra_steps,
@@ -773,7 +798,19 @@ def main() -> None:
         lap('graph_cells')
         emit()
 
+    if also:
+        optional('tuned', tuned_section)
+    if 'striped' in sections and world >= 3:
+        optional('striped', striped_section)
+    if 'graph_cells' in sections and kind == 'unet' and world > 1:
+        optional('amoebanet_graph_cells', graph_cells_section)
+
     if world > 1:
+        if failed:
+            # the communicators may be mid-exchange: no barrier, no orderly teardown
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
         dist.barrier()
         dist.destroy_process_group()
 

@@ -11,6 +11,7 @@ import os
 import socket
 import subprocess
 import sys
+from typing import Optional
 
 import pytest
 
@@ -29,8 +30,9 @@ def _run(nproc: int, *extra: str) -> dict:
     return _run_lines(nproc, *extra)[-1]
 
 
-def _run_lines(nproc: int, *extra: str) -> list:
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='', OMP_NUM_THREADS='2')
+def _run_lines(nproc: int, *extra: str, env_extra: Optional[dict] = None) -> list:
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='', OMP_NUM_THREADS='2',
+               **(env_extra or {}))
     args = ['bench.py', '--gpus', str(nproc), '--steps', '1', '--warmup', '1', '--tiny',
             '--batch', '4', '--chunks', '2', *extra]
     if nproc > 1:
@@ -121,6 +123,19 @@ def test_bench_headline_printed_before_the_sections_eight_ranks():
     assert [set(r['section_s']) for r in records[1:]] == [
         {'headline', 'baseline'}, {'headline', 'baseline', 'amoebanet'},
         {'headline', 'baseline', 'amoebanet', 'striped'}]
+
+
+def test_bench_failed_optional_section_keeps_the_run():
+    """N > 1: an opt-in variant that raises on every rank (here injected into ``striped``)
+    is recorded under its key, the sections after it are skipped, the earlier lines stand
+    and the ranks exit cleanly instead of tearing down communicators mid-exchange."""
+    records = _run_lines(3, '--model', 'unet', '--sections', 'baseline,striped,graph_cells',
+                         env_extra={'TGPIPE_BENCH_FAIL': 'striped'})
+    last = records[-1]
+    assert 'failure injected' in last['striped']['error']
+    assert 'amoebanet_graph_cells' not in last
+    assert last['baseline']['value'] > 0 and last['value'] == records[0]['value']
+    assert set(last['section_s']) == {'headline', 'baseline', 'striped'}
 
 
 def test_bench_striped_eight_ranks():
