@@ -522,7 +522,8 @@ def test_presplit_follows_data_updates_across_steps():
 
 
 @pytest.mark.parametrize('stride', [1, 2])
-@pytest.mark.parametrize('hw', [(7, 7), (12, 9), (1, 1), (2, 3), (120, 121)])
+@pytest.mark.parametrize('hw', [(7, 7), (12, 9), (1, 1), (2, 3), (120, 121), (28, 28), (56, 56),
+                                (14, 14)])
 @pytest.mark.parametrize('with_add', [False, True])
 @pytest.mark.parametrize('nc', [(3, 5), (7, 37)])
 def test_avgpool3_matches_fp64(stride, hw, with_add, nc):
@@ -626,11 +627,11 @@ def test_backward_reads_channel_sliced_gradients_in_place():
     from torchgpipe_amd.ops.pool import AvgPool3x3
     _ext.require()
     torch.manual_seed(0)
-    x = torch.randn(4, 16, 14, 14, device='cuda', requires_grad=True)
+    x = torch.randn(4, 16, 28, 28, device='cuda', requires_grad=True)
     op = ReLUConvBN(nn.ReLU(), nn.Conv2d(16, 24, 1, bias=False), nn.BatchNorm2d(24)).cuda()
     pool = AvgPool3x3(1)
     outs = [op(x), pool(x)]
-    big = torch.randn(4, 24 + 16 + 8, 14, 14, device='cuda')
+    big = torch.randn(4, 24 + 16 + 8, 28, 28, device='cuda')
     grads = [big[:, 8:32], big[:, 32:48]]
     assert not grads[0].is_contiguous()
     torch.autograd.backward(outs, grads)
