@@ -175,10 +175,11 @@ def parse() -> argparse.Namespace:
     p.add_argument('--overlap-recompute', choices=['auto', 'on', 'off'], default='auto',
                    help="recompute the next micro-batch on a second stream during this one's "
                         'backward (PipelineStage(overlap_recompute=True); auto: on for '
-                        'U-Net)')
+                        'U-Net, and for ResNet-101 at N=1)')
     p.add_argument('--overlap-forward', choices=['auto', 'on', 'off'], default='auto',
-                   help='alternate the forward micro-batches of a stateless partition (no '
-                        'running statistics: U-Net) between two streams (auto: on for U-Net)')
+                   help='alternate the forward micro-batches of a partition between two '
+                        'streams (BatchNorm statistics slotted and folded in order; auto: on '
+                        'for U-Net, and for ResNet-101 at N=1)')
     p.add_argument('--graph-cells', choices=['auto', 'on', 'off'], default='auto',
                    help='replay each micro-batch of a stage as captured hipGraphs, transfers '
                         'issued between them (PipelineStage(graph_cells=True), '
@@ -338,8 +339,13 @@ class Bench:
         # lanes (parallel/stage.py), parity-tested on shared-GPU gloo rehearsals.
         # (ResNet-101 p1: 1459 vs 1411 samples/s with the recompute lane,
         # profiles/r4/resnet_p1_engine.md)
-        overlap = choice(args.overlap_recompute, self.gpu and kind in ('unet', 'resnet'))
-        overlap_fwd = choice(args.overlap_forward, self.gpu and kind in ('unet', 'resnet'))
+        # ResNet-101: lanes at pipeline-1 (110-image micro-batches: 1741-1754 -> 1781-1785
+        # samples/s), none at N > 1, where its 15-36-image stages are host-bound and the
+        # lanes' extra host work costs the bottleneck stage 2-5 % (p4 stage 3 1656 vs 1745 ms,
+        # p8 stage 7 833 vs 850; profiles/r6/resnet_lanes/)
+        lanes = self.gpu and (kind == 'unet' or (kind == 'resnet' and self.world == 1))
+        overlap = choice(args.overlap_recompute, lanes)
+        overlap_fwd = choice(args.overlap_forward, lanes)
         cell_streams = kind == 'amoebanet' and choice(args.cell_streams, self.gpu)
         # captured cells (parallel/segments.py): one GPU, AmoebaNet -- three-stream cells in
         # per-pass captures, 392.0 vs 389.4 samples/s for the two-stream whole-step graph

@@ -88,13 +88,14 @@ def run_stage(args: argparse.Namespace, k: int, dev: torch.device) -> Dict[str, 
     pending = dict(tracker.tensors)
     del batch, tracker
 
-    lanes = {'auto': args.model in ('unet', 'resnet101'), 'on': True, 'off': False}[args.lanes]
+    auto = args.model == 'unet' or (args.model == 'resnet101' and len(args.balance) == 1)
+    lanes = {'auto': auto, 'on': True, 'off': False}[args.lanes]
     # placeholder transport until the stage knows its skip routes
     sizes = [len(c) for c in torch.empty(args.batch, 0).chunk(args.chunks)]
     transport = LoopbackP2P(dev, acts, atomic, {}, sizes)
-    # (as bench.py: forward and recompute lanes for U-Net and ResNet-101; AmoebaNet runs
-    # its cells on several streams instead)
-    recompute_lane = lanes or (args.lanes == 'auto' and args.model == 'resnet101')
+    # (as bench.py: forward and recompute lanes for U-Net, and for ResNet-101 at pipeline-1
+    # only; AmoebaNet runs its cells on several streams instead)
+    recompute_lane = lanes
     stage = PipelineStage(model, args.balance, rank=k, device=dev, chunks=args.chunks,
                           checkpoint=args.checkpoint, transport=transport,
                           overlap_recompute=recompute_lane, overlap_forward=lanes,
