@@ -27,6 +27,7 @@ RESNET_SHAPES = [
     (22, 256, 56, 64, 1, 1), (22, 64, 56, 256, 1, 1), (22, 512, 28, 128, 1, 1),
     (22, 128, 28, 512, 1, 1), (22, 1024, 14, 256, 1, 1), (22, 256, 14, 1024, 1, 1),
     (22, 2048, 7, 512, 1, 1), (22, 512, 7, 2048, 1, 1), (22, 256, 14, 256, 3, 3),
+    (22, 1024, 7, 2048, 1, 1), (22, 2048, 7, 1024, 1, 1),
 ]
 
 
