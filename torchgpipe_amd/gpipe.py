@@ -159,6 +159,9 @@ class _JoinLanes(torch.autograd.Function):
     def forward(ctx, lanes: List[AbstractStream], *outputs: Tensor):  # type: ignore[override]
         ctx.lanes = lanes
         views = tuple(t.view_as(t) for t in outputs)
+        frozen = [v for v, t in zip(views, outputs) if not t.requires_grad]
+        if frozen:
+            ctx.mark_non_differentiable(*frozen)
         return views if len(views) > 1 else views[0]
 
     @staticmethod
