@@ -153,8 +153,10 @@ def main():
             cells.append(batch / (simulate(args, st, g, plan, lt) / 1e3))
             striped.append(lt)
         plain = []
-        simulate(args, st, LINKS[0], None, plain)
-        link_tables.append((name, args['balance'], plan[0], plain, striped[0]))
+        t_plain = simulate(args, st, LINKS[0], None, plain)
+        t_striped = simulate(args, st, LINKS[0], plan)
+        link_tables.append((name, args['balance'], plan[0], plain, striped[0], args['chunks'],
+                            t_plain, t_striped))
         fmt = [f'{c / d:.3f}' if d else f'{c:.1f}/s' for c in cells]
         stages = ' / '.join('%.1f' % s['device_ms'] for s in st)
         print(f"| {name} B {batch} m {args['chunks']} {args['balance']} | {stages} | " +
@@ -162,7 +164,7 @@ def main():
     if not a.links:
         return
     g = LINKS[0]
-    for name, bal, routes, plain, striped in link_tables:
+    for name, bal, routes, plain, striped, m, t_plain, t_striped in link_tables:
         if len(bal) < 2:
             continue
         print(f'\n#### {name} {bal}: forward routes at {g:.0f} GB/s')
@@ -172,6 +174,39 @@ def main():
         for (src, dst, kind, nb, _, ms, cell), (_, _, _, _, rl, sms, _) in zip(plain, striped):
             print(f'| {src}->{dst} | {kind} | {nb / 1e6:.0f} | {ms:.2f} | {rl or "-"} | '
                   f'{sms:.2f} | {cell:.2f} | {ms / cell:.2f}, {sms / cell:.2f} |')
+        print(f'\n{name} {bal}: per directed link at {g:.0f} GB/s, bytes per step (forward '
+              'messages one way, their gradients the mirrored way) and the share of the '
+              'simulated step the link is busy')
+        print('| link | direct GB / step | direct busy | striped GB / step | striped busy |')
+        print('|---|---:|---:|---:|---:|')
+        for a_, b_, direct, strip in link_bytes(plain, routes, m):
+            print(f'| {a_}->{b_} | {direct / 1e9:.2f} | {direct / (g * 1e6) / t_plain:.2f} | '
+                  f'{strip / 1e9:.2f} | {strip / (g * 1e6) / t_striped:.2f} |')
+
+
+def link_bytes(plain, routes, m):
+    """[(a, b, direct bytes, striped bytes)] per directed link and step: every forward
+    route's bytes per micro-batch x m on its link(s), the gradients on the mirrored ones;
+    striped, the direct link keeps its ``w0 / (w0 + relays)`` share and each relay hop
+    (src -> r, r -> dst) carries ``1 / (w0 + relays)``."""
+    w0 = (SUB + 1) / SUB
+    direct, striped = {}, {}
+
+    def add(table, a_, b_, nbytes):
+        table[(a_, b_)] = table.get((a_, b_), 0.0) + nbytes
+        table[(b_, a_)] = table.get((b_, a_), 0.0) + nbytes  # the gradients, mirrored
+
+    for src, dst, _, nb, _, _, _ in plain:
+        add(direct, src, dst, nb * m)
+        rl = routes.get((src, dst), [])
+        share = w0 / (w0 + len(rl))
+        add(striped, src, dst, nb * m * share)
+        for r in rl:
+            add(striped, src, r, nb * m * (1 - share) / len(rl))
+            add(striped, r, dst, nb * m * (1 - share) / len(rl))
+    links = sorted(set(direct) | set(striped))
+    return [(a_, b_, direct.get((a_, b_), 0.0), striped.get((a_, b_), 0.0))
+            for a_, b_ in links]
 
 
 if __name__ == '__main__':
