@@ -618,6 +618,27 @@ Parts make_parts(const at::Tensor& x, at::TensorList weights, at::IntArrayRef ge
   return p;
 }
 
+// One allocation for a BatchNorm's small outputs -- sums [2][C] (the backward's reduction
+// buffer), mean [C], invstd [C], each starting on a 16-byte boundary -- followed by `extra`
+// scratch floats (the statistics partials): allocations are host time on the launch-bound
+// stages (ResNet-101 at 22-image micro-batches runs ~15 k of these ops per step).  The views
+// share one storage, so the partials live as long as the saved statistics (a few MB).
+struct StatBlock {
+  at::Tensor sums, mean, invstd;
+  float* extra;
+};
+
+StatBlock stat_block(const at::Tensor& like, int64_t c, int64_t extra) {
+  const int64_t seg = (c + 3) / 4 * 4;
+  auto all = at::empty({4 * seg + extra}, like.options());
+  StatBlock b;
+  b.sums = all.narrow(0, 0, 2 * c).view({2, c});
+  b.mean = all.narrow(0, 2 * seg, c);
+  b.invstd = all.narrow(0, 3 * seg, c);
+  b.extra = all.data_ptr<float>() + 4 * seg;
+  return b;
+}
+
 // Forward (training): returns {y, z, mean, invstd} with z the convolution output and
 // mean / invstd its batch statistics (saved for the backward).
 std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList weights,
@@ -663,7 +684,6 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
                 "num_batches_tracked must be a 1-element int64 tensor on the input's device");
     tracked = num_batches_tracked->data_ptr<int64_t>();
   }
-  auto sums = at::empty({2, c}, x.options());  // zeroed by the finalize, for the backward
   const float* ga = opt_ptr(gamma, "gamma", x, c);
   const float* be = opt_ptr(beta, "beta", x, c);
   const float* ad = nullptr;
@@ -677,9 +697,13 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
   // relu_out with a node sum: relu(bn(z) + add) (ResNet's residual join); the caller masks
   // the gradient with the saved output (the backward's re-derived mask cannot see `add`)
   auto y = at::empty_like(z);
-  auto mean = at::empty({c}, x.options());
-  auto invstd = at::empty({c}, x.options());
-  if (fused_stats && split_bn_small_ok(n, s)) {
+  const bool small = fused_stats && split_bn_small_ok(n, s);
+  const int width = split ? static_cast<int>(s) : plans[0].col_width;
+  const int blocks = split ? static_cast<int>(n) : plans[0].col_blocks;
+  // mean / invstd / the backward's sums and the statistics partials: one allocation
+  StatBlock st = stat_block(x, c, small ? 0 : 2 * static_cast<int64_t>(blocks) * c);
+  auto mean = st.mean, invstd = st.invstd, sums = st.sums;  // (sums: zeroed by the finalize)
+  if (small) {
     // small planes: the split partials reduced, normalised and their statistics taken by
     // one per-channel launch (launch_split_bn_small) instead of two
     const ConvGemmPlan& pl = plans[0];
@@ -694,12 +718,9 @@ std::vector<at::Tensor> convbn_forward(const at::Tensor& x_in, at::TensorList we
                           be, ad, y.data_ptr<float>(), stream, relu_out);
     return {y, z, mean, invstd, sums};
   }
-  const int width = split ? static_cast<int>(s) : plans[0].col_width;
-  const int blocks = split ? static_cast<int>(n) : plans[0].col_blocks;
-  auto part = at::empty({2, blocks, c}, x.options());
   // the two halves by pointer: part[k] would be an aten::select per use (host time of a
   // launch-bound stage, profiles/r5/host_profile.md)
-  float* const part0 = part.data_ptr<float>();
+  float* const part0 = st.extra;
   float* const part1 = part0 + static_cast<int64_t>(blocks) * c;
   const bool epilogue_stats = !split || fused_stats;
   for (size_t i = 0; i < p.geo.size(); ++i) {
@@ -1426,11 +1447,12 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t n = x.size(0), c = x.size(1), s = n * c == 0 ? 0 : x.numel() / (n * c);
   const auto stream = cur_stream(x);
-  auto part = at::empty({2, n, c}, x.options());
-  float* const part0 = part.data_ptr<float>();
+  // the statistics outputs and the partials in one allocation (stat_block): a launch-bound
+  // stage pays host time per allocation
+  StatBlock st = stat_block(x, c, 2 * n * c);
+  float* const part0 = st.extra;
   float* const part1 = part0 + n * c;
-  auto mean = at::empty({c}, x.options());
-  auto invstd = at::empty({c}, x.options());
+  auto mean = st.mean, invstd = st.invstd;
   auto y = at::empty_like(x);
   if (x.numel() == 0) return {y, mean.zero_(), invstd.fill_(1.f), at::zeros({2, c}, x.options())};
   double* accp = nullptr;
@@ -1453,7 +1475,7 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
   }
   launch_bn_stats(x.data_ptr<float>(), part0, part1, n, c,
                   s, stream);
-  auto sums = at::empty({2, c}, x.options());  // zeroed by the finalize, for the backward
+  auto sums = st.sums;  // zeroed by the finalize, for the backward
   launch_bn_finalize_apply(part0, part1,
                            static_cast<int>(n), static_cast<int>(s), n, c, s,
                            static_cast<float>(eps), rm != nullptr ? momentum : 0.0,
