@@ -173,23 +173,38 @@ __global__ __launch_bounds__(256) void bn_finalize_apply_kernel(
   const float mu = kb[0], k = kb[1], bb = kb[2];
   const int n0 = blockIdx.y * n_per, n1 = min(n, n0 + n_per);
   if constexpr (kVec) {
+    // two quads per thread per round, both loads issued before either is used: one
+    // 16-byte load in flight per wave left the pass short of HBM bandwidth
     const int sq = s >> 2, quads = (n1 - n0) * sq;
-    for (int q = tid; q < quads; q += 256) {
-      const int img = n0 + q / sq;
-      const int64_t off = (static_cast<int64_t>(img) * c + ch) * sq + (q - (img - n0) * sq);
-      // (z - mean) * k, not z * k - mean * k: no cancellation when |mean| >> std; one
-      // fma, the same rounding the backward's ReLU mask recomputes (bn_relu_mask)
-      const floatx4 zv = reinterpret_cast<const floatx4*>(z)[off];
-      floatx4 v;
+    for (int q0 = tid; q0 < quads; q0 += 2 * 256) {
+      int64_t zo[2], yo[2];
+      floatx4 zv[2], av[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(zv[e] - mu, k, bb);
-      if constexpr (kAdd) v += reinterpret_cast<const floatx4*>(add)[off];
-      if constexpr (kRelu) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+      for (int u = 0; u < 2; ++u) {
+        const int q = q0 + u * 256;
+        const int img = n0 + q / sq, p = q - (img - n0) * sq;
+        zo[u] = (static_cast<int64_t>(img) * c + ch) * sq + p;
+        yo[u] = (static_cast<int64_t>(img) * yc + ych) * sq + p;
+        if (q < quads) {
+          zv[u] = reinterpret_cast<const floatx4*>(z)[zo[u]];
+          if constexpr (kAdd) av[u] = reinterpret_cast<const floatx4*>(add)[zo[u]];
+        }
       }
-      reinterpret_cast<floatx4*>(y)[(static_cast<int64_t>(img) * yc + ych) * sq +
-                                    (q - (img - n0) * sq)] = v;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (q0 + u * 256 >= quads) break;
+        // (z - mean) * k, not z * k - mean * k: no cancellation when |mean| >> std; one
+        // fma, the same rounding the backward's ReLU mask recomputes (bn_relu_mask)
+        floatx4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(zv[u][e] - mu, k, bb);
+        if constexpr (kAdd) v += av[u];
+        if constexpr (kRelu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        }
+        reinterpret_cast<floatx4*>(y)[yo[u]] = v;
+      }
     }
   } else {
     // planes of s % 4 != 0 pixels (7^2, 14^2): four elements per thread per round, loads
@@ -525,17 +540,29 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
     return;
   }
   if constexpr (kVec) {
-    for (int e = threadIdx.x; e < total; e += 256) {
-      const int img = e / per, q = e - img * per;
-      const int64_t zoff = (static_cast<int64_t>(img) * c + ch) * s;
-      const float* dyp = dy + img * dy_img + static_cast<int64_t>(dyc) * s;
-      const floatx4 g = reinterpret_cast<const floatx4*>(dyp)[q];
-      const floatx4 v = reinterpret_cast<const floatx4*>(z + zoff)[q];
+    // two quads per thread per round, loads first (summed in the same order as one per
+    // round)
+    for (int e0 = threadIdx.x; e0 < total; e0 += 2 * 256) {
+      floatx4 g[2], v[2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float ge = !relu_out || bn_relu_mask(v[k], mu, k1, rb) ? g[k] : 0.f;
-        sd += ge;
-        sdz += ge * (v[k] - mu);
+      for (int u = 0; u < 2; ++u) {
+        const int e = e0 + u * 256;
+        if (e >= total) break;
+        const int img = e / per, q = e - img * per;
+        const int64_t zoff = (static_cast<int64_t>(img) * c + ch) * s;
+        g[u] = reinterpret_cast<const floatx4*>(dy + img * dy_img +
+                                                static_cast<int64_t>(dyc) * s)[q];
+        v[u] = reinterpret_cast<const floatx4*>(z + zoff)[q];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (e0 + u * 256 >= total) break;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float ge = !relu_out || bn_relu_mask(v[u][k], mu, k1, rb) ? g[u][k] : 0.f;
+          sd += ge;
+          sdz += ge * (v[u][k] - mu);
+        }
       }
     }
   } else {
@@ -582,19 +609,30 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
   const float k2 = sd * inv_m;
   const float k3 = is * is * sdz * inv_m;
   if constexpr (kVec) {
-    for (int e = threadIdx.x; e < total; e += 256) {
-      const int img = e / per, q = e - img * per;
-      const int64_t zoff = (static_cast<int64_t>(img) * c + ch) * s;
-      const float* dyp = dy + img * dy_img + static_cast<int64_t>(dyc) * s;
-      floatx4 g = reinterpret_cast<const floatx4*>(dyp)[q];
-      const floatx4 v = reinterpret_cast<const floatx4*>(z + zoff)[q];
-      floatx4 o;
+    for (int e0 = threadIdx.x; e0 < total; e0 += 2 * 256) {
+      floatx4 g[2], v[2];
+      int64_t zo[2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (relu_out && !bn_relu_mask(v[k], mu, k1, rb)) g[k] = 0.f;
-        o[k] = k1 * (g[k] - k2 - (v[k] - mu) * k3);
+      for (int u = 0; u < 2; ++u) {
+        const int e = e0 + u * 256;
+        if (e >= total) break;
+        const int img = e / per, q = e - img * per;
+        zo[u] = (static_cast<int64_t>(img) * c + ch) * s + 4 * q;
+        g[u] = reinterpret_cast<const floatx4*>(dy + img * dy_img +
+                                                static_cast<int64_t>(dyc) * s)[q];
+        v[u] = *reinterpret_cast<const floatx4*>(z + zo[u]);
       }
-      reinterpret_cast<floatx4*>(dz + zoff)[q] = o;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (e0 + u * 256 >= total) break;
+        floatx4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float gk = relu_out && !bn_relu_mask(v[u][k], mu, k1, rb) ? 0.f : g[u][k];
+          o[k] = k1 * (gk - k2 - (v[u][k] - mu) * k3);
+        }
+        *reinterpret_cast<floatx4*>(dz + zo[u]) = o;
+      }
     }
   } else {
     for (int e0 = threadIdx.x; e0 < total; e0 += 4 * 256) {
