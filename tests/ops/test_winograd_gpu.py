@@ -242,6 +242,9 @@ BG_SHAPES = [  # (N, C, K, H, W)
     (3, 70, 130, 13, 11),      # ragged channels / planes: every padding path
     (1, 16, 8, 5, 7),
     (40, 128, 96, 12, 12),     # 360 tiles: BN 128
+    # the split-bf16 input image at 4 channels per thread (the smaller grids above take 2
+    # or 1: launch_bg_conv)
+    (4, 64, 48, 192, 192),
 ]
 
 

@@ -1576,6 +1576,47 @@ __device__ __forceinline__ void bg_emu_store(float* out, const float (&v)[4][NPO
   }
 }
 
+// CPT (1 / 2 / 4) consecutive reduction values k = q*CPT .. of one row at every position:
+// one 2 / 4 / 8-byte store per (position, plane) -- the input images of small tile counts
+// run 2-4x as many threads as the 4-value stores allow (see launch_bg_conv).
+template <int NPOS, int CPT>
+__device__ __forceinline__ void bg_emu_store_n(float* out, const float (&v)[CPT][NPOS], int st,
+                                               int row, int q, int rows, int ksteps) {
+  if constexpr (CPT == 4) {
+    bg_emu_store<NPOS>(out, v, st, row, q, rows, ksteps);
+  } else {
+    __bf16* base = reinterpret_cast<__bf16*>(out);
+    const int k0 = q * CPT, g = k0 >> 2;
+    const int64_t pstride = static_cast<int64_t>(rows) * 8;
+    const int64_t off = (static_cast<int64_t>(st) * 6 + (g >> 1)) * pstride +
+                        static_cast<int64_t>(row) * 8 + 4 * (g & 1) + (k0 & 3);
+    const int64_t pos_stride = static_cast<int64_t>(ksteps) * 6 * pstride;
+#pragma unroll
+    for (int b = 0; b < NPOS; ++b) {
+      __bf16 pl[3][CPT];
+#pragma unroll
+      for (int e = 0; e < CPT; ++e) {  // bg_split3's arithmetic, element by element
+        const __bf16 h = static_cast<__bf16>(v[e][b]);
+        const float r = v[e][b] - static_cast<float>(h);
+        const __bf16 m = static_cast<__bf16>(r);
+        pl[0][e] = h;
+        pl[1][e] = m;
+        pl[2][e] = static_cast<__bf16>(r - static_cast<float>(m));
+      }
+      __bf16* dst = base + b * pos_stride + off;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        if constexpr (CPT == 2) {
+          typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<bf16x2_t*>(dst + 2 * p * pstride) = bf16x2_t{pl[p][0], pl[p][1]};
+        } else {
+          dst[2 * p * pstride] = pl[p][0];
+        }
+      }
+    }
+  }
+}
+
 // U (EMU image) of (output channel m, reduction channels st*16 + 4g .. +3).
 __global__ __launch_bounds__(256) void bg_weight_f4_emu_kernel(const float* __restrict__ w,
                                                               float* __restrict__ a, int O, int R,
@@ -1592,25 +1633,26 @@ __global__ __launch_bounds__(256) void bg_weight_f4_emu_kernel(const float* __re
   bg_emu_store<kP>(a, v, st, m, g, Mp, ksteps);
 }
 
-// V (EMU image) of (tile t, channels st*16 + 4g .. +3); zeros in the padding.
-template <bool kVec>
+// V (EMU image) of (tile t, channels st*16 + CPT*q .. +CPT-1); zeros in the padding.
+template <bool kVec, int CPT>
 __global__ __launch_bounds__(256) void bg_input_f4_emu_kernel(const float* __restrict__ x,
                                                              float* __restrict__ v, int R, int H,
                                                              int W, int TW, int tpi, int P, int Np,
                                                              int ksteps, uint32_t x_bytes) {
+  constexpr int kQ = 16 / CPT;  // threads per (tile, step)
   const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (idx >= static_cast<int64_t>(ksteps) * 4 * Np) return;
-  const int g = static_cast<int>(idx & 3);
-  const int64_t rest = idx >> 2;
+  if (idx >= static_cast<int64_t>(ksteps) * kQ * Np) return;
+  const int g = static_cast<int>(idx % kQ);
+  const int64_t rest = idx / kQ;
   const int t = static_cast<int>(rest % Np);
   const int st = static_cast<int>(rest / Np);
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), static_cast<short>(0),
                                         static_cast<int>(x_bytes), 0x00020000);
-  float out[4][kP];
+  float out[CPT][kP];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int c = st * 16 + 4 * g + e;
+  for (int e = 0; e < CPT; ++e) {
+    const int c = st * 16 + CPT * g + e;
     F4Patch p;
     if (t < P && c < R) {
       f4_fwd_offsets(p, t, c, P, tpi, TW, R, H, W);
@@ -1623,7 +1665,7 @@ __global__ __launch_bounds__(256) void bg_input_f4_emu_kernel(const float* __res
 #pragma unroll
     for (int b = 0; b < kP; ++b) out[e][b] = p.d[b];
   }
-  bg_emu_store<kP>(v, out, st, t, g, Np, ksteps);
+  bg_emu_store_n<kP, CPT>(v, out, st, t, g, Np, ksteps);
 }
 
 // C[z][b][Mp][Np] = sum over the split's steps of A[b]^T B[b] on split-bf16 operands.
@@ -2080,20 +2122,23 @@ __global__ __launch_bounds__(256) void bg_weight_f2_emu_kernel(const float* __re
   bg_emu_store<kP2>(a, v, st, m, g, Mp, ksteps);
 }
 
+template <int CPT>
 __global__ __launch_bounds__(256) void bg_input_f2_emu_kernel(const float* __restrict__ x,
                                                              float* __restrict__ v, int R, int H,
                                                              int W, int TW, int tpi, int P, int Np,
                                                              int ksteps) {
+  constexpr int kQ = 16 / CPT;
   const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (idx >= static_cast<int64_t>(ksteps) * 4 * Np) return;
-  const int g = static_cast<int>(idx & 3);
-  const int64_t rest = idx >> 2;
+  if (idx >= static_cast<int64_t>(ksteps) * kQ * Np) return;
+  const int g = static_cast<int>(idx % kQ);
+  const int64_t rest = idx / kQ;
   const int t = static_cast<int>(rest % Np);
   const int st = static_cast<int>(rest / Np);
-  float vv[4][kP2];
+  float vv[CPT][kP2];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) f2_input_tile(x, R, H, W, TW, tpi, P, t, st * 16 + 4 * g + e, vv[e]);
-  bg_emu_store<kP2>(v, vv, st, t, g, Np, ksteps);
+  for (int e = 0; e < CPT; ++e)
+    f2_input_tile(x, R, H, W, TW, tpi, P, t, st * 16 + CPT * g + e, vv[e]);
+  bg_emu_store_n<kP2, CPT>(v, vv, st, t, g, Np, ksteps);
 }
 
 __global__ __launch_bounds__(256) void bg_output_f2_kernel(
@@ -2495,20 +2540,29 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
   float* cbuf = ws + npos * plan.ksteps * (plan.emu ? 24 : 16) * plan.np;
   const int64_t vt = plan.ksteps * 16 * plan.np;
   if (plan.emu) {
+    // channels per thread: 4 (8-byte stores) while that fills the chip with >= 512
+    // workgroups, else 2 or 1 -- ResNet's 14^2 / 7^2 layers at 22-image micro-batches
+    // gave 96-workgroup grids at 4
     const int64_t vt4 = plan.ksteps * 4 * plan.np;
-    const dim3 grid(static_cast<unsigned>((vt4 + 255) / 256));
-    if (plan.kind == 2)
-      hipLaunchKernelGGL(bg_input_f2_emu_kernel, grid, dim3(256), 0, stream, x, v,
-                         static_cast<int>(red_channels), static_cast<int>(h), static_cast<int>(w),
-                         static_cast<int>(tw), static_cast<int>(th * tw), static_cast<int>(P),
-                         static_cast<int>(plan.np), static_cast<int>(plan.ksteps));
-    else
-      hipLaunchKernelGGL((w & 3) == 0 ? bg_input_f4_emu_kernel<true> : bg_input_f4_emu_kernel<false>,
-                         grid, dim3(256), 0, stream, x, v, static_cast<int>(red_channels),
-                         static_cast<int>(h), static_cast<int>(w), static_cast<int>(tw),
-                         static_cast<int>(th * tw), static_cast<int>(P), static_cast<int>(plan.np),
-                         static_cast<int>(plan.ksteps),
+    const int cpt = (vt4 + 255) / 256 >= 512 ? 4 : (vt4 * 2 + 255) / 256 >= 512 ? 2 : 1;
+    const dim3 grid(static_cast<unsigned>((vt4 * (4 / cpt) + 255) / 256));
+    const int ri = static_cast<int>(red_channels), hi = static_cast<int>(h),
+              wi = static_cast<int>(w), twi = static_cast<int>(tw), tpi = static_cast<int>(th * tw),
+              pi = static_cast<int>(P), npi = static_cast<int>(plan.np),
+              ki = static_cast<int>(plan.ksteps);
+    if (plan.kind == 2) {
+      auto kern = cpt == 4 ? bg_input_f2_emu_kernel<4>
+                  : cpt == 2 ? bg_input_f2_emu_kernel<2> : bg_input_f2_emu_kernel<1>;
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, x, v, ri, hi, wi, twi, tpi, pi, npi,
+                         ki);
+    } else {
+      const bool vec = (w & 3) == 0;
+      auto kern = vec ? bg_input_f4_emu_kernel<true, 4> : bg_input_f4_emu_kernel<false, 4>;
+      if (cpt == 2) kern = vec ? bg_input_f4_emu_kernel<true, 2> : bg_input_f4_emu_kernel<false, 2>;
+      if (cpt == 1) kern = vec ? bg_input_f4_emu_kernel<true, 1> : bg_input_f4_emu_kernel<false, 1>;
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, x, v, ri, hi, wi, twi, tpi, pi, npi, ki,
                          static_cast<uint32_t>(n * red_channels * h * w * 4));
+    }
   } else if (plan.kind == 2) {
     hipLaunchKernelGGL(bg_input_f2_kernel, dim3(static_cast<unsigned>((vt + 255) / 256)),
                        dim3(256), 0, stream, x, v, static_cast<int>(red_channels),
