@@ -107,22 +107,3 @@ def test_refresh_step_caches_names_the_stage_sources(monkeypatch):
     assert seen[0][0] is derived
     assert seen[0][1:] == fakes
 
-
-def test_f4_weight_gradient_variant_choice():
-    """``ops/conv.py`` ``_wgrad_f4_variant`` (shapes only, measured in
-    profiles/r6/wgrad_small_probe.json): fused below 256 channels and on U-Net's 48^2 level,
-    non-fused f32 for ResNet's 256-channel 14^2 layers, split-bf16 for the deep wide grids."""
-    from torchgpipe_amd.ops.conv import _wgrad_f4_variant
-
-    def pick(n, c, k, h):
-        return _wgrad_f4_variant(torch.empty(n, c, h, h, device='meta'),
-                                 torch.empty(k, c, 3, 3, device='meta'))
-
-    assert pick(22, 128, 128, 28) == 0
-    assert pick(22, 256, 256, 14) == 1
-    assert pick(110, 256, 256, 14) == 1
-    assert pick(16, 256, 256, 48) == 0
-    assert pick(40, 512, 256, 48) == 2
-    assert pick(16, 512, 256, 48) == 0
-    assert pick(22, 512, 512, 7) == 1
-    assert pick(40, 512, 512, 24) == 2

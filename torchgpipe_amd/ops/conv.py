@@ -487,18 +487,15 @@ def _wgrad_f4_variant(x: Tensor, weight: Tensor) -> int:
     (40 x 512^2 at 24^2: 0.321 vs 0.401 ms; 40 x 1024^2 at 12^2: 0.286 vs 0.334), the f32
     one (1) below (16 x 2048^2 at 6^2: 0.294 vs 0.474).
 
-    Round 6 (benchmarks/diag/wgrad_small_probe.py, profiles/r6/wgrad_small_probe.json):
-    256-511 channels at up to 2048 tiles (ResNet-101's 14^2 layers at its pipeline
-    micro-batches) take the non-fused f32 kernel too (22 images: 57.1 vs 59.0 us; 110:
-    152.5 vs 177.7), U-Net's 48^2 level stays fused (16 images, 2304 tiles: 178.9 vs
-    219.1); 512 -> 256 channels at >= 4096 tiles the split-bf16 one (U-Net's decoder at
-    48^2, 40 images: 737.9 vs 819.6)."""
-    lo, hi = sorted((weight.shape[0], weight.shape[1]))
+    Round 6 (benchmarks/diag/wgrad_small_probe.py, profiles/r6/wgrad_small_probe.json): in
+    isolation the non-fused kernel led by 3-14 % on ResNet-101's 256-channel 14^2 layers,
+    but inside the stage (after the backward-data pass, with x / dy warm in L2) the fused
+    kernel's 1792 dispatches plus the rest came to 125.9 ms of ResNet p4 stage 3's kernel
+    time against 130.5 ms for the non-fused passes (profiles/r6/bg_input_cpt/
+    p4_new_wgrad_rule.md), so the rule stayed as it was."""
+    if min(weight.shape[0], weight.shape[1]) < 512:
+        return 0
     tiles = x.shape[0] * -(-x.shape[2] // 4) * -(-x.shape[3] // 4)
-    if lo < 512:
-        if lo >= 256 and WGRAD_EMU and hi >= 512 and tiles >= 4096:
-            return 2
-        return 1 if lo >= 256 and tiles <= 2048 else 0
     return 2 if WGRAD_EMU and tiles >= WGRAD_EMU_MIN_TILES else 1
 
 
