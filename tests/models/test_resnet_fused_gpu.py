@@ -37,6 +37,9 @@ CASES = [
     (2, 128, 56, 128, 3, 2, 1),
     (2, 256, 56, 512, 1, 2, 0),
     (2, 512, 14, 512, 3, 2, 1),
+    (2, 3, 224, 64, 7, 2, 3),     # (round 6: the stem and the 28^2 / 14^2 downsamples)
+    (2, 512, 28, 1024, 1, 2, 0),
+    (2, 1024, 14, 2048, 1, 2, 0),
 ]
 
 

@@ -194,12 +194,19 @@ STRIDED_CHOICE = os.environ.get('TGPIPE_STRIDED_CHOICE', '0') != '0'
 # statistics in its epilogue, stride-phase backward-data -- measured faster than MIOpen +
 # the native BatchNorm at ResNet-101's pipeline-1 micro-batch of 110
 # (benchmarks/diag/resnet_strided_probe.py, profiles/r4/resnet/resnet_strided_probe_r4ac.jsonl:
-# 1386 / 1612 / 1178 vs 1440 / 1714 / 1355 us forward + backward); the other strided
-# convolutions (the 7x7 stem, the 28^2 3x3, the 28^2 / 14^2 downsamples) stay on MIOpen.
+# 1386 / 1612 / 1178 vs 1440 / 1714 / 1355 us forward + backward).  Round 6 re-timed every
+# strided geometry on the split-bf16 kernels at 15 / 22 / 36 / 110 images
+# (benchmarks/diag/strided_picks.py, profiles/r6/strided_picks.json): the 7x7 stem and the
+# 28^2 / 14^2 downsamples now win at every size too (ResNet p4 stage 3 / p8 stage 3 kernel
+# time -1.1 / -1.4 %, 3.8 k / 1.9 k launches fewer per step: profiles/r6/strided/); the 28^2
+# 3x3 wins at 15 and 36 images but not at 22 or 110 and stays on MIOpen.
 STRIDED_FUSED = frozenset({
+    (3, 64, (7, 7), (2, 2), (3, 3), 224),
     (128, 128, (3, 3), (2, 2), (1, 1), 56),
     (256, 512, (1, 1), (2, 2), (0, 0), 56),
+    (512, 1024, (1, 1), (2, 2), (0, 0), 28),
     (512, 512, (3, 3), (2, 2), (1, 1), 14),
+    (1024, 2048, (1, 1), (2, 2), (0, 0), 14),
 })
 
 
