@@ -195,6 +195,39 @@ def test_residual_join_runs_conv3_bn3_add_relu_as_one_op(shape):
     assert rel_err(fused.bn3.running_var, plain.bn3.running_var) < 2e-6
 
 
+@pytest.mark.parametrize('shape', [(4, 256, 14), (2, 1024, 7), (12, 128, 56)],
+                         ids=['vec', 'scalar', 'two-pass'])
+def test_join_mask_inside_batchnorm_backward_matches_separate_relu(shape):
+    """The residual join's ReLU mask applied inside the BatchNorm backward (the mask from the
+    saved output, the masked gradient written for the identity: ``convbn_backward``'s
+    ``y_mask``) against the same join computed as Conv-BN, then ``relu(y + identity)`` by
+    autograd -- same forward arithmetic, so the same ReLU decisions: every gradient equal.
+    14^2: the 16-byte one-pass kernel, 7^2: its scalar loop, 56^2 at 12 images (37.6 k
+    values per channel): the two-pass backward after a separate masking pass."""
+    from torchgpipe_amd.ops.convbn import relu_conv_bn
+    n, c, hw = shape
+    torch.manual_seed(3)
+    conv = nn.Conv2d(c, c, 1, bias=False).cuda()
+    bn = nn.BatchNorm2d(c).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    x = torch.randn(n, c, hw, hw, device='cuda')
+    ident = torch.randn(n, c, hw, hw, device='cuda')
+    g = torch.randn(n, c, hw, hw, device='cuda')
+    xa, ia = x.clone().requires_grad_(True), ident.clone().requires_grad_(True)
+    ya = relu_conv_bn(xa, [(conv, 0)], bn, relu=False, add=ia, relu_out=True)
+    ya.backward(g)
+    xb, ib = x.clone().requires_grad_(True), ident.clone().requires_grad_(True)
+    yb = torch.relu(relu_conv_bn(xb, [(conv2, 0)], bn2, relu=False) + ib)
+    yb.backward(g)
+    torch.testing.assert_close(ya, yb, rtol=0, atol=0)
+    for a, b in [(xa.grad, xb.grad), (ia.grad, ib.grad), (conv.weight.grad, conv2.weight.grad),
+                 (bn.weight.grad, bn2.weight.grad), (bn.bias.grad, bn2.bias.grad)]:
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6 * (b.abs().max().item() + 1))
+
+
 def test_native_batchnorm_affine_gradients_accumulate_across_micro_batches():
     """The native BatchNorm(+ReLU) after a Winograd 3x3 (``_BNAct``) adds its gamma / beta
     gradients into ``.grad`` in the kernel (ops/gradacc.py) -- over several backward

@@ -498,13 +498,18 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(
 // sums -- one launch instead of bn_bwd_reduce + bn_bwd_dz, no atomics, for channels small
 // enough (n * s elements) that the second read of dy / z comes back from L2.  Same
 // arithmetic per element as the two-pass kernels.
-template <bool kVec>
+// kOutMask (ResNet's residual join, relu(bn(z) + identity)): the ReLU mask comes from the
+// join's saved output y (same layout as z), the masked gradient -- the identity's gradient
+// as well -- is written to gout in the first pass and read back from there in the second,
+// instead of a separate threshold_backward pass over dy before this kernel.
+template <bool kVec, bool kOutMask>
 __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
     const float* __restrict__ dy, const float* __restrict__ z, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ dz, float* __restrict__ dgamma,
     float* __restrict__ dbeta, int acc_gamma, int acc_beta, int n, int c, int s, float inv_m,
-    int64_t dy_img, int relu_out, BnParts parts) {
+    int64_t dy_img, int relu_out, BnParts parts, const float* __restrict__ ymask,
+    float* __restrict__ gout) {
   const int ch = blockIdx.x;
   int dyc = ch;  // dy's channel index (its own part's, with parts)
   if (parts.count > 0) {
@@ -543,26 +548,34 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
     // two quads per thread per round, loads first (summed in the same order as one per
     // round)
     for (int e0 = threadIdx.x; e0 < total; e0 += 2 * 256) {
-      floatx4 g[2], v[2];
+      floatx4 g[2], v[2], ym[2];
+      int64_t zo[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int e = e0 + u * 256;
         if (e >= total) break;
         const int img = e / per, q = e - img * per;
-        const int64_t zoff = (static_cast<int64_t>(img) * c + ch) * s;
+        zo[u] = (static_cast<int64_t>(img) * c + ch) * s + 4 * q;
         g[u] = reinterpret_cast<const floatx4*>(dy + img * dy_img +
                                                 static_cast<int64_t>(dyc) * s)[q];
-        v[u] = reinterpret_cast<const floatx4*>(z + zoff)[q];
+        v[u] = *reinterpret_cast<const floatx4*>(z + zo[u]);
+        if constexpr (kOutMask) ym[u] = *reinterpret_cast<const floatx4*>(ymask + zo[u]);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (e0 + u * 256 >= total) break;
+        floatx4 gm;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float ge = !relu_out || bn_relu_mask(v[u][k], mu, k1, rb) ? g[u][k] : 0.f;
+          bool keep;
+          if constexpr (kOutMask) keep = ym[u][k] > 0.f;
+          else keep = !relu_out || bn_relu_mask(v[u][k], mu, k1, rb);
+          const float ge = keep ? g[u][k] : 0.f;
+          gm[k] = ge;
           sd += ge;
           sdz += ge * (v[u][k] - mu);
         }
+        if constexpr (kOutMask) *reinterpret_cast<floatx4*>(gout + zo[u]) = gm;
       }
     }
   } else {
@@ -570,19 +583,26 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
     // element per round left a load latency per element exposed: 27.6 us per 1024-channel
     // 7^2 BatchNorm at 40 images in the stage-6 trace); summed in the same order
     for (int e0 = threadIdx.x; e0 < total; e0 += 4 * 256) {
-      float gv[4], zv[4];
+      float gv[4], zv[4], yv[4];
+      int64_t zo[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int e = e0 + u * 256;
         const int img = e / per, q = e - img * per;
         const bool in = e < total;
-        zv[u] = in ? z[(static_cast<int64_t>(img) * c + ch) * s + q] : 0.f;
+        zo[u] = (static_cast<int64_t>(img) * c + ch) * s + q;
+        zv[u] = in ? z[zo[u]] : 0.f;
         gv[u] = in ? dy[img * dy_img + static_cast<int64_t>(dyc) * s + q] : 0.f;
+        if constexpr (kOutMask) yv[u] = in ? ymask[zo[u]] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (e0 + u * 256 >= total) break;
-        const float g = !relu_out || bn_relu_mask(zv[u], mu, k1, rb) ? gv[u] : 0.f;
+        bool keep;
+        if constexpr (kOutMask) keep = yv[u] > 0.f;
+        else keep = !relu_out || bn_relu_mask(zv[u], mu, k1, rb);
+        const float g = keep ? gv[u] : 0.f;
+        if constexpr (kOutMask) gout[zo[u]] = g;
         sd += g;
         sdz += g * (zv[u] - mu);
       }
@@ -618,8 +638,10 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
         if (e >= total) break;
         const int img = e / per, q = e - img * per;
         zo[u] = (static_cast<int64_t>(img) * c + ch) * s + 4 * q;
-        g[u] = reinterpret_cast<const floatx4*>(dy + img * dy_img +
-                                                static_cast<int64_t>(dyc) * s)[q];
+        // (kOutMask: this thread's own first-pass store, masked already)
+        if constexpr (kOutMask) g[u] = *reinterpret_cast<const floatx4*>(gout + zo[u]);
+        else g[u] = reinterpret_cast<const floatx4*>(dy + img * dy_img +
+                                                     static_cast<int64_t>(dyc) * s)[q];
         v[u] = *reinterpret_cast<const floatx4*>(z + zo[u]);
       }
 #pragma unroll
@@ -628,7 +650,8 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
         floatx4 o;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float gk = relu_out && !bn_relu_mask(v[u][k], mu, k1, rb) ? 0.f : g[u][k];
+          const float gk =
+              !kOutMask && relu_out && !bn_relu_mask(v[u][k], mu, k1, rb) ? 0.f : g[u][k];
           o[k] = k1 * (gk - k2 - (v[u][k] - mu) * k3);
         }
         *reinterpret_cast<floatx4*>(dz + zo[u]) = o;
@@ -645,13 +668,14 @@ __global__ __launch_bounds__(256) void bn_bwd_channel_kernel(
         const bool in = e < total;
         zo[u] = (static_cast<int64_t>(img) * c + ch) * s + q;
         zv[u] = in ? z[zo[u]] : 0.f;
-        gv[u] = in ? dy[img * dy_img + static_cast<int64_t>(dyc) * s + q] : 0.f;
+        if constexpr (kOutMask) gv[u] = in ? gout[zo[u]] : 0.f;
+        else gv[u] = in ? dy[img * dy_img + static_cast<int64_t>(dyc) * s + q] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (e0 + u * 256 >= total) break;
         float g = gv[u];
-        if (relu_out && !bn_relu_mask(zv[u], mu, k1, rb)) g = 0.f;
+        if (!kOutMask && relu_out && !bn_relu_mask(zv[u], mu, k1, rb)) g = 0.f;
         dz[zo[u]] = k1 * (g - k2 - (zv[u] - mu) * k3);
       }
     }
@@ -864,38 +888,55 @@ void launch_bn_backward_parts(const BnParts& parts, const float* z, const float*
                        static_cast<const float*>(nullptr), static_cast<const float*>(nullptr),
                        dz, static_cast<float*>(nullptr), static_cast<float*>(nullptr), 0, 0,
                        static_cast<int>(n), static_cast<int>(c), static_cast<int>(s), inv_m1,
-                       int64_t{0}, 0, parts);
+                       int64_t{0}, 0, parts, static_cast<const float*>(nullptr),
+                       static_cast<float*>(nullptr));
   };
-  if (vec) go(bn_bwd_channel_kernel<true>);
-  else go(bn_bwd_channel_kernel<false>);
+  if (vec) go(bn_bwd_channel_kernel<true, false>);
+  else go(bn_bwd_channel_kernel<false, false>);
+}
+
+bool bn_backward_one_pass(int64_t n, int64_t c, int64_t s, int64_t dy_img) {
+  // Channels of up to 32 k elements: one workgroup per channel does both passes (its dy /
+  // z stay in L2 between them).  TGPIPE_BN_BWD_ONEPASS=0: always two passes.
+  static const int64_t one_pass_max = [] {
+    const char* v = std::getenv("TGPIPE_BN_BWD_ONEPASS");
+    return v != nullptr && std::string(v) == "0" ? int64_t{0} : int64_t{32768};
+  }();
+  if (dy_img <= 0) dy_img = c * s;
+  return n * s <= one_pass_max && c >= 64 && n * s * c < (int64_t{1} << 31) &&
+         dy_img < (int64_t{1} << 31);
 }
 
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
                         bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
-                        int64_t dy_img, hipStream_t stream, bool relu_out, const float* beta) {
+                        int64_t dy_img, hipStream_t stream, bool relu_out, const float* beta,
+                        const float* ymask, float* gout) {
   if (dy_img <= 0) dy_img = c * s;
   const int64_t total = n * c * s;
   if (total == 0) return;
-  // Channels of up to kBwdChannelMax elements: one workgroup per channel does both passes
-  // (its dy / z stay in L2 between them).  TGPIPE_BN_BWD_ONEPASS=0: always two passes.
-  static const int64_t one_pass_max = [] {
-    const char* v = std::getenv("TGPIPE_BN_BWD_ONEPASS");
-    return v != nullptr && std::string(v) == "0" ? int64_t{0} : int64_t{32768};
-  }();
-  if (n * s <= one_pass_max && c >= 64 && n * s * c < (int64_t{1} << 31) &&
-      dy_img < (int64_t{1} << 31)) {
+  if (bn_backward_one_pass(n, c, s, dy_img)) {
     const float inv_m1 = 1.f / static_cast<float>(n * s);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(c)), dim3(256), 0, stream, dy, z, mean,
                          invstd, gamma, beta, dz, dgamma, dbeta, acc_gamma ? 1 : 0,
                          acc_beta ? 1 : 0, static_cast<int>(n), static_cast<int>(c),
-                         static_cast<int>(s), inv_m1, dy_img, relu_out ? 1 : 0, BnParts{});
+                         static_cast<int>(s), inv_m1, dy_img, relu_out ? 1 : 0, BnParts{},
+                         ymask, gout);
     };
-    if ((s & 3) == 0 && (dy_img & 3) == 0) go(bn_bwd_channel_kernel<true>);
-    else go(bn_bwd_channel_kernel<false>);
+    const bool vec = (s & 3) == 0 && (dy_img & 3) == 0;
+    if (ymask != nullptr) {
+      if (vec) go(bn_bwd_channel_kernel<true, true>);
+      else go(bn_bwd_channel_kernel<false, true>);
+    } else if (vec) {
+      go(bn_bwd_channel_kernel<true, false>);
+    } else {
+      go(bn_bwd_channel_kernel<false, false>);
+    }
     return;
   }
+  // (ymask / gout only where bn_backward_one_pass holds: convbn_backward masks dy itself
+  // elsewhere)
   // enough (channel, image range) workgroups to cover the chip ~4x
   int64_t splits = (1024 + c - 1) / c;
   if (splits > n) splits = n;

@@ -951,11 +951,38 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                                         const c10::List<c10::optional<at::Tensor>>& slabs,
                                         at::IntArrayRef slab_first,
                                         const c10::optional<at::Tensor>& beta, bool relu_out,
-                                        const c10::optional<at::Tensor>& dx_into) {
+                                        const c10::optional<at::Tensor>& dx_into,
+                                        const c10::optional<at::Tensor>& y_mask,
+                                        const c10::optional<at::Tensor>& dy_masked) {
   auto x = x_in.contiguous();
   // dy is read in place when it is a channel slice (a concatenated cell output's gradient)
   int64_t dy_img = image_stride_if_channel_slice(dy_in);
   auto dy = dy_img > 0 ? dy_in : dy_in.contiguous();
+  // y_mask (the residual join relu(bn(z) + add)'s output): dy is the join's output gradient;
+  // masked by y > 0 into dy_masked (the add's gradient too) -- inside the BatchNorm backward
+  // where its one-pass kernel runs, by threshold_backward before it otherwise
+  const bool out_mask = y_mask.has_value() && y_mask->defined();
+  const float* ymask_ptr = nullptr;
+  float* gout_ptr = nullptr;
+  if (out_mask) {
+    TORCH_CHECK(!relu_out, "y_mask and relu_out exclude each other");
+    TORCH_CHECK(dy_masked.has_value() && dy_masked->defined() && dy_masked->is_contiguous() &&
+                    dy_masked->sizes() == z.sizes() && y_mask->is_contiguous() &&
+                    y_mask->sizes() == z.sizes(),
+                "y_mask needs a contiguous dy_masked output, both of z's shape");
+    check_f32(*y_mask, "y_mask", x_in);
+    check_f32(*dy_masked, "dy_masked", x_in);
+    // (dy read through its image stride; y / dy_masked in z's contiguous layout)
+    const int64_t zs = z.size(2) * z.size(3);
+    if (bn_backward_one_pass(z.size(0), z.size(1), zs, dy_img > 0 ? dy_img : z.size(1) * zs)) {
+      ymask_ptr = y_mask->data_ptr<float>();
+      gout_ptr = dy_masked->data_ptr<float>();
+    } else {
+      at::threshold_backward_out(const_cast<at::Tensor&>(*dy_masked), dy, *y_mask, 0);
+      dy = *dy_masked;
+      dy_img = 0;
+    }
+  }
   if (dy_img == 0) {
     check_f32(dy, "dy", x);
   } else {
@@ -994,7 +1021,7 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
                      invstd.data_ptr<float>(), ga, sums.data_ptr<float>(), dz.data_ptr<float>(),
                      dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), into[0].defined(),
                      into[1].defined(), n, c, s, dy_img, stream, relu_out,
-                     opt_ptr(beta, "beta", x, c));
+                     opt_ptr(beta, "beta", x, c), ymask_ptr, gout_ptr);
   std::vector<at::Tensor> out;
   at::Tensor dx;
   // `dx_into`: a gradient of the same input from another consumer (ResNet's identity path,
@@ -1702,8 +1729,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("convbn_backward(Tensor dy, Tensor x, Tensor z, Tensor mean, Tensor invstd, "
         "Tensor(a!) sums, Tensor? gamma, Tensor[] weights, int[] geo, bool relu, bool need_dx, "
         "Tensor?[] accum, Tensor[] weights_t, bool defer_wgrad, Tensor?[] slabs, "
-        "int[] slab_first, Tensor? beta=None, bool relu_out=False, Tensor? dx_into=None) "
-        "-> Tensor[]");
+        "int[] slab_first, Tensor? beta=None, bool relu_out=False, Tensor? dx_into=None, "
+        "Tensor? y_mask=None, Tensor(b!)? dy_masked=None) -> Tensor[]");
   m.def("convbn_group_forward(Tensor x, Tensor w_cat, int[] geo, bool relu, int[] channels, "
         "Tensor?[] gammas, Tensor?[] betas, Tensor?[] running_means, Tensor?[] running_vars, "
         "Tensor?[] tracked, float momentum, float eps) -> Tensor[]");

@@ -326,11 +326,16 @@ void launch_bn_backward_parts(const BnParts& parts, const float* z, const float*
                               hipStream_t stream);
 // relu_out: the forward applied a ReLU after the normalisation (launch_bn_finalize_apply's
 // `relu`); dy is that ReLU's output gradient and its mask is re-derived from z (needs beta).
+// ymask / gout (ResNet's residual join relu(bn(z) + identity), relu_out false): dy is masked
+// by ymask > 0 (the join's output, z's layout) inside the kernel and the masked gradient
+// written to gout -- only where bn_backward_one_pass(n, c, s, dy_img) holds.
+bool bn_backward_one_pass(int64_t n, int64_t c, int64_t s, int64_t dy_img);
 void launch_bn_backward(const float* dy, const float* z, const float* mean, const float* invstd,
                         const float* gamma, float* sums, float* dz, float* dgamma, float* dbeta,
                         bool acc_gamma, bool acc_beta, int64_t n, int64_t c, int64_t s,
                         int64_t dy_img, hipStream_t stream,  // dy_img: dy's image stride
-                        bool relu_out = false, const float* beta = nullptr);
+                        bool relu_out = false, const float* beta = nullptr,
+                        const float* ymask = nullptr, float* gout = nullptr);
 
 // 3x3 average pool, padding 1, count_include_pad = False, stride 1 / 2 (pool.hip):
 // y = pool(x) (+ add) over `planes` = N*C planes of h x w; backward gathers dx.

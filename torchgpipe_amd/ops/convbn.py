@@ -172,8 +172,11 @@ class _ConvBN(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy: Tensor):  # type: ignore[override]
         x, z, mean, invstd, sums, gamma, beta, y, *weights = ctx.saved_tensors
-        if y is not None:  # relu(bn(z) + add): the gradient of both terms, masked once
-            dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
+        masked = None
+        if y is not None:
+            # relu(bn(z) + add): the gradient of both terms, masked once -- by the BatchNorm
+            # backward kernel, which also writes the masked gradient (the add's) to `masked`
+            masked = torch.empty_like(z)
         need_dx = ctx.needs_input_grad[0]
         fused = [gradacc.target(p) for p in ctx.params]
         # the backward-data GEMM reads W^T: transposed once per step, not per micro-batch
@@ -197,7 +200,9 @@ class _ConvBN(torch.autograd.Function):
         dx, dgamma, dbeta, *dws = ops.convbn_backward(
             dy, x, z, mean, invstd, sums, gamma, weights, ctx.geo, ctx.relu, need_dx,
             [into for _, into in fused], wts, side is not None, slabs, firsts, beta,
-            ctx.relu_out, dx_into)
+            ctx.relu_out, dx_into, y, masked)
+        if masked is not None:
+            dy = masked
         dadd = dy if ctx.has_add and ctx.needs_input_grad[1] else None
         if dadd is not None and ctx.sink_out is not None:
             ctx.sink_out.grad = dadd  # the reader's backward adds it (see GradSink)
