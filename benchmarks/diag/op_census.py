@@ -1,8 +1,9 @@
 """Which aten ops launch the non-native kernels of a pipeline partition: one micro-batch's
-forward + backward of ResNet-101 layers [lo, hi) under ``torch.profiler``, CPU ops with
-their CUDA kernel counts, grouped by a short Python stack.
+forward + backward of ResNet-101's / AmoebaNet-D(18,256)'s layers [lo, hi) under
+``torch.profiler``, CPU ops with their CUDA kernel counts, grouped by a short Python stack.
 
     python benchmarks/diag/op_census.py --lo 260 --hi 370 --batch 22
+    python benchmarks/diag/op_census.py --model amoebanet --lo 9 --hi 24 --batch 40
 """
 import argparse
 import os
@@ -15,7 +16,7 @@ from torch.profiler import ProfilerActivity, profile
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
-from torchgpipe_amd.models import resnet101  # noqa: E402
+from torchgpipe_amd.models import amoebanetd, resnet101  # noqa: E402
 from torchgpipe_amd.ops.fusion import relink  # noqa: E402
 from torchgpipe_amd.skip.tracker import SkipTracker, use_skip_tracker  # noqa: E402
 
@@ -25,9 +26,13 @@ def main():
     p.add_argument('--lo', type=int, default=260)
     p.add_argument('--hi', type=int, default=370)
     p.add_argument('--batch', type=int, default=22)
+    p.add_argument('--model', choices=['resnet101', 'amoebanet'], default='resnet101')
     a = p.parse_args()
     dev = torch.device('cuda')
-    model = resnet101(num_classes=1000).to(dev)
+    if a.model == 'amoebanet':
+        model = amoebanetd(num_classes=1000, num_layers=18, num_filters=256).to(dev)
+    else:
+        model = resnet101(num_classes=1000).to(dev)
     layers = list(model.children())
     head = torch.nn.Sequential(*layers[:a.lo])
     part = torch.nn.Sequential(*layers[a.lo:a.hi])
@@ -42,7 +47,10 @@ def main():
         with use_skip_tracker(SkipTracker()):
             with torch.no_grad():
                 x = head(image)
-            y = part(x.detach().requires_grad_(a.lo > 0))
+            if isinstance(x, tuple):  # AmoebaNet's (x, skip) boundary
+                y = part(tuple(t.detach().requires_grad_(True) for t in x))
+            else:
+                y = part(x.detach().requires_grad_(a.lo > 0))
             if last:
                 F.cross_entropy(y, target).backward()
             else:
