@@ -978,8 +978,9 @@ std::vector<at::Tensor> convbn_backward(const at::Tensor& dy_in, const at::Tenso
       ymask_ptr = y_mask->data_ptr<float>();
       gout_ptr = dy_masked->data_ptr<float>();
     } else {
-      at::threshold_backward_out(const_cast<at::Tensor&>(*dy_masked), dy, *y_mask, 0);
-      dy = *dy_masked;
+      at::Tensor masked = *dy_masked;  // (a handle to the caller's buffer)
+      at::threshold_backward_out(masked, dy, *y_mask, 0);
+      dy = masked;
       dy_img = 0;
     }
   }
