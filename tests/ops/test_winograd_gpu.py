@@ -371,3 +371,35 @@ def test_module_weight_gradient_picks_split_bf16_gemm_for_deep_layers():
         [1, 1], False, [0, 0], 1, [False, True, False])[1]
     torch.testing.assert_close(m.weight.grad.double(), want, rtol=1e-4,
                                atol=5e-5 * (want.abs().max().item() + 1))
+
+
+@pytest.mark.parametrize('shape,kind', [((22, 256, 256, 14, 14), 4), ((22, 512, 512, 7, 7), 2),
+                                        ((3, 70, 130, 13, 11), 4), ((3, 70, 130, 13, 11), 2),
+                                        ((9, 256, 64, 28, 28), 4)])
+def test_batched_gemm_output_pass_leaves_batchnorm_statistics(shape, kind):
+    """``bg_conv(..., stats=)``: the same output as without (same arithmetic), plus per
+    (image group, channel) mean / centred M2 partials that merge to the output's batch
+    mean and variance (float64 reference)."""
+    n, c, k, h, w = shape
+    torch.manual_seed(4)
+    ops = _ext.require(torch.empty(1, device=cuda))
+    x = torch.randn(n, c, h, w, device=cuda)
+    wt = torch.randn(k, c, 3, 3, device=cuda) / (3 * c ** 0.5)
+    u = ops.bg_weight(wt, False, kind, emu=1)
+    ipg = ops.bg_stats_images(n, h, w, kind)
+    groups = -(-n // ipg)
+    stats = torch.full((2, groups, k), float('nan'), device=cuda)
+    y = ops.bg_conv(x, u, None, k, 0, 0, kind, emu=1, stats=stats)
+    y_plain = ops.bg_conv(x, u, None, k, 0, 0, kind, emu=1)
+    torch.testing.assert_close(y, y_plain, rtol=0, atol=0)
+    counts = torch.tensor([min(ipg, n - g * ipg) * h * w for g in range(groups)],
+                          dtype=torch.float64, device=cuda)[:, None]
+    mean_g, m2_g = stats[0].double(), stats[1].double()
+    total = counts.sum()
+    mean = (counts * mean_g).sum(0) / total
+    m2 = (m2_g + counts * (mean_g - mean) ** 2).sum(0)
+    want = y.double()
+    torch.testing.assert_close(mean, want.mean((0, 2, 3)), rtol=1e-5,
+                               atol=1e-6 * want.abs().max().item())
+    torch.testing.assert_close(m2 / total, want.var((0, 2, 3), unbiased=False), rtol=1e-5,
+                               atol=1e-7)

@@ -342,7 +342,8 @@ at::Tensor bg_weight(const at::Tensor& w, bool flip, int64_t kind,
 
 at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
                    const c10::optional<at::Tensor>& bias, int64_t out_channels, int64_t bn,
-                   int64_t splits, int64_t kind, int64_t waves, int64_t sub, int64_t emu) {
+                   int64_t splits, int64_t kind, int64_t waves, int64_t sub, int64_t emu,
+                   const c10::optional<at::Tensor>& stats) {
   auto x = x_in.contiguous();
   check_f32_gpu(x, "x");
   check_f32_gpu(a, "a");
@@ -372,10 +373,28 @@ at::Tensor bg_conv(const at::Tensor& x_in, const at::Tensor& a,
   TORCH_CHECK(plan.ksteps * 16 * plan.np < (int64_t{1} << 31) &&
                   plan.mp * plan.np < (int64_t{1} << 31),
               "operands too large for the batched-GEMM kernels");
+  // stats: the BatchNorm (mean, M2) partials of y, [2][groups][out_channels] with groups =
+  // ceil(n / bg_stats_ipg(n, h, w, kind)) -- the caller's bn_train_forward reads them
+  float* pm = nullptr;
+  int ipg = 0;
+  if (stats.has_value() && stats->defined()) {
+    check_f32_gpu(*stats, "stats");
+    ipg = bg_stats_ipg(n, h, w, static_cast<int>(kind));
+    const int64_t groups = (n + ipg - 1) / ipg;
+    TORCH_CHECK(stats->device() == x.device() && stats->is_contiguous() &&
+                    stats->numel() == 2 * groups * out_channels,
+                "stats must be a contiguous [2][ceil(n / bg_stats_ipg)][K] float32 tensor");
+    pm = stats->data_ptr<float>();
+  }
   auto ws = at::empty({plan.workspace}, x.options());
   launch_bg_conv(x.data_ptr<float>(), a.data_ptr<float>(), bptr, y.data_ptr<float>(),
-                 ws.data_ptr<float>(), n, r, h, w, out_channels, plan, stream_of(x));
+                 ws.data_ptr<float>(), n, r, h, w, out_channels, plan, stream_of(x), pm,
+                 pm == nullptr ? nullptr : pm + stats->numel() / 2, ipg);
   return y;
+}
+
+int64_t bg_stats_images(int64_t n, int64_t h, int64_t w, int64_t kind) {
+  return bg_stats_ipg(n, h, w, static_cast<int>(kind));
 }
 
 // Split-K count of the F(4x4) kernels for one convolution: variant 0 = the weight gradient,
@@ -413,7 +432,9 @@ TORCH_LIBRARY(tgpipe, m) {
   m.def("wino4_splits(int n, int c, int k, int h, int w, int variant) -> int",
         &tgpipe::wino4_splits);
   m.def("bg_conv(Tensor x, Tensor a, Tensor? bias, int out_channels, int bn=0, int splits=0, "
-        "int kind=4, int waves=0, int sub=0, int emu=-1) -> Tensor");
+        "int kind=4, int waves=0, int sub=0, int emu=-1, Tensor(b!)? stats=None) -> Tensor");
+  // images per BatchNorm-statistics group of bg_conv's `stats` (host only)
+  m.def("bg_stats_images(int n, int h, int w, int kind) -> int", &tgpipe::bg_stats_images);
 }
 
 TORCH_LIBRARY_IMPL(tgpipe, CUDA, m) {

@@ -1468,18 +1468,31 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
                                          const c10::optional<at::Tensor>& running_mean,
                                          const c10::optional<at::Tensor>& running_var,
                                          const c10::optional<at::Tensor>& num_batches_tracked,
-                                         double momentum, bool relu) {
+                                         double momentum, bool relu,
+                                         const c10::optional<at::Tensor>& part,
+                                         int64_t part_images) {
   auto x = x_in.contiguous();
   check_f32(x, "x", x);
   TORCH_CHECK(x.dim() >= 2, "x must be [N][C][*]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t n = x.size(0), c = x.size(1), s = n * c == 0 ? 0 : x.numel() / (n * c);
   const auto stream = cur_stream(x);
+  // `part`: x's (mean, M2) partials left by its producer ([2][groups][C], `part_images`
+  // images per group: bg_conv's `stats`) -- no statistics pass here
+  const bool given = part.has_value() && part->defined();
+  int64_t groups = n, width = s;
+  if (given) {
+    check_f32(*part, "part", x);
+    TORCH_CHECK(part_images > 0, "part needs part_images > 0");
+    groups = (n + part_images - 1) / part_images;
+    width = part_images * s;
+    TORCH_CHECK(part->numel() == 2 * groups * c, "part must be [2][ceil(n / part_images)][C]");
+  }
   // the statistics outputs and the partials in one allocation (stat_block): a launch-bound
   // stage pays host time per allocation
-  StatBlock st = stat_block(x, c, 2 * n * c);
-  float* const part0 = st.extra;
-  float* const part1 = part0 + n * c;
+  StatBlock st = stat_block(x, c, given ? 0 : 2 * n * c);
+  float* const part0 = given ? part->data_ptr<float>() : st.extra;
+  float* const part1 = part0 + groups * c;
   auto mean = st.mean, invstd = st.invstd;
   auto y = at::empty_like(x);
   if (x.numel() == 0) return {y, mean.zero_(), invstd.fill_(1.f), at::zeros({2, c}, x.options())};
@@ -1501,11 +1514,10 @@ std::vector<at::Tensor> bn_train_forward(const at::Tensor& x_in,
                 "num_batches_tracked must be a 1-element int64 tensor on the input's device");
     tracked = num_batches_tracked->data_ptr<int64_t>();
   }
-  launch_bn_stats(x.data_ptr<float>(), part0, part1, n, c,
-                  s, stream);
+  if (!given) launch_bn_stats(x.data_ptr<float>(), part0, part1, n, c, s, stream);
   auto sums = st.sums;  // zeroed by the finalize, for the backward
   launch_bn_finalize_apply(part0, part1,
-                           static_cast<int>(n), static_cast<int>(s), n, c, s,
+                           static_cast<int>(groups), static_cast<int>(width), n, c, s,
                            static_cast<float>(eps), rm != nullptr ? momentum : 0.0,
                            mean.data_ptr<float>(), invstd.data_ptr<float>(),
                            const_cast<float*>(rm), const_cast<float*>(rv), tracked, accp,
@@ -1716,8 +1728,8 @@ TORCH_LIBRARY_FRAGMENT(tgpipe, m) {
   m.def("avgpool3_backward(Tensor dy, int h, int w, int stride) -> Tensor");
   m.def("bn_train_forward(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!)? acc, float eps, "
         "Tensor(b!)? running_mean=None, Tensor(c!)? running_var=None, "
-        "Tensor(d!)? num_batches_tracked=None, float momentum=0.0, bool relu=False) "
-        "-> Tensor[]");
+        "Tensor(d!)? num_batches_tracked=None, float momentum=0.0, bool relu=False, "
+        "Tensor? part=None, int part_images=0) -> Tensor[]");
   m.def("bn_train_backward(Tensor dy, Tensor x, Tensor mean, Tensor invstd, Tensor(a!) sums, "
         "Tensor? gamma, Tensor? beta=None, bool relu=False, Tensor(b!)? accum_gamma=None, "
         "Tensor(c!)? accum_beta=None) -> Tensor[]");

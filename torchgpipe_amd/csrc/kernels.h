@@ -112,9 +112,14 @@ BgPlan bg_plan(int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t ou
 int64_t bg_weight_numel(int64_t out_channels, int64_t red_channels, int kind, int emu = -1);
 void launch_bg_weight(const float* w, float* a, int64_t out_channels, int64_t red_channels,
                       bool flip, int kind, hipStream_t stream, int emu = -1);
+// pm / pm2 (optional, [groups][out_channels] each, groups = ceil(n / ipg)): the output pass
+// also leaves the BatchNorm (mean, M2) partials of y per (image group, channel), count
+// ipg * h * w (bn_stats_kernel's role); ipg from bg_stats_ipg.
+int bg_stats_ipg(int64_t n, int64_t h, int64_t w, int kind);
 void launch_bg_conv(const float* x, const float* a, const float* bias, float* y, float* ws,
                     int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
-                    const BgPlan& plan, hipStream_t stream);
+                    const BgPlan& plan, hipStream_t stream, float* pm = nullptr,
+                    float* pm2 = nullptr, int ipg = 0);
 
 
 // F(4x4,3x3) weight gradient (winograd_f4.hip): dw[K][C][3][3], 36 MFMA multiplies per

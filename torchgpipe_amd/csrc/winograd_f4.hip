@@ -2181,6 +2181,138 @@ __global__ __launch_bounds__(256) void bg_output_f2_kernel(
   }
 }
 
+
+// The output transform of the batched-GEMM Winograd with the BatchNorm statistics of its
+// output in the same pass (a following bn_finalize_apply reads them instead of a
+// bn_stats pass re-reading y): wave w of workgroup (x, g) owns output channel 4x + w and the
+// tiles of images [g * ipg, (g + 1) * ipg); each lane writes its tiles' outputs exactly as
+// bg_output_f4_kernel / bg_output_f2_kernel do, takes each tile's mean and centred M2 over
+// its pixels inside the plane, Chan-merges them, and the wave merges its lanes: one
+// (mean, M2) partial per (image group, channel), count ipg * H * W (fewer in the last).
+__device__ __forceinline__ void chan_merge_f(float& na, float& ma, float& m2a, float nb,
+                                             float mb, float m2b) {
+  const float nn = na + nb;
+  if (nn <= 0.f) return;
+  const float d = mb - ma;
+  const float f = nb / nn;
+  ma += d * f;
+  m2a += m2b + d * d * na * f;
+  na = nn;
+}
+
+template <int TILE>
+__global__ __launch_bounds__(256) void bg_output_stats_kernel(
+    const float* __restrict__ cbuf, const float* __restrict__ bias, float* __restrict__ y,
+    float* __restrict__ pm, float* __restrict__ pm2, int O, int Mp, int Np, int P, int tpi,
+    int TW, int H, int W, int splits, int ipg) {
+  constexpr int NPOS = TILE == 4 ? kP : kP2;
+  const int lane = threadIdx.x & 63;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int g = blockIdx.y;
+  if (o >= O) return;  // (whole waves: no barrier below)
+  const int t0 = g * ipg * tpi;
+  const int t1 = min(P, t0 + ipg * tpi);
+  const int64_t pos = static_cast<int64_t>(Mp) * Np;
+  const float bv = bias ? bias[o] : 0.f;
+  float cnt = 0.f, mean = 0.f, m2 = 0.f;
+  for (int t = t0 + lane; t < t1; t += 64) {
+    const float* src = cbuf + static_cast<int64_t>(o) * Np + t;
+    float m[NPOS];
+#pragma unroll
+    for (int b = 0; b < NPOS; ++b) m[b] = src[b * pos];
+    for (int z = 1; z < splits; ++z) {
+      const float* sz = src + static_cast<int64_t>(z) * NPOS * pos;
+#pragma unroll
+      for (int b = 0; b < NPOS; ++b) m[b] += sz[b * pos];
+    }
+    float v[TILE][TILE];
+    if constexpr (TILE == 4) {  // bg_output_f4_kernel's arithmetic
+      float sr[4][6];
+#pragma unroll
+      for (int jc = 0; jc < 6; ++jc) {
+        const float a = m[6 + jc] + m[12 + jc], bq = m[6 + jc] - m[12 + jc];
+        const float cc = m[18 + jc] + m[24 + jc], d = m[18 + jc] - m[24 + jc];
+        sr[0][jc] = m[jc] + a + cc;
+        sr[1][jc] = bq + 2.f * d;
+        sr[2][jc] = a + 4.f * cc;
+        sr[3][jc] = bq + 8.f * d + m[30 + jc];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float a = sr[k][1] + sr[k][2], bq = sr[k][1] - sr[k][2];
+        const float cc = sr[k][3] + sr[k][4], d = sr[k][3] - sr[k][4];
+        v[k][0] = sr[k][0] + a + cc + bv;
+        v[k][1] = bq + 2.f * d + bv;
+        v[k][2] = a + 4.f * cc + bv;
+        v[k][3] = bq + 8.f * d + sr[k][5] + bv;
+      }
+    } else {  // bg_output_f2_kernel's arithmetic
+      float sr[2][4];
+#pragma unroll
+      for (int jc = 0; jc < 4; ++jc) {
+        sr[0][jc] = m[jc] + m[4 + jc] + m[8 + jc];
+        sr[1][jc] = m[4 + jc] - m[8 + jc] - m[12 + jc];
+      }
+#pragma unroll
+      for (int kr = 0; kr < 2; ++kr) {
+        v[kr][0] = sr[kr][0] + sr[kr][1] + sr[kr][2] + bv;
+        v[kr][1] = sr[kr][1] - sr[kr][2] - sr[kr][3] + bv;
+      }
+    }
+    const int n = t / tpi;
+    const int rem = t - n * tpi;
+    const int ty = rem / TW;
+    const int py = TILE * ty, px = TILE * (rem - ty * TW);
+    float* yp = y + (static_cast<int64_t>(n) * O + o) * H * W + static_cast<int64_t>(py) * W + px;
+    const int rows = min(TILE, H - py), cols = min(TILE, W - px);
+    float ts = 0.f;
+#pragma unroll
+    for (int k = 0; k < TILE; ++k) {
+      if (k >= rows) break;
+      bool stored = false;
+      if constexpr (TILE == 4) {
+        if (cols == 4 && (W & 3) == 0) {
+          *reinterpret_cast<floatx4*>(yp + k * W) = floatx4{v[k][0], v[k][1], v[k][2], v[k][3]};
+          stored = true;
+        }
+      }
+      if (!stored) {
+#pragma unroll
+        for (int l = 0; l < TILE; ++l)
+          if (l < cols) yp[k * W + l] = v[k][l];
+      }
+#pragma unroll
+      for (int l = 0; l < TILE; ++l)
+        if (l < cols) ts += v[k][l];
+    }
+    const float tc = static_cast<float>(rows * cols);
+    const float tm = ts / tc;
+    float tq = 0.f;
+#pragma unroll
+    for (int k = 0; k < TILE; ++k) {
+      if (k >= rows) break;
+#pragma unroll
+      for (int l = 0; l < TILE; ++l) {
+        if (l < cols) {
+          const float d = v[k][l] - tm;
+          tq += d * d;
+        }
+      }
+    }
+    chan_merge_f(cnt, mean, m2, tc, tm, tq);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float nb = __shfl_xor(cnt, off), mb = __shfl_xor(mean, off);
+    const float qb = __shfl_xor(m2, off);
+    chan_merge_f(cnt, mean, m2, nb, mb, qb);
+  }
+  if (lane == 0) {
+    pm[static_cast<int64_t>(g) * O + o] = mean;
+    pm2[static_cast<int64_t>(g) * O + o] = m2;
+  }
+}
+
 }  // namespace
 
 int64_t wino4_pad_reduction(int64_t r) { return (r + kC - 1) / kC * kC; }
@@ -2529,9 +2661,17 @@ void launch_bg_weight(const float* w, float* a, int64_t out_channels, int64_t re
                      static_cast<int>(mp), static_cast<int>(ksteps), flip);
 }
 
+int bg_stats_ipg(int64_t n, int64_t h, int64_t w, int kind) {
+  // images per statistics group: >= 64 tiles (one per lane of the channel's wave) when the
+  // batch allows
+  const int64_t tile = kind == 2 ? 2 : 4;
+  const int64_t tpi = std::max<int64_t>(1, ((h + tile - 1) / tile) * ((w + tile - 1) / tile));
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(n, (64 + tpi - 1) / tpi)));
+}
+
 void launch_bg_conv(const float* x, const float* a, const float* bias, float* y, float* ws,
                     int64_t n, int64_t red_channels, int64_t h, int64_t w, int64_t out_channels,
-                    const BgPlan& plan, hipStream_t stream) {
+                    const BgPlan& plan, hipStream_t stream, float* pm, float* pm2, int ipg) {
   const int tile = plan.kind;
   const int npos = plan.kind == 2 ? kP2 : kP;
   const int64_t th = (h + tile - 1) / tile, tw = (w + tile - 1) / tile;
@@ -2606,6 +2746,18 @@ void launch_bg_conv(const float* x, const float* a, const float* bias, float* y,
                      v, cbuf, static_cast<int>(plan.mp), static_cast<int>(plan.np),
                      static_cast<int>(plan.ksteps), mtiles, ntiles, static_cast<int>(npos),
                      plan.splits);
+  if (pm != nullptr) {  // with the BatchNorm statistics of y (bg_output_stats_kernel)
+    const int64_t groups = (n + ipg - 1) / ipg;
+    const dim3 sgrid(static_cast<unsigned>((out_channels + 3) / 4),
+                     static_cast<unsigned>(groups));
+    hipLaunchKernelGGL(plan.kind == 2 ? bg_output_stats_kernel<2> : bg_output_stats_kernel<4>,
+                       sgrid, dim3(256), 0, stream, cbuf, bias, y, pm, pm2,
+                       static_cast<int>(out_channels), static_cast<int>(plan.mp),
+                       static_cast<int>(plan.np), static_cast<int>(P),
+                       static_cast<int>(th * tw), static_cast<int>(tw), static_cast<int>(h),
+                       static_cast<int>(w), plan.splits, ipg);
+    return;
+  }
   const int64_t ot = out_channels * P;
   hipLaunchKernelGGL(plan.kind == 2 ? bg_output_f2_kernel : bg_output_f4_kernel,
                      dim3(static_cast<unsigned>((ot + 255) / 256)), dim3(256),

@@ -49,7 +49,7 @@ from torchgpipe_amd.ops import _ext, gradacc
 
 __all__ = ['WinogradConv2d', 'winograd_conv2d', 'wino_eligible', 'new_step',
            'clear_winograd_caches', 'cache_bytes', 'refresh_step_caches', 'hold_cache',
-           'size_cache_budget']
+           'size_cache_budget', 'conv_with_bn_stats']
 
 _STEP = 0
 _CACHE_BYTES: Dict[torch.device, int] = {}  # cached bytes per device
@@ -428,6 +428,63 @@ class _WinogradConv(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum((0, 2, 3))
         return dx, dw, db, None
+
+
+class _WinogradConvStats(torch.autograd.Function):
+    """The batched-GEMM forward of :class:`_WinogradConv` whose output pass also leaves the
+    BatchNorm (mean, M2) partials of its output (``bg_conv``'s ``stats``): a linked
+    BatchNorm (``ops/fusion.py`` ``ConvBN2d``) normalises from them without its own
+    statistics pass.  Backward as :class:`_WinogradConv`."""
+
+    @staticmethod
+    def forward(ctx, x: Tensor, weight: Tensor, cache: _TransformCache,  # type: ignore[override]
+                kind: int) -> Tuple[Tensor, Tensor]:
+        ops = _ext.require(x)
+        x = x.contiguous()
+        n, _, h, w = x.shape
+        k = weight.shape[0]
+        groups = -(-n // ops.bg_stats_images(n, h, w, kind))
+        stats = torch.empty(2, groups, k, device=x.device, dtype=torch.float32)
+        y = ops.bg_conv(x, cache.get(weight, False, bg=kind), None, k, 0, 0, kind,
+                        stats=stats)
+        ctx.save_for_backward(x, weight)
+        ctx.cache = cache
+        ctx.param = weight
+        ctx.mark_non_differentiable(stats)
+        # (no zero-filled gradient for `stats` per backward: one fill kernel per call)
+        ctx.set_materialize_grads(False)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy: Optional[Tensor], _dstats: Optional[Tensor]):  # type: ignore[override]
+        if dy is None:
+            ctx.param = None
+            return None, None, None, None
+        x, weight = ctx.saved_tensors
+        dx, dw = _conv_grads(x, weight, dy.contiguous(), ctx.cache, ctx.needs_input_grad[0],
+                             ctx.needs_input_grad[1], ctx.param)
+        ctx.param = None
+        return dx, dw, None, None
+
+
+# TGPIPE_BG_BN_STATS=0: a linked BatchNorm after a batched-GEMM Winograd layer takes its own
+# statistics pass (bn_stats_kernel) instead of the output pass's partials
+BG_BN_STATS = os.environ.get('TGPIPE_BG_BN_STATS', '1') != '0'
+
+
+def conv_with_bn_stats(module: nn.Conv2d, x: Tensor
+                       ) -> Optional[Tuple[Tensor, Tensor, int]]:
+    """``(y, stats, images per group)`` of a bias-free 3x3 ``WinogradConv2d`` on the
+    batched-GEMM path, with its output's BatchNorm partials (``_WinogradConvStats``);
+    ``None`` when the layer takes another path.  Callers checked ``wino_eligible``."""
+    if not BG_BN_STATS or module.bias is not None:
+        return None
+    kind = _bg_kind(x, module.out_channels)
+    if not kind:
+        return None
+    y, stats = _WinogradConvStats.apply(x, module.weight, module._wino, kind)
+    n, _, h, w = x.shape
+    return y, stats, _ext.require(x).bg_stats_images(n, h, w, kind)
 
 
 def _conv_grads(x: Tensor, weight: Tensor, dy: Tensor, cache: _TransformCache, need_x: bool,

@@ -15,11 +15,12 @@ one native op needs the layers to cooperate:
     (``ops.convbn.relu_conv_bn`` with ``relu_out``); the backward re-derives the ReLU
     mask from the saved convolution output;
   - 3x3 stride-1 convolutions: the Winograd F(4x4) / batched-GEMM kernels
-    (``ops.conv``), then the native BatchNorm(+ReLU) pass (:func:`bn_act`);
+    (``ops.conv``), then the native BatchNorm(+ReLU) pass (:func:`bn_act`) -- from the
+    batched-GEMM output pass's statistics partials where it ran (``conv_with_bn_stats``);
   - strided convolutions (the 7x7 stem, the stride-2 3x3 and 1x1 of each stage's first
     block): the fused native op (implicit-GEMM forward, stride-phase backward-data) for the
-    three geometries where it measured faster (``STRIDED_FUSED``), MIOpen then
-    :func:`bn_act` for the others;
+    geometries where it measured faster (``STRIDED_FUSED``), MIOpen then :func:`bn_act`
+    for the others;
 
   and marks its output as normalised (and rectified) by that BatchNorm;
 * :class:`BatchNormAct2d` passes a marked input through; otherwise it runs the native
@@ -41,7 +42,7 @@ from torch import Tensor, nn
 import torch.nn.functional as F
 
 from torchgpipe_amd.ops import _ext, gradacc
-from torchgpipe_amd.ops.conv import WinogradConv2d, wino_eligible
+from torchgpipe_amd.ops.conv import WinogradConv2d, conv_with_bn_stats, wino_eligible
 from torchgpipe_amd.ops.convbn import (GradSink, _bn_ok, fusable, gemm_conv2d,
                                        gemm_conv_eligible, relu_conv_bn)
 
@@ -68,13 +69,15 @@ class _BNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x: Tensor, gamma: Optional[Tensor], beta: Optional[Tensor],  # type: ignore[override]
-                bn: nn.BatchNorm2d, relu: bool) -> Tensor:
+                bn: nn.BatchNorm2d, relu: bool, part: Optional[Tensor] = None,
+                part_images: int = 0) -> Tensor:
         track = bn.track_running_stats and bn.running_mean is not None
+        # part: x's statistics partials from its producer (ops/conv.py conv_with_bn_stats)
         y, mean, invstd, sums = _ext.require(x).bn_train_forward(
             x, gamma, beta, None, float(bn.eps),
             bn.running_mean if track else None, bn.running_var if track else None,
             bn.num_batches_tracked if track else None,
-            float(bn.momentum) if track else 0.0, relu)
+            float(bn.momentum) if track else 0.0, relu, part, part_images)
         ctx.save_for_backward(x, mean, invstd, sums, gamma, beta)
         ctx.relu = relu
         ctx.params = (bn.weight, bn.bias)
@@ -98,17 +101,18 @@ class _BNAct(torch.autograd.Function):
                     gradacc.commit(p, grads[k])
                 grads[k] = None
         ctx.params = None
-        return (dx, grads[0], grads[1], None, None)
+        return (dx, grads[0], grads[1], None, None, None, None)
 
 
 def _native_bn_ok(bn: nn.BatchNorm2d, x: Tensor) -> bool:
     return _bn_ok(bn, x) and x.numel() > 0 and _ext.available()
 
 
-def bn_act(x: Tensor, bn: nn.BatchNorm2d, relu: bool) -> Tensor:
+def bn_act(x: Tensor, bn: nn.BatchNorm2d, relu: bool, part: Optional[Tensor] = None,
+           part_images: int = 0) -> Tensor:
     """``relu(bn(x))`` (or ``bn(x)``) in training mode on the native kernels; callers check
-    :func:`_native_bn_ok` first."""
-    return _BNAct.apply(x.contiguous(), bn.weight, bn.bias, bn, relu)
+    :func:`_native_bn_ok` first.  ``part``: x's (mean, M2) partials from its producer."""
+    return _BNAct.apply(x.contiguous(), bn.weight, bn.bias, bn, relu, part, part_images)
 
 
 def _mark(y: Tensor, bn: nn.Module, relu: bool) -> Tensor:
@@ -280,6 +284,11 @@ class ConvBN2d(WinogradConv2d):
                 return out
             if self.bias is None and _native_bn_ok(bn, input):
                 if wino:
+                    # the batched-GEMM Winograd's output pass leaves the BatchNorm partials
+                    with_stats = conv_with_bn_stats(self, input)
+                    if with_stats is not None:
+                        z, part, images = with_stats
+                        return _mark(bn_act(z, bn, relu, part, images), bn, relu)
                     z = WinogradConv2d.forward(self, input)
                     return _mark(bn_act(z, bn, relu), bn, relu)
                 if _pointwise(self) and fusable(input, [self], bn):
