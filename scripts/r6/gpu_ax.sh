@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-out=gpurun_out/r6ax
+out=gpurun_out/${R6AX_OUT:-r6ax}
 mkdir -p $out
 bash scripts/r6/gpu_r.sh || exit 1
 for r in 1 2; do
