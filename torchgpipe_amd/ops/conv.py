@@ -40,6 +40,7 @@ the transform runs once per optimizer step instead of once per call.
 import os
 import threading
 from typing import Any, Dict, List, Optional, Sequence, Tuple
+import weakref
 
 import torch
 from torch import Tensor, nn
@@ -190,6 +191,7 @@ class _TransformCache:
     __slots__ = ('_entries', '_weight', '__weakref__')
 
     def __init__(self) -> None:
+        cache_created()
         self._entries: Dict[Tuple, Tuple[Tuple[int, int, torch.device, int], Tensor,
                                          Optional[Any]]] = {}
         # a detached alias of the weight (same storage and version counter): the caller may
@@ -276,20 +278,45 @@ class _TransformCache:
         return (type(self), ())
 
 
+# bumped whenever a step-scoped cache object (_TransformCache, convbn._GroupCache) is made:
+# refresh_step_caches re-scans a module's attributes only then
+_CACHE_EPOCH = 0
+
+
+def cache_created() -> None:
+    global _CACHE_EPOCH
+    _CACHE_EPOCH += 1
+
+
+# module -> (cache epoch, weak references to its cache objects); outside the module, so
+# pickling or copying a module carries none of it
+_SCANS: 'weakref.WeakKeyDictionary[nn.Module, Tuple[int, List[Any]]]' = \
+    weakref.WeakKeyDictionary()
+
+
+def _step_caches(module: nn.Module) -> List[Any]:
+    """The cache objects held by ``module``'s (sub)modules: scanned once per cache epoch (a
+    ResNet-101 scan is ~2.5 ms of host time at every step start otherwise)."""
+    from torchgpipe_amd.ops.convbn import _GroupCache
+    hit = _SCANS.get(module)
+    if hit is None or hit[0] != _CACHE_EPOCH:
+        refs = [weakref.ref(v) for m in module.modules() for v in list(vars(m).values())
+                if isinstance(v, (_TransformCache, _GroupCache))]
+        hit = _SCANS[module] = (_CACHE_EPOCH, refs)
+    return [v for v in (r() for r in hit[1]) if v is not None]
+
+
 def refresh_step_caches(module: nn.Module) -> None:
     """Refresh every step-scoped derived-weight cache in ``module`` in place (current
     stream): Winograd transforms, transposed weights, grouped-GEMM concatenations and the
     split-bf16 GEMMs' pre-split weights."""
-    from torchgpipe_amd.ops.convbn import _GroupCache
     sources: List[Tensor] = []
-    for m in module.modules():
-        for v in list(vars(m).values()):
-            if isinstance(v, _TransformCache):
-                v.refresh()
-                sources += v.derived()
-            elif isinstance(v, _GroupCache):
-                v.refresh()
-                sources += [t for t in (v.cat, v.cat_t) if t is not None]
+    for v in _step_caches(module):
+        v.refresh()
+        if isinstance(v, _TransformCache):
+            sources += v.derived()
+        else:
+            sources += [t for t in (v.cat, v.cat_t) if t is not None]
     if _ext._loaded:
         # then the implicit-GEMM kernels' pre-split weights (csrc/convbn.cpp presplit_of)
         # derived from this module's parameters and the transposes / concatenations above

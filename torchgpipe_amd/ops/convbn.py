@@ -368,6 +368,8 @@ class _GroupCache:
     __slots__ = ('key', 'cat', 'cat_t', 'weights', 'ready', '__weakref__')
 
     def __init__(self) -> None:
+        from torchgpipe_amd.ops.conv import cache_created
+        cache_created()
         self.key: Optional[Tuple] = None
         self.cat: Optional[Tensor] = None
         self.cat_t: Optional[Tensor] = None
