@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-out=gpurun_out/r6bg
+out=gpurun_out/${R6BG_OUT:-r6bg}
 mkdir -p $out
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/p_resnet -o run -- python3 bench.py --gpus 1 --model resnet --steps 2 --warmup 3 --sections none > $out/resnet_p1.json 2> $out/resnet_p1.err || { tail -20 $out/resnet_p1.err; exit 1; }
 ms=$(python3 -c "import json;d=json.loads(open('$out/resnet_p1.json').read().splitlines()[-1]);print(d['ms_per_step']*2)")
