@@ -28,7 +28,8 @@ def main():
     for i in frees:
         print(f'--- {a.name} {(regs[i][2] - regs[i][1]) / 1e3:.1f} us')
         for j in range(max(0, i - 6), min(len(regs), i + 4)):
-            print(f'   {"*" if j == i else " "} {regs[j][0]} {(regs[j][2] - regs[j][1]) / 1e3:.1f}')
+            mark = '*' if j == i else ' '
+            print(f'   {mark} {regs[j][0]} {(regs[j][2] - regs[j][1]) / 1e3:.1f}')
         nxt = [k[0][:80] for k in kerns if k[1] > regs[i][2]][:3]
         print('   next kernels:', nxt)
     names = {}
